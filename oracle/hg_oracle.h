@@ -1,0 +1,82 @@
+/*
+ * hg_oracle.h -- TEST INFRASTRUCTURE. CPU restatement of the reference Hashgraph
+ * consensus path (datatypevoid/babble v0.2.0, hashgraph/hashgraph.go) used ONLY as
+ * the parity checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg. It is never linked into or called by the product library (babble_amd/libhgx.so).
+ *
+ * Pinning: checked against every structural known-answer assertion of the
+ * reference's own tests (hashgraph/hashgraph_test.go, node/core_test.go) via the
+ * fixtures in tests/golden/ (see tests/test_oracle_kat.py). Event/block hash bytes
+ * follow SURVEY.md Appendix B and are "parity unpinned" (no reference test pins a hash).
+ *
+ * Identity: events are dense ids (gid) in insertion order; "" (no parent) is -1,
+ * an unknown parent hash is HGO_UNKNOWN (-2). Participants are ids 0..n-1.
+ * Only the genesis Root (X=Y="", Index=-1, Round=-1; hashgraph/root.go:70-77) is
+ * supported: Reset/Frame (hashgraph.go:879-1002) is out of scope.
+ */
+#ifndef HG_ORACLE_H
+#define HG_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGO_UNKNOWN (-2)
+
+typedef struct hgo hgo;
+
+hgo* hgo_new(int n_participants);
+void hgo_free(hgo* h);
+
+/* InsertEvent(event, setWireInfo=true) (hashgraph.go:356-401). Returns 0 on success,
+ * else a StoreErr-like kind code (>0) with the Go error string in err (if non-NULL).
+ * txs: ntx payloads concatenated in tx_data with lengths tx_len (may be NULL if ntx==0). */
+int hgo_insert(hgo* h, int creator, int64_t index, int64_t self_parent, int64_t other_parent,
+               int64_t ts_ns, const uint8_t* hash32, const uint8_t* s32, int ntx, int tx_nil,
+               const uint8_t* tx_data, const int32_t* tx_len, char* err, int errlen);
+
+int hgo_divide_rounds(hgo* h);                       /* hashgraph.go:616-646 */
+int hgo_decide_fame(hgo* h, char* err, int errlen);  /* hashgraph.go:649-730 */
+int hgo_decide_round_received(hgo* h, char* err, int errlen); /* :753-799 */
+int hgo_find_order(hgo* h, char* err, int errlen);   /* hashgraph.go:801-858 */
+
+/* primitives (hashgraph.go:73-339); gids, -1 = "" */
+int hgo_ancestor(hgo* h, int64_t x, int64_t y);
+int hgo_self_ancestor(hgo* h, int64_t x, int64_t y);
+int hgo_see(hgo* h, int64_t x, int64_t y);
+int hgo_strongly_see(hgo* h, int64_t x, int64_t y);
+int64_t hgo_oldest_self_ancestor_to_see(hgo* h, int64_t x, int64_t y);
+int hgo_parent_round(hgo* h, int64_t x, int* is_root);
+int hgo_round_inc(hgo* h, int64_t x);
+int hgo_round(hgo* h, int64_t x);
+int hgo_witness(hgo* h, int64_t x);
+
+/* state / getters */
+int64_t hgo_num_events(hgo* h);
+int hgo_super_majority(hgo* h);
+int hgo_last_round(hgo* h);
+int hgo_round_event_count(hgo* h, int r);
+int hgo_round_witnesses(hgo* h, int r, int64_t* out, int cap);
+int hgo_famous(hgo* h, int64_t x);            /* 0 Undefined, 1 True, 2 False (roundInfo.go:9-15) */
+int hgo_round_received(hgo* h, int64_t x);    /* -1 = nil */
+int64_t hgo_consensus_timestamp(hgo* h, int64_t x);
+void hgo_coords(hgo* h, int64_t x, int32_t* la, int32_t* fd);
+void hgo_wire_info(hgo* h, int64_t x, int32_t* sp_index, int32_t* op_creator, int32_t* op_index);
+int hgo_undecided_rounds(hgo* h, int32_t* out, int cap);
+int hgo_last_consensus_round(hgo* h, int* has);   /* value, has=0 => nil */
+int hgo_last_commited_round_events(hgo* h);
+int64_t hgo_consensus_transactions(hgo* h);
+int64_t hgo_pending_loaded_events(hgo* h);
+int64_t hgo_consensus_events(hgo* h, int64_t* out, int64_t cap); /* full order, all FindOrder calls */
+void hgo_known(hgo* h, int32_t* out);   /* [participant] -> last index (-1 none) */
+/* blocks produced by FindOrder, in SetBlock order */
+int64_t hgo_num_blocks(hgo* h);
+void hgo_block(hgo* h, int64_t b, int32_t* rr, int32_t* ntx, int32_t* tx_nil,
+               int32_t* committed, uint8_t* hash32);
+int64_t hgo_block_tx(hgo* h, int64_t b, int32_t t, uint8_t* out, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
