@@ -1,0 +1,102 @@
+"""ctypes binding of libhgx.so (the C ABI declared in include/hgx.h).
+
+The library is built in-tree by __graft_entry__.build() (babble_amd/build.py).
+Loading fails loudly if it is missing: there is no Python or CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhgx.so")
+
+_L = None
+
+
+class HgxError(RuntimeError):
+    """A Go-equivalent error returned through the C ABI (code + verbatim message)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+        self.msg = msg
+
+
+class hgx_error(C.Structure):
+    _fields_ = [("code", C.c_int32), ("msg", C.c_char * 252)]
+
+
+class hgx_events(C.Structure):
+    _fields_ = [(nm, C.c_void_p) for nm in
+                ("creator", "index", "self_parent", "other_parent", "timestamp_ns", "hash", "sig_s",
+                 "ntx", "tx_nil")]
+
+
+def ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _sig(L, name, res, args):
+    f = getattr(L, name, None)
+    if f is None:
+        return
+    f.restype = res
+    f.argtypes = args
+
+
+def lib():
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    i32, i64, u64, p, d = C.c_int32, C.c_int64, C.c_uint64, C.c_void_p, C.c_double
+    E = C.POINTER(hgx_error)
+    _sig(L, "hgx_trace_gossip", i32, [i32, i32, i64, u64, d, i32] + [p] * 10)
+    _sig(L, "hgx_trace_tx_payload", i32, [i32, i64, p, i32])
+    _sig(L, "hgx_abi_version", i32, [])
+    _sig(L, "hgx_create", p, [i32, i64, i32, E])
+    _sig(L, "hgx_create_batch", p, [i32, i32, i64, i32, E])
+    _sig(L, "hgx_destroy", None, [p])
+    _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
+    for nm in ("hgx_divide_rounds", "hgx_decide_fame", "hgx_find_order", "hgx_run_consensus"):
+        _sig(L, nm, i32, [p, E])
+    _sig(L, "hgx_num_events", i64, [p])
+    _sig(L, "hgx_super_majority", i32, [p])
+    _sig(L, "hgx_num_undetermined", i64, [p, i32])
+    _sig(L, "hgx_undecided_rounds", i32, [p, i32, p, i32])
+    _sig(L, "hgx_last_consensus_round", i32, [p, i32, C.POINTER(C.c_int32)])
+    _sig(L, "hgx_last_commited_round_events", i32, [p, i32])
+    _sig(L, "hgx_consensus_transactions", i64, [p, i32])
+    _sig(L, "hgx_pending_loaded_events", i64, [p, i32])
+    _sig(L, "hgx_last_round", i32, [p, i32])
+    _sig(L, "hgx_round_event_count", i32, [p, i32, i32])
+    _sig(L, "hgx_round_witnesses", i32, [p, i32, i32, p, i32])
+    _sig(L, "hgx_known", i32, [p, i32, p])
+    _sig(L, "hgx_consensus_events_count", i64, [p, i32])
+    _sig(L, "hgx_consensus_events", i32, [p, i32, i64, i64, p])
+    _sig(L, "hgx_num_blocks", i64, [p, i32])
+    _sig(L, "hgx_block_info", i32, [p, i32, i64, p, p, p, p, p, p])
+    _sig(L, "hgx_get_rounds", i32, [p, i64, i64, p, p, p])
+    _sig(L, "hgx_get_received", i32, [p, i64, i64, p, p])
+    _sig(L, "hgx_get_coords", i32, [p, i64, p, p])
+    for nm in ("hgx_ancestor", "hgx_self_ancestor", "hgx_see", "hgx_strongly_see", "hgx_round", "hgx_witness"):
+        _sig(L, nm, i32, [p, i64, i64] if nm not in ("hgx_round", "hgx_witness") else [p, i64])
+    _sig(L, "hgx_oldest_self_ancestor_to_see", i64, [p, i64, i64])
+    _sig(L, "hgx_block_hash", i32, [i64, i32, p, p, i32, p])
+    _sig(L, "hgx_phase_times", i32, [p, p, i32])
+    _sig(L, "hgx_kernel_stats", i32, [p, i32, C.c_char_p, i32, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_double)])
+    _sig(L, "hgx_reset_stats", i32, [p])
+    _L = L
+    return L
+
+
+def check(rc: int, err: hgx_error):
+    if rc != 0:
+        raise HgxError(int(err.code or rc), err.msg.decode(errors="replace"))

@@ -1,0 +1,179 @@
+/*
+ * hgx.h -- C ABI of the MI355X-native Hashgraph consensus engine (libhgx.so).
+ *
+ * Drop-in boundary for the reference's consensus hot path (datatypevoid/babble
+ * v0.2.0, package hashgraph). A thin cgo shim keeps the Go API
+ *   (*Hashgraph).InsertEvent(Event, bool) error   hashgraph/hashgraph.go:356
+ *   (*Hashgraph).DivideRounds() error             hashgraph/hashgraph.go:616
+ *   (*Hashgraph).DecideFame() error               hashgraph/hashgraph.go:649
+ *   (*Hashgraph).FindOrder() error                hashgraph/hashgraph.go:801
+ * and the exported state Core reads (UndeterminedEvents, PendingLoadedEvents,
+ * LastConsensusRound, LastCommitedRoundEvents, ConsensusTransactions;
+ * hashgraph.go:15-37, node/core.go:335-369), mapping event hex ids to dense ids.
+ *
+ * Conventions
+ *  - Events get dense ids ("gid") in insertion order (the reference's
+ *    topologicalIndex, hashgraph.go:373). A parent that is "" is -1; a parent
+ *    hash the shim cannot resolve is HGX_UNKNOWN_PARENT.
+ *  - Participants are ids 0..n-1 (Hashgraph.Participants, hashgraph.go:16).
+ *    A batched context holds n_graphs independent hashgraphs; graph g owns
+ *    participant ids [g*n, (g+1)*n).
+ *  - All input arrays are copied before the call returns; no caller pointer is
+ *    retained (cgo pointer rules). Output arrays are caller-allocated.
+ *  - Every entry point returns HGX_OK (0) or an error code; the message of the
+ *    last error is written to hgx_error.msg verbatim as the Go error string.
+ *  - A context is single-caller (the reference serialises calls under
+ *    node.coreLock, node/node.go:226-237); it owns one HIP stream.
+ *  - The library fails loudly (HGX_ERR_DEVICE) when no gfx950 device is usable:
+ *    there is no CPU fallback.
+ */
+#ifndef HGX_H
+#define HGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGX_ABI_VERSION 1
+
+/* Error codes. 1..5 mirror common.StoreErrType + 1 (common/errors.go:7-13). */
+enum {
+    HGX_OK = 0,
+    HGX_ERR_KEY_NOT_FOUND = 1,  /* "%s, Not Found"        errors.go:27 */
+    HGX_ERR_TOO_LATE = 2,       /* "%s, Too Late"         errors.go:29 */
+    HGX_ERR_PASSED_INDEX = 3,   /* "%s, Passed Index"     errors.go:31 */
+    HGX_ERR_SKIPPED_INDEX = 4,  /* "%s, Skipped Index"    errors.go:33 */
+    HGX_ERR_NO_ROOT = 5,        /* "%s, No Root"          errors.go:35 */
+    HGX_ERR_SELF_PARENT = 100,  /* "CheckSelfParent: Self-parent not last known event by creator" hashgraph.go:366,416 */
+    HGX_ERR_OTHER_PARENT = 101, /* "CheckOtherParent: Other-parent not known" hashgraph.go:370,441 */
+    HGX_ERR_INVALID = 102,      /* bad argument to the C ABI itself */
+    HGX_ERR_CAPACITY = 103,     /* context capacity exceeded */
+    HGX_ERR_DEVICE = 200,       /* HIP error / no gfx950 device */
+    HGX_ERR_PANIC = 300         /* the reference would panic here (e.g. UndecidedRounds[0] on empty) */
+};
+
+#define HGX_UNKNOWN_PARENT (-2)
+
+typedef struct {
+    int32_t code;
+    char msg[252];
+} hgx_error;
+
+typedef struct hgx_ctx hgx_ctx;
+
+/* Event batch, structure of arrays, `count` entries each (hashgraph/event.go:14-76). */
+typedef struct {
+    const int32_t* creator;       /* participant id (global id in a batched ctx) */
+    const int64_t* index;         /* Body.Index */
+    const int64_t* self_parent;   /* gid, -1 for "" */
+    const int64_t* other_parent;  /* gid, -1 for "", HGX_UNKNOWN_PARENT if not known */
+    const int64_t* timestamp_ns;  /* Body.Timestamp as Unix ns (UTC) */
+    const uint8_t* hash;          /* 32 bytes per event: SHA-256 event id (Event.Hash) */
+    const uint8_t* sig_s;         /* 32 bytes per event: signature S, big-endian, zero-padded */
+    const int32_t* ntx;           /* len(Body.Transactions) */
+    const int32_t* tx_nil;        /* 1 if Body.Transactions == nil */
+} hgx_events;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int32_t hgx_abi_version(void);
+/* NewHashgraph(participants, store, ...) (hashgraph.go:39-66) with an InmemStore of
+ * cacheSize >= capacity_events (no eviction). device = HIP device ordinal. */
+hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t device, hgx_error* err);
+/* n_graphs independent hashgraphs of n_participants each (seed-sharded simulations) */
+hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capacity_events,
+                          int32_t device, hgx_error* err);
+void hgx_destroy(hgx_ctx* ctx);
+
+/* ---- the four drop-in calls ------------------------------------------------ */
+/* InsertEvent(e, true) for each event in order; stops at the first failure
+ * (like Core.Sync, node/core.go:199-211). *n_inserted = events accepted. */
+int32_t hgx_insert_events(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
+                          hgx_error* err);
+int32_t hgx_divide_rounds(hgx_ctx* ctx, hgx_error* err);
+int32_t hgx_decide_fame(hgx_ctx* ctx, hgx_error* err);
+int32_t hgx_find_order(hgx_ctx* ctx, hgx_error* err);
+/* Core.RunConsensus (node/core.go:277-303): the three calls in sequence */
+int32_t hgx_run_consensus(hgx_ctx* ctx, hgx_error* err);
+
+/* ---- Hashgraph state (hashgraph.go:15-37) --------------------------------- */
+int64_t hgx_num_events(hgx_ctx* ctx);
+int32_t hgx_super_majority(hgx_ctx* ctx);
+int64_t hgx_num_undetermined(hgx_ctx* ctx, int32_t graph);
+int32_t hgx_undecided_rounds(hgx_ctx* ctx, int32_t graph, int32_t* out, int32_t cap); /* returns length */
+int32_t hgx_last_consensus_round(hgx_ctx* ctx, int32_t graph, int32_t* has_value);
+int32_t hgx_last_commited_round_events(hgx_ctx* ctx, int32_t graph);
+int64_t hgx_consensus_transactions(hgx_ctx* ctx, int32_t graph);
+int64_t hgx_pending_loaded_events(hgx_ctx* ctx, int32_t graph);
+
+/* ---- Store views (hashgraph/store.go:3-25) -------------------------------- */
+int32_t hgx_last_round(hgx_ctx* ctx, int32_t graph);                       /* Store.LastRound */
+int32_t hgx_round_event_count(hgx_ctx* ctx, int32_t graph, int32_t r);     /* Store.RoundEvents */
+int32_t hgx_round_witnesses(hgx_ctx* ctx, int32_t graph, int32_t r, int64_t* out, int32_t cap);
+int32_t hgx_known(hgx_ctx* ctx, int32_t graph, int32_t* last_index);     /* Store.Known */
+int64_t hgx_consensus_events_count(hgx_ctx* ctx, int32_t graph);         /* Store.ConsensusEventsCount */
+/* full consensus order (AddConsensusEvent sequence) of one graph: gids */
+int32_t hgx_consensus_events(hgx_ctx* ctx, int32_t graph, int64_t first, int64_t count, int64_t* gids);
+/* Blocks in SetBlock order (hashgraph.go:826-854): rr, first position in the
+ * graph's consensus order, number of events, number of transactions, nil flag,
+ * committed (sent on commitCh: len(Transactions) > 0). */
+int64_t hgx_num_blocks(hgx_ctx* ctx, int32_t graph);
+int32_t hgx_block_info(hgx_ctx* ctx, int32_t graph, int64_t b, int32_t* round_received, int64_t* first,
+                       int32_t* n_events, int64_t* n_tx, int32_t* tx_nil, int32_t* committed);
+
+/* ---- per-event results (bulk) --------------------------------------------- */
+/* round (Round), witness (Witness), famous (RoundEvent.Famous: 0 Undefined,1 True,2 False) */
+int32_t hgx_get_rounds(hgx_ctx* ctx, int64_t first, int64_t count, int32_t* round, int8_t* witness,
+                       int8_t* famous);
+/* RoundReceived (-1 = nil) and consensusTimestamp (Unix ns) */
+int32_t hgx_get_received(hgx_ctx* ctx, int64_t first, int64_t count, int32_t* round_received,
+                         int64_t* consensus_ts);
+/* lastAncestors / firstDescendants indexes of one event (n values each) */
+int32_t hgx_get_coords(hgx_ctx* ctx, int64_t gid, int32_t* last_ancestors, int32_t* first_descendants);
+
+/* ---- primitives (hashgraph.go:73-339), valid after hgx_divide_rounds ------ */
+int32_t hgx_ancestor(hgx_ctx* ctx, int64_t x, int64_t y);
+int32_t hgx_self_ancestor(hgx_ctx* ctx, int64_t x, int64_t y);
+int32_t hgx_see(hgx_ctx* ctx, int64_t x, int64_t y);
+int32_t hgx_strongly_see(hgx_ctx* ctx, int64_t x, int64_t y);
+int64_t hgx_oldest_self_ancestor_to_see(hgx_ctx* ctx, int64_t x, int64_t y);
+int32_t hgx_round(hgx_ctx* ctx, int64_t x);
+int32_t hgx_witness(hgx_ctx* ctx, int64_t x);
+
+/* ---- Go encodings (parity unpinned) -------------------- */
+/* SHA256(json.Encoder(Block)) with Block{RoundReceived, Transactions} (block.go:26-53) */
+int32_t hgx_block_hash(int64_t round_received, int32_t ntx, const uint8_t* const* tx, const int64_t* tx_len,
+                       int32_t tx_nil, uint8_t* out32);
+
+/* ---- timing / instrumentation --------------------------------------------- */
+/* per-phase device times (ms) of the last calls: coords, rounds, fame, order */
+int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
+/* dominant-kernel accounting for the roofline line of bench.py:
+ * name of the kernel, summed device ms, launches, algorithmic bytes moved */
+int32_t hgx_kernel_stats(hgx_ctx* ctx, int32_t k, char* name, int32_t name_cap, double* ms, int64_t* launches,
+                         double* bytes);
+int32_t hgx_reset_stats(hgx_ctx* ctx);
+
+/* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
+/* Seeded random gossip modelled on node/core_test.go:514-537: every active peer
+ * emits a genesis event, then each step a uniformly chosen `to` emits
+ * (sp = head[to], op = head[from]); ts = t0 + step*1000 ns; w.p. 1/2 one
+ * 16-byte-class payload "p%03d tx %08d", else an empty non-nil payload; S and
+ * the event id are PRNG bytes (synthetic ids). Silent peers are the last
+ * `n_silent` ids (never to/from, no genesis). With probability stale_prob the
+ * `from` head is replaced by one of from's last stale_depth events. Fills
+ * caller arrays of length n_events (index/parents as in hgx_events; tx_seq =
+ * per-creator payload counter or -1). Returns HGX_OK. */
+int32_t hgx_trace_gossip(int32_t n_participants, int32_t n_silent, int64_t n_events, uint64_t seed,
+                         double stale_prob, int32_t stale_depth,
+                         int32_t* creator, int64_t* index, int64_t* self_parent, int64_t* other_parent,
+                         int64_t* timestamp_ns, uint8_t* hash, uint8_t* sig_s, int32_t* ntx, int32_t* tx_nil,
+                         int64_t* tx_seq);
+/* payload bytes of generated transaction (creator, seq); returns length */
+int32_t hgx_trace_tx_payload(int32_t creator, int64_t seq, uint8_t* out, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGX_H */

@@ -283,8 +283,9 @@ class Oracle:
     def insert_trace(self, t: Trace, lo: int = 0, hi: Optional[int] = None):
         hi = t.E if hi is None else hi
         for i in range(lo, hi):
+            txs = t.txs(i) if callable(getattr(t, "txs", None)) else (None if t.txnil[i] else t.txs[i])
             rc, msg = self.insert(t.creator[i], t.index[i], t.sp[i], t.op[i], t.ts[i], t.hash[i].tobytes(),
-                                  t.s[i].tobytes(), None if t.txnil[i] else t.txs[i])
+                                  t.s[i].tobytes(), txs)
             if rc:
                 raise RuntimeError(f"oracle insert {i}: {msg}")
 
