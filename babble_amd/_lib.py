@@ -93,6 +93,7 @@ def lib():
     _sig(L, "hgx_kernel_stats", i32, [p, i32, C.c_char_p, i32, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_double)])
     _sig(L, "hgx_reset_stats", i32, [p])
+    _sig(L, "hgx_set_kernel_timing", i32, [p, i32])
     _L = L
     return L
 

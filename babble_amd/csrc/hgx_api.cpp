@@ -1,0 +1,576 @@
+// C ABI of libhgx (include/hgx.h) and the host-side mirror of the reference's
+// Hashgraph bookkeeping. The device engine computes every DAG-pure quantity
+// (coordinates, rounds, witnesses, fame decisions, round-received, consensus
+// timestamps, order); this file keeps exactly the schedule-dependent state the Go
+// code keeps (hashgraph/hashgraph.go:15-37): UndecidedRounds with its duplicate-0
+// quirk, per-witness fame frozen once decided, LastConsensusRound /
+// LastCommitedRoundEvents, received events, blocks, counters.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "hgx.h"
+#include "hgx_engine.h"
+
+namespace {
+
+struct Block {
+    int32_t rr;
+    int64_t first;     // position in the graph's consensus order
+    int32_t nev;
+    int64_t ntx;
+    int32_t tx_nil;
+    int32_t committed;
+};
+
+struct GraphState {
+    std::vector<int32_t> undecided{0};     // Hashgraph.UndecidedRounds, init []int{0} (hashgraph.go:64)
+    int32_t queued_upto = -1;              // rounds <= this have RoundInfo.queued
+    bool has_lcr = false;
+    int32_t lcr = 0;
+    int32_t lcre = 0;
+    int64_t consensus_tx = 0, pending_loaded = 0, undetermined = 0;
+    int32_t last_round = -1;
+    std::vector<int8_t> fame;              // [(last_round+1) x n] RoundEvent.Famous (host state)
+    std::vector<int32_t> round_events;     // [last_round+1]
+    std::vector<int32_t> order;            // consensus order (gids)
+    std::vector<Block> blocks;
+};
+
+}  // namespace
+
+struct hgx_ctx {
+    hgx::Engine eng;
+    int G = 1, n = 0, C = 0, sm = 0;
+    int64_t cap = 0;
+    // host event mirror (gid order)
+    std::vector<int32_t> creator, index32, sp, op, ntx;
+    std::vector<int64_t> ts;
+    std::vector<uint8_t> S, coin, loaded, txnil;
+    std::vector<int32_t> chain_len, chain_base;
+    std::vector<int64_t> last_gid, last_index;
+    std::vector<std::vector<int32_t>> chain_gids;
+    int64_t E = 0, E_div = 0;
+    bool divided = false;
+    hgx::RoundsHost rh;
+    std::vector<GraphState> gs;
+    // getter caches
+    bool rounds_cached = false;
+    std::vector<int32_t> round_cache;
+    bool recv_cached = false;
+    std::vector<int32_t> rr_cache;
+    std::vector<int64_t> cts_cache;
+};
+
+static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
+    if (!err) return;
+    err->code = code;
+    std::snprintf(err->msg, sizeof(err->msg), "%s", msg.c_str());
+}
+
+static int32_t dev_err(hgx_error* err, hipError_t e, const char* where) {
+    set_err(err, HGX_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+    return HGX_ERR_DEVICE;
+}
+
+// Go's string(int): UTF-8 of the rune (common/rolling_index.go passes string(index))
+static std::string go_rune(int64_t v) {
+    uint32_t r = (v < 0 || v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) ? 0xFFFD : (uint32_t)v;
+    std::string s;
+    if (r < 0x80) s += (char)r;
+    else if (r < 0x800) { s += (char)(0xC0 | (r >> 6)); s += (char)(0x80 | (r & 63)); }
+    else if (r < 0x10000) { s += (char)(0xE0 | (r >> 12)); s += (char)(0x80 | ((r >> 6) & 63)); s += (char)(0x80 | (r & 63)); }
+    else { s += (char)(0xF0 | (r >> 18)); s += (char)(0x80 | ((r >> 12) & 63)); s += (char)(0x80 | ((r >> 6) & 63)); s += (char)(0x80 | (r & 63)); }
+    return s;
+}
+
+extern "C" {
+
+int32_t hgx_abi_version(void) { return HGX_ABI_VERSION; }
+
+hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capacity_events, int32_t device,
+                          hgx_error* err) {
+    if (n_graphs <= 0 || n_participants <= 0 || n_participants > 1024 || capacity_events < 0 ||
+        (int64_t)n_graphs * n_participants > (1 << 24) || capacity_events >= (1LL << 31)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_create: invalid sizes (1 <= n <= 1024, capacity < 2^31)");
+        return nullptr;
+    }
+    hgx_ctx* c = new (std::nothrow) hgx_ctx();
+    if (!c) { set_err(err, HGX_ERR_CAPACITY, "hgx_create: out of host memory"); return nullptr; }
+    c->G = n_graphs;
+    c->n = n_participants;
+    c->C = n_graphs * n_participants;
+    c->sm = 2 * n_participants / 3 + 1;
+    c->cap = capacity_events;
+    std::string why;
+    hipError_t e = c->eng.init(device, n_graphs, n_participants, capacity_events, why);
+    if (e != hipSuccess) {
+        set_err(err, HGX_ERR_DEVICE, "hgx_create: " + (why.empty() ? std::string(hipGetErrorString(e)) : why));
+        delete c;
+        return nullptr;
+    }
+    c->chain_len.assign(c->C, 0);
+    c->chain_base.assign(c->C, 0);
+    c->last_gid.assign(c->C, -1);
+    c->last_index.assign(c->C, -1);
+    c->chain_gids.assign(c->C, {});
+    c->gs.assign(n_graphs, GraphState());
+    const size_t rsv = (size_t)std::min<int64_t>(capacity_events, 1 << 22);
+    c->creator.reserve(rsv);
+    if (err) set_err(err, HGX_OK, "");
+    return c;
+}
+
+hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t device, hgx_error* err) {
+    return hgx_create_batch(1, n_participants, capacity_events, device, err);
+}
+
+void hgx_destroy(hgx_ctx* ctx) { delete ctx; }
+
+// ---- InsertEvent (hashgraph.go:356-401) ------------------------------------------
+int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !ev || count < 0) { set_err(err, HGX_ERR_INVALID, "hgx_insert_events: bad arguments"); return HGX_ERR_INVALID; }
+    const int64_t first = c->E;
+    int32_t rc = HGX_OK;
+    std::string msg;
+    int64_t k = 0;
+    for (; k < count; k++) {
+        const int32_t cr = ev->creator[k];
+        const int64_t sp = ev->self_parent[k], op = ev->other_parent[k], idx = ev->index[k];
+        // event.Verify(): signature verification stays on the Go side
+        if (cr < 0 || cr >= c->C) {   // Store.LastFrom -> KeyNotFound (inmem_store.go:85-90)
+            rc = HGX_ERR_KEY_NOT_FOUND;
+            msg = "CheckSelfParent: " + std::to_string(cr) + ", Not Found";
+            break;
+        }
+        if (sp != c->last_gid[cr]) {   // CheckSelfParent (hashgraph.go:404-420)
+            rc = HGX_ERR_SELF_PARENT;
+            msg = "CheckSelfParent: Self-parent not last known event by creator";
+            break;
+        }
+        if (op != -1) {                // CheckOtherParent (hashgraph.go:423-445), genesis Root only
+            const bool known = op >= 0 && op < c->E && c->creator[op] / c->n == cr / c->n;
+            if (!known) {
+                rc = HGX_ERR_OTHER_PARENT;
+                msg = "CheckOtherParent: Other-parent not known";
+                break;
+            }
+        }
+        if (c->E >= c->cap) {
+            rc = HGX_ERR_CAPACITY;
+            msg = "hgx_insert_events: context capacity exceeded";
+            break;
+        }
+        const int64_t li = c->last_index[cr];   // RollingIndex.Add (common/rolling_index.go:54-68)
+        if (idx <= li) { rc = HGX_ERR_PASSED_INDEX; msg = "SetEvent: " + go_rune(idx) + ", Passed Index"; break; }
+        if (li >= 0 && idx > li + 1) { rc = HGX_ERR_SKIPPED_INDEX; msg = "SetEvent: " + go_rune(idx) + ", Skipped Index"; break; }
+        if (idx > 2147483646) { rc = HGX_ERR_INVALID; msg = "hgx_insert_events: index out of int32 range"; break; }
+        const int64_t gid = c->E++;
+        c->creator.push_back(cr);
+        c->index32.push_back((int32_t)idx);
+        c->sp.push_back((int32_t)sp);
+        c->op.push_back((int32_t)op);
+        c->ts.push_back(ev->timestamp_ns[k]);
+        c->S.insert(c->S.end(), ev->sig_s + 32 * k, ev->sig_s + 32 * k + 32);
+        c->coin.push_back(ev->hash[32 * k + 16] != 0 ? 1 : 0);   // middleBit (hashgraph.go:1039-1048)
+        const int32_t nt = ev->ntx[k];
+        const int32_t nil = ev->tx_nil[k] ? 1 : 0;
+        c->ntx.push_back(nt);
+        c->txnil.push_back((uint8_t)nil);
+        const bool ld = idx == 0 || (!nil && nt > 0);          // IsLoaded (event.go:119-126)
+        c->loaded.push_back(ld ? 1 : 0);
+        if (c->chain_len[cr] == 0) c->chain_base[cr] = (int32_t)idx;
+        c->chain_len[cr]++;
+        c->chain_gids[cr].push_back((int32_t)gid);
+        c->last_gid[cr] = gid;
+        c->last_index[cr] = idx;
+        GraphState& g = c->gs[cr / c->n];
+        if (ld) g.pending_loaded++;
+        g.undetermined++;
+    }
+    const int64_t added = c->E - first;
+    if (added > 0) {
+        hipError_t e = c->eng.upload_events(first, added, c->creator.data() + first, c->index32.data() + first,
+                                            c->op.data() + first, c->ts.data() + first, c->S.data() + 32 * first,
+                                            c->coin.data() + first, c->ntx.data() + first, c->loaded.data() + first);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events");
+        c->rounds_cached = c->recv_cached = false;
+    }
+    if (n_inserted) *n_inserted = added;
+    if (rc != HGX_OK) { set_err(err, rc, msg); return rc; }
+    if (err) set_err(err, HGX_OK, "");
+    return HGX_OK;
+}
+
+// ---- DivideRounds (hashgraph.go:616-646) -----------------------------------------
+int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
+    if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    if (c->divided && c->E_div == c->E) return HGX_OK;   // nothing new: AddEvent is idempotent
+    hipError_t e = c->eng.divide_rounds(c->E, c->chain_len, c->chain_base, c->rh);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_divide_rounds");
+    c->divided = true;
+    c->E_div = c->E;
+    c->rounds_cached = false;
+    const int C = c->C, n = c->n;
+    for (int g = 0; g < c->G; g++) {
+        GraphState& s = c->gs[g];
+        const int32_t LR = c->rh.last_round[g];
+        // rounds first seen in this call are queued in ascending order
+        for (int32_t r = s.queued_upto + 1; r <= LR; r++) s.undecided.push_back(r);
+        s.queued_upto = std::max(s.queued_upto, LR);
+        s.last_round = LR;
+        s.fame.resize((size_t)(LR + 1) * n, 0);
+        s.round_events.assign(LR + 1, 0);
+        for (int32_t r = 0; r <= LR; r++) {
+            int64_t cnt = 0;
+            for (int cl = 0; cl < n; cl++) {
+                const int gc = g * n + cl;
+                cnt += c->rh.bm[(size_t)(r + 1) * C + gc] - c->rh.bm[(size_t)r * C + gc];
+            }
+            s.round_events[r] = (int32_t)cnt;
+        }
+    }
+    if (err) set_err(err, HGX_OK, "");
+    return HGX_OK;
+}
+
+static bool is_witness(const hgx_ctx* c, int32_t r, int gc) {
+    return r >= 0 && r < c->rh.R && c->rh.wflag[(size_t)r * c->C + gc] == 2;
+}
+
+// RoundInfo.WitnessesDecided (roundInfo.go:64-71); rounds never stored are vacuously decided
+static bool witnesses_decided(const hgx_ctx* c, int g, int32_t r) {
+    const GraphState& s = c->gs[g];
+    if (r < 0 || r > s.last_round) return true;
+    for (int cl = 0; cl < c->n; cl++)
+        if (is_witness(c, r, g * c->n + cl) && s.fame[(size_t)r * c->n + cl] == 0) return false;
+    return true;
+}
+
+// ---- DecideFame (hashgraph.go:649-750) -------------------------------------------
+int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
+    if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    std::vector<int8_t> dev;
+    if (c->divided) {
+        hipError_t e = c->eng.decide_fame(dev);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_decide_fame");
+    }
+    int32_t rc = HGX_OK;
+    std::string msg;
+    const int n = c->n, C = c->C;
+    for (int g = 0; g < c->G; g++) {
+        GraphState& s = c->gs[g];
+        std::vector<int32_t> decided;
+        int32_t grc = HGX_OK;
+        for (size_t pos = 0; pos < s.undecided.size(); pos++) {
+            const int32_t i = s.undecided[pos];
+            if (i < 0 || i > s.last_round) {          // Store.GetRound miss -> error
+                grc = HGX_ERR_KEY_NOT_FOUND;
+                if (rc == HGX_OK) { rc = grc; msg = std::to_string(i) + ", Not Found"; }
+                break;
+            }
+            for (int cl = 0; cl < n; cl++) {
+                const int gc = g * n + cl;
+                if (!is_witness(c, i, gc)) continue;
+                int8_t& f = s.fame[(size_t)i * n + cl];
+                if (f == 0) f = dev[(size_t)i * C + gc];   // SetFame; decided fame is never revisited
+            }
+            if (witnesses_decided(c, g, i)) {
+                decided.push_back(i);
+                if (!s.has_lcr || i > s.lcr) {             // setLastConsensusRound (:743-750)
+                    s.has_lcr = true;
+                    s.lcr = i;
+                    s.lcre = (i - 1 >= 0 && i - 1 <= s.last_round) ? s.round_events[i - 1] : 0;
+                }
+            }
+        }
+        // deferred updateUndecidedRounds (:733-741)
+        std::vector<int32_t> keep;
+        for (int32_t r : s.undecided)
+            if (std::find(decided.begin(), decided.end(), r) == decided.end()) keep.push_back(r);
+        s.undecided.swap(keep);
+    }
+    if (rc != HGX_OK) { set_err(err, rc, msg); return rc; }
+    if (err) set_err(err, HGX_OK, "");
+    return HGX_OK;
+}
+
+// ---- FindOrder (hashgraph.go:801-858) --------------------------------------------
+int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
+    if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    if (!c->divided) { if (err) set_err(err, HGX_OK, ""); return HGX_OK; }
+    const int n = c->n, C = c->C, G = c->G;
+    const int32_t R = c->rh.R;
+    std::vector<uint8_t> elig((size_t)G * std::max(R, 1), 0), fw((size_t)std::max(R, 1) * C, 0), ure(G, 0);
+    for (int g = 0; g < G; g++) {
+        const GraphState& s = c->gs[g];
+        ure[g] = s.undecided.empty() ? 1 : 0;
+        const int32_t U0 = s.undecided.empty() ? -1 : s.undecided[0];
+        for (int32_t i = 0; i <= s.last_round; i++) {
+            // DecideRoundReceived skip rule (hashgraph.go:763)
+            elig[(size_t)g * R + i] = (U0 >= 0 && i < U0 && witnesses_decided(c, g, i)) ? 1 : 0;
+            for (int cl = 0; cl < n; cl++)
+                if (is_witness(c, i, g * n + cl) && s.fame[(size_t)i * n + cl] == 1) fw[(size_t)i * C + g * n + cl] = 1;
+        }
+    }
+    hgx::OrderHost oh;
+    hipError_t e = c->eng.find_order(elig, fw, ure, oh);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
+    if (oh.panic) {
+        set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
+        return HGX_ERR_PANIC;
+    }
+    c->recv_cached = false;
+    const int32_t* order = c->eng.pinned_order();
+    int64_t at = 0;
+    for (int g = 0; g < G && oh.m > 0; g++) {
+        GraphState& s = c->gs[g];
+        const int64_t base_pos = (int64_t)s.order.size();
+        int64_t mg = 0;
+        for (int32_t rr = 0; rr < R; rr++) mg += oh.blk_cnt[(size_t)g * R + rr];
+        if (mg == 0) continue;
+        s.order.insert(s.order.end(), order + at, order + at + mg);
+        int64_t off = 0;
+        for (int32_t rr = 0; rr < R; rr++) {    // one Block per rr, ascending (blockOrder)
+            const int32_t cnt = oh.blk_cnt[(size_t)g * R + rr];
+            if (!cnt) continue;
+            Block b;
+            b.rr = rr;
+            b.first = base_pos + off;
+            b.nev = cnt;
+            b.ntx = oh.blk_ntx[(size_t)g * R + rr];
+            const int32_t first_gid = order[at + off];
+            // NewBlock(rr, first.Transactions()) then append(...): nil iff first nil and nothing appended
+            b.tx_nil = (c->txnil[first_gid] && b.ntx == 0) ? 1 : 0;
+            b.committed = b.ntx > 0 ? 1 : 0;   // commitCh only if len(Transactions) > 0
+            s.blocks.push_back(b);
+            s.consensus_tx += b.ntx;
+            s.pending_loaded -= oh.blk_loaded[(size_t)g * R + rr];
+            off += cnt;
+        }
+        s.undetermined -= mg;
+        at += mg;
+    }
+    if (err) set_err(err, HGX_OK, "");
+    return HGX_OK;
+}
+
+int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
+    int32_t rc = hgx_divide_rounds(c, err);
+    if (rc) return rc;
+    rc = hgx_decide_fame(c, err);
+    if (rc) return rc;
+    return hgx_find_order(c, err);
+}
+
+// ---- state getters ----------------------------------------------------------------
+static GraphState* graph(hgx_ctx* c, int32_t g) {
+    if (!c || g < 0 || g >= c->G) return nullptr;
+    return &c->gs[g];
+}
+
+int64_t hgx_num_events(hgx_ctx* c) { return c ? c->E : 0; }
+int32_t hgx_super_majority(hgx_ctx* c) { return c ? c->sm : 0; }
+int64_t hgx_num_undetermined(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? s->undetermined : 0; }
+int32_t hgx_undecided_rounds(hgx_ctx* c, int32_t g, int32_t* out, int32_t cap) {
+    GraphState* s = graph(c, g);
+    if (!s) return 0;
+    const int32_t m = (int32_t)s->undecided.size();
+    for (int32_t i = 0; i < m && i < cap; i++) out[i] = s->undecided[i];
+    return m;
+}
+int32_t hgx_last_consensus_round(hgx_ctx* c, int32_t g, int32_t* has) {
+    GraphState* s = graph(c, g);
+    if (has) *has = (s && s->has_lcr) ? 1 : 0;
+    return (s && s->has_lcr) ? s->lcr : 0;
+}
+int32_t hgx_last_commited_round_events(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? s->lcre : 0; }
+int64_t hgx_consensus_transactions(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? s->consensus_tx : 0; }
+int64_t hgx_pending_loaded_events(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? s->pending_loaded : 0; }
+int32_t hgx_last_round(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? s->last_round : -1; }
+int32_t hgx_round_event_count(hgx_ctx* c, int32_t g, int32_t r) {
+    GraphState* s = graph(c, g);
+    if (!s || r < 0 || r > s->last_round) return 0;
+    return s->round_events[r];
+}
+int32_t hgx_round_witnesses(hgx_ctx* c, int32_t g, int32_t r, int64_t* out, int32_t cap) {
+    GraphState* s = graph(c, g);
+    if (!s || r < 0 || r > s->last_round) return 0;
+    int32_t m = 0;
+    for (int cl = 0; cl < c->n; cl++) {
+        const int gc = g * c->n + cl;
+        if (!is_witness(c, r, gc)) continue;
+        if (m < cap) out[m] = c->chain_gids[gc][c->rh.bm[(size_t)r * c->C + gc]];
+        m++;
+    }
+    return m;
+}
+int32_t hgx_known(hgx_ctx* c, int32_t g, int32_t* out) {
+    if (!graph(c, g)) return HGX_ERR_INVALID;
+    for (int cl = 0; cl < c->n; cl++) out[cl] = (int32_t)c->last_index[g * c->n + cl];
+    return HGX_OK;
+}
+int64_t hgx_consensus_events_count(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->order.size() : 0; }
+int32_t hgx_consensus_events(hgx_ctx* c, int32_t g, int64_t first, int64_t count, int64_t* gids) {
+    GraphState* s = graph(c, g);
+    if (!s || first < 0 || count < 0 || first + count > (int64_t)s->order.size()) return HGX_ERR_INVALID;
+    for (int64_t i = 0; i < count; i++) gids[i] = s->order[(size_t)(first + i)];
+    return HGX_OK;
+}
+int64_t hgx_num_blocks(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->blocks.size() : 0; }
+int32_t hgx_block_info(hgx_ctx* c, int32_t g, int64_t b, int32_t* rr, int64_t* first, int32_t* nev, int64_t* ntx,
+                       int32_t* tx_nil, int32_t* committed) {
+    GraphState* s = graph(c, g);
+    if (!s || b < 0 || b >= (int64_t)s->blocks.size()) return HGX_ERR_INVALID;
+    const Block& B = s->blocks[(size_t)b];
+    if (rr) *rr = B.rr;
+    if (first) *first = B.first;
+    if (nev) *nev = B.nev;
+    if (ntx) *ntx = B.ntx;
+    if (tx_nil) *tx_nil = B.tx_nil;
+    if (committed) *committed = B.committed;
+    return HGX_OK;
+}
+
+// ---- per-event results -------------------------------------------------------------
+static int32_t ensure_rounds(hgx_ctx* c) {
+    if (c->rounds_cached) return HGX_OK;
+    if (c->eng.get_rounds(c->round_cache) != hipSuccess) return HGX_ERR_DEVICE;
+    c->rounds_cached = true;
+    return HGX_OK;
+}
+static int32_t round_of(hgx_ctx* c, int64_t x) {
+    if (x < 0 || x >= (int64_t)c->round_cache.size()) return -1;   // Round("") = -1
+    return c->round_cache[(size_t)x];
+}
+static int32_t witness_of(hgx_ctx* c, int64_t x) {   // Witness (hashgraph.go:265-282)
+    if (x < 0 || x >= (int64_t)c->round_cache.size()) return 0;
+    if (c->sp[x] == -1 && c->op[x] == -1) return 1;
+    return round_of(c, x) > round_of(c, c->sp[x]) ? 1 : 0;
+}
+
+int32_t hgx_get_rounds(hgx_ctx* c, int64_t first, int64_t count, int32_t* round, int8_t* witness, int8_t* famous) {
+    if (!c || first < 0 || count < 0 || first + count > c->E) return HGX_ERR_INVALID;
+    if (ensure_rounds(c)) return HGX_ERR_DEVICE;
+    for (int64_t k = 0; k < count; k++) {
+        const int64_t x = first + k;
+        const int32_t r = round_of(c, x);
+        const int32_t w = witness_of(c, x);
+        if (round) round[k] = r;
+        if (witness) witness[k] = (int8_t)w;
+        if (famous) {
+            int8_t f = 0;
+            if (w && r >= 0) {
+                const int gc = c->creator[x];
+                const GraphState& s = c->gs[gc / c->n];
+                if (r <= s.last_round) f = s.fame[(size_t)r * c->n + gc % c->n];
+            }
+            famous[k] = f;
+        }
+    }
+    return HGX_OK;
+}
+
+int32_t hgx_get_received(hgx_ctx* c, int64_t first, int64_t count, int32_t* rr, int64_t* cts) {
+    if (!c || first < 0 || count < 0 || first + count > c->E) return HGX_ERR_INVALID;
+    if (!c->recv_cached) {
+        if (c->eng.get_received(c->rr_cache, c->cts_cache) != hipSuccess) return HGX_ERR_DEVICE;
+        c->recv_cached = true;
+    }
+    for (int64_t k = 0; k < count; k++) {
+        const size_t x = (size_t)(first + k);
+        const bool have = x < c->rr_cache.size();
+        if (rr) rr[k] = have ? c->rr_cache[x] : -1;
+        if (cts) cts[k] = (have && c->rr_cache[x] >= 0) ? c->cts_cache[x] : 0;
+    }
+    return HGX_OK;
+}
+
+int32_t hgx_get_coords(hgx_ctx* c, int64_t gid, int32_t* la, int32_t* fd) {
+    if (!c || gid < 0 || gid >= c->E_div || !c->divided) return HGX_ERR_INVALID;
+    return c->eng.get_coords(gid, la, fd) == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+// ---- primitives (hashgraph.go:73-339) ----------------------------------------------
+static bool known_div(hgx_ctx* c, int64_t x) { return c && x >= 0 && x < c->E_div && c->divided; }
+
+int32_t hgx_ancestor(hgx_ctx* c, int64_t x, int64_t y) {
+    if (x == y) return 1;
+    if (!known_div(c, x) || !known_div(c, y)) return 0;
+    std::vector<int32_t> la(c->n), fd(c->n);
+    if (c->eng.get_coords(x, la.data(), fd.data()) != hipSuccess) return 0;
+    return la[c->creator[y] % c->n] >= c->index32[y] ? 1 : 0;
+}
+int32_t hgx_self_ancestor(hgx_ctx* c, int64_t x, int64_t y) {
+    if (x == y) return 1;
+    if (!c || x < 0 || y < 0 || x >= c->E || y >= c->E) return 0;
+    return (c->creator[x] == c->creator[y] && c->index32[x] >= c->index32[y]) ? 1 : 0;
+}
+int32_t hgx_see(hgx_ctx* c, int64_t x, int64_t y) { return hgx_ancestor(c, x, y); }
+int32_t hgx_strongly_see(hgx_ctx* c, int64_t x, int64_t y) {
+    if (!known_div(c, x) || !known_div(c, y)) return 0;
+    std::vector<int32_t> lx(c->n), fx(c->n), ly(c->n), fy(c->n);
+    if (c->eng.get_coords(x, lx.data(), fx.data()) != hipSuccess) return 0;
+    if (c->eng.get_coords(y, ly.data(), fy.data()) != hipSuccess) return 0;
+    int cnt = 0;
+    for (int i = 0; i < c->n; i++) cnt += lx[i] >= fy[i];
+    return cnt >= c->sm ? 1 : 0;
+}
+int64_t hgx_oldest_self_ancestor_to_see(hgx_ctx* c, int64_t x, int64_t y) {
+    if (!known_div(c, x) || !known_div(c, y)) return -1;
+    std::vector<int32_t> la(c->n), fd(c->n);
+    if (c->eng.get_coords(y, la.data(), fd.data()) != hipSuccess) return -1;
+    const int cx = c->creator[x];
+    const int32_t a = fd[cx % c->n];
+    if (a <= c->index32[x]) return c->chain_gids[cx][(size_t)(a - c->chain_base[cx])];
+    return -1;
+}
+int32_t hgx_round(hgx_ctx* c, int64_t x) {
+    if (!c || ensure_rounds(c)) return -1;
+    return round_of(c, x);
+}
+int32_t hgx_witness(hgx_ctx* c, int64_t x) {
+    if (!c || ensure_rounds(c)) return 0;
+    return witness_of(c, x);
+}
+
+// ---- instrumentation ----------------------------------------------------------------
+int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
+    if (!c || !out) return 0;
+    const int32_t m = std::min<int32_t>(cap, 6);
+    double v[6] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
+                   (double)c->eng.la_sweeps, (double)c->eng.R};
+    for (int32_t i = 0; i < m; i++) out[i] = v[i];
+    return m;
+}
+
+static const char* kKernelNames[hgx::K_NUM] = {"layout", "la_sweep", "fd_build", "round_gather", "round_search",
+                                              "fame", "threshold", "round_received", "cts_median", "order_sort"};
+
+int32_t hgx_kernel_stats(hgx_ctx* c, int32_t k, char* name, int32_t name_cap, double* ms, int64_t* launches,
+                         double* bytes) {
+    if (!c || k < 0 || k >= hgx::K_NUM) return HGX_ERR_INVALID;
+    if (name && name_cap > 0) std::snprintf(name, (size_t)name_cap, "%s", kKernelNames[k]);
+    if (ms) *ms = c->eng.kstat[k].ms;
+    if (launches) *launches = c->eng.kstat[k].launches;
+    if (bytes) *bytes = c->eng.kstat[k].bytes;
+    return HGX_OK;
+}
+
+int32_t hgx_reset_stats(hgx_ctx* c) {
+    if (!c) return HGX_ERR_INVALID;
+    for (auto& s : c->eng.kstat) s = hgx::KernelStat();
+    return HGX_OK;
+}
+
+int32_t hgx_set_kernel_timing(hgx_ctx* c, int32_t on) {
+    if (!c) return HGX_ERR_INVALID;
+    c->eng.time_kernels = on != 0;
+    return HGX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,413 @@
+// Engine host code: device allocation, per-call orchestration of the kernels,
+// D2H of the small per-round tables the Go-semantics bookkeeping needs.
+#include "hgx_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace hgx {
+
+#define HGX_TRY(x)                              \
+    do {                                        \
+        hipError_t _e = (x);                    \
+        if (_e != hipSuccess) return _e;        \
+    } while (0)
+
+template <typename T>
+hipError_t DBuf<T>::alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+    if (e == hipSuccess) n = count; else p = nullptr;
+    return e;
+}
+
+template <typename T>
+hipError_t DBuf<T>::grow_copy(size_t count, size_t keep, hipStream_t s) {
+    if (count <= n) return hipSuccess;
+    T* q = nullptr;
+    HGX_TRY(hipMalloc((void**)&q, count * sizeof(T)));
+    if (p && keep) {
+        HGX_TRY(hipMemcpyAsync(q, p, std::min(keep, n) * sizeof(T), hipMemcpyDeviceToDevice, s));
+        HGX_TRY(hipStreamSynchronize(s));
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    n = count;
+    return hipSuccess;
+}
+
+template <typename T>
+void DBuf<T>::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+}
+
+template struct DBuf<int32_t>;
+template struct DBuf<int64_t>;
+template struct DBuf<uint8_t>;
+template struct DBuf<int8_t>;
+template struct DBuf<uint32_t>;
+template struct DBuf<uint64_t>;
+
+static int bitlen(uint64_t v) {
+    int b = 0;
+    while (v) { b++; v >>= 1; }
+    return b;
+}
+
+Engine::~Engine() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto e : kev) (void)hipEventDestroy(e);
+    if (ph0) (void)hipEventDestroy(ph0);
+    if (ph1) (void)hipEventDestroy(ph1);
+    if (h_order) (void)hipHostFree(h_order);
+    if (h_small) (void)hipHostFree(h_small);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events, std::string& why) {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) {
+        why = "no HIP device available (libhgx has no CPU fallback)";
+        return e != hipSuccess ? e : hipErrorNoDevice;
+    }
+    if (device < 0 || device >= count) {
+        why = "invalid HIP device ordinal";
+        return hipErrorInvalidDevice;
+    }
+    hipDeviceProp_t prop;
+    HGX_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        why = std::string("device is ") + prop.gcnArchName + ", libhgx is built for gfx950 (MI355X) only";
+        return hipErrorInvalidDeviceFunction;
+    }
+    dev = device;
+    HGX_TRY(hipSetDevice(dev));
+    HGX_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HGX_TRY(hipEventCreate(&ph0));
+    HGX_TRY(hipEventCreate(&ph1));
+    G = n_graphs;
+    n = n_part;
+    C = G * n;
+    sm = 2 * n / 3 + 1;   // hashgraph.go:63
+    nw = (n + 63) / 64;
+    cap = std::max<int64_t>(cap_events, 1);
+    const size_t P = (size_t)cap;
+    HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_op.alloc(P)); HGX_TRY(g_ntx.alloc(P));
+    HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P)); HGX_TRY(g_cts.alloc(P));
+    HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
+    HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
+    HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_round.alloc(P));
+    HGX_TRY(p_rr.alloc(P)); HGX_TRY(p_ts.alloc(P)); HGX_TRY(p_cts.alloc(P));
+    HGX_TRY(LA.alloc(P * n));
+    HGX_TRY(FDT.alloc(P * n));
+    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(4)); HGX_TRY(order_gid.alloc(P));
+    HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
+    HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
+    HGX_TRY(minmax.alloc(2));
+    HGX_TRY(lr.alloc(G));
+    HGX_TRY(hipHostMalloc((void**)&h_order, P * sizeof(int32_t), hipHostMallocDefault));
+    HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
+    // rounds: initial guess, grown on demand
+    const int lg = std::max(1, bitlen((uint64_t)n));
+    int32_t guess = (int32_t)std::min<int64_t>(1 << 20, std::max<int64_t>(64, 2 * cap / std::max(1, n * lg) + 16));
+    HGX_TRY(ensure_round_cap(guess));
+    return hipSuccess;
+}
+
+hipError_t Engine::ensure_round_cap(int32_t need) {
+    if (need <= r_cap) return hipSuccess;
+    const int32_t old = r_cap;
+    int32_t nc = std::max<int32_t>(need, old * 2);
+    const size_t Cz = (size_t)C;
+    HGX_TRY(Bm.grow_copy((size_t)(nc + 1) * Cz, (size_t)(old + 1) * Cz, stream));
+    HGX_TRY(WLA.grow_copy((size_t)nc * Cz * n, (size_t)old * Cz * n, stream));
+    HGX_TRY(WFD.grow_copy((size_t)nc * Cz * n, (size_t)old * Cz * n, stream));
+    HGX_TRY(wflag.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
+    HGX_TRY(wcoin.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
+    HGX_TRY(active.grow_copy((size_t)nc + 1, (size_t)old + 1, stream));
+    HGX_TRY(Tthr.grow_copy((size_t)nc * Cz, 0, stream));
+    HGX_TRY(fw.grow_copy((size_t)nc * Cz, 0, stream));
+    HGX_TRY(elig.grow_copy((size_t)nc * G, 0, stream));
+    HGX_TRY(ur_empty.grow_copy((size_t)G, 0, stream));
+    HGX_TRY(Smat.grow_copy((size_t)nc * Cz * nw, 0, stream));
+    HGX_TRY(Vbuf.grow_copy((size_t)nc * 2 * Cz * nw, 0, stream));
+    HGX_TRY(fame.grow_copy((size_t)nc * Cz, 0, stream));
+    HGX_TRY(blk_cnt.grow_copy((size_t)nc * G, 0, stream));
+    HGX_TRY(blk_loaded.grow_copy((size_t)nc * G, 0, stream));
+    HGX_TRY(blk_ntx.grow_copy((size_t)nc * G, 0, stream));
+    if (old < nc) HGX_TRY(hipMemsetAsync(active.p + old + 1, 0, (size_t)(nc - old) * sizeof(int32_t), stream));
+    r_cap = nc;
+    return hipSuccess;
+}
+
+DevArrays Engine::arrays() {
+    DevArrays a;
+    a.g_creator = g_creator.p; a.g_index = g_index.p; a.g_op = g_op.p; a.g_ntx = g_ntx.p;
+    a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p;
+    a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p;
+    a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
+    a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
+    a.p_ts = p_ts.p; a.p_cts = p_cts.p;
+    a.LA = LA.p; a.FDT = FDT.p;
+    a.Bm = Bm.p; a.wflag = wflag.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p;
+    a.active = active.p; a.lr = lr.p;
+    a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
+    a.elig = elig.p; a.fw = fw.p; a.ur_empty = ur_empty.p; a.T = Tthr.p;
+    a.recv_list = recv_list.p; a.counters = counters.p;
+    a.key_a = key_a.p; a.key_b = key_b.p; a.val_a = val_a.p; a.val_b = val_b.p; a.hist = hist.p;
+    a.minmax = minmax.p; a.order_gid = order_gid.p;
+    a.blk_cnt = blk_cnt.p; a.blk_loaded = blk_loaded.p; a.blk_ntx = blk_ntx.p;
+    return a;
+}
+
+// ---- per-kernel timing (only when time_kernels) ---------------------------------
+void Engine::kbeg(int k) {
+    kstat[k].launches++;
+    if (!time_kernels) return;
+    while (kev.size() < kev_used + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        kev.push_back(e);
+    }
+    (void)hipEventRecord(kev[kev_used], stream);
+    kopen.push_back({k, kev_used, 0});
+    kev_used += 2;
+}
+
+void Engine::kend(int k, double bytes) {
+    kstat[k].bytes += bytes;
+    if (!time_kernels || kopen.empty()) return;
+    Open& o = kopen.back();
+    o.bytes = bytes;
+    (void)hipEventRecord(kev[o.e0 + 1], stream);
+}
+
+hipError_t Engine::collect_kernel_times() {
+    if (kopen.empty()) return hipSuccess;
+    HGX_TRY(hipStreamSynchronize(stream));
+    for (const Open& o : kopen) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, kev[o.e0], kev[o.e0 + 1]) == hipSuccess) kstat[o.k].ms += ms;
+    }
+    kopen.clear();
+    kev_used = 0;
+    return hipSuccess;
+}
+
+// ---- inputs ---------------------------------------------------------------------
+hipError_t Engine::upload_events(int64_t first, int64_t count, const int32_t* creator, const int32_t* index,
+                                 const int32_t* op, const int64_t* ts, const uint8_t* S, const uint8_t* coin,
+                                 const int32_t* ntx, const uint8_t* loaded) {
+    if (count <= 0) return hipSuccess;
+    const size_t f = (size_t)first, c = (size_t)count;
+    HGX_TRY(hipMemcpyAsync(g_creator.p + f, creator, c * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_index.p + f, index, c * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_op.p + f, op, c * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_ts.p + f, ts, c * 8, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_S.p + 32 * f, S, c * 32, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_coin.p + f, coin, c, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_ntx.p + f, ntx, c * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(g_loaded.p + f, loaded, c, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemsetAsync(g_rr.p + f, 0xFF, c * 4, stream));   // roundReceived = nil
+    HGX_TRY(hipMemsetAsync(g_cts.p + f, 0, c * 8, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    E = std::max<int64_t>(E, first + count);
+    return hipSuccess;
+}
+
+// ---- DivideRounds ---------------------------------------------------------------
+hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_len,
+                                 const std::vector<int32_t>& chain_base, RoundsHost& out) {
+    E = En;
+    E_div = En;
+    h_off.assign(C + 1, 0);
+    max_len = 0;
+    for (int c = 0; c < C; c++) {
+        h_off[c + 1] = h_off[c] + chain_len[c];
+        max_len = std::max(max_len, chain_len[c]);
+    }
+    HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(c_len.p, chain_len.data(), C * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
+    DevArrays a = arrays();
+    HGX_TRY(hipEventRecord(ph0, stream));
+    kbeg(K_LAYOUT);
+    launch_layout(stream, E, a);
+    kend(K_LAYOUT, (double)E * 60);
+    // lastAncestors: fixed point from all -1
+    HGX_TRY(hipMemsetAsync(LA.p, 0xFF, (size_t)E * n * 4, stream));
+    la_sweeps = 0;
+    for (;;) {
+        HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 4, stream));
+        kbeg(K_LA_SWEEP);
+        launch_la_sweep(stream, a, C, n, max_len, counters.p + 2);
+        kend(K_LA_SWEEP, (double)E * (12.0 * n + 4));
+        la_sweeps++;
+        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 4, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipStreamSynchronize(stream));
+        if (h_small[0] == 0) break;
+        if (la_sweeps > 100000) return hipErrorUnknown;
+    }
+    kbeg(K_FD_BUILD);
+    launch_fd_build(stream, a, C, n, max_len, cap);
+    kend(K_FD_BUILD, (double)E * 8.0 * n);
+    HGX_TRY(hipEventRecord(ph1, stream));
+    HGX_TRY(hipEventSynchronize(ph1));
+    float ms = 0;
+    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    phase_ms[0] = ms;
+
+    // rounds, step by step
+    HGX_TRY(hipEventRecord(ph0, stream));
+    HGX_TRY(hipMemsetAsync(lr.p, 0xFF, (size_t)G * 4, stream));
+    HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(active.p, 0, (size_t)(r_cap + 1) * 4, stream));
+    const int kBatch = 8;
+    int r = 0;
+    for (;;) {
+        if (r + kBatch + 1 > r_cap) {
+            HGX_TRY(ensure_round_cap(r + kBatch + 1));
+            a = arrays();
+        }
+        for (int k = 0; k < kBatch; k++) {
+            kbeg(K_ROUND_GATHER);
+            launch_round_gather(stream, a, r + k, C, n, cap);
+            kend(K_ROUND_GATHER, (double)C * n * 16);
+            kbeg(K_ROUND_SEARCH);
+            launch_round_search(stream, a, r + k, C, n, sm);
+            kend(K_ROUND_SEARCH, 0);
+        }
+        r += kBatch;
+        HGX_TRY(hipMemcpyAsync(h_small, active.p + (r - 1), 4, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipStreamSynchronize(stream));
+        if (h_small[0] == 0) break;
+    }
+    out.last_round.assign(G, -1);
+    HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    int32_t mx = -1;
+    for (int g = 0; g < G; g++) mx = std::max(mx, out.last_round[g]);
+    R = mx + 1;
+    out.R = R;
+    out.bm.resize((size_t)(R + 1) * C);
+    out.wflag.resize((size_t)R * C);
+    HGX_TRY(hipMemcpyAsync(out.bm.data(), Bm.p, out.bm.size() * 4, hipMemcpyDeviceToHost, stream));
+    if (R) HGX_TRY(hipMemcpyAsync(out.wflag.data(), wflag.p, out.wflag.size(), hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipEventRecord(ph1, stream));
+    HGX_TRY(hipEventSynchronize(ph1));
+    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    phase_ms[1] = ms;
+    return collect_kernel_times();
+}
+
+// ---- DecideFame -----------------------------------------------------------------
+hipError_t Engine::decide_fame(std::vector<int8_t>& fame_out) {
+    fame_out.assign((size_t)R * C, 0);
+    if (R == 0) return hipSuccess;
+    DevArrays a = arrays();
+    HGX_TRY(hipEventRecord(ph0, stream));
+    kbeg(K_FAME);
+    launch_fame(stream, a, R, C, n, nw, sm, G);
+    kend(K_FAME, 0);
+    HGX_TRY(hipMemcpyAsync(fame_out.data(), fame.p, fame_out.size(), hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipEventRecord(ph1, stream));
+    HGX_TRY(hipEventSynchronize(ph1));
+    float ms = 0;
+    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    phase_ms[2] = ms;
+    return collect_kernel_times();
+}
+
+// ---- FindOrder ------------------------------------------------------------------
+hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
+                              const std::vector<uint8_t>& ure, OrderHost& out) {
+    out = OrderHost();
+    out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
+    if (R == 0 || E_div == 0) return hipSuccess;
+    DevArrays a = arrays();
+    HGX_TRY(hipEventRecord(ph0, stream));
+    HGX_TRY(hipMemcpyAsync(elig.p, el.data(), (size_t)G * R, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(fw.p, famous.data(), (size_t)R * C, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(ur_empty.p, ure.data(), (size_t)G, hipMemcpyHostToDevice, stream));
+    kbeg(K_THRESHOLD);
+    launch_threshold(stream, a, R, C, n);
+    kend(K_THRESHOLD, 0);
+    HGX_TRY(hipMemsetAsync(counters.p, 0, 8, stream));
+    kbeg(K_ROUND_RECEIVED);
+    launch_round_received(stream, a, E_div, R, C, n);
+    kend(K_ROUND_RECEIVED, (double)E_div * 16);
+    HGX_TRY(hipMemcpyAsync(h_small, counters.p, 8, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    const int32_t m = h_small[0];
+    out.panic = h_small[1] != 0;
+    out.m = m;
+    if (out.panic || m == 0) return collect_kernel_times();
+    kbeg(K_CTS);
+    launch_cts(stream, a, m, C, n, cap);
+    kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
+    // sort keys: cts range, then (graph, rr)
+    const unsigned long long init[2] = {~0ull, 0ull};
+    HGX_TRY(hipMemcpyAsync(minmax.p, init, 16, hipMemcpyHostToDevice, stream));
+    launch_minmax(stream, a, m);
+    unsigned long long mm[2];
+    HGX_TRY(hipMemcpyAsync(mm, minmax.p, 16, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    const int64_t cmin = (int64_t)(mm[0] ^ 0x8000000000000000ull);
+    const int64_t cmax = (int64_t)(mm[1] ^ 0x8000000000000000ull);
+    const int cts_bits = bitlen((uint64_t)(cmax - cmin));
+    const int seg_bits = bitlen((uint64_t)G * (uint64_t)R - 1);
+    uint32_t* vals = nullptr;
+    uint64_t* keys = nullptr;
+    kbeg(K_SORT);
+    launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
+    kend(K_SORT, (double)m * 24.0 * ((cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+    HGX_TRY(hipMemsetAsync(blk_cnt.p, 0, (size_t)G * R * 4, stream));
+    HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
+    HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
+    launch_finish_order(stream, a, m, vals, R, n);
+    HGX_TRY(hipMemcpyAsync(h_order, order_gid.p, (size_t)m * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipEventRecord(ph1, stream));
+    HGX_TRY(hipEventSynchronize(ph1));
+    float ms = 0;
+    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    phase_ms[3] = ms;
+    return collect_kernel_times();
+}
+
+// ---- getters --------------------------------------------------------------------
+hipError_t Engine::get_rounds(std::vector<int32_t>& round_by_gid) {
+    round_by_gid.assign((size_t)E_div, -1);
+    if (E_div == 0) return hipSuccess;
+    launch_gather_i32(stream, E_div, p_round.p, g_pos.p, recv_list.p);
+    HGX_TRY(hipMemcpyAsync(round_by_gid.data(), recv_list.p, (size_t)E_div * 4, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_received(std::vector<int32_t>& rr, std::vector<int64_t>& cts) {
+    rr.assign((size_t)E, -1);
+    cts.assign((size_t)E, 0);
+    if (E == 0) return hipSuccess;
+    HGX_TRY(hipMemcpyAsync(rr.data(), g_rr.p, (size_t)E * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(cts.data(), g_cts.p, (size_t)E * 8, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_coords(int64_t gid, int32_t* la, int32_t* fd) {
+    int32_t pos = 0;
+    HGX_TRY(hipMemcpyAsync(&pos, g_pos.p + gid, 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    HGX_TRY(hipMemcpyAsync(la, LA.p + (size_t)pos * n, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpy2DAsync(fd, 4, FDT.p + pos, (size_t)cap * 4, 4, (size_t)n, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+}  // namespace hgx

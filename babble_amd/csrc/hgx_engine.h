@@ -1,0 +1,123 @@
+// Device engine of libhgx: HBM-resident event DAG + the consensus kernels
+// (hgx_kernels.hip). One Engine per context, one HIP stream. See DESIGN.md.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+enum KernelId {
+    K_LAYOUT = 0, K_LA_SWEEP, K_FD_BUILD, K_ROUND_GATHER, K_ROUND_SEARCH, K_FAME, K_THRESHOLD,
+    K_ROUND_RECEIVED, K_CTS, K_SORT, K_NUM
+};
+
+struct KernelStat {
+    double ms = 0;        // summed device time (HIP events around each launch)
+    int64_t launches = 0;
+    double bytes = 0;     // algorithmic bytes summed over launches
+};
+
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count);
+    hipError_t grow_copy(size_t count, size_t keep, hipStream_t s);
+    void release();
+    ~DBuf() { release(); }
+};
+
+// What the host bookkeeping needs after DivideRounds
+struct RoundsHost {
+    int32_t R = 0;                    // rounds materialised: max over graphs of LastRound + 1
+    std::vector<int32_t> last_round;  // [G], -1 = no events
+    std::vector<int32_t> bm;          // [(R+1) x C] first chain offset with round >= r
+    std::vector<uint8_t> wflag;       // [R x C] 0 none, 1 candidate with higher round, 2 witness
+};
+
+struct OrderHost {
+    int32_t m = 0;                    // newly received events
+    std::vector<int32_t> order_gid;   // [m] graph-major (rr, cts, S) order
+    std::vector<int32_t> blk_cnt;     // [G x R]
+    std::vector<int64_t> blk_ntx;     // [G x R]
+    std::vector<int32_t> blk_loaded;  // [G x R]
+    bool panic = false;
+};
+
+class Engine {
+   public:
+    ~Engine();
+    hipError_t init(int device, int n_graphs, int n_part, int64_t cap_events, std::string& why);
+
+    hipError_t upload_events(int64_t first, int64_t count, const int32_t* creator, const int32_t* index,
+                             const int32_t* op, const int64_t* ts, const uint8_t* S, const uint8_t* coin,
+                             const int32_t* ntx, const uint8_t* loaded);
+    hipError_t divide_rounds(int64_t E, const std::vector<int32_t>& chain_len,
+                             const std::vector<int32_t>& chain_base, RoundsHost& out);
+    hipError_t decide_fame(std::vector<int8_t>& fame_out);
+    hipError_t find_order(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
+                          const std::vector<uint8_t>& ur_empty, OrderHost& out);
+    const int32_t* pinned_order() const { return h_order; }
+
+    hipError_t get_rounds(std::vector<int32_t>& round_by_gid);
+    hipError_t get_received(std::vector<int32_t>& rr, std::vector<int64_t>& cts);
+    hipError_t get_coords(int64_t gid, int32_t* la, int32_t* fd);
+
+    int n = 0, G = 0, C = 0, sm = 0, nw = 1;
+    int64_t cap = 0, E = 0, E_div = 0;   // E_div: events laid out by the last divide_rounds
+    int32_t R = 0;
+    int la_sweeps = 0;
+    hipStream_t stream = nullptr;
+    double phase_ms[4] = {0, 0, 0, 0};   // coordinates, rounds, fame, order (last calls)
+    KernelStat kstat[K_NUM];
+    bool time_kernels = false;
+
+   private:
+    hipError_t ensure_round_cap(int32_t need);
+    void kbeg(int k);
+    void kend(int k, double bytes);
+    hipError_t collect_kernel_times();
+    DevArrays arrays();
+
+    int dev = 0;
+    int max_len = 0;
+    std::vector<int32_t> h_off;
+    // gid order
+    DBuf<int32_t> g_creator, g_index, g_op, g_ntx, g_rr, g_pos;
+    DBuf<int64_t> g_ts, g_cts;
+    DBuf<uint8_t> g_S, g_coin, g_loaded;
+    // chains
+    DBuf<int32_t> c_off, c_len, c_base;
+    // positions
+    DBuf<int32_t> p_gid, p_chain, p_op, p_round, p_rr;
+    DBuf<int64_t> p_ts, p_cts;
+    // coordinates
+    DBuf<int32_t> LA, FDT;
+    // per round
+    int32_t r_cap = 0;
+    DBuf<int32_t> Bm, WLA, WFD, Tthr, active, lr;
+    DBuf<uint8_t> wflag, wcoin, elig, fw, ur_empty;
+    DBuf<uint64_t> Smat, Vbuf;
+    DBuf<int8_t> fame;
+    // order
+    DBuf<int32_t> recv_list, counters, order_gid, blk_cnt, blk_loaded;
+    DBuf<uint64_t> key_a, key_b;
+    DBuf<uint32_t> val_a, val_b, hist;
+    DBuf<int64_t> minmax, blk_ntx;
+    int32_t* h_order = nullptr;   // pinned
+    int32_t* h_small = nullptr;   // pinned scratch (flags)
+    // timing
+    hipEvent_t ph0 = nullptr, ph1 = nullptr;
+    std::vector<hipEvent_t> kev;
+    struct Open { int k; size_t e0; double bytes; };
+    std::vector<Open> kopen;
+    size_t kev_used = 0;
+};
+
+}  // namespace hgx

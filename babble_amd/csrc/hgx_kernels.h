@@ -1,0 +1,66 @@
+// Launchers for the HIP kernels in hgx_kernels.hip (all asynchronous on `s`).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hgx {
+
+constexpr int32_t kMaxI32 = 2147483647;
+
+// Raw device pointers of one context (see hgx_engine.h for meaning/sizes).
+struct DevArrays {
+    // gid order
+    const int32_t *g_creator, *g_index, *g_op, *g_ntx;
+    const int64_t* g_ts;
+    const uint8_t *g_S, *g_coin, *g_loaded;
+    int32_t *g_rr, *g_pos;
+    int64_t* g_cts;
+    // chains
+    const int32_t *c_off, *c_len, *c_base;
+    // positions
+    int32_t *p_gid, *p_chain, *p_op, *p_round, *p_rr;
+    int64_t *p_ts, *p_cts;
+    // coordinates
+    int32_t *LA, *FDT;
+    // rounds
+    int32_t* Bm;
+    uint8_t *wflag, *wcoin;
+    int32_t *WLA, *WFD;
+    int32_t *active, *lr;
+    // fame
+    uint64_t *Smat, *Vbuf;
+    int8_t* fame;
+    // round received
+    uint8_t *elig, *fw, *ur_empty;
+    int32_t* T;
+    int32_t* recv_list;
+    int32_t* counters;   // [0] received count, [1] panic flag, [2] LA changed
+    // order
+    uint64_t *key_a, *key_b;
+    uint32_t *val_a, *val_b;
+    uint32_t* hist;
+    int64_t* minmax;
+    int32_t* order_gid;
+    int32_t *blk_cnt, *blk_loaded;
+    int64_t* blk_ntx;
+};
+
+int fd_tile_rows(int n);
+void launch_layout(hipStream_t s, int64_t E, const DevArrays& a);
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int32_t* changed);
+void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
+void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
+void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm);
+void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
+void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
+void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
+void launch_cts(hipStream_t s, const DevArrays& a, int32_t m, int C, int n, int64_t P);
+void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
+void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
+                 int seg_bits, uint32_t** final_vals, uint64_t** final_keys);
+void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n);
+void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst);
+
+}  // namespace hgx

@@ -1,0 +1,891 @@
+// HIP kernels of libhgx for gfx950 (CDNA4, wave64). See DESIGN.md for the data
+// layout, the reformulation of the reference loops, and the roofline of each kernel.
+//
+// Layout recap (all int32 unless noted):
+//   positions p: events in chain-major order, p = c_off[c] + (Index - c_base[c])
+//   LA  [P x n]  lastAncestors  (row-major per position)      hashgraph.go:448-499
+//   FDT [n x P]  firstDescendants, column-major (FDT[c][p])     hashgraph.go:502-530
+//   per round r and global chain gc: Bm[r][gc] = first chain offset with round >= r,
+//   WLA/WFD[r][gc][:] = coordinate rows of that candidate event, wflag 1/2.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ uint64_t group_mask(int gs, int grp) {
+    return (gs >= 64) ? ~0ull : (((1ull << gs) - 1ull) << (gs * grp));
+}
+
+// ---------------------------------------------------------------------------------
+// layout: gid order -> chain-major positions
+__global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const int32_t* __restrict__ g_index,
+                         const int32_t* __restrict__ g_op, const int64_t* __restrict__ g_ts,
+                         const int32_t* __restrict__ g_rr, const int64_t* __restrict__ g_cts,
+                         const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
+                         int32_t* __restrict__ g_pos, int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
+                         int32_t* __restrict__ p_op, int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
+                         int64_t* __restrict__ p_cts) {
+    int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= E) return;
+    int c = g_creator[gid];
+    int p = c_off[c] + g_index[gid] - c_base[c];
+    g_pos[gid] = p;
+    p_gid[p] = (int32_t)gid;
+    p_chain[p] = c;
+    int op = g_op[gid];
+    int opp = -1;
+    if (op >= 0) {
+        int oc = g_creator[op];
+        opp = c_off[oc] + g_index[op] - c_base[oc];
+    }
+    p_op[p] = opp;
+    p_ts[p] = g_ts[gid];
+    p_rr[p] = g_rr[gid];
+    p_cts[p] = g_cts[gid];
+}
+
+// ---------------------------------------------------------------------------------
+// lastAncestors: in-place monotone sweep (Gauss-Seidel) over chain segments.
+// LA[x] = max(LA[sp(x)], LA[op(x)]), LA[x][cr(x)] = Index(x)   (hashgraph.go:470-496)
+// A unit = (segment s of SEG rows, chain c); units are enumerated time-major so
+// that earlier segments of every chain are usually finished before later ones read
+// them. Converges when a launch writes nothing (values only grow; stale reads are
+// lower bounds).
+template <int GS, int CPL>
+__global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
+                           const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
+                           const int32_t* __restrict__ c_base, int C, int n, int nseg, int seg,
+                           int32_t* __restrict__ changed) {
+    const int lane = lane_id();
+    const int gl = lane % GS;
+    const int64_t unit = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    bool any = false;
+    if (unit < (int64_t)nseg * C) {
+        const int s = (int)(unit / C), c = (int)(unit % C);
+        const int len = c_len[c];
+        const int k0 = s * seg;
+        if (k0 < len) {
+            const int k1 = min(len, k0 + seg);
+            const int off = c_off[c], base = c_base[c], cl = c % n;
+            int32_t carry[CPL];
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int i = gl + GS * q;
+                carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
+            }
+            for (int k = k0; k < k1; k += 4) {
+                int32_t opr[4][CPL], old[4][CPL];
+                int opp[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+#pragma unroll
+                    for (int q = 0; q < CPL; q++) {
+                        const int i = gl + GS * q;
+                        opr[u][q] = (opp[u] >= 0 && i < n) ? LA[(size_t)opp[u] * n + i] : -1;
+                        old[u][q] = (k + u < k1 && i < n) ? LA[(size_t)(off + k + u) * n + i] : -1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (k + u >= k1) break;
+#pragma unroll
+                    for (int q = 0; q < CPL; q++) {
+                        const int i = gl + GS * q;
+                        int32_t v = max(carry[q], opr[u][q]);
+                        if (i == cl) v = base + k + u;
+                        carry[q] = v;
+                        if (i < n && v > old[u][q]) {
+                            LA[(size_t)(off + k + u) * n + i] = v;
+                            any = true;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    const uint64_t b = __ballot(any);
+    if (b && lane == __ffsll((unsigned long long)b) - 1) atomicOr(changed, 1);
+}
+
+// ---------------------------------------------------------------------------------
+// firstDescendants: FD[(d,j)][c] = min{k : LA[(c,k)][d] >= j}, written
+// column-major FDT[c][pos(d,j)]. Block = (chain c, tile of FT rows). Each (d, j, c)
+// is written exactly once; j beyond the chain's last LA value gets MaxInt32.
+__global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__ FDT,
+                           const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
+                           const int32_t* __restrict__ c_base, int n, int FT, int64_t P) {
+    extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+    const int c = blockIdx.x, t = blockIdx.y;
+    const int len = c_len[c];
+    const int ntiles = max(1, (len + FT - 1) / FT);
+    if (t >= ntiles) return;
+    const int k0 = t * FT, k1 = min(len, k0 + FT), rows = k1 - k0;
+    const int off = c_off[c], base_c = c_base[c];
+    const int g = c / n, cl = c % n;
+    const int ld = n + 1;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        sm[i] = (k0 > 0) ? LA[(size_t)(off + k0 - 1) * n + i] : -2147483647 - 1;
+    for (int idx = threadIdx.x; idx < rows * n; idx += blockDim.x) {
+        const int r = idx / n, i = idx % n;
+        sm[(r + 1) * ld + i] = LA[(size_t)(off + k0 + r) * n + i];
+    }
+    __syncthreads();
+    const bool last = (k1 == len);
+    const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    for (int d = wave; d < n; d += nwaves) {
+        const int dc = g * n + d;
+        const int len_d = c_len[dc];
+        if (len_d == 0) continue;
+        const int base_d = c_base[dc], off_d = c_off[dc];
+        int lo = (k0 > 0) ? sm[d] : base_d - 1;
+        if (lo < base_d - 1) lo = base_d - 1;
+        const int hi_val = (rows > 0) ? sm[rows * ld + d] : lo;
+        const int hi = last ? (base_d + len_d - 1) : min(hi_val, base_d + len_d - 1);
+        int32_t* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
+        for (int j = lo + 1 + lane; j <= hi; j += 64) {
+            int a = 0, b = rows;
+            while (a < b) {
+                const int m = (a + b) >> 1;
+                if (sm[(m + 1) * ld + d] >= j) b = m; else a = m + 1;
+            }
+            out[j] = (a < rows) ? (base_c + k0 + a) : kMaxI32;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// rounds. Step r: W'_r = {first event of each chain with round >= r}.
+// gather: copy the candidates' coordinate rows into compact per-round tables.
+__global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
+                               const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA,
+                               const int32_t* __restrict__ FDT, const int32_t* __restrict__ p_gid,
+                               const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
+                               int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
+                               int C, int n, int64_t P) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)C * n) return;
+    const int gc = (int)(t / n), i = (int)(t % n);
+    const int b = Bm[(size_t)r * C + gc];
+    const int len = c_len[gc];
+    const size_t wrow = ((size_t)r * C + gc) * n + i;
+    if (b < len) {
+        const int p = c_off[gc] + b;
+        WLA[wrow] = LA[(size_t)p * n + i];
+        WFD[wrow] = FDT[(size_t)i * P + p];
+        if (i == 0) {
+            wflag[(size_t)r * C + gc] = 1;
+            wcoin[(size_t)r * C + gc] = g_coin[p_gid[p]];
+        }
+    } else if (i == 0) {
+        wflag[(size_t)r * C + gc] = 0;
+    }
+}
+
+// search: per chain, first offset k >= Bm[r] whose event strongly sees >= SM
+// candidates of W'_r (RoundInc, hashgraph.go:285-305, with the witness set of the
+// parent round replaced by W'_r -- exact). One block per chain,
+// probes k = base + group in parallel; counts by ballot + popcount.
+template <int GS, int CPL, bool FD_LDS>
+__global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
+                               const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA,
+                               const int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag,
+                               int32_t* __restrict__ p_round, int32_t* __restrict__ active,
+                               int32_t* __restrict__ lr, int C, int n, int sm) {
+    extern __shared__ __attribute__((aligned(16))) int32_t fds[];  // [ncand x n] when FD_LDS
+    __shared__ int32_t cand[1024];
+    __shared__ int32_t s_ncand, s_first;
+    const int gc = blockIdx.x;
+    const int g = gc / n, cl = gc % n;
+    const int len = c_len[gc];
+    const int b = Bm[(size_t)r * C + gc];
+    if (b >= len) {
+        if (threadIdx.x == 0) Bm[(size_t)(r + 1) * C + gc] = len;
+        return;
+    }
+    if (threadIdx.x == 0) { s_ncand = 0; s_first = 0x7fffffff; }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += blockDim.x)
+        if (wflag[(size_t)r * C + g * n + j] == 1) cand[atomicAdd(&s_ncand, 1)] = j;
+    __syncthreads();
+    const int ncand = s_ncand;
+    const int32_t* __restrict__ wfd_r = WFD + ((size_t)r * C + (size_t)g * n) * n;
+    if (FD_LDS) {
+        for (int idx = threadIdx.x; idx < ncand * n; idx += blockDim.x) {
+            const int w = idx / n, i = idx % n;
+            fds[idx] = wfd_r[(size_t)cand[w] * n + i];
+        }
+        __syncthreads();
+    }
+    const int lane = lane_id(), gl = lane % GS;
+    const int grp_w = lane / GS;                          // group within wave
+    const int grp = (threadIdx.x >> 6) * (64 / GS) + grp_w;  // group within block
+    const int ngroups = (blockDim.x >> 6) * (64 / GS);
+    const uint64_t gmask = group_mask(GS, grp_w);
+    const int off = c_off[gc];
+    int kbase = b, kstar = len;
+    for (;;) {
+        const int k = kbase + grp;
+        const bool valid = k < len;
+        int32_t la[CPL];
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int i = gl + GS * q;
+            la[q] = (valid && i < n) ? LA[(size_t)(off + k) * n + i] : -1;
+        }
+        int cnt = 0;
+        for (int w = 0; w < ncand; w++) {
+            const int wc = cand[w];
+            int tot = 0;
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int i = gl + GS * q;
+                int32_t f = kMaxI32;
+                if (i < n) f = FD_LDS ? fds[w * n + i] : wfd_r[(size_t)wc * n + i];
+                tot += __popcll(__ballot(la[q] >= f) & gmask);
+            }
+            if (tot >= sm && !(wc == cl && k == b)) cnt++;
+        }
+        if (valid && gl == 0 && cnt >= sm) atomicMin(&s_first, grp);
+        __syncthreads();
+        const int f = s_first;
+        if (f != 0x7fffffff) { kstar = kbase + f; break; }
+        kbase += ngroups;
+        if (kbase >= len) { kstar = len; break; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        Bm[(size_t)(r + 1) * C + gc] = kstar;
+        wflag[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
+        if (kstar < len) atomicOr(&active[r], 1);
+        if (kstar > b) atomicMax(&lr[g], r);
+    }
+    for (int k = b + (int)threadIdx.x; k < kstar; k += blockDim.x) p_round[off + k] = r;
+}
+
+// ---------------------------------------------------------------------------------
+// fame. S_j[y] = { w in W_{j-1} : StronglySee(y, w) } as bit masks (one wave per y).
+template <int GS, int CPL, int NW>
+__global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restrict__ wflag, const int32_t* __restrict__ WLA,
+                          const int32_t* __restrict__ WFD, uint64_t* __restrict__ Smat, int C, int n, int sm) {
+    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // (r-1)*C + gc
+    if (item >= (int64_t)(R - 1) * C) return;
+    const int r = (int)(item / C) + 1, gc = (int)(item % C);
+    if (wflag[(size_t)r * C + gc] != 2) return;
+    const int g = gc / n;
+    const int lane = lane_id(), gl = lane % GS, grp_w = lane / GS;
+    const int ngw = 64 / GS;
+    const uint64_t gmask = group_mask(GS, grp_w);
+    int32_t la[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int i = gl + GS * q;
+        la[q] = (i < n) ? WLA[((size_t)r * C + gc) * n + i] : -1;
+    }
+    uint64_t mask[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) mask[w] = 0;
+    const size_t prev = (size_t)(r - 1) * C + (size_t)g * n;
+    for (int wb = 0; wb < n; wb += ngw) {
+        const int w = wb + grp_w;
+        const bool ok = (w < n) && wflag[prev + w] == 2;
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int i = gl + GS * q;
+            const int32_t f = (ok && i < n) ? WFD[(prev + w) * n + i] : kMaxI32;
+            tot += __popcll(__ballot(la[q] >= f) & gmask);
+        }
+        const uint64_t bits = __ballot(ok && gl == 0 && tot >= sm);
+        for (int gg = 0; gg < ngw; gg++) {
+            if ((bits >> (gg * GS)) & 1ull) {
+                const int ww = wb + gg;
+#pragma unroll
+                for (int x = 0; x < NW; x++)
+                    if ((ww >> 6) == x) mask[x] |= 1ull << (ww & 63);
+            }
+        }
+    }
+#pragma unroll
+    for (int x = 0; x < NW; x++)
+        if (lane == x) Smat[((size_t)r * C + gc) * NW + x] = mask[x];
+}
+
+// vote tally and decisions (DecideFame, hashgraph.go:649-730). One block per
+// (graph g, round i). Votes V[x] are bit masks over the witnesses of the previous
+// round; yays = popcount(S_j[y] & V[x]). Ties vote yes; coin rounds use middleBit.
+__global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t* __restrict__ lr,
+                            const uint8_t* __restrict__ wflag, const uint8_t* __restrict__ wcoin,
+                            const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
+                            const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
+                            uint64_t* __restrict__ Vbuf, int8_t* __restrict__ fame, int C, int n, int sm) {
+    __shared__ int32_t xs[1024];
+    __shared__ int32_t dec[1024];
+    __shared__ int32_t s_nx, s_und;
+    const int g = blockIdx.x / R, i = blockIdx.x % R;
+    const int LR = lr[g];
+    if (i > LR) return;
+    const size_t gi = (size_t)g * n;
+    if (threadIdx.x == 0) s_nx = 0;
+    __syncthreads();
+    for (int c = threadIdx.x; c < n; c += blockDim.x)
+        if (wflag[(size_t)i * C + gi + c] == 2) xs[atomicAdd(&s_nx, 1)] = c;
+    __syncthreads();
+    const int nx = s_nx;
+    for (int x = threadIdx.x; x < nx; x += blockDim.x) dec[x] = 0;
+    __syncthreads();
+    if (i + 2 > LR) {   // no round can decide: fame stays undefined
+        for (int x = threadIdx.x; x < nx; x += blockDim.x) fame[(size_t)i * C + gi + xs[x]] = 0;
+        return;
+    }
+    // V buffers for this (g,i): [2][n][nw]
+    uint64_t* V0 = Vbuf + (((size_t)i * 2 + 0) * C + gi) * nw;
+    uint64_t* V1 = Vbuf + (((size_t)i * 2 + 1) * C + gi) * nw;
+    // j = i+1: vote(y, x) = See(y, x) = LA[y][cr(x)] >= Index(x)
+    for (int t = threadIdx.x; t < nx * nw; t += blockDim.x) {
+        const int x = t / nw, wd = t % nw;
+        const int xc = xs[x];
+        const int32_t xidx = c_base[gi + xc] + Bm[(size_t)i * C + gi + xc];
+        uint64_t bits = 0;
+        for (int bb = 0; bb < 64; bb++) {
+            const int y = wd * 64 + bb;
+            if (y >= n) break;
+            if (wflag[(size_t)(i + 1) * C + gi + y] != 2) continue;
+            if (WLA[((size_t)(i + 1) * C + gi + y) * n + xc] >= xidx) bits |= 1ull << bb;
+        }
+        V0[(size_t)x * nw + wd] = bits;
+    }
+    __syncthreads();
+    uint64_t* Vc = V0;
+    uint64_t* Vn = V1;
+    for (int j = i + 2; j <= LR; j++) {
+        const bool normal = ((j - i) % n) != 0;
+        const size_t jr = (size_t)j * C + gi;
+        for (int t = threadIdx.x; t < nx * nw; t += blockDim.x) {
+            const int x = t / nw, wd = t % nw;
+            if (dec[x] != 0) continue;
+            uint64_t bits = 0;
+            for (int bb = 0; bb < 64; bb++) {
+                const int y = wd * 64 + bb;
+                if (y >= n) break;
+                if (wflag[jr + y] != 2) continue;
+                int yays = 0, tot = 0;
+                for (int k = 0; k < nw; k++) {
+                    const uint64_t s = Smat[(jr + y) * nw + k];
+                    tot += __popcll(s);
+                    yays += __popcll(s & Vc[(size_t)x * nw + k]);
+                }
+                const int nays = tot - yays;
+                const bool v = yays >= nays;
+                const int tt = v ? yays : nays;
+                bool bit;
+                if (normal) {
+                    if (tt >= sm) atomicCAS(&dec[x], 0, v ? 1 : 2);
+                    bit = v;
+                } else {
+                    bit = (tt >= sm) ? v : (wcoin[jr + y] != 0);
+                }
+                if (bit) bits |= 1ull << bb;
+            }
+            Vn[(size_t)x * nw + wd] = bits;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int u = 0;
+            for (int x = 0; x < nx; x++) u += (dec[x] == 0);
+            s_und = u;
+        }
+        __syncthreads();
+        if (s_und == 0) break;
+        uint64_t* tmp = Vc; Vc = Vn; Vn = tmp;
+    }
+    for (int x = threadIdx.x; x < nx; x += blockDim.x) fame[(size_t)i * C + gi + xs[x]] = (int8_t)dec[x];
+}
+
+// ---------------------------------------------------------------------------------
+// round received: T[i][d] = (m/2+1)-th largest LA[w][d] over famous witnesses w of
+// round i (DecideRoundReceived hashgraph.go:767-775). One wave per (i, d).
+template <int CPL>
+__global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restrict__ elig, const uint8_t* __restrict__ fw,
+                            const int32_t* __restrict__ WLA, int32_t* __restrict__ T, int C, int n) {
+    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (item >= (int64_t)R * C) return;
+    const int i = (int)(item / C), gd = (int)(item % C);
+    const int g = gd / n, dl = gd % n;
+    if (!elig[(size_t)g * R + i]) return;
+    const int lane = lane_id();
+    const size_t base = (size_t)i * C + (size_t)g * n;
+    int32_t v[CPL];
+    bool ok[CPL];
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int c = lane + 64 * q;
+        ok[q] = c < n && fw[base + c];
+        v[q] = ok[q] ? WLA[(base + c) * n + dl] : 0;
+        m += __popcll(__ballot(ok[q]));
+    }
+    const int K = m / 2;   // 0-based rank in descending order
+    int32_t res = -1;
+    bool found = false;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        int rank = 0;
+        for (int q2 = 0; q2 < CPL; q2++) {
+            for (int src = 0; src < 64; src++) {
+                const int32_t u = __shfl(v[q2], src);
+                const bool uok = __shfl((int)ok[q2], src) != 0;
+                const int fi = src + 64 * q2, mi = lane + 64 * q;
+                if (uok && (u > v[q] || (u == v[q] && fi < mi))) rank++;
+            }
+        }
+        if (ok[q] && rank == K) { res = v[q]; found = true; }
+    }
+    const uint64_t b = __ballot(found);
+    const int src = b ? (__ffsll((unsigned long long)b) - 1) : 0;
+    res = __shfl(res, src);
+    if (lane == 0) T[(size_t)i * C + gd] = (m > 0) ? res : -1;
+}
+
+// rr(x) = first eligible i > round(x) with Index(x) <= T[i][cr(x)]; compacts the
+// newly received positions (block-aggregated append).
+__global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const int32_t* __restrict__ p_chain,
+                                 const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
+                                 const int32_t* __restrict__ p_round, const int32_t* __restrict__ lr,
+                                 const uint8_t* __restrict__ elig, const uint8_t* __restrict__ ur_empty,
+                                 const int32_t* __restrict__ T, int32_t* __restrict__ p_rr,
+                                 int32_t* __restrict__ recv_list, int32_t* __restrict__ counters, int C, int n) {
+    __shared__ int32_t s_cnt, s_base;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int slot = -1;
+    if (p < Pn && p_rr[p] < 0) {
+        const int gc = p_chain[p], g = gc / n;
+        const int j = c_base[gc] + (int)(p - c_off[gc]);
+        const int r = p_round[p];
+        const int LR = lr[g];
+        if (r + 1 <= LR && ur_empty[g]) atomicOr(&counters[1], 1);   // Go panics on UndecidedRounds[0]
+        int rr = -1;
+        for (int i = r + 1; i <= LR; i++) {
+            if (elig[(size_t)g * R + i] && j <= T[(size_t)i * C + gc]) { rr = i; break; }
+        }
+        if (rr >= 0) {
+            p_rr[p] = rr;
+            slot = atomicAdd(&s_cnt, 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counters[0], s_cnt) : 0;
+    __syncthreads();
+    if (slot >= 0) recv_list[s_base + slot] = (int32_t)p;
+}
+
+// consensus timestamp: upper median of the timestamps of OldestSelfAncestorToSee(a, x)
+// = FD[x][cr(a)] over famous witnesses a of round rr(x) that see x
+// (hashgraph.go:780-787, 860-868). One wave per received event.
+template <int CPL>
+__global__ void __launch_bounds__(256) k_cts(int32_t m, const int32_t* __restrict__ recv_list, const int32_t* __restrict__ p_chain,
+                      const int32_t* __restrict__ p_rr, const int32_t* __restrict__ c_off,
+                      const int32_t* __restrict__ c_base, const uint8_t* __restrict__ fw,
+                      const int32_t* __restrict__ WLA, const int32_t* __restrict__ FDT,
+                      const int64_t* __restrict__ p_ts, int64_t* __restrict__ p_cts, int C, int n, int64_t P) {
+    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (item >= m) return;
+    const int p = recv_list[item];
+    const int gc = p_chain[p], g = gc / n, dl = gc % n;
+    const int j = c_base[gc] + (p - c_off[gc]);
+    const int i = p_rr[p];
+    const int lane = lane_id();
+    const size_t base = (size_t)i * C + (size_t)g * n;
+    int64_t v[CPL];
+    bool ok[CPL];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int c = lane + 64 * q;
+        ok[q] = c < n && fw[base + c] && WLA[(base + c) * n + dl] >= j;
+        v[q] = 0;
+        if (ok[q]) {
+            const int ch = g * n + c;
+            const int32_t fd = FDT[(size_t)c * P + p];
+            v[q] = p_ts[c_off[ch] + (fd - c_base[ch])];
+        }
+        cnt += __popcll(__ballot(ok[q]));
+    }
+    const int K = cnt / 2;   // index in ascending order
+    int64_t res = 0;
+    bool found = false;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        int rank = 0;
+        for (int q2 = 0; q2 < CPL; q2++) {
+            for (int src = 0; src < 64; src++) {
+                const int64_t u = __shfl(v[q2], src);
+                const bool uok = __shfl((int)ok[q2], src) != 0;
+                const int fi = src + 64 * q2, mi = lane + 64 * q;
+                if (uok && (u < v[q] || (u == v[q] && fi < mi))) rank++;
+            }
+        }
+        if (ok[q] && rank == K) { res = v[q]; found = true; }
+    }
+    const uint64_t b = __ballot(found);
+    const int src = b ? (__ffsll((unsigned long long)b) - 1) : 0;
+    res = __shfl(res, src);
+    if (lane == 0) p_cts[p] = res;
+}
+
+// ---------------------------------------------------------------------------------
+// order: LSD radix sort (8-bit digits) of (u64 key, u32 value), stable.
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 8;
+constexpr int kSortTile = kSortThreads * kSortItems;
+
+__global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* __restrict__ keys, int32_t m, int shift,
+                                                             uint32_t* __restrict__ hist, int nblocks) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int s = 0; s < kSortItems; s++) {
+        const int idx = blockIdx.x * kSortTile + s * kSortThreads + threadIdx.x;
+        if (idx < m) atomicAdd(&h[(keys[idx] >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of `total` u32 in place, single block of 1024 threads
+__global__ void __launch_bounds__(1024) k_scan_u32(uint32_t* __restrict__ a, int64_t total) {
+    __shared__ uint32_t part[1024];
+    const int64_t chunk = (total + 1023) / 1024;
+    const int64_t lo = threadIdx.x * chunk, hi = min(total, lo + chunk);
+    uint32_t s = 0;
+    for (int64_t k = lo; k < hi; k++) s += a[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = (threadIdx.x >= (unsigned)d) ? part[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (int64_t k = lo; k < hi; k++) {
+        const uint32_t x = a[k];
+        a[k] = run;
+        run += x;
+    }
+}
+
+__global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                                int32_t m, int shift, const uint32_t* __restrict__ hist,
+                                                                int nblocks, uint64_t* __restrict__ kout,
+                                                                uint32_t* __restrict__ vout) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[kSortThreads / 64][256];
+    __shared__ uint32_t woff[kSortThreads / 64][256];
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    run[threadIdx.x] = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int s = 0; s < kSortItems; s++) {
+        for (int w = 0; w < kSortThreads / 64; w++) wcnt[w][threadIdx.x] = 0;
+        __syncthreads();
+        const int idx = blockIdx.x * kSortTile + s * kSortThreads + threadIdx.x;
+        const bool valid = idx < m;
+        const uint64_t key = valid ? kin[idx] : 0;
+        const uint32_t val = valid ? vin[idx] : 0;
+        const int d = (int)((key >> shift) & 255);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const uint64_t bb = __ballot(valid && ((d >> bit) & 1));
+            peers &= ((d >> bit) & 1) ? bb : ~bb;
+        }
+        const int rk = __popcll(peers & lt);
+        if (valid && rk == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        {
+            uint32_t rr = run[threadIdx.x];
+            for (int w = 0; w < kSortThreads / 64; w++) {
+                woff[w][threadIdx.x] = rr;
+                rr += wcnt[w][threadIdx.x];
+            }
+            run[threadIdx.x] = rr;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint32_t o = hist[(size_t)d * nblocks + blockIdx.x] + woff[wave][d] + (uint32_t)rk;
+            kout[o] = key;
+            vout[o] = val;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_keys_cts(int32_t m, const int32_t* __restrict__ list, const int64_t* __restrict__ p_cts,
+                           int64_t cmin, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int p = list[i];
+    keys[i] = (uint64_t)(p_cts[p] - cmin);
+    vals[i] = (uint32_t)p;
+}
+
+__global__ void k_keys_seg(int32_t m, const uint32_t* __restrict__ vals, const int32_t* __restrict__ p_chain,
+                           const int32_t* __restrict__ p_rr, int R, int n, uint64_t* __restrict__ keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int p = (int)vals[i];
+    keys[i] = (uint64_t)(p_chain[p] / n) * (uint64_t)R + (uint64_t)p_rr[p];
+}
+
+__global__ void k_minmax_cts(int32_t m, const int32_t* __restrict__ list, const int64_t* __restrict__ p_cts,
+                             unsigned long long* __restrict__ mm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t v = (i < m) ? p_cts[list[i]] : 0;
+    // bias to unsigned order
+    unsigned long long u = (unsigned long long)v ^ 0x8000000000000000ull;
+    unsigned long long lo = (i < m) ? u : ~0ull, hi = (i < m) ? u : 0ull;
+    for (int o = 32; o >= 1; o >>= 1) {
+        lo = min(lo, (unsigned long long)__shfl_xor(lo, o));
+        hi = max(hi, (unsigned long long)__shfl_xor(hi, o));
+    }
+    if (lane_id() == 0 && i - lane_id() < m) {
+        atomicMin(&mm[0], lo);
+        atomicMax(&mm[1], hi);
+    }
+}
+
+// equal (graph, rr, cts) runs are ordered by S (big-endian 256-bit; consensus_sorter.go:37-42)
+__device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
+    for (int k = 0; k < 32; k++)
+        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return 0;
+}
+
+__global__ void k_tiefix(int32_t m, uint32_t* __restrict__ vals, const uint64_t* __restrict__ segk,
+                         const int64_t* __restrict__ p_cts, const int32_t* __restrict__ p_gid,
+                         const uint8_t* __restrict__ g_S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int p = (int)vals[i];
+    if (i > 0) {
+        const int pp = (int)vals[i - 1];
+        if (segk[i - 1] == segk[i] && p_cts[pp] == p_cts[p]) return;   // not a run start
+    }
+    int e = i + 1;
+    while (e < m && segk[e] == segk[i] && p_cts[vals[e]] == p_cts[p]) e++;
+    if (e - i < 2) return;
+    for (int a = i + 1; a < e; a++) {   // insertion sort by S (run owned by this thread)
+        const uint32_t va = vals[a];
+        const uint8_t* sa = g_S + (size_t)p_gid[va] * 32;
+        int b = a - 1;
+        while (b >= i && cmp_s(g_S + (size_t)p_gid[vals[b]] * 32, sa) > 0) {
+            vals[b + 1] = vals[b];
+            b--;
+        }
+        vals[b + 1] = va;
+    }
+}
+
+// final: order gids, block stats per (graph, rr), persist rr/cts to gid order
+__global__ void k_finish_order(int32_t m, const uint32_t* __restrict__ vals, const int32_t* __restrict__ p_gid,
+                               const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+                               const int64_t* __restrict__ p_cts, const int32_t* __restrict__ g_ntx,
+                               const uint8_t* __restrict__ g_loaded, int R, int n, int32_t* __restrict__ order_gid,
+                               int32_t* __restrict__ g_rr, int64_t* __restrict__ g_cts,
+                               int32_t* __restrict__ blk_cnt, int64_t* __restrict__ blk_ntx,
+                               int32_t* __restrict__ blk_loaded) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int p = (int)vals[i];
+    const int gid = p_gid[p];
+    order_gid[i] = gid;
+    g_rr[gid] = p_rr[p];
+    g_cts[gid] = p_cts[p];
+    const size_t b = (size_t)(p_chain[p] / n) * R + p_rr[p];
+    atomicAdd(&blk_cnt[b], 1);
+    if (g_ntx[gid]) atomicAdd((unsigned long long*)&blk_ntx[b], (unsigned long long)g_ntx[gid]);
+    if (g_loaded[gid]) atomicAdd(&blk_loaded[b], 1);
+}
+
+__global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const int32_t* __restrict__ g_pos,
+                             int32_t* __restrict__ dst) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < E) dst[gid] = src[g_pos[gid]];
+}
+
+// ---------------------------------------------------------------------------------
+// host-side launchers (template dispatch on n)
+#define HGX_DISPATCH_N(n, MACRO)                      \
+    do {                                              \
+        if ((n) <= 4) { MACRO(4, 1, 1); }             \
+        else if ((n) <= 8) { MACRO(8, 1, 1); }        \
+        else if ((n) <= 16) { MACRO(16, 1, 1); }      \
+        else if ((n) <= 32) { MACRO(32, 1, 1); }      \
+        else if ((n) <= 64) { MACRO(64, 1, 1); }      \
+        else if ((n) <= 128) { MACRO(64, 2, 2); }     \
+        else if ((n) <= 256) { MACRO(64, 4, 4); }     \
+        else if ((n) <= 512) { MACRO(64, 8, 8); }     \
+        else { MACRO(64, 16, 16); }                   \
+    } while (0)
+
+static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
+
+void launch_layout(hipStream_t s, int64_t E, const DevArrays& a) {
+    if (E <= 0) return;
+    hipLaunchKernelGGL(k_layout, dim3(nblk(E, 256)), dim3(256), 0, s, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
+                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_ts, a.p_rr,
+                       a.p_cts);
+}
+
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int32_t* changed) {
+    const int seg = 16;
+    const int nseg = (max_len + seg - 1) / seg;
+    if (nseg == 0) return;
+#define LA_LAUNCH(GS, CPL, NW)                                                                                \
+    {                                                                                                         \
+        const int64_t threads = (int64_t)nseg * C * GS;                                                       \
+        hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, a.LA, a.p_op,   \
+                           a.c_off, a.c_len, a.c_base, C, n, nseg, seg, changed);                             \
+    }
+    HGX_DISPATCH_N(n, LA_LAUNCH);
+#undef LA_LAUNCH
+}
+
+int fd_tile_rows(int n) {
+    int ft = 16384 / n;
+    if (ft > 64) ft = 64;
+    if (ft < 4) ft = 4;
+    return ft;
+}
+
+void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P) {
+    const int ft = fd_tile_rows(n);
+    const int tiles = max(1, (max_len + ft - 1) / ft);
+    const size_t lds = (size_t)(ft + 1) * (n + 1) * sizeof(int32_t);
+    hipLaunchKernelGGL(k_fd_build, dim3(C, tiles), dim3(256), lds, s, a.LA, a.FDT, a.c_off, a.c_len, a.c_base, n,
+                       ft, P);
+}
+
+void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
+    hipLaunchKernelGGL(k_round_gather, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm, a.c_off, a.c_len,
+                       a.LA, a.FDT, a.p_gid, a.g_coin, a.WLA, a.WFD, a.wflag, a.wcoin, C, n, P);
+}
+
+void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm) {
+#define RS_LAUNCH(GS, CPL, NW)                                                                                \
+    {                                                                                                         \
+        if (n <= 128) {                                                                                       \
+            const size_t lds = (size_t)n * n * sizeof(int32_t);                                               \
+            hipLaunchKernelGGL((k_round_search<GS, CPL, true>), dim3(C), dim3(256), lds, s, r, a.Bm, a.c_off, \
+                               a.c_len, a.LA, a.WFD, a.wflag, a.p_round, a.active, a.lr, C, n, sm);           \
+        } else {                                                                                              \
+            hipLaunchKernelGGL((k_round_search<GS, CPL, false>), dim3(C), dim3(256), 0, s, r, a.Bm, a.c_off,  \
+                               a.c_len, a.LA, a.WFD, a.wflag, a.p_round, a.active, a.lr, C, n, sm);           \
+        }                                                                                                     \
+    }
+    HGX_DISPATCH_N(n, RS_LAUNCH);
+#undef RS_LAUNCH
+}
+
+void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G) {
+    if (R > 1) {
+#define SS_LAUNCH(GS, CPL, NW)                                                                                \
+    {                                                                                                         \
+        const int64_t threads = (int64_t)(R - 1) * C * 64;                                                    \
+        hipLaunchKernelGGL((k_fame_ss<GS, CPL, NW>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.wflag,  \
+                           a.WLA, a.WFD, a.Smat, C, n, sm);                                                   \
+    }
+        HGX_DISPATCH_N(n, SS_LAUNCH);
+#undef SS_LAUNCH
+    }
+    hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wflag, a.wcoin, a.Bm,
+                       a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
+}
+
+void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n) {
+    if (R <= 0) return;
+#define TH_LAUNCH(GS, CPL, NW)                                                                                \
+    {                                                                                                         \
+        const int64_t threads = (int64_t)R * C * 64;                                                          \
+        hipLaunchKernelGGL((k_threshold<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.elig, a.fw,   \
+                           a.WLA, a.T, C, n);                                                                 \
+    }
+    HGX_DISPATCH_N(n, TH_LAUNCH);
+#undef TH_LAUNCH
+}
+
+void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n) {
+    if (Pn <= 0) return;
+    hipLaunchKernelGGL(k_round_received, dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, R, a.p_chain, a.c_off, a.c_base,
+                       a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.recv_list, a.counters, C, n);
+}
+
+void launch_cts(hipStream_t s, const DevArrays& a, int32_t m, int C, int n, int64_t P) {
+    if (m <= 0) return;
+#define CT_LAUNCH(GS, CPL, NW)                                                                                \
+    {                                                                                                         \
+        const int64_t threads = (int64_t)m * 64;                                                              \
+        hipLaunchKernelGGL((k_cts<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, m, a.recv_list, a.p_chain, \
+                           a.p_rr, a.c_off, a.c_base, a.fw, a.WLA, a.FDT, a.p_ts, a.p_cts, C, n, P);          \
+    }
+    HGX_DISPATCH_N(n, CT_LAUNCH);
+#undef CT_LAUNCH
+}
+
+void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {
+    hipLaunchKernelGGL(k_minmax_cts, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts,
+                       (unsigned long long*)a.minmax);
+}
+
+static void radix_pass(hipStream_t s, const DevArrays& a, int32_t m, int shift, const uint64_t* kin,
+                       const uint32_t* vin, uint64_t* kout, uint32_t* vout) {
+    const int nb = (m + kSortTile - 1) / kSortTile;
+    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kSortThreads), 0, s, kin, m, shift, a.hist, nb);
+    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, a.hist, (int64_t)256 * nb);
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kSortThreads), 0, s, kin, vin, m, shift, a.hist, nb, kout,
+                       vout);
+}
+
+// sorts the received list by (graph, rr, cts, S); result values (positions) are
+// returned in *final_vals (one of the two ping-pong buffers).
+void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
+                 int seg_bits, uint32_t** final_vals, uint64_t** final_keys) {
+    uint64_t *ka = a.key_a, *kb = a.key_b;
+    uint32_t *va = a.val_a, *vb = a.val_b;
+    hipLaunchKernelGGL(k_keys_cts, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, cmin, ka, va);
+    for (int sh = 0; sh < cts_bits; sh += 8) {
+        radix_pass(s, a, m, sh, ka, va, kb, vb);
+        uint64_t* tk = ka; ka = kb; kb = tk;
+        uint32_t* tv = va; va = vb; vb = tv;
+    }
+    hipLaunchKernelGGL(k_keys_seg, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, a.p_chain, a.p_rr, R, n, ka);
+    for (int sh = 0; sh < seg_bits; sh += 8) {
+        radix_pass(s, a, m, sh, ka, va, kb, vb);
+        uint64_t* tk = ka; ka = kb; kb = tk;
+        uint32_t* tv = va; va = vb; vb = tv;
+    }
+    hipLaunchKernelGGL(k_tiefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_cts, a.p_gid, a.g_S);
+    *final_vals = va;
+    *final_keys = ka;
+}
+
+void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n) {
+    hipLaunchKernelGGL(k_finish_order, dim3(nblk(m, 256)), dim3(256), 0, s, m, vals, a.p_gid, a.p_chain, a.p_rr,
+                       a.p_cts, a.g_ntx, a.g_loaded, R, n, a.order_gid, a.g_rr, a.g_cts, a.blk_cnt, a.blk_ntx,
+                       a.blk_loaded);
+}
+
+void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst) {
+    if (E <= 0) return;
+    hipLaunchKernelGGL(k_gather_i32, dim3(nblk(E, 256)), dim3(256), 0, s, E, src, g_pos, dst);
+}
+
+}  // namespace hgx

@@ -1,0 +1,262 @@
+"""Python mirror of the reference's hashgraph.Hashgraph API over libhgx's C ABI.
+
+Reference: datatypevoid/babble v0.2.0 hashgraph/hashgraph.go. Method names follow
+the Go API (InsertEvent, DivideRounds, DecideFame, FindOrder, Round, Witness,
+StronglySee, ...) with the same argument meaning and the same error strings
+(raised as babble_amd._lib.HgxError). Events are addressed by dense ids (gid, in
+insertion order) -- the cgo shim described in INTEGRATION.md maps Go hex ids to
+these. All computation happens in the HIP kernels of libhgx.so; this module only
+marshals arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HgxError, hgx_error, hgx_events, ptr
+
+UNKNOWN_PARENT = -2
+
+
+class Hashgraph:
+    """One context = NewHashgraph(participants, NewInmemStore(participants, cap)) (hashgraph.go:39-66).
+
+    n_graphs > 1 makes a batched context of independent hashgraphs (graph g owns
+    participant ids g*n .. g*n+n-1); per-graph getters take `graph`.
+    """
+
+    def __init__(self, n_participants: int, capacity: int = 1 << 16, device: int = 0, n_graphs: int = 1):
+        self.L = _lib.lib()
+        self.n = n_participants
+        self.G = n_graphs
+        err = hgx_error()
+        self.ctx = self.L.hgx_create_batch(n_graphs, n_participants, capacity, device, C.byref(err))
+        if not self.ctx:
+            raise HgxError(err.code, err.msg.decode(errors="replace"))
+        self.capacity = capacity
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.hgx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ inserts
+    def insert_arrays(self, creator, index, sp, op, ts, hash32, s32, ntx, txnil) -> int:
+        """Bulk InsertEvent(e, true) in order; raises HgxError on the first rejected event."""
+        a = dict(creator=np.ascontiguousarray(creator, np.int32), index=np.ascontiguousarray(index, np.int64),
+                 sp=np.ascontiguousarray(sp, np.int64), op=np.ascontiguousarray(op, np.int64),
+                 ts=np.ascontiguousarray(ts, np.int64), h=np.ascontiguousarray(hash32, np.uint8),
+                 s=np.ascontiguousarray(s32, np.uint8), ntx=np.ascontiguousarray(ntx, np.int32),
+                 nil=np.ascontiguousarray(txnil, np.int32))
+        cnt = int(a["creator"].shape[0])
+        ev = hgx_events(ptr(a["creator"]), ptr(a["index"]), ptr(a["sp"]), ptr(a["op"]), ptr(a["ts"]),
+                        ptr(a["h"]), ptr(a["s"]), ptr(a["ntx"]), ptr(a["nil"]))
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_events(self.ctx, C.byref(ev), cnt, C.byref(n_ins), C.byref(err))
+        _lib.check(rc, err)
+        return n_ins.value
+
+    def insert_trace(self, t, lo: int = 0, hi: Optional[int] = None) -> int:
+        hi = t.E if hi is None else hi
+        sl = slice(lo, hi)
+        return self.insert_arrays(t.creator[sl], t.index[sl], t.sp[sl], t.op[sl], t.ts[sl], t.hash[sl], t.s[sl],
+                                  t.ntx[sl], t.txnil[sl])
+
+    def InsertEvent(self, creator: int, index: int, self_parent: int, other_parent: int, timestamp_ns: int,
+                    hash32: bytes, s32: bytes, transactions: Optional[Sequence[bytes]]):
+        """InsertEvent(event, true) (hashgraph.go:356-401): raises HgxError with the Go error string."""
+        txs = [] if transactions is None else list(transactions)
+        self.insert_arrays([creator], [index], [self_parent], [other_parent], [timestamp_ns],
+                           np.frombuffer(hash32, np.uint8).reshape(1, 32), np.frombuffer(s32, np.uint8).reshape(1, 32),
+                           [len(txs)], [1 if transactions is None else 0])
+
+    # ------------------------------------------------------------------ the consensus calls
+    def _call(self, fn):
+        err = hgx_error()
+        rc = fn(self.ctx, C.byref(err))
+        _lib.check(rc, err)
+
+    def DivideRounds(self):
+        self._call(self.L.hgx_divide_rounds)
+
+    def DecideFame(self):
+        self._call(self.L.hgx_decide_fame)
+
+    def FindOrder(self):
+        self._call(self.L.hgx_find_order)
+
+    def RunConsensus(self):
+        """node/core.go:277-303"""
+        self._call(self.L.hgx_run_consensus)
+
+    # ------------------------------------------------------------------ state (hashgraph.go:15-37)
+    def UndecidedRounds(self, graph: int = 0) -> List[int]:
+        k = self.L.hgx_undecided_rounds(self.ctx, graph, None, 0)
+        buf = np.zeros(max(k, 1), np.int32)
+        self.L.hgx_undecided_rounds(self.ctx, graph, ptr(buf), k)
+        return [int(v) for v in buf[:k]]
+
+    def LastConsensusRound(self, graph: int = 0) -> Optional[int]:
+        has = C.c_int32(0)
+        v = self.L.hgx_last_consensus_round(self.ctx, graph, C.byref(has))
+        return int(v) if has.value else None
+
+    def LastCommitedRoundEvents(self, graph: int = 0) -> int:
+        return int(self.L.hgx_last_commited_round_events(self.ctx, graph))
+
+    def ConsensusTransactions(self, graph: int = 0) -> int:
+        return int(self.L.hgx_consensus_transactions(self.ctx, graph))
+
+    def PendingLoadedEvents(self, graph: int = 0) -> int:
+        return int(self.L.hgx_pending_loaded_events(self.ctx, graph))
+
+    def SuperMajority(self) -> int:
+        return int(self.L.hgx_super_majority(self.ctx))
+
+    # ------------------------------------------------------------------ Store views
+    def LastRound(self, graph: int = 0) -> int:
+        return int(self.L.hgx_last_round(self.ctx, graph))
+
+    def RoundEvents(self, r: int, graph: int = 0) -> int:
+        return int(self.L.hgx_round_event_count(self.ctx, graph, r))
+
+    def RoundWitnesses(self, r: int, graph: int = 0) -> List[int]:
+        buf = np.zeros(self.n, np.int64)
+        k = self.L.hgx_round_witnesses(self.ctx, graph, r, ptr(buf), self.n)
+        return [int(v) for v in buf[:k]]
+
+    def Known(self, graph: int = 0) -> np.ndarray:
+        out = np.zeros(self.n, np.int32)
+        self.L.hgx_known(self.ctx, graph, ptr(out))
+        return out
+
+    def ConsensusEvents(self, graph: int = 0) -> np.ndarray:
+        k = int(self.L.hgx_consensus_events_count(self.ctx, graph))
+        out = np.zeros(max(k, 1), np.int64)
+        if k:
+            rc = self.L.hgx_consensus_events(self.ctx, graph, 0, k, ptr(out))
+            if rc:
+                raise HgxError(rc, "hgx_consensus_events failed")
+        return out[:k]
+
+    def Blocks(self, graph: int = 0) -> List[dict]:
+        res = []
+        for b in range(int(self.L.hgx_num_blocks(self.ctx, graph))):
+            rr, nev, nil, com = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+            first, ntx = C.c_int64(), C.c_int64()
+            self.L.hgx_block_info(self.ctx, graph, b, C.byref(rr), C.byref(first), C.byref(nev), C.byref(ntx),
+                                  C.byref(nil), C.byref(com))
+            res.append(dict(rr=rr.value, first=first.value, n_events=nev.value, ntx=ntx.value,
+                            tx_nil=bool(nil.value), committed=bool(com.value)))
+        return res
+
+    # ------------------------------------------------------------------ primitives
+    def Ancestor(self, x: int, y: int) -> bool:
+        return bool(self.L.hgx_ancestor(self.ctx, x, y))
+
+    def SelfAncestor(self, x: int, y: int) -> bool:
+        return bool(self.L.hgx_self_ancestor(self.ctx, x, y))
+
+    def See(self, x: int, y: int) -> bool:
+        return bool(self.L.hgx_see(self.ctx, x, y))
+
+    def StronglySee(self, x: int, y: int) -> bool:
+        return bool(self.L.hgx_strongly_see(self.ctx, x, y))
+
+    def OldestSelfAncestorToSee(self, x: int, y: int) -> int:
+        return int(self.L.hgx_oldest_self_ancestor_to_see(self.ctx, x, y))
+
+    def Round(self, x: int) -> int:
+        return int(self.L.hgx_round(self.ctx, x))
+
+    def Witness(self, x: int) -> bool:
+        return bool(self.L.hgx_witness(self.ctx, x))
+
+    def coords(self, x: int):
+        la = np.zeros(self.n, np.int32)
+        fd = np.zeros(self.n, np.int32)
+        rc = self.L.hgx_get_coords(self.ctx, x, ptr(la), ptr(fd))
+        if rc:
+            raise HgxError(rc, "hgx_get_coords failed")
+        return la, fd
+
+    # ------------------------------------------------------------------ bulk results
+    def num_events(self) -> int:
+        return int(self.L.hgx_num_events(self.ctx))
+
+    def rounds(self):
+        E = self.num_events()
+        rnd = np.zeros(max(E, 1), np.int32)
+        wit = np.zeros(max(E, 1), np.int8)
+        fam = np.zeros(max(E, 1), np.int8)
+        if E:
+            rc = self.L.hgx_get_rounds(self.ctx, 0, E, ptr(rnd), ptr(wit), ptr(fam))
+            if rc:
+                raise HgxError(rc, "hgx_get_rounds failed")
+        return rnd[:E], wit[:E], fam[:E]
+
+    def received(self):
+        E = self.num_events()
+        rr = np.zeros(max(E, 1), np.int32)
+        cts = np.zeros(max(E, 1), np.int64)
+        if E:
+            rc = self.L.hgx_get_received(self.ctx, 0, E, ptr(rr), ptr(cts))
+            if rc:
+                raise HgxError(rc, "hgx_get_received failed")
+        return rr[:E], cts[:E]
+
+    def results(self, graph: int = 0) -> dict:
+        """Same shape as tests' oracle results() for parity comparison (single-graph contexts)."""
+        rnd, wit, fam = self.rounds()
+        rr, cts = self.received()
+        return dict(round=rnd, witness=wit, famous=fam, rr=rr, cts=np.where(rr >= 0, cts, 0),
+                    order=self.ConsensusEvents(graph), last_round=self.LastRound(graph),
+                    undecided=self.UndecidedRounds(graph), lcr=self.LastConsensusRound(graph),
+                    lcre=self.LastCommitedRoundEvents(graph), consensus_tx=self.ConsensusTransactions(graph),
+                    pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
+
+    def phase_times(self):
+        out = np.zeros(6, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 6)
+        return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
+                    la_sweeps=int(out[4]), rounds=int(out[5]))
+
+    def kernel_stats(self):
+        res = {}
+        for k in range(10):
+            name = C.create_string_buffer(32)
+            ms, launches, nbytes = C.c_double(), C.c_int64(), C.c_double()
+            if self.L.hgx_kernel_stats(self.ctx, k, name, 32, C.byref(ms), C.byref(launches), C.byref(nbytes)):
+                break
+            res[name.value.decode()] = dict(ms=ms.value, launches=launches.value, bytes=nbytes.value)
+        return res
+
+    def set_kernel_timing(self, on: bool):
+        self.L.hgx_set_kernel_timing(self.ctx, 1 if on else 0)
+
+    def reset_stats(self):
+        self.L.hgx_reset_stats(self.ctx)
+
+
+def block_hash(rr: int, txs: List[bytes], tx_nil: bool) -> bytes:
+    """SHA256(json.Encoder(Block)) (hashgraph/block.go:44-53), computed by libhgx."""
+    L = _lib.lib()
+    ntx = len(txs)
+    bufs = [C.create_string_buffer(t, max(len(t), 1)) for t in txs]
+    ptrs = (C.c_void_p * max(ntx, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
+    lens = (C.c_int64 * max(ntx, 1))(*[len(t) for t in txs])
+    out = C.create_string_buffer(32)
+    rc = L.hgx_block_hash(rr, ntx, ptrs, lens, 1 if tx_nil else 0, out)
+    if rc:
+        raise HgxError(rc, "hgx_block_hash failed")
+    return out.raw

@@ -154,6 +154,8 @@ int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 int32_t hgx_kernel_stats(hgx_ctx* ctx, int32_t k, char* name, int32_t name_cap, double* ms, int64_t* launches,
                          double* bytes);
 int32_t hgx_reset_stats(hgx_ctx* ctx);
+/* time every kernel launch with HIP events on the context stream (bench.py roofline) */
+int32_t hgx_set_kernel_timing(hgx_ctx* ctx, int32_t on);
 
 /* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
 /* Seeded random gossip modelled on node/core_test.go:514-537: every active peer
