@@ -64,6 +64,7 @@ def lib():
     _sig(L, "hgx_create_batch", p, [i32, i32, i64, i32, E])
     _sig(L, "hgx_destroy", None, [p])
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
+    _sig(L, "hgx_reset_consensus", i32, [p])
     for nm in ("hgx_divide_rounds", "hgx_decide_fame", "hgx_find_order", "hgx_run_consensus"):
         _sig(L, nm, i32, [p, E])
     _sig(L, "hgx_num_events", i64, [p])

@@ -367,6 +367,20 @@ int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
     return hgx_find_order(c, err);
 }
 
+int32_t hgx_reset_consensus(hgx_ctx* c) {
+    if (!c) return HGX_ERR_INVALID;
+    for (int g = 0; g < c->G; g++) c->gs[g] = GraphState();
+    for (int64_t x = 0; x < c->E; x++) {
+        GraphState& s = c->gs[c->creator[x] / c->n];
+        s.undetermined++;
+        if (c->loaded[x]) s.pending_loaded++;
+    }
+    c->divided = false;
+    c->E_div = 0;
+    c->rounds_cached = c->recv_cached = false;
+    return c->eng.reset_received() == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
 // ---- state getters ----------------------------------------------------------------
 static GraphState* graph(hgx_ctx* c, int32_t g) {
     if (!c || g < 0 || g >= c->G) return nullptr;
@@ -569,7 +583,7 @@ int32_t hgx_reset_stats(hgx_ctx* c) {
 
 int32_t hgx_set_kernel_timing(hgx_ctx* c, int32_t on) {
     if (!c) return HGX_ERR_INVALID;
-    c->eng.time_kernels = on != 0;
+    c->eng.time_mask = (uint32_t)on;
     return HGX_OK;
 }
 

@@ -167,7 +167,7 @@ DevArrays Engine::arrays() {
 // ---- per-kernel timing (only when time_kernels) ---------------------------------
 void Engine::kbeg(int k) {
     kstat[k].launches++;
-    if (!time_kernels) return;
+    if (!((time_mask >> k) & 1u)) return;
     while (kev.size() < kev_used + 2) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return;
@@ -180,7 +180,7 @@ void Engine::kbeg(int k) {
 
 void Engine::kend(int k, double bytes) {
     kstat[k].bytes += bytes;
-    if (!time_kernels || kopen.empty()) return;
+    if (!((time_mask >> k) & 1u) || kopen.empty()) return;
     Open& o = kopen.back();
     o.bytes = bytes;
     (void)hipEventRecord(kev[o.e0 + 1], stream);
@@ -381,6 +381,16 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[3] = ms;
     return collect_kernel_times();
+}
+
+hipError_t Engine::reset_received() {
+    if (E > 0) {
+        HGX_TRY(hipMemsetAsync(g_rr.p, 0xFF, (size_t)E * 4, stream));
+        HGX_TRY(hipMemsetAsync(g_cts.p, 0, (size_t)E * 8, stream));
+    }
+    E_div = 0;
+    R = 0;
+    return hipStreamSynchronize(stream);
 }
 
 // ---- getters --------------------------------------------------------------------

@@ -65,6 +65,7 @@ class Engine {
                           const std::vector<uint8_t>& ur_empty, OrderHost& out);
     const int32_t* pinned_order() const { return h_order; }
 
+    hipError_t reset_received();
     hipError_t get_rounds(std::vector<int32_t>& round_by_gid);
     hipError_t get_received(std::vector<int32_t>& rr, std::vector<int64_t>& cts);
     hipError_t get_coords(int64_t gid, int32_t* la, int32_t* fd);
@@ -76,7 +77,7 @@ class Engine {
     hipStream_t stream = nullptr;
     double phase_ms[4] = {0, 0, 0, 0};   // coordinates, rounds, fame, order (last calls)
     KernelStat kstat[K_NUM];
-    bool time_kernels = false;
+    uint32_t time_mask = 0;   // kernels (bit = KernelId) timed with HIP events
 
    private:
     hipError_t ensure_round_cap(int32_t need);

@@ -99,6 +99,12 @@ class Hashgraph:
         """node/core.go:277-303"""
         self._call(self.L.hgx_run_consensus)
 
+    def reset_consensus(self):
+        """Fresh consensus state over the same resident events (Bootstrap replay)."""
+        rc = self.L.hgx_reset_consensus(self.ctx)
+        if rc:
+            raise HgxError(rc, "hgx_reset_consensus failed")
+
     # ------------------------------------------------------------------ state (hashgraph.go:15-37)
     def UndecidedRounds(self, graph: int = 0) -> List[int]:
         k = self.L.hgx_undecided_rounds(self.ctx, graph, None, 0)
@@ -241,8 +247,18 @@ class Hashgraph:
             res[name.value.decode()] = dict(ms=ms.value, launches=launches.value, bytes=nbytes.value)
         return res
 
-    def set_kernel_timing(self, on: bool):
-        self.L.hgx_set_kernel_timing(self.ctx, 1 if on else 0)
+    KERNELS = ("layout", "la_sweep", "fd_build", "round_gather", "round_search", "fame", "threshold",
+               "round_received", "cts_median", "order_sort")
+
+    def set_kernel_timing(self, which=True):
+        """True = time every kernel launch with HIP events; a kernel name = only that one; False = off."""
+        if which is True:
+            mask = -1
+        elif not which:
+            mask = 0
+        else:
+            mask = 1 << self.KERNELS.index(which)
+        self.L.hgx_set_kernel_timing(self.ctx, mask)
 
     def reset_stats(self):
         self.L.hgx_reset_stats(self.ctx)

@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py -- consensus-ordered events/sec of the MI355X Hashgraph engine.
+
+Workload (BASELINE.json metric "consensus-ordered events/sec at N=256 peers"):
+one synthetic random-gossip hashgraph per GPU (configs[2]: 256 peers, 10M events,
+fits one MI355X), seeded per rank (weak scaling: independent replicas, no
+data-path collective -- DESIGN.md §6). A step = one full pass of the hot path over
+the HBM-resident trace: DivideRounds (coordinates + rounds), DecideFame,
+FindOrder (round-received, median timestamps, total order, blocks), ending with
+the order in host memory.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints one JSON line (rank 0) with roofline and cpu_baseline objects.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (n, events per graph, graphs per GPU, silent, stale_prob, stale_depth, description)
+    "c1": (4, 1024, 1, 0, 0.0, 1, "4 peers, 1,024 gossip events"),
+    "c2": (64, 1 << 20, 1, 0, 0.0, 1, "64 peers, 1,048,576 gossip events, one hashgraph"),
+    "c3": (256, 10_000_000, 1, 0, 0.0, 1, "256 peers, 10,000,000 gossip events, one hashgraph per GPU"),
+    "c4": (16, 16384, 512, 0, 0.0, 1, "512 independent 16-peer sims x 16,384 events per GPU (4096 over 8 GPUs)"),
+    "c5": (1024, 1 << 20, 1, 300, 0.3, 4, "1024 peers (300 silent, 30% stale other-parents), 1,048,576 events"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_trace(cfg, rank):
+    from babble_amd import trace
+    n, E, G, silent, stale, depth, _ = CONFIGS[cfg]
+    seeds = [1 + rank * G + g for g in range(G)]
+    if G == 1:
+        return trace.gossip(n, E, seeds[0], n_silent=silent, stale_prob=stale, stale_depth=depth), G
+    return trace.concat_graphs([trace.gossip(n, E, s, n_silent=silent, stale_prob=stale, stale_depth=depth)
+                                for s in seeds]), G
+
+
+def cpu_baseline(cfg, budget_s=20.0):
+    """The oracle (single-threaded C restatement of the reference loops) on a bounded
+    prefix of the same workload: consensus-ordered events / wall seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hgref
+    from babble_amd import trace
+    n, E, G, silent, stale, depth, _ = CONFIGS[cfg]
+    sample = min(E, {4: 1024, 16: 16384, 64: 60000, 256: 40000, 1024: 12000}.get(n, 20000))
+    t = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
+    o = hgref.Oracle(n)
+    t0 = time.perf_counter()
+    o.insert_trace(t)
+    o.divide_rounds()
+    o.decide_fame()
+    o.find_order()
+    dt = time.perf_counter() - t0
+    ordered = len(o.consensus_events())
+    return dict(value=ordered / dt, unit="consensus-ordered events/s", cores=1, kind="port",
+                sample=f"first {sample} events of the {CONFIGS[cfg][6]} trace (seed 1), oracle "
+                       f"InsertEvent+DivideRounds+DecideFame+FindOrder single-threaded, {ordered} events "
+                       f"ordered in {dt:.2f}s on {platform.processor() or platform.machine()}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    from babble_amd.hashgraph import Hashgraph
+    n, E, G, *_ = CONFIGS[args.config]
+    t0 = time.time()
+    tr, G = make_trace(args.config, rank)
+    log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
+    h = Hashgraph(n, capacity=tr.E, device=local_rank if dist is None else local_rank, n_graphs=G)
+    t0 = time.time()
+    h.insert_trace(tr)
+    log(f"[rank {rank}] inserted (host validation + H2D) in {time.time() - t0:.1f}s")
+
+    def step():
+        h.reset_consensus()
+        h.DivideRounds()
+        h.DecideFame()
+        h.FindOrder()
+        return sum(int(h.L.hgx_consensus_events_count(h.ctx, g)) for g in range(G))
+
+    # warmup: also profiles every kernel to pick the dominant one
+    h.set_kernel_timing(True)
+    h.reset_stats()
+    ordered = 0
+    for w in range(max(1, args.warmup)):
+        tw = time.time()
+        ordered = step()
+        log(f"[rank {rank}] warmup {w}: {ordered} ordered in {time.time() - tw:.2f}s  {h.phase_times()}")
+    ks = h.kernel_stats()
+    dom = max(ks, key=lambda k: ks[k]["ms"])
+    log(f"[rank {rank}] kernel profile (warmup): " +
+        ", ".join(f"{k}={v['ms']:.1f}ms/{v['launches']}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1]['ms'])))
+    # roofline is reported for the dominant HBM-streaming kernel
+    hbm_kernels = ("la_sweep", "fd_build", "cts_median", "round_received", "order_sort", "layout")
+    roof_k = max(hbm_kernels, key=lambda k: ks.get(k, {"ms": 0})["ms"])
+
+    # timed region: only the roofline kernel is instrumented (HIP events on the context stream)
+    h.set_kernel_timing(roof_k)
+    h.reset_stats()
+    barrier()
+    t_start = time.perf_counter()   # every hgx call returns with its work complete (order in host memory)
+    total = 0
+    for _ in range(args.steps):
+        total += step()
+    t_el = time.perf_counter() - t_start
+    barrier()
+    t_max = max_over_ranks(t_el)
+    total_all = sum_over_ranks(total)
+    ks = h.kernel_stats()
+    phases = h.phase_times()
+
+    result = None
+    if rank == 0:
+        r = ks.get(roof_k, {"ms": 0, "launches": 0, "bytes": 0})
+        avg_ms = r["ms"] / max(1, r["launches"])
+        per_launch_bytes = r["bytes"] / max(1, r["launches"])
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get(roof_k)
+            except Exception:
+                traffic = None
+        result = {
+            "metric": "consensus-ordered events/sec at N=256 peers (1 GPU and 8-GPU batched sims)",
+            "value": total_all / t_max,
+            "unit": "consensus-ordered events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded random-gossip traces, synthetic event ids/signatures)",
+            "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
+                       "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
+                       "ordered_events_per_step_per_gpu": int(total // max(1, args.steps)),
+                       "parallelism": f"replicas x{world} (seed-sharded)",
+                       "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
+                       "dominant_kernel": dom},
+            "roofline": {"kernel": roof_k, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                result["cpu_baseline"] = cpu_baseline(args.config)
+            except Exception as e:  # reported, never fatal
+                result["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,6 +96,10 @@ int32_t hgx_decide_fame(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_find_order(hgx_ctx* ctx, hgx_error* err);
 /* Core.RunConsensus (node/core.go:277-303): the three calls in sequence */
 int32_t hgx_run_consensus(hgx_ctx* ctx, hgx_error* err);
+/* Forget every consensus result but keep the inserted events resident in HBM:
+ * the state of a fresh NewHashgraph after InsertEvent of the same events
+ * (Bootstrap replay, hashgraph.go:1008-1022). Used to repeat timed passes. */
+int32_t hgx_reset_consensus(hgx_ctx* ctx);
 
 /* ---- Hashgraph state (hashgraph.go:15-37) --------------------------------- */
 int64_t hgx_num_events(hgx_ctx* ctx);
@@ -154,8 +158,8 @@ int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 int32_t hgx_kernel_stats(hgx_ctx* ctx, int32_t k, char* name, int32_t name_cap, double* ms, int64_t* launches,
                          double* bytes);
 int32_t hgx_reset_stats(hgx_ctx* ctx);
-/* time every kernel launch with HIP events on the context stream (bench.py roofline) */
-int32_t hgx_set_kernel_timing(hgx_ctx* ctx, int32_t on);
+/* time the kernels in bitmask `mask` (bit k = kernel id of hgx_kernel_stats; -1 = all) with HIP events on the context stream (bench.py roofline) */
+int32_t hgx_set_kernel_timing(hgx_ctx* ctx, int32_t mask);
 
 /* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
 /* Seeded random gossip modelled on node/core_test.go:514-537: every active peer

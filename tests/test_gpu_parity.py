@@ -36,7 +36,7 @@ def block_hashes_gpu(h, t, graph=0):
     for b in h.Blocks(graph):
         txs = []
         for g in order[b["first"]:b["first"] + b["n_events"]]:
-            txs.extend(t.txs(int(g)) if callable(getattr(t, "txs", None)) else (t.txs[int(g)] or []))
+            txs.extend((t.txs(int(g)) if callable(getattr(t, "txs", None)) else t.txs[int(g)]) or [])
         out.append(block_hash(b["rr"], txs, b["tx_nil"]))
     return out
 
