@@ -62,8 +62,11 @@ Engine::~Engine() {
     for (auto e : kev) (void)hipEventDestroy(e);
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
+    for (auto e : flag_ev)
+        if (e) (void)hipEventDestroy(e);
     if (h_order) (void)hipHostFree(h_order);
     if (h_small) (void)hipHostFree(h_small);
+    drop_step_graph();
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -105,10 +108,15 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(LA.alloc(P * n));
     HGX_TRY(FDT.alloc(P * n));
     HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(4)); HGX_TRY(order_gid.alloc(P));
+    HGX_TRY(p_new.alloc(P));
+    HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
     HGX_TRY(minmax.alloc(2));
     HGX_TRY(lr.alloc(G));
+    HGX_TRY(d_round.alloc(1));
+    HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
+    HGX_TRY(hipEventCreateWithFlags(&flag_ev[1], hipEventDisableTiming));
     HGX_TRY(hipHostMalloc((void**)&h_order, P * sizeof(int32_t), hipHostMallocDefault));
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
     // rounds: initial guess, grown on demand
@@ -127,6 +135,8 @@ hipError_t Engine::ensure_round_cap(int32_t need) {
     HGX_TRY(WLA.grow_copy((size_t)nc * Cz * n, (size_t)old * Cz * n, stream));
     HGX_TRY(WFD.grow_copy((size_t)nc * Cz * n, (size_t)old * Cz * n, stream));
     HGX_TRY(wflag.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
+    HGX_TRY(wstat.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
+    drop_step_graph();
     HGX_TRY(wcoin.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
     HGX_TRY(active.grow_copy((size_t)nc + 1, (size_t)old + 1, stream));
     HGX_TRY(Tthr.grow_copy((size_t)nc * Cz, 0, stream));
@@ -153,11 +163,12 @@ DevArrays Engine::arrays() {
     a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
     a.LA = LA.p; a.FDT = FDT.p;
-    a.Bm = Bm.p; a.wflag = wflag.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p;
+    a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p;
+    a.d_round = d_round.p;
     a.active = active.p; a.lr = lr.p;
     a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
     a.elig = elig.p; a.fw = fw.p; a.ur_empty = ur_empty.p; a.T = Tthr.p;
-    a.recv_list = recv_list.p; a.counters = counters.p;
+    a.recv_list = recv_list.p; a.counters = counters.p; a.p_new = p_new.p; a.scan_part = scan_part.p;
     a.key_a = key_a.p; a.key_b = key_b.p; a.val_a = val_a.p; a.val_b = val_b.p; a.hist = hist.p;
     a.minmax = minmax.p; a.order_gid = order_gid.p;
     a.blk_cnt = blk_cnt.p; a.blk_loaded = blk_loaded.p; a.blk_ntx = blk_ntx.p;
@@ -266,25 +277,71 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemsetAsync(lr.p, 0xFF, (size_t)G * 4, stream));
     HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
     HGX_TRY(hipMemsetAsync(active.p, 0, (size_t)(r_cap + 1) * 4, stream));
-    const int kBatch = 8;
+    kbeg(K_ROUND_GATHER);
+    launch_round_gather(stream, a, 0, C, n, cap);   // W'_0 = first event of every chain
+    kend(K_ROUND_GATHER, (double)C * n * 16);
     int r = 0;
-    for (;;) {
-        if (r + kBatch + 1 > r_cap) {
-            HGX_TRY(ensure_round_cap(r + kBatch + 1));
-            a = arrays();
-        }
-        for (int k = 0; k < kBatch; k++) {
-            kbeg(K_ROUND_GATHER);
-            launch_round_gather(stream, a, r + k, C, n, cap);
-            kend(K_ROUND_GATHER, (double)C * n * 16);
+    if (n <= 256) {
+        // fused steps: kStepBatch step nodes (round = base + k) + one node advancing the
+        // device-resident base, replayed as one hipGraph; batch i+1 is queued before
+        // the host looks at batch i's "any candidate left" flag (pipelined check)
+        HGX_TRY(hipMemsetAsync(d_round.p, 0, 4, stream));
+        int launched = 0, checked = 0;
+        auto launch_batch = [&]() -> hipError_t {
+            const int need = (launched + 2) * kStepBatch + 2;
+            if (need > r_cap) {
+                HGX_TRY(ensure_round_cap(need));
+                a = arrays();
+            }
+            if (!step_exec) {
+                HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+                for (int k = 0; k < kStepBatch; k++) launch_round_step(stream, a, k, C, n, sm, cap);
+                launch_advance_round(stream, a, kStepBatch);
+                HGX_TRY(hipStreamEndCapture(stream, &step_graph));
+                HGX_TRY(hipGraphInstantiate(&step_exec, step_graph, nullptr, nullptr, 0));
+            }
             kbeg(K_ROUND_SEARCH);
-            launch_round_search(stream, a, r + k, C, n, sm);
+            HGX_TRY(hipGraphLaunch(step_exec, stream));
             kend(K_ROUND_SEARCH, 0);
+            const int slot = launched & 1;
+            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + ((launched + 1) * kStepBatch - 1), 4,
+                                   hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipEventRecord(flag_ev[slot], stream));
+            launched++;
+            return hipSuccess;
+        };
+        HGX_TRY(launch_batch());
+        HGX_TRY(launch_batch());
+        for (;;) {
+            HGX_TRY(hipEventSynchronize(flag_ev[checked & 1]));
+            const int more = h_small[checked & 1];
+            checked++;
+            if (!more) break;
+            HGX_TRY(launch_batch());
         }
-        r += kBatch;
-        HGX_TRY(hipMemcpyAsync(h_small, active.p + (r - 1), 4, hipMemcpyDeviceToHost, stream));
-        HGX_TRY(hipStreamSynchronize(stream));
-        if (h_small[0] == 0) break;
+        r = launched * kStepBatch;
+    } else {
+        const int kBatch = 8;
+        for (;;) {
+            if (r + kBatch + 1 > r_cap) {
+                HGX_TRY(ensure_round_cap(r + kBatch + 1));
+                a = arrays();
+            }
+            for (int k = 0; k < kBatch; k++) {
+                if (r + k > 0) {
+                    kbeg(K_ROUND_GATHER);
+                    launch_round_gather(stream, a, r + k, C, n, cap);
+                    kend(K_ROUND_GATHER, (double)C * n * 16);
+                }
+                kbeg(K_ROUND_SEARCH);
+                launch_round_search(stream, a, r + k, C, n, sm);
+                kend(K_ROUND_SEARCH, 0);
+            }
+            r += kBatch;
+            HGX_TRY(hipMemcpyAsync(h_small, active.p + (r - 1), 4, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+            if (h_small[0] == 0) break;
+        }
     }
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
@@ -296,7 +353,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
     HGX_TRY(hipMemcpyAsync(out.bm.data(), Bm.p, out.bm.size() * 4, hipMemcpyDeviceToHost, stream));
-    if (R) HGX_TRY(hipMemcpyAsync(out.wflag.data(), wflag.p, out.wflag.size(), hipMemcpyDeviceToHost, stream));
+    if (R) HGX_TRY(hipMemcpyAsync(out.wflag.data(), wstat.p, out.wflag.size(), hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
@@ -339,6 +396,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     launch_threshold(stream, a, R, C, n);
     kend(K_THRESHOLD, 0);
     HGX_TRY(hipMemsetAsync(counters.p, 0, 8, stream));
+    HGX_TRY(hipMemsetAsync(p_new.p, 0, (size_t)E_div, stream));
     kbeg(K_ROUND_RECEIVED);
     launch_round_received(stream, a, E_div, R, C, n);
     kend(K_ROUND_RECEIVED, (double)E_div * 16);
@@ -349,7 +407,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     out.m = m;
     if (out.panic || m == 0) return collect_kernel_times();
     kbeg(K_CTS);
-    launch_cts(stream, a, m, C, n, cap);
+    launch_cts(stream, a, E_div, C, n, cap);
     kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
     // sort keys: cts range, then (graph, rr)
     const unsigned long long init[2] = {~0ull, 0ull};
@@ -420,4 +478,13 @@ hipError_t Engine::get_coords(int64_t gid, int32_t* la, int32_t* fd) {
     return hipStreamSynchronize(stream);
 }
 
+}  // namespace hgx
+
+namespace hgx {
+void Engine::drop_step_graph() {
+    if (step_exec) (void)hipGraphExecDestroy(step_exec);
+    if (step_graph) (void)hipGraphDestroy(step_graph);
+    step_exec = nullptr;
+    step_graph = nullptr;
+}
 }  // namespace hgx

@@ -12,6 +12,8 @@
 
 namespace hgx {
 
+constexpr int kStepBatch = 16;   // fused round steps per hipGraph replay
+
 enum KernelId {
     K_LAYOUT = 0, K_LA_SWEEP, K_FD_BUILD, K_ROUND_GATHER, K_ROUND_SEARCH, K_FAME, K_THRESHOLD,
     K_ROUND_RECEIVED, K_CTS, K_SORT, K_NUM
@@ -102,12 +104,18 @@ class Engine {
     DBuf<int32_t> LA, FDT;
     // per round
     int32_t r_cap = 0;
-    DBuf<int32_t> Bm, WLA, WFD, Tthr, active, lr;
-    DBuf<uint8_t> wflag, wcoin, elig, fw, ur_empty;
+    DBuf<int32_t> Bm, WLA, WFD, Tthr, active, lr, d_round;
+    hipEvent_t flag_ev[2] = {nullptr, nullptr};
+    DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
+    hipGraph_t step_graph = nullptr;       // kStepBatch fused round steps, replayed per batch
+    hipGraphExec_t step_exec = nullptr;
+    void drop_step_graph();
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<int8_t> fame;
     // order
     DBuf<int32_t> recv_list, counters, order_gid, blk_cnt, blk_loaded;
+    DBuf<uint8_t> p_new;
+    DBuf<uint32_t> scan_part;
     DBuf<uint64_t> key_a, key_b;
     DBuf<uint32_t> val_a, val_b, hist;
     DBuf<int64_t> minmax, blk_ntx;

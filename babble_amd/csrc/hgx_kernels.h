@@ -26,7 +26,8 @@ struct DevArrays {
     int32_t *LA, *FDT;
     // rounds
     int32_t* Bm;
-    uint8_t *wflag, *wcoin;
+    uint8_t *wflag, *wstat, *wcoin;   // wflag: candidate of round r exists; wstat: 2 witness, 1 jumped, 0 none
+    int32_t* d_round;     // device round base of the current step batch
     int32_t *WLA, *WFD;
     int32_t *active, *lr;
     // fame
@@ -36,6 +37,8 @@ struct DevArrays {
     uint8_t *elig, *fw, *ur_empty;
     int32_t* T;
     int32_t* recv_list;
+    uint8_t* p_new;       // [P] received by the current FindOrder
+    uint32_t* scan_part;  // scan partials
     int32_t* counters;   // [0] received count, [1] panic flag, [2] LA changed
     // order
     uint64_t *key_a, *key_b;
@@ -53,10 +56,13 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
 void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm);
+// fused step (n <= 256, hgx_rounds.hip): round = *a.d_round + kstep; false if n is unsupported
+bool launch_round_step(hipStream_t s, const DevArrays& a, int kstep, int C, int n, int sm, int64_t P);
+void launch_advance_round(hipStream_t s, const DevArrays& a, int by);
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
-void launch_cts(hipStream_t s, const DevArrays& a, int32_t m, int C, int n, int64_t P);
+void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P);
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);

@@ -11,15 +11,11 @@
 
 #include <cstdint>
 
+#include "hgx_device.h"
 #include "hgx_kernels.h"
 
 namespace hgx {
 
-__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
-
-__device__ __forceinline__ uint64_t group_mask(int gs, int grp) {
-    return (gs >= 64) ? ~0ull : (((1ull << gs) - 1ull) << (gs * grp));
-}
 
 // ---------------------------------------------------------------------------------
 // layout: gid order -> chain-major positions
@@ -132,9 +128,22 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
     const int ld = n + 1;
     for (int i = threadIdx.x; i < n; i += blockDim.x)
         sm[i] = (k0 > 0) ? LA[(size_t)(off + k0 - 1) * n + i] : -2147483647 - 1;
-    for (int idx = threadIdx.x; idx < rows * n; idx += blockDim.x) {
-        const int r = idx / n, i = idx % n;
-        sm[(r + 1) * ld + i] = LA[(size_t)(off + k0 + r) * n + i];
+    {   // the tile's rows are contiguous in LA: 4 independent loads in flight per thread
+        const int32_t* __restrict__ src = LA + (size_t)(off + k0) * n;
+        const int nel = rows * n;
+        for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * blockDim.x) {
+            int32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * blockDim.x;
+                v[u] = (t < nel) ? src[t] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * blockDim.x;
+                if (t < nel) sm[(t / n + 1) * ld + (t % n)] = v[u];
+            }
+        }
     }
     __syncthreads();
     const bool last = (k1 == len);
@@ -195,9 +204,9 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
 template <int GS, int CPL, bool FD_LDS>
 __global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
                                const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA,
-                               const int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag,
-                               int32_t* __restrict__ p_round, int32_t* __restrict__ active,
-                               int32_t* __restrict__ lr, int C, int n, int sm) {
+                               const int32_t* __restrict__ WFD, const uint8_t* __restrict__ wflag,
+                               uint8_t* __restrict__ wstat, int32_t* __restrict__ p_round,
+                               int32_t* __restrict__ active, int32_t* __restrict__ lr, int C, int n, int sm) {
     extern __shared__ __attribute__((aligned(16))) int32_t fds[];  // [ncand x n] when FD_LDS
     __shared__ int32_t cand[1024];
     __shared__ int32_t s_ncand, s_first;
@@ -206,7 +215,10 @@ __global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict
     const int len = c_len[gc];
     const int b = Bm[(size_t)r * C + gc];
     if (b >= len) {
-        if (threadIdx.x == 0) Bm[(size_t)(r + 1) * C + gc] = len;
+        if (threadIdx.x == 0) {
+            Bm[(size_t)(r + 1) * C + gc] = len;
+            wstat[(size_t)r * C + gc] = 0;
+        }
         return;
     }
     if (threadIdx.x == 0) { s_ncand = 0; s_first = 0x7fffffff; }
@@ -262,7 +274,7 @@ __global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict
     }
     if (threadIdx.x == 0) {
         Bm[(size_t)(r + 1) * C + gc] = kstar;
-        wflag[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
+        wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
         if (kstar < len) atomicOr(&active[r], 1);
         if (kstar > b) atomicMax(&lr[g], r);
     }
@@ -272,12 +284,12 @@ __global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict
 // ---------------------------------------------------------------------------------
 // fame. S_j[y] = { w in W_{j-1} : StronglySee(y, w) } as bit masks (one wave per y).
 template <int GS, int CPL, int NW>
-__global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restrict__ wflag, const int32_t* __restrict__ WLA,
+__global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restrict__ wstat, const int32_t* __restrict__ WLA,
                           const int32_t* __restrict__ WFD, uint64_t* __restrict__ Smat, int C, int n, int sm) {
     const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // (r-1)*C + gc
     if (item >= (int64_t)(R - 1) * C) return;
     const int r = (int)(item / C) + 1, gc = (int)(item % C);
-    if (wflag[(size_t)r * C + gc] != 2) return;
+    if (wstat[(size_t)r * C + gc] != 2) return;
     const int g = gc / n;
     const int lane = lane_id(), gl = lane % GS, grp_w = lane / GS;
     const int ngw = 64 / GS;
@@ -294,7 +306,7 @@ __global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restric
     const size_t prev = (size_t)(r - 1) * C + (size_t)g * n;
     for (int wb = 0; wb < n; wb += ngw) {
         const int w = wb + grp_w;
-        const bool ok = (w < n) && wflag[prev + w] == 2;
+        const bool ok = (w < n) && wstat[prev + w] == 2;
         int tot = 0;
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
@@ -321,13 +333,14 @@ __global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restric
 // (graph g, round i). Votes V[x] are bit masks over the witnesses of the previous
 // round; yays = popcount(S_j[y] & V[x]). Ties vote yes; coin rounds use middleBit.
 __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t* __restrict__ lr,
-                            const uint8_t* __restrict__ wflag, const uint8_t* __restrict__ wcoin,
+                            const uint8_t* __restrict__ wstat, const uint8_t* __restrict__ wcoin,
                             const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
                             const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
                             uint64_t* __restrict__ Vbuf, int8_t* __restrict__ fame, int C, int n, int sm) {
     __shared__ int32_t xs[1024];
     __shared__ int32_t dec[1024];
     __shared__ int32_t s_nx, s_und;
+    __shared__ unsigned long long wm[16];   // witnesses of round j-1 (S rows may cover jumped candidates)
     const int g = blockIdx.x / R, i = blockIdx.x % R;
     const int LR = lr[g];
     if (i > LR) return;
@@ -335,7 +348,7 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
     if (threadIdx.x == 0) s_nx = 0;
     __syncthreads();
     for (int c = threadIdx.x; c < n; c += blockDim.x)
-        if (wflag[(size_t)i * C + gi + c] == 2) xs[atomicAdd(&s_nx, 1)] = c;
+        if (wstat[(size_t)i * C + gi + c] == 2) xs[atomicAdd(&s_nx, 1)] = c;
     __syncthreads();
     const int nx = s_nx;
     for (int x = threadIdx.x; x < nx; x += blockDim.x) dec[x] = 0;
@@ -356,7 +369,7 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
         for (int bb = 0; bb < 64; bb++) {
             const int y = wd * 64 + bb;
             if (y >= n) break;
-            if (wflag[(size_t)(i + 1) * C + gi + y] != 2) continue;
+            if (wstat[(size_t)(i + 1) * C + gi + y] != 2) continue;
             if (WLA[((size_t)(i + 1) * C + gi + y) * n + xc] >= xidx) bits |= 1ull << bb;
         }
         V0[(size_t)x * nw + wd] = bits;
@@ -367,6 +380,11 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
     for (int j = i + 2; j <= LR; j++) {
         const bool normal = ((j - i) % n) != 0;
         const size_t jr = (size_t)j * C + gi;
+        for (int k = threadIdx.x; k < nw; k += blockDim.x) wm[k] = 0;
+        __syncthreads();
+        for (int c = threadIdx.x; c < n; c += blockDim.x)
+            if (wstat[(size_t)(j - 1) * C + gi + c] == 2) atomicOr(&wm[c >> 6], 1ull << (c & 63));
+        __syncthreads();
         for (int t = threadIdx.x; t < nx * nw; t += blockDim.x) {
             const int x = t / nw, wd = t % nw;
             if (dec[x] != 0) continue;
@@ -374,10 +392,10 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
             for (int bb = 0; bb < 64; bb++) {
                 const int y = wd * 64 + bb;
                 if (y >= n) break;
-                if (wflag[jr + y] != 2) continue;
+                if (wstat[jr + y] != 2) continue;
                 int yays = 0, tot = 0;
                 for (int k = 0; k < nw; k++) {
-                    const uint64_t s = Smat[(jr + y) * nw + k];
+                    const uint64_t s = Smat[(jr + y) * nw + k] & wm[k];
                     tot += __popcll(s);
                     yays += __popcll(s & Vc[(size_t)x * nw + k]);
                 }
@@ -460,7 +478,8 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
                                  const int32_t* __restrict__ p_round, const int32_t* __restrict__ lr,
                                  const uint8_t* __restrict__ elig, const uint8_t* __restrict__ ur_empty,
                                  const int32_t* __restrict__ T, int32_t* __restrict__ p_rr,
-                                 int32_t* __restrict__ recv_list, int32_t* __restrict__ counters, int C, int n) {
+                                 uint8_t* __restrict__ p_new, int32_t* __restrict__ recv_list,
+                                 int32_t* __restrict__ counters, int C, int n) {
     __shared__ int32_t s_cnt, s_base;
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
@@ -478,6 +497,7 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
         }
         if (rr >= 0) {
             p_rr[p] = rr;
+            p_new[p] = 1;
             slot = atomicAdd(&s_cnt, 1);
         }
     }
@@ -541,6 +561,96 @@ __global__ void __launch_bounds__(256) k_cts(int32_t m, const int32_t* __restric
     if (lane == 0) p_cts[p] = res;
 }
 
+// Tiled consensus timestamp. A block owns T consecutive positions (one chain
+// mostly). Phase A, lanes = events: for each witness chain c, FDT[c][p0..p0+T) is a
+// coalesced read and the timestamp gathers p_ts[pos(c, FD)] hit a few adjacent
+// lines (FD is monotone along a chain); values go to LDS as vals[e][c] (+inf when
+// the famous witness of chain c does not see the event). Phase B: one wave per
+// event bitonic-sorts its NPAD values in LDS and takes element floor(|s|/2).
+
+template <int NPAD, int T>
+__global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
+                                                  const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+                                                  const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
+                                                  const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLA,
+                                                  const int32_t* __restrict__ FDT, const int64_t* __restrict__ p_ts,
+                                                  int64_t* __restrict__ p_cts, int C, int n, int64_t P) {
+    extern __shared__ __attribute__((aligned(16))) int64_t vals[];   // [T][NPAD+1]
+    __shared__ int32_t cnt[T];
+    __shared__ int32_t s_any;
+    constexpr int LD = NPAD + 1;
+    constexpr int NCG = 256 / T;
+    const int64_t p0 = (int64_t)blockIdx.x * T;
+    const int e = threadIdx.x % T, cg = threadIdx.x / T;
+    const int64_t p = p0 + e;
+    const bool valid = p < Pn && p_new[p];
+    if (threadIdx.x == 0) s_any = 0;
+    if (threadIdx.x < T) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (valid) s_any = 1;
+    __syncthreads();
+    if (!s_any) return;
+    int g = 0, dl = 0, j = 0, i = 0;
+    if (valid) {
+        const int gc = p_chain[p];
+        g = gc / n;
+        dl = gc % n;
+        j = c_base[gc] + (int)(p - c_off[gc]);
+        i = p_rr[p];
+    }
+    const size_t base = (size_t)i * C + (size_t)g * n;
+    int mycnt = 0;
+    constexpr int U = 4;   // chains per batch: issue all independent loads, then the dependent gathers
+    for (int c0 = cg; c0 < NPAD; c0 += NCG * U) {
+        bool mem[U];
+        int32_t fdv[U], pb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = c0 + u * NCG;
+            mem[u] = false;
+            fdv[u] = 0;
+            pb[u] = 0;
+            if (valid && c < n) {
+                const int ch = g * n + c;
+                mem[u] = fw[base + c] && WLA[(base + c) * n + dl] >= j;
+                fdv[u] = FDT[(size_t)c * P + p];
+                pb[u] = c_off[ch] - c_base[ch];
+            }
+        }
+        int64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = mem[u] ? p_ts[pb[u] + fdv[u]] : 0x7fffffffffffffffLL;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = c0 + u * NCG;
+            if (c < NPAD) vals[e * LD + c] = v[u];
+            mycnt += mem[u] ? 1 : 0;
+        }
+    }
+    if (mycnt) atomicAdd(&cnt[e], mycnt);
+    __syncthreads();
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    for (int ee = wave; ee < T; ee += 4) {
+        const int64_t pe = p0 + ee;
+        if (pe >= Pn || !p_new[pe]) continue;   // wave-uniform
+        int64_t* col = vals + ee * LD;
+        for (int k = 2; k <= NPAD; k <<= 1) {
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                for (int t = lane; t < NPAD / 2; t += 64) {
+                    const int i1 = (t / jj) * (jj << 1) + (t % jj);
+                    const int i2 = i1 + jj;
+                    const bool up = (i1 & k) == 0;
+                    const int64_t a = col[i1], bb = col[i2];
+                    if ((a > bb) == up) { col[i1] = bb; col[i2] = a; }
+                }
+                wave_lds_fence();
+            }
+        }
+        if (lane == 0) p_cts[pe] = col[cnt[ee] / 2];
+        wave_lds_fence();
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // order: LSD radix sort (8-bit digits) of (u64 key, u32 value), stable.
 constexpr int kSortThreads = 256;
@@ -560,26 +670,71 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* __r
     hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of `total` u32 in place, single block of 1024 threads
-__global__ void __launch_bounds__(1024) k_scan_u32(uint32_t* __restrict__ a, int64_t total) {
-    __shared__ uint32_t part[1024];
-    const int64_t chunk = (total + 1023) / 1024;
-    const int64_t lo = threadIdx.x * chunk, hi = min(total, lo + chunk);
-    uint32_t s = 0;
-    for (int64_t k = lo; k < hi; k++) s += a[k];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const uint32_t v = (threadIdx.x >= (unsigned)d) ? part[threadIdx.x - d] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
+// exclusive scan of `total` u32 in place: per-2048 chunk sums, scan of the sums in
+// one block, then per-chunk rescan with the chunk offset.
+constexpr int kScanChunk = 2048;
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh, uint32_t* total) {
+    // 256 threads: wave-level inclusive scan by shuffles, then wave totals
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    uint32_t run = part[threadIdx.x] - s;
-    for (int64_t k = lo; k < hi; k++) {
-        const uint32_t x = a[k];
-        a[k] = run;
-        run += x;
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < wave; w++) wbase += sh[w];
+    *total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return wbase + x - v;
+}
+
+__global__ void __launch_bounds__(256) k_scan_reduce(const uint32_t* __restrict__ a, int64_t total,
+                                                     uint32_t* __restrict__ part) {
+    __shared__ uint32_t sh[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+    uint32_t s = 0;
+    for (int k = threadIdx.x; k < kScanChunk; k += 256)
+        if (base + k < total) s += a[base + k];
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane_id() == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void __launch_bounds__(256) k_scan_top(uint32_t* __restrict__ part, int nparts) {
+    __shared__ uint32_t sh[4];
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nparts; b0 += 256) {
+        const int k = b0 + threadIdx.x;
+        const uint32_t v = (k < nparts) ? part[k] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan256(v, sh, &tot);
+        if (k < nparts) part[k] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ a, int64_t total,
+                                                   const uint32_t* __restrict__ part) {
+    __shared__ uint32_t sh[4];
+    constexpr int IT = kScanChunk / 256;
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * IT;
+    uint32_t v[IT];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        v[k] = (base + k < total) ? a[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = part[blockIdx.x] + block_excl_scan256(s, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        if (base + k < total) a[base + k] = run;
+        run += v[k];
     }
 }
 
@@ -645,18 +800,28 @@ __global__ void k_keys_seg(int32_t m, const uint32_t* __restrict__ vals, const i
     keys[i] = (uint64_t)(p_chain[p] / n) * (uint64_t)R + (uint64_t)p_rr[p];
 }
 
-__global__ void k_minmax_cts(int32_t m, const int32_t* __restrict__ list, const int64_t* __restrict__ p_cts,
-                             unsigned long long* __restrict__ mm) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t v = (i < m) ? p_cts[list[i]] : 0;
-    // bias to unsigned order
-    unsigned long long u = (unsigned long long)v ^ 0x8000000000000000ull;
-    unsigned long long lo = (i < m) ? u : ~0ull, hi = (i < m) ? u : 0ull;
+// grid-stride min/max of the received events' timestamps (biased to unsigned order);
+// one atomic pair per block
+__global__ void __launch_bounds__(256) k_minmax_cts(int32_t m, const int32_t* __restrict__ list,
+                                                    const int64_t* __restrict__ p_cts,
+                                                    unsigned long long* __restrict__ mm) {
+    __shared__ unsigned long long slo[4], shi[4];
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const unsigned long long u = (unsigned long long)p_cts[list[i]] ^ 0x8000000000000000ull;
+        lo = min(lo, u);
+        hi = max(hi, u);
+    }
     for (int o = 32; o >= 1; o >>= 1) {
         lo = min(lo, (unsigned long long)__shfl_xor(lo, o));
         hi = max(hi, (unsigned long long)__shfl_xor(hi, o));
     }
-    if (lane_id() == 0 && i - lane_id() < m) {
+    if (lane_id() == 0) { slo[threadIdx.x >> 6] = lo; shi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) { lo = min(lo, slo[w]); hi = max(hi, shi[w]); }
+        lo = min(lo, slo[0]);
+        hi = max(hi, shi[0]);
         atomicMin(&mm[0], lo);
         atomicMax(&mm[1], hi);
     }
@@ -703,16 +868,38 @@ __global__ void k_finish_order(int32_t m, const uint32_t* __restrict__ vals, con
                                int32_t* __restrict__ blk_cnt, int64_t* __restrict__ blk_ntx,
                                int32_t* __restrict__ blk_loaded) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const int p = (int)vals[i];
-    const int gid = p_gid[p];
-    order_gid[i] = gid;
-    g_rr[gid] = p_rr[p];
-    g_cts[gid] = p_cts[p];
-    const size_t b = (size_t)(p_chain[p] / n) * R + p_rr[p];
-    atomicAdd(&blk_cnt[b], 1);
-    if (g_ntx[gid]) atomicAdd((unsigned long long*)&blk_ntx[b], (unsigned long long)g_ntx[gid]);
-    if (g_loaded[gid]) atomicAdd(&blk_loaded[b], 1);
+    const bool ok = i < m;
+    int64_t b = -1;
+    int cnt = 0, ntx = 0, ld = 0;
+    if (ok) {
+        const int p = (int)vals[i];
+        const int gid = p_gid[p];
+        order_gid[i] = gid;
+        g_rr[gid] = p_rr[p];
+        g_cts[gid] = p_cts[p];
+        b = (int64_t)(p_chain[p] / n) * R + p_rr[p];
+        cnt = 1;
+        ntx = g_ntx[gid];
+        ld = g_loaded[gid] ? 1 : 0;
+    }
+    // the order is sorted by (graph, rr): most waves hit one block -> one atomic per wave
+    const int64_t b0 = __shfl(b, 0);
+    if (__all(!ok || b == b0)) {
+        for (int o = 32; o >= 1; o >>= 1) {
+            cnt += __shfl_xor(cnt, o);
+            ntx += __shfl_xor(ntx, o);
+            ld += __shfl_xor(ld, o);
+        }
+        if (lane_id() == 0 && b0 >= 0) {
+            atomicAdd(&blk_cnt[b0], cnt);
+            if (ntx) atomicAdd((unsigned long long*)&blk_ntx[b0], (unsigned long long)ntx);
+            if (ld) atomicAdd(&blk_loaded[b0], ld);
+        }
+    } else if (ok) {
+        atomicAdd(&blk_cnt[b], 1);
+        if (ntx) atomicAdd((unsigned long long*)&blk_ntx[b], (unsigned long long)ntx);
+        if (ld) atomicAdd(&blk_loaded[b], 1);
+    }
 }
 
 __global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const int32_t* __restrict__ g_pos,
@@ -785,10 +972,10 @@ void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n,
         if (n <= 128) {                                                                                       \
             const size_t lds = (size_t)n * n * sizeof(int32_t);                                               \
             hipLaunchKernelGGL((k_round_search<GS, CPL, true>), dim3(C), dim3(256), lds, s, r, a.Bm, a.c_off, \
-                               a.c_len, a.LA, a.WFD, a.wflag, a.p_round, a.active, a.lr, C, n, sm);           \
+                               a.c_len, a.LA, a.WFD, a.wflag, a.wstat, a.p_round, a.active, a.lr, C, n, sm);  \
         } else {                                                                                              \
             hipLaunchKernelGGL((k_round_search<GS, CPL, false>), dim3(C), dim3(256), 0, s, r, a.Bm, a.c_off,  \
-                               a.c_len, a.LA, a.WFD, a.wflag, a.p_round, a.active, a.lr, C, n, sm);           \
+                               a.c_len, a.LA, a.WFD, a.wflag, a.wstat, a.p_round, a.active, a.lr, C, n, sm);  \
         }                                                                                                     \
     }
     HGX_DISPATCH_N(n, RS_LAUNCH);
@@ -796,17 +983,17 @@ void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n,
 }
 
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G) {
-    if (R > 1) {
+    if (R > 1 && n > 256) {   // n <= 256: S rows were produced by the fused round step
 #define SS_LAUNCH(GS, CPL, NW)                                                                                \
     {                                                                                                         \
         const int64_t threads = (int64_t)(R - 1) * C * 64;                                                    \
-        hipLaunchKernelGGL((k_fame_ss<GS, CPL, NW>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.wflag,  \
+        hipLaunchKernelGGL((k_fame_ss<GS, CPL, NW>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.wstat,  \
                            a.WLA, a.WFD, a.Smat, C, n, sm);                                                   \
     }
         HGX_DISPATCH_N(n, SS_LAUNCH);
 #undef SS_LAUNCH
     }
-    hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wflag, a.wcoin, a.Bm,
+    hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wstat, a.wcoin, a.Bm,
                        a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
 }
 
@@ -825,31 +1012,52 @@ void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n) {
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n) {
     if (Pn <= 0) return;
     hipLaunchKernelGGL(k_round_received, dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, R, a.p_chain, a.c_off, a.c_base,
-                       a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.recv_list, a.counters, C, n);
+                       a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.p_new, a.recv_list, a.counters, C, n);
 }
 
-void launch_cts(hipStream_t s, const DevArrays& a, int32_t m, int C, int n, int64_t P) {
-    if (m <= 0) return;
-#define CT_LAUNCH(GS, CPL, NW)                                                                                \
-    {                                                                                                         \
-        const int64_t threads = (int64_t)m * 64;                                                              \
-        hipLaunchKernelGGL((k_cts<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, m, a.recv_list, a.p_chain, \
-                           a.p_rr, a.c_off, a.c_base, a.fw, a.WLA, a.FDT, a.p_ts, a.p_cts, C, n, P);          \
+template <int NPAD, int T>
+static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+    const size_t lds = (size_t)T * (NPAD + 1) * sizeof(int64_t);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr = true;
     }
-    HGX_DISPATCH_N(n, CT_LAUNCH);
-#undef CT_LAUNCH
+    hipLaunchKernelGGL((k_cts_tile<NPAD, T>), dim3(nblk(Pn, T)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLA, a.FDT, a.p_ts, a.p_cts, C, n, P);
+}
+
+void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+    if (Pn <= 0) return;
+    if (n <= 4) cts_tile_launch<4, 64>(s, a, Pn, C, n, P);
+    else if (n <= 8) cts_tile_launch<8, 64>(s, a, Pn, C, n, P);
+    else if (n <= 16) cts_tile_launch<16, 64>(s, a, Pn, C, n, P);
+    else if (n <= 32) cts_tile_launch<32, 64>(s, a, Pn, C, n, P);
+    else if (n <= 64) cts_tile_launch<64, 64>(s, a, Pn, C, n, P);
+    else if (n <= 128) cts_tile_launch<128, 64>(s, a, Pn, C, n, P);
+    else if (n <= 256) cts_tile_launch<256, 32>(s, a, Pn, C, n, P);
+    else if (n <= 512) cts_tile_launch<512, 32>(s, a, Pn, C, n, P);
+    else cts_tile_launch<1024, 16>(s, a, Pn, C, n, P);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {
-    hipLaunchKernelGGL(k_minmax_cts, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts,
+    hipLaunchKernelGGL(k_minmax_cts, dim3(std::min(1024u, nblk(m, 256))), dim3(256), 0, s, m, a.recv_list, a.p_cts,
                        (unsigned long long*)a.minmax);
+}
+
+static void scan_u32(hipStream_t s, const DevArrays& a, uint32_t* buf, int64_t total) {
+    const int nparts = (int)((total + kScanChunk - 1) / kScanChunk);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nparts), dim3(256), 0, s, buf, total, a.scan_part);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, a.scan_part, nparts);
+    hipLaunchKernelGGL(k_scan_down, dim3(nparts), dim3(256), 0, s, buf, total, a.scan_part);
 }
 
 static void radix_pass(hipStream_t s, const DevArrays& a, int32_t m, int shift, const uint64_t* kin,
                        const uint32_t* vin, uint64_t* kout, uint32_t* vout) {
     const int nb = (m + kSortTile - 1) / kSortTile;
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kSortThreads), 0, s, kin, m, shift, a.hist, nb);
-    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, a.hist, (int64_t)256 * nb);
+    scan_u32(s, a, a.hist, (int64_t)256 * nb);
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kSortThreads), 0, s, kin, vin, m, shift, a.hist, nb, kout,
                        vout);
 }
