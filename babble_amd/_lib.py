@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhgx.so")
+LIB_PATH = os.path.join(HERE, os.environ.get("HGX_LIB", "libhgx.so"))  # HGX_LIB: in-tree variant (profiling builds)
 
 _L = None
 

@@ -25,13 +25,16 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force: bool = False, verbose: bool = True) -> str:
+def build_lib(force: bool = False, verbose: bool = True, variant: str = "") -> str:
+    """variant "prof": -DHGX_STEP_PROF build into libhgx_prof.so (phase timing of the round step)."""
+    out = OUT if not variant else os.path.join(HERE, f"libhgx_{variant}.so")
+    extra = ["-DHGX_STEP_PROF"] if variant == "prof" else []
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
         [os.path.join(ROOT, "include", "hgx.h")]
-    if not force and not _newer(OUT, deps):
-        return OUT
-    objdir = os.path.join(HERE, "build")
+    if not force and not _newer(out, deps):
+        return out
+    objdir = os.path.join(HERE, "build" + (f"_{variant}" if variant else ""))
     os.makedirs(objdir, exist_ok=True)
     objs = []
     procs = []
@@ -39,9 +42,9 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
         o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(o, [s] + deps[len(srcs):]):
-            cmd = [HIPCC] + FLAGS + ["-c", s, "-o", o]
+            cmd = [HIPCC] + FLAGS + extra + ["-c", s, "-o", o]
             if s.endswith(".cpp"):
-                cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", s, "-o", o] if "engine" in s else \
+                cmd = [HIPCC] + FLAGS + extra + ["-x", "hip", "-c", s, "-o", o] if "engine" in s else \
                     [HIPCC] + [f for f in FLAGS if not f.startswith("--offload")] + ["-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd), flush=True)
@@ -49,11 +52,11 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    return OUT
+    return out
 
 
 def build_oracle(verbose: bool = True) -> str:
@@ -62,5 +65,8 @@ def build_oracle(verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build_lib(force="--force" in sys.argv)
-    build_oracle()
+    if "--variant" in sys.argv:
+        build_lib(force="--force" in sys.argv, variant=sys.argv[sys.argv.index("--variant") + 1])
+    else:
+        build_lib(force="--force" in sys.argv)
+        build_oracle()

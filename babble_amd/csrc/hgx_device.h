@@ -19,4 +19,98 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// Wave-cooperative exact selection: the K-th smallest (0-based) of the valid values
+// held by the wave (CPL per lane). Radix select on (v - min) with 8-bit buckets from
+// the top set bit of the range down: each pass histograms the still-active values in
+// a 256-entry LDS scratch owned by this wave, finds the bucket holding rank K by a
+// wave prefix scan and keeps only that bucket. ceil(bits(range)/8) passes (<= 8).
+// Requires 0 <= K < #valid. Every lane returns the result.
+template <int CPL>
+__device__ uint64_t wave_select_kth(const uint64_t (&v)[CPL], const bool (&ok)[CPL], int K,
+                                    uint32_t* __restrict__ hist) {
+    const int lane = lane_id();
+    uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++)
+        if (ok[q]) { lo = v[q] < lo ? v[q] : lo; hi = v[q] > hi ? v[q] : hi; }
+    lo = wave_min_u64(lo);
+    hi = wave_max_u64(hi);
+    bool act[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) act[q] = ok[q];
+    uint64_t base = lo;
+    uint64_t range = hi - lo;
+    int k = K;
+    while (range != 0) {
+        int bits = 64 - __clzll((long long)range);
+        const int shift = bits > 8 ? bits - 8 : 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) hist[lane * 4 + t] = 0;
+        wave_lds_fence();
+#pragma unroll
+        for (int q = 0; q < CPL; q++)
+            if (act[q]) atomicAdd(&hist[(uint32_t)((v[q] - base) >> shift)], 1u);
+        wave_lds_fence();
+        uint32_t h[4], s = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) { h[t] = hist[lane * 4 + t]; s += h[t]; }
+        uint32_t incl = s;   // inclusive prefix over lanes
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t excl = incl - s;
+        // the lane whose [excl, incl) holds k owns the bucket
+        int bucket = -1;
+        uint32_t below = 0;
+        if ((uint32_t)k >= excl && (uint32_t)k < incl) {
+            uint32_t acc = excl;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if (bucket < 0 && (uint32_t)k < acc + h[t]) { bucket = lane * 4 + t; below = acc; }
+                acc += h[t];
+            }
+        }
+        const uint64_t bm = __ballot(bucket >= 0);
+        const int src = __ffsll((unsigned long long)bm) - 1;
+        bucket = __shfl(bucket, src);
+        below = __shfl(below, src);
+        wave_lds_fence();
+        k -= (int)below;
+        const uint64_t nb = base + ((uint64_t)bucket << shift);
+#pragma unroll
+        for (int q = 0; q < CPL; q++) act[q] = act[q] && ((v[q] - base) >> shift) == (uint64_t)bucket;
+        if (shift == 0) return nb;
+        const uint64_t top = nb + ((1ull << shift) - 1);
+        base = nb;
+        range = (top < hi ? top : hi) - nb;
+        // shrink to the actual active values for a tighter next pass
+        uint64_t alo = ~0ull, ahi = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++)
+            if (act[q]) { alo = v[q] < alo ? v[q] : alo; ahi = v[q] > ahi ? v[q] : ahi; }
+        alo = wave_min_u64(alo);
+        ahi = wave_max_u64(ahi);
+        base = alo;
+        range = ahi - alo;
+    }
+    return base;
+}
+
 }  // namespace hgx

@@ -3,6 +3,8 @@
 #include "hgx_engine.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace hgx {
@@ -197,6 +199,13 @@ void Engine::kend(int k, double bytes) {
     (void)hipEventRecord(kev[o.e0 + 1], stream);
 }
 
+// bytes known only after the launch completed (attributed to the last open launch of k)
+void Engine::kadd_bytes(int k, double bytes) {
+    kstat[k].bytes += bytes;
+    for (auto it = kopen.rbegin(); it != kopen.rend(); ++it)
+        if (it->k == k) { it->bytes += bytes; break; }
+}
+
 hipError_t Engine::collect_kernel_times() {
     if (kopen.empty()) return hipSuccess;
     HGX_TRY(hipStreamSynchronize(stream));
@@ -251,16 +260,26 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kend(K_LAYOUT, (double)E * 60);
     // lastAncestors: fixed point from all -1
     HGX_TRY(hipMemsetAsync(LA.p, 0xFF, (size_t)E * n * 4, stream));
+    static const bool la_debug = getenv("HGX_DEBUG_LA") != nullptr;
+    static const int la_seg = getenv("HGX_LA_SEG") ? std::max(1, atoi(getenv("HGX_LA_SEG"))) : 16;
     la_sweeps = 0;
+    la_rows = 0;
+    int32_t g_final = 0;   // rows with gid < g_final are final
     for (;;) {
-        HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 4, stream));
+        HGX_TRY(hipMemsetD32Async((hipDeviceptr_t)(counters.p + 2), kMaxI32, 1, stream));
+        HGX_TRY(hipMemsetAsync(counters.p + 3, 0, 4, stream));
         kbeg(K_LA_SWEEP);
-        launch_la_sweep(stream, a, C, n, max_len, counters.p + 2);
-        kend(K_LA_SWEEP, (double)E * (12.0 * n + 4));
+        launch_la_sweep(stream, a, C, n, max_len, la_seg, g_final, counters.p + 2);
+        kend(K_LA_SWEEP, 0);
         la_sweeps++;
-        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 4, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 8, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
-        if (h_small[0] == 0) break;
+        // algorithmic bytes of the rows this sweep processed
+        la_rows += h_small[1];
+        kadd_bytes(K_LA_SWEEP, (double)h_small[1] * (12.0 * n + 8));
+        if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows %d, min gid written %d\n", la_sweeps, h_small[1], h_small[0]);
+        if (h_small[0] == kMaxI32) break;
+        g_final = h_small[0];
         if (la_sweeps > 100000) return hipErrorUnknown;
     }
     kbeg(K_FD_BUILD);
@@ -358,6 +377,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipEventSynchronize(ph1));
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[1] = ms;
+    if (la_debug) step_prof_dump();
     return collect_kernel_times();
 }
 

@@ -76,6 +76,7 @@ class Engine {
     int64_t cap = 0, E = 0, E_div = 0;   // E_div: events laid out by the last divide_rounds
     int32_t R = 0;
     int la_sweeps = 0;
+    int64_t la_rows = 0;   // rows processed over all sweeps of the last divide_rounds
     hipStream_t stream = nullptr;
     double phase_ms[4] = {0, 0, 0, 0};   // coordinates, rounds, fame, order (last calls)
     KernelStat kstat[K_NUM];
@@ -85,6 +86,7 @@ class Engine {
     hipError_t ensure_round_cap(int32_t need);
     void kbeg(int k);
     void kend(int k, double bytes);
+    void kadd_bytes(int k, double bytes);
     hipError_t collect_kernel_times();
     DevArrays arrays();
 

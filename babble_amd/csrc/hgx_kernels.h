@@ -52,12 +52,16 @@ struct DevArrays {
 
 int fd_tile_rows(int n);
 void launch_layout(hipStream_t s, int64_t E, const DevArrays& a);
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int32_t* changed);
+// one Gauss-Seidel sweep over units with a row of gid >= g_final; out[0] = atomicMin of
+// the gids written, out[1] += rows processed
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int32_t g_final,
+                     int32_t* out);
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
 void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm);
 // fused step (n <= 256, hgx_rounds.hip): round = *a.d_round + kstep; false if n is unsupported
 bool launch_round_step(hipStream_t s, const DevArrays& a, int kstep, int C, int n, int sm, int64_t P);
+void step_prof_dump();   // -DHGX_STEP_PROF builds only
 void launch_advance_round(hipStream_t s, const DevArrays& a, int by);
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);

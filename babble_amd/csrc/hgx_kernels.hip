@@ -9,6 +9,7 @@
 //   WLA/WFD[r][gc][:] = coordinate rows of that candidate event, wflag 1/2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "hgx_device.h"
@@ -51,29 +52,41 @@ __global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const
 // A unit = (segment s of SEG rows, chain c); units are enumerated time-major so
 // that earlier segments of every chain are usually finished before later ones read
 // them. Converges when a launch writes nothing (values only grow; stale reads are
-// lower bounds).
+// lower bounds, and the register carry takes max(computed, stored) so it is one too).
+// Frontier: gids are topological (parents are inserted first), so if g is the
+// smallest gid written by sweep k, every row with gid < g is final after sweep k
+// (the smallest non-final one would have read only final inputs in sweep k). Sweep
+// k+1 therefore skips units whose last row has gid < g (SURVEY C.1 fixed point).
 template <int GS, int CPL>
 __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
-                           const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
-                           const int32_t* __restrict__ c_base, int C, int n, int nseg, int seg,
-                           int32_t* __restrict__ changed) {
+                           const int32_t* __restrict__ p_gid, const int32_t* __restrict__ c_off,
+                           const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
+                           int nseg, int seg, int32_t g_final, int32_t* __restrict__ out) {
     const int lane = lane_id();
     const int gl = lane % GS;
-    const int64_t unit = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS;
-    bool any = false;
-    if (unit < (int64_t)nseg * C) {
+    int first_w = kMaxI32;   // smallest gid this lane wrote
+    int rows = 0;
+    // grid-stride over units in time-major order (one reduction + atomic per wave)
+    const int64_t nunits = (int64_t)nseg * C;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x / GS;
+    for (int64_t unit = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS;
+         unit - (lane / GS) < nunits; unit += stride) {
+        if (unit >= nunits) continue;
         const int s = (int)(unit / C), c = (int)(unit % C);
         const int len = c_len[c];
         const int k0 = s * seg;
-        if (k0 < len) {
-            const int k1 = min(len, k0 + seg);
-            const int off = c_off[c], base = c_base[c], cl = c % n;
+        const int off = c_off[c];
+        const int k1 = min(len, k0 + seg);
+        if (k0 < len && p_gid[off + k1 - 1] >= g_final) {
+            if (gl == 0) rows += k1 - k0;
+            const int base = c_base[c], cl = c % n;
             int32_t carry[CPL];
 #pragma unroll
             for (int q = 0; q < CPL; q++) {
                 const int i = gl + GS * q;
                 carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
             }
+            int kw = kMaxI32;   // first chain offset written by this lane
             for (int k = k0; k < k1; k += 4) {
                 int32_t opr[4][CPL], old[4][CPL];
                 int opp[4];
@@ -96,18 +109,26 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
                         const int i = gl + GS * q;
                         int32_t v = max(carry[q], opr[u][q]);
                         if (i == cl) v = base + k + u;
-                        carry[q] = v;
                         if (i < n && v > old[u][q]) {
                             LA[(size_t)(off + k + u) * n + i] = v;
-                            any = true;
+                            kw = min(kw, k + u);
                         }
+                        carry[q] = max(v, old[u][q]);
                     }
                 }
             }
+            if (kw != kMaxI32) first_w = min(first_w, p_gid[off + kw]);
         }
     }
-    const uint64_t b = __ballot(any);
-    if (b && lane == __ffsll((unsigned long long)b) - 1) atomicOr(changed, 1);
+    // wave reductions: smallest gid written -> out[0], rows processed -> out[1]
+    for (int o = 32; o >= 1; o >>= 1) first_w = min(first_w, __shfl_xor(first_w, o));
+    if (GS < 64) {
+        for (int o = 32; o >= GS; o >>= 1) rows += __shfl_xor(rows, o);
+    }
+    if (lane == 0) {
+        if (first_w != kMaxI32) atomicMin(out, first_w);
+        if (rows) atomicAdd(out + 1, rows);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -126,22 +147,43 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
     const int off = c_off[c], base_c = c_base[c];
     const int g = c / n, cl = c % n;
     const int ld = n + 1;
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
+    // per target chain d of this graph, after the (FT+1) x ld tile
+    int32_t* m_len = sm + (FT + 1) * ld;
+    int32_t* m_base = m_len + n;
+    int32_t* m_off = m_base + n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
         sm[i] = (k0 > 0) ? LA[(size_t)(off + k0 - 1) * n + i] : -2147483647 - 1;
-    {   // the tile's rows are contiguous in LA: 4 independent loads in flight per thread
+        m_len[i] = c_len[g * n + i];
+        m_base[i] = c_base[g * n + i];
+        m_off[i] = c_off[g * n + i];
+    }
+    {   // the tile's rows are contiguous in LA
         const int32_t* __restrict__ src = LA + (size_t)(off + k0) * n;
-        const int nel = rows * n;
-        for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * blockDim.x) {
-            int32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * blockDim.x;
-                v[u] = (t < nel) ? src[t] : 0;
+        if ((n & 63) == 0) {
+            // straight into LDS (global_load_lds): one wave instruction = 64 ints of one row
+            typedef __attribute__((address_space(3))) void* lds_ptr_t;
+            const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+            const int per_row = n >> 6;
+            for (int q = wave; q < rows * per_row; q += nwaves) {
+                const int rr = q / per_row, cc = (q % per_row) << 6;
+                __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)rr * n + cc + lane),
+                                                 (lds_ptr_t)(sm + (rr + 1) * ld + cc), 4, 0, 0);
             }
+            __builtin_amdgcn_s_waitcnt(0);
+        } else {
+            const int nel = rows * n;
+            for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * blockDim.x) {
+                int32_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * blockDim.x;
-                if (t < nel) sm[(t / n + 1) * ld + (t % n)] = v[u];
+                for (int u = 0; u < 4; u++) {
+                    const int t = t0 + u * blockDim.x;
+                    v[u] = (t < nel) ? src[t] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int t = t0 + u * blockDim.x;
+                    if (t < nel) sm[(t / n + 1) * ld + (t % n)] = v[u];
+                }
             }
         }
     }
@@ -149,10 +191,9 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
     const bool last = (k1 == len);
     const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     for (int d = wave; d < n; d += nwaves) {
-        const int dc = g * n + d;
-        const int len_d = c_len[dc];
+        const int len_d = m_len[d];
         if (len_d == 0) continue;
-        const int base_d = c_base[dc], off_d = c_off[dc];
+        const int base_d = m_base[d], off_d = m_off[d];
         int lo = (k0 > 0) ? sm[d] : base_d - 1;
         if (lo < base_d - 1) lo = base_d - 1;
         const int hi_val = (rows > 0) ? sm[rows * ld + d] : lo;
@@ -437,38 +478,26 @@ __global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restr
     const int i = (int)(item / C), gd = (int)(item % C);
     const int g = gd / n, dl = gd % n;
     if (!elig[(size_t)g * R + i]) return;
+    __shared__ uint32_t whist[4][256];
     const int lane = lane_id();
     const size_t base = (size_t)i * C + (size_t)g * n;
-    int32_t v[CPL];
+    uint64_t v[CPL];
     bool ok[CPL];
     int m = 0;
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int c = lane + 64 * q;
         ok[q] = c < n && fw[base + c];
-        v[q] = ok[q] ? WLA[(base + c) * n + dl] : 0;
+        const int32_t x = ok[q] ? WLA[(base + c) * n + dl] : 0;
+        v[q] = (uint64_t)(int64_t)x ^ 0x8000000000000000ull;
         m += __popcll(__ballot(ok[q]));
     }
-    const int K = m / 2;   // 0-based rank in descending order
     int32_t res = -1;
-    bool found = false;
-#pragma unroll
-    for (int q = 0; q < CPL; q++) {
-        int rank = 0;
-        for (int q2 = 0; q2 < CPL; q2++) {
-            for (int src = 0; src < 64; src++) {
-                const int32_t u = __shfl(v[q2], src);
-                const bool uok = __shfl((int)ok[q2], src) != 0;
-                const int fi = src + 64 * q2, mi = lane + 64 * q;
-                if (uok && (u > v[q] || (u == v[q] && fi < mi))) rank++;
-            }
-        }
-        if (ok[q] && rank == K) { res = v[q]; found = true; }
+    if (m > 0) {   // (m/2)-th largest = (m-1-m/2)-th smallest
+        const uint64_t u = wave_select_kth<CPL>(v, ok, m - 1 - m / 2, whist[(threadIdx.x >> 6) & 3]);
+        res = (int32_t)(int64_t)(u ^ 0x8000000000000000ull);
     }
-    const uint64_t b = __ballot(found);
-    const int src = b ? (__ffsll((unsigned long long)b) - 1) : 0;
-    res = __shfl(res, src);
-    if (lane == 0) T[(size_t)i * C + gd] = (m > 0) ? res : -1;
+    if (lane == 0) T[(size_t)i * C + gd] = res;
 }
 
 // rr(x) = first eligible i > round(x) with Index(x) <= T[i][cr(x)]; compacts the
@@ -600,7 +629,8 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     }
     const size_t base = (size_t)i * C + (size_t)g * n;
     int mycnt = 0;
-    constexpr int U = 4;   // chains per batch: issue all independent loads, then the dependent gathers
+    constexpr int U = (NPAD / NCG) < 8 ? (NPAD / NCG > 0 ? NPAD / NCG : 1) : 8;   // chains per batch: issue
+                                   // all independent loads, then the dependent gathers
     for (int c0 = cg; c0 < NPAD; c0 += NCG * U) {
         bool mem[U];
         int32_t fdv[U], pb[U];
@@ -629,25 +659,25 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     }
     if (mycnt) atomicAdd(&cnt[e], mycnt);
     __syncthreads();
+    // phase B: one wave per event, exact radix select of element floor(|s|/2)
+    constexpr int SCPL = NPAD >= 64 ? NPAD / 64 : 1;
+    __shared__ uint32_t whist[4][256];
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     for (int ee = wave; ee < T; ee += 4) {
         const int64_t pe = p0 + ee;
         if (pe >= Pn || !p_new[pe]) continue;   // wave-uniform
-        int64_t* col = vals + ee * LD;
-        for (int k = 2; k <= NPAD; k <<= 1) {
-            for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                for (int t = lane; t < NPAD / 2; t += 64) {
-                    const int i1 = (t / jj) * (jj << 1) + (t % jj);
-                    const int i2 = i1 + jj;
-                    const bool up = (i1 & k) == 0;
-                    const int64_t a = col[i1], bb = col[i2];
-                    if ((a > bb) == up) { col[i1] = bb; col[i2] = a; }
-                }
-                wave_lds_fence();
-            }
+        const int64_t* col = vals + ee * LD;
+        uint64_t v[SCPL];
+        bool ok[SCPL];
+#pragma unroll
+        for (int q = 0; q < SCPL; q++) {
+            const int c = lane + 64 * q;
+            const int64_t x = (c < NPAD) ? col[c] : 0x7fffffffffffffffLL;
+            ok[q] = x != 0x7fffffffffffffffLL;
+            v[q] = (uint64_t)x ^ 0x8000000000000000ull;   // order-preserving signed -> unsigned
         }
-        if (lane == 0) p_cts[pe] = col[cnt[ee] / 2];
-        wave_lds_fence();
+        const uint64_t u = wave_select_kth<SCPL>(v, ok, cnt[ee] / 2, whist[wave]);
+        if (lane == 0) p_cts[pe] = (int64_t)(u ^ 0x8000000000000000ull);
     }
 }
 
@@ -932,22 +962,23 @@ void launch_layout(hipStream_t s, int64_t E, const DevArrays& a) {
                        a.p_cts);
 }
 
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int32_t* changed) {
-    const int seg = 16;
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int32_t g_final,
+                     int32_t* out) {
     const int nseg = (max_len + seg - 1) / seg;
     if (nseg == 0) return;
 #define LA_LAUNCH(GS, CPL, NW)                                                                                \
     {                                                                                                         \
         const int64_t threads = (int64_t)nseg * C * GS;                                                       \
-        hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, a.LA, a.p_op,   \
-                           a.c_off, a.c_len, a.c_base, C, n, nseg, seg, changed);                             \
+        hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, s,  \
+                           a.LA, a.p_op,                                                                     \
+                           a.p_gid, a.c_off, a.c_len, a.c_base, C, n, nseg, seg, g_final, out);              \
     }
     HGX_DISPATCH_N(n, LA_LAUNCH);
 #undef LA_LAUNCH
 }
 
 int fd_tile_rows(int n) {
-    int ft = 16384 / n;
+    int ft = 8192 / n;   // ~33 KB of LDS per block: 4 blocks (32 waves) per CU
     if (ft > 64) ft = 64;
     if (ft < 4) ft = 4;
     return ft;
@@ -956,8 +987,8 @@ int fd_tile_rows(int n) {
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P) {
     const int ft = fd_tile_rows(n);
     const int tiles = max(1, (max_len + ft - 1) / ft);
-    const size_t lds = (size_t)(ft + 1) * (n + 1) * sizeof(int32_t);
-    hipLaunchKernelGGL(k_fd_build, dim3(C, tiles), dim3(256), lds, s, a.LA, a.FDT, a.c_off, a.c_len, a.c_base, n,
+    const size_t lds = ((size_t)(ft + 1) * (n + 1) + 3 * (size_t)n) * sizeof(int32_t);
+    hipLaunchKernelGGL(k_fd_build, dim3(C, tiles), dim3(512), lds, s, a.LA, a.FDT, a.c_off, a.c_len, a.c_base, n,
                        ft, P);
 }
 
@@ -1036,9 +1067,9 @@ void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int
     else if (n <= 32) cts_tile_launch<32, 64>(s, a, Pn, C, n, P);
     else if (n <= 64) cts_tile_launch<64, 64>(s, a, Pn, C, n, P);
     else if (n <= 128) cts_tile_launch<128, 64>(s, a, Pn, C, n, P);
-    else if (n <= 256) cts_tile_launch<256, 32>(s, a, Pn, C, n, P);
-    else if (n <= 512) cts_tile_launch<512, 32>(s, a, Pn, C, n, P);
-    else cts_tile_launch<1024, 16>(s, a, Pn, C, n, P);
+    else if (n <= 256) cts_tile_launch<256, 16>(s, a, Pn, C, n, P);
+    else if (n <= 512) cts_tile_launch<512, 16>(s, a, Pn, C, n, P);
+    else cts_tile_launch<1024, 8>(s, a, Pn, C, n, P);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

@@ -14,11 +14,30 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
 
 namespace hgx {
+
+// Optional phase timing of the round step (build with -DHGX_STEP_PROF): thread 0 of
+// every block adds clock deltas per phase into hgx_step_prof[8].
+#ifdef HGX_STEP_PROF
+__device__ unsigned long long hgx_step_prof[8];
+#define HGX_PROF_BEGIN() long long _pt = clock64()
+#define HGX_PROF(i)                                                  \
+    do {                                                             \
+        if (threadIdx.x == 0) {                                      \
+            const long long _t = clock64();                          \
+            atomicAdd(&hgx_step_prof[i], (unsigned long long)(_t - _pt)); \
+            _pt = _t;                                                \
+        }                                                            \
+    } while (0)
+#else
+#define HGX_PROF_BEGIN() (void)0
+#define HGX_PROF(i) (void)0
+#endif
 
 template <int CPL>
 __device__ __forceinline__ bool ss_test(const int32_t* __restrict__ la_row, const int32_t (&fd)[CPL], int lane,
@@ -27,7 +46,10 @@ __device__ __forceinline__ bool ss_test(const int32_t* __restrict__ la_row, cons
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int i = lane + 64 * q;
-        const int32_t la = (i < n) ? la_row[i] : -1;
+        // unconditional LDS read (rows are staged with CPL*64 slack, see la_s), then a
+        // select: a guarded read becomes an exec branch + lgkmcnt(0) per read
+        const int32_t raw = la_row[i];
+        const int32_t la = (i < n) ? raw : -1;
         tot += __popcll(__ballot(la >= fd[q]));
     }
     return tot >= sm;
@@ -42,11 +64,18 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
     uint64_t* __restrict__ Smat, int32_t* __restrict__ p_round, int32_t* __restrict__ active, int32_t* __restrict__ lr,
     int C, int n, int nw, int sm, int64_t Pcap) {
     constexpr int NT = NWAVES * 64;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
     __shared__ int32_t cand[256];
+    __shared__ int32_t kf_s[256];   // per candidate slot: first probe that strongly sees it
     __shared__ int32_t hist[P + 1];
     __shared__ int32_t s_ncand, s_first;
     __shared__ unsigned long long s_mask[4];
-    __shared__ __attribute__((aligned(16))) int32_t la_s[P * 64 * CPL];
+    // P probe rows at stride n; + 64*CPL slack so ss_test may read a full CPL*64 row
+    __shared__ __attribute__((aligned(16))) int32_t la_s[P * 64 * CPL + 64 * CPL];
+    HGX_PROF_BEGIN();
+#ifdef HGX_STEP_PROF
+    if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[0], 1ull);
+#endif
     const int r = *d_base + kstep;
     const int gc = blockIdx.x;
     const int g = gc / n, cl = gc % n;
@@ -62,15 +91,14 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
         for (int j = threadIdx.x; j < n; j += NT)
             if (wflag[(size_t)r * C + (size_t)g * n + j] == 1) cand[atomicAdd(&s_ncand, 1)] = j;
         __syncthreads();
+        HGX_PROF(1);
         const int ncand = s_ncand;
         int32_t fd[OWN][CPL];
-        int own_c[OWN];
-        int kfirst[OWN];
+        int own_c[OWN];   // wave-uniform (SGPRs)
 #pragma unroll
         for (int o = 0; o < OWN; o++) {
             const int wi = wave + NWAVES * o;
-            own_c[o] = (wi < ncand) ? cand[wi] : -1;
-            kfirst[o] = 0;
+            own_c[o] = __builtin_amdgcn_readfirstlane((wi < ncand) ? cand[wi] : -1);
 #pragma unroll
             for (int q = 0; q < CPL; q++) {
                 const int i = lane + 64 * q;
@@ -80,38 +108,68 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
         }
         int kbase = b;
         for (;;) {
+#ifdef HGX_STEP_PROF
+            if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[6], 1ull);
+#endif
             const int np = min(P, len - kbase);
             const int nel = np * n;
             const int32_t* __restrict__ src = LA + (size_t)(off + kbase) * n;
-            // stage the probe rows: 4 independent loads in flight per thread
-            for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * NT) {
-                int32_t v[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * NT;
-                    v[u] = (t < nel) ? src[t] : 0;
+            // stage the probe rows straight into LDS (global_load_lds): one wave
+            // instruction moves 64 lanes x 16 B (or x 4 B when rows are not 16-B aligned)
+            if ((n & 3) == 0) {
+                for (int c0 = wave * 256; c0 < nel; c0 += NWAVES * 256) {
+                    const int t = c0 + lane * 4;
+                    if (t < nel)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
                 }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * NT;
-                    if (t < nel) la_s[t] = v[u];
+            } else {
+                for (int c0 = wave * 64; c0 < nel; c0 += NWAVES * 64) {
+                    const int t = c0 + lane;
+                    if (t < nel)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
                 }
             }
             for (int t = threadIdx.x; t <= P; t += NT) hist[t] = 0;
+            __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
+            HGX_PROF(2);
+            // four candidates' searches interleaved (independent LDS/ballot chains)
+            static_assert(OWN % 4 == 0, "candidates are searched four at a time");
 #pragma unroll
-            for (int o = 0; o < OWN; o++) {
-                if (own_c[o] < 0) continue;                       // wave-uniform
-                int lo = 0, hi = np;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (ss_test<CPL>(la_s + mid * n, fd[o], lane, n, sm)) hi = mid; else lo = mid + 1;
+            for (int o0 = 0; o0 < OWN; o0 += 4) {
+                if (own_c[o0] < 0) break;                         // wave-uniform; own_c fills in order
+                int lo[4], hi[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) { lo[u] = 0; hi[u] = (own_c[o0 + u] >= 0) ? np : 0; }
+                for (;;) {
+                    bool open = false;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) open |= lo[u] < hi[u];
+                    if (!open) break;
+                    int mid[4];
+                    bool t[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) mid[u] = min((lo[u] + hi[u]) >> 1, np - 1);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) t[u] = ss_test<CPL>(la_s + mid[u] * n, fd[o0 + u], lane, n, sm);
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (lo[u] < hi[u]) { if (t[u]) hi[u] = mid[u]; else lo[u] = mid[u] + 1; }
                 }
-                if (own_c[o] == cl && kbase + lo == b && lo < np) lo++;   // x == w never counts (n == 1)
-                kfirst[o] = lo;
-                if (lane == 0) atomicAdd(&hist[lo], 1);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int o = o0 + u;
+                    if (own_c[o] < 0) continue;
+                    int l = lo[u];
+                    if (own_c[o] == cl && kbase + l == b && l < np) l++;   // x == w never counts (n == 1)
+                    if (lane == 0) {
+                        kf_s[wave + NWAVES * o] = l;
+                        atomicAdd(&hist[l], 1);
+                    }
+                }
             }
             __syncthreads();
+            HGX_PROF(3);
             if (threadIdx.x == 0) {
                 int acc = 0, f = 0x7fffffff;
                 for (int pp = 0; pp < np; pp++) {
@@ -121,13 +179,12 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
                 s_first = f;
             }
             __syncthreads();
+            HGX_PROF(4);
             const int f = s_first;
             if (f != 0x7fffffff) {
                 kstar = kbase + f;
-#pragma unroll
-                for (int o = 0; o < OWN; o++)
-                    if (own_c[o] >= 0 && kfirst[o] <= f && lane == 0)
-                        atomicOr(&s_mask[own_c[o] >> 6], 1ull << (own_c[o] & 63));
+                for (int j = threadIdx.x; j < ncand; j += NT)
+                    if (kf_s[j] <= f) atomicOr(&s_mask[cand[j] >> 6], 1ull << (cand[j] & 63));
                 break;
             }
             kbase += P;
@@ -135,6 +192,7 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
             __syncthreads();
         }
         __syncthreads();
+        HGX_PROF(5);
         for (int k = b + (int)threadIdx.x; k < kstar; k += NT) p_round[off + k] = r;
         if (threadIdx.x == 0) {
             wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
@@ -163,6 +221,7 @@ __global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
     } else if (threadIdx.x == 0) {
         wflag[(size_t)(r + 1) * C + gc] = 0;
     }
+    HGX_PROF(7);
 }
 
 __global__ void k_advance_round(int32_t* d_base, int by) { *d_base += by; }
@@ -181,6 +240,18 @@ bool launch_round_step(hipStream_t s, const DevArrays& a, int kstep, int C, int 
 #undef STEP2
     return true;
 }
+
+#ifdef HGX_STEP_PROF
+void step_prof_dump() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_step_prof), sizeof(h)) != hipSuccess) return;
+    fprintf(stderr, "[hgx] step phases (clk sums):");
+    for (int i = 0; i < 8; i++) fprintf(stderr, " %d:%llu", i, h[i]);
+    fprintf(stderr, "\n");
+}
+#else
+void step_prof_dump() {}
+#endif
 
 void launch_advance_round(hipStream_t s, const DevArrays& a, int by) {
     hipLaunchKernelGGL(k_advance_round, dim3(1), dim3(1), 0, s, a.d_round, by);
