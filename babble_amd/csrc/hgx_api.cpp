@@ -26,6 +26,29 @@ struct Block {
     int32_t committed;
 };
 
+// growable pinned host array: the consensus order is copied D2H straight into it
+struct PinnedOrder {
+    int32_t* p = nullptr;
+    size_t n = 0, cap = 0;
+    PinnedOrder() = default;
+    PinnedOrder(const PinnedOrder&) = delete;
+    PinnedOrder& operator=(const PinnedOrder&) = delete;
+    ~PinnedOrder() { if (p) (void)hipHostFree(p); }
+    bool reserve(size_t want) {
+        if (want <= cap) return true;
+        size_t nc = std::max<size_t>(want, cap * 2 + 1024);
+        int32_t* q = nullptr;
+        if (hipHostMalloc((void**)&q, nc * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) return false;
+        if (n) std::memcpy(q, p, n * sizeof(int32_t));
+        if (p) (void)hipHostFree(p);
+        p = q;
+        cap = nc;
+        return true;
+    }
+    size_t size() const { return n; }
+    int32_t operator[](size_t i) const { return p[i]; }
+};
+
 struct GraphState {
     std::vector<int32_t> undecided{0};     // Hashgraph.UndecidedRounds, init []int{0} (hashgraph.go:64)
     int32_t queued_upto = -1;              // rounds <= this have RoundInfo.queued
@@ -36,8 +59,18 @@ struct GraphState {
     int32_t last_round = -1;
     std::vector<int8_t> fame;              // [(last_round+1) x n] RoundEvent.Famous (host state)
     std::vector<int32_t> round_events;     // [last_round+1]
-    std::vector<int32_t> order;            // consensus order (gids)
     std::vector<Block> blocks;
+    void reset() {   // a fresh NewHashgraph's consensus state (keeps allocations)
+        undecided.assign(1, 0);
+        queued_upto = -1;
+        has_lcr = false;
+        lcr = lcre = 0;
+        consensus_tx = pending_loaded = undetermined = 0;
+        last_round = -1;
+        fame.clear();
+        round_events.clear();
+        blocks.clear();
+    }
 };
 
 }  // namespace
@@ -57,6 +90,8 @@ struct hgx_ctx {
     bool divided = false;
     hgx::RoundsHost rh;
     std::vector<GraphState> gs;
+    std::vector<PinnedOrder> order;          // [G] consensus order (gids) per graph
+    std::vector<int64_t> g_events, g_loaded;  // [G] inserted events / loaded events per graph
     // getter caches
     bool rounds_cached = false;
     std::vector<int32_t> round_cache;
@@ -118,6 +153,9 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->last_index.assign(c->C, -1);
     c->chain_gids.assign(c->C, {});
     c->gs.assign(n_graphs, GraphState());
+    c->order = std::vector<PinnedOrder>(n_graphs);
+    c->g_events.assign(n_graphs, 0);
+    c->g_loaded.assign(n_graphs, 0);
     const size_t rsv = (size_t)std::min<int64_t>(capacity_events, 1 << 22);
     c->creator.reserve(rsv);
     if (err) set_err(err, HGX_OK, "");
@@ -189,8 +227,9 @@ int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64
         c->last_gid[cr] = gid;
         c->last_index[cr] = idx;
         GraphState& g = c->gs[cr / c->n];
-        if (ld) g.pending_loaded++;
+        if (ld) { g.pending_loaded++; c->g_loaded[cr / c->n]++; }
         g.undetermined++;
+        c->g_events[cr / c->n]++;
     }
     const int64_t added = c->E - first;
     if (added > 0) {
@@ -288,10 +327,13 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
                 }
             }
         }
-        // deferred updateUndecidedRounds (:733-741)
+        // deferred updateUndecidedRounds (:733-741): drop every copy of a decided round
+        std::vector<uint8_t> is_dec((size_t)std::max(0, s.last_round) + 1, 0);
+        for (int32_t r : decided) is_dec[(size_t)r] = 1;
         std::vector<int32_t> keep;
+        keep.reserve(s.undecided.size());
         for (int32_t r : s.undecided)
-            if (std::find(decided.begin(), decided.end(), r) == decided.end()) keep.push_back(r);
+            if (r < 0 || r > s.last_round || !is_dec[(size_t)r]) keep.push_back(r);
         s.undecided.swap(keep);
     }
     if (rc != HGX_OK) { set_err(err, rc, msg); return rc; }
@@ -325,15 +367,39 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
         return HGX_ERR_PANIC;
     }
     c->recv_cached = false;
-    const int32_t* order = c->eng.pinned_order();
-    int64_t at = 0;
-    for (int g = 0; g < G && oh.m > 0; g++) {
-        GraphState& s = c->gs[g];
-        const int64_t base_pos = (int64_t)s.order.size();
-        int64_t mg = 0;
-        for (int32_t rr = 0; rr < R; rr++) mg += oh.blk_cnt[(size_t)g * R + rr];
+    // per-graph segments of the device order (graph-major), copied D2H straight into
+    // each graph's pinned order array
+    std::vector<int64_t> seg_at(G, 0), seg_len(G, 0);
+    {
+        int64_t at = 0;
+        for (int g = 0; g < G; g++) {
+            int64_t mg = 0;
+            for (int32_t rr = 0; rr < R; rr++) mg += oh.blk_cnt[(size_t)g * R + rr];
+            seg_at[g] = at;
+            seg_len[g] = mg;
+            at += mg;
+        }
+        for (int g = 0; g < G; g++) {
+            if (!seg_len[g]) continue;
+            PinnedOrder& o = c->order[g];
+            if (!o.reserve(o.n + (size_t)seg_len[g])) {
+                set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
+                return HGX_ERR_CAPACITY;
+            }
+            e = c->eng.copy_order(o.p + o.n, seg_at[g], seg_len[g]);
+            if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
+        }
+        e = c->eng.sync();
+        if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
+    }
+    for (int g = 0; g < G; g++) {
+        const int64_t mg = seg_len[g];
         if (mg == 0) continue;
-        s.order.insert(s.order.end(), order + at, order + at + mg);
+        GraphState& s = c->gs[g];
+        PinnedOrder& o = c->order[g];
+        const int64_t base_pos = (int64_t)o.n;
+        const int32_t* order = o.p + o.n;
+        o.n += (size_t)mg;
         int64_t off = 0;
         for (int32_t rr = 0; rr < R; rr++) {    // one Block per rr, ascending (blockOrder)
             const int32_t cnt = oh.blk_cnt[(size_t)g * R + rr];
@@ -343,7 +409,7 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
             b.first = base_pos + off;
             b.nev = cnt;
             b.ntx = oh.blk_ntx[(size_t)g * R + rr];
-            const int32_t first_gid = order[at + off];
+            const int32_t first_gid = order[off];
             // NewBlock(rr, first.Transactions()) then append(...): nil iff first nil and nothing appended
             b.tx_nil = (c->txnil[first_gid] && b.ntx == 0) ? 1 : 0;
             b.committed = b.ntx > 0 ? 1 : 0;   // commitCh only if len(Transactions) > 0
@@ -353,7 +419,6 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
             off += cnt;
         }
         s.undetermined -= mg;
-        at += mg;
     }
     if (err) set_err(err, HGX_OK, "");
     return HGX_OK;
@@ -369,11 +434,12 @@ int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
 
 int32_t hgx_reset_consensus(hgx_ctx* c) {
     if (!c) return HGX_ERR_INVALID;
-    for (int g = 0; g < c->G; g++) c->gs[g] = GraphState();
-    for (int64_t x = 0; x < c->E; x++) {
-        GraphState& s = c->gs[c->creator[x] / c->n];
-        s.undetermined++;
-        if (c->loaded[x]) s.pending_loaded++;
+    for (int g = 0; g < c->G; g++) {
+        GraphState& s = c->gs[g];
+        s.reset();
+        s.undetermined = c->g_events[g];
+        s.pending_loaded = c->g_loaded[g];
+        c->order[g].n = 0;
     }
     c->divided = false;
     c->E_div = 0;
@@ -428,11 +494,11 @@ int32_t hgx_known(hgx_ctx* c, int32_t g, int32_t* out) {
     for (int cl = 0; cl < c->n; cl++) out[cl] = (int32_t)c->last_index[g * c->n + cl];
     return HGX_OK;
 }
-int64_t hgx_consensus_events_count(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->order.size() : 0; }
+int64_t hgx_consensus_events_count(hgx_ctx* c, int32_t g) { return graph(c, g) ? (int64_t)c->order[g].size() : 0; }
 int32_t hgx_consensus_events(hgx_ctx* c, int32_t g, int64_t first, int64_t count, int64_t* gids) {
-    GraphState* s = graph(c, g);
-    if (!s || first < 0 || count < 0 || first + count > (int64_t)s->order.size()) return HGX_ERR_INVALID;
-    for (int64_t i = 0; i < count; i++) gids[i] = s->order[(size_t)(first + i)];
+    if (!graph(c, g) || first < 0 || count < 0 || first + count > (int64_t)c->order[g].size()) return HGX_ERR_INVALID;
+    const int32_t* o = c->order[g].p;
+    for (int64_t i = 0; i < count; i++) gids[i] = o[first + i];
     return HGX_OK;
 }
 int64_t hgx_num_blocks(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->blocks.size() : 0; }

@@ -64,10 +64,9 @@ Engine::~Engine() {
     for (auto e : kev) (void)hipEventDestroy(e);
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
+    if (h_small) (void)hipHostFree(h_small);
     for (auto e : flag_ev)
         if (e) (void)hipEventDestroy(e);
-    if (h_order) (void)hipHostFree(h_order);
-    if (h_small) (void)hipHostFree(h_small);
     drop_step_graph();
     if (stream) (void)hipStreamDestroy(stream);
 }
@@ -105,11 +104,11 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P)); HGX_TRY(g_cts.alloc(P));
     HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
     HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
-    HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_round.alloc(P));
+    HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_opu.alloc(P)); HGX_TRY(p_round.alloc(P));
     HGX_TRY(p_rr.alloc(P)); HGX_TRY(p_ts.alloc(P)); HGX_TRY(p_cts.alloc(P));
     HGX_TRY(LA.alloc(P * n));
     HGX_TRY(FDT.alloc(P * n));
-    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(4)); HGX_TRY(order_gid.alloc(P));
+    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8)); HGX_TRY(order_gid.alloc(P));
     HGX_TRY(p_new.alloc(P));
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
@@ -119,7 +118,6 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(d_round.alloc(1));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[1], hipEventDisableTiming));
-    HGX_TRY(hipHostMalloc((void**)&h_order, P * sizeof(int32_t), hipHostMallocDefault));
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
     // rounds: initial guess, grown on demand
     const int lg = std::max(1, bitlen((uint64_t)n));
@@ -162,11 +160,10 @@ DevArrays Engine::arrays() {
     a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p;
     a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p;
     a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
-    a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
+    a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
     a.LA = LA.p; a.FDT = FDT.p;
     a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p;
-    a.d_round = d_round.p;
     a.active = active.p; a.lr = lr.p;
     a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
     a.elig = elig.p; a.fw = fw.p; a.ur_empty = ur_empty.p; a.T = Tthr.p;
@@ -255,31 +252,35 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
+    const int seg = kLaSeg;
     kbeg(K_LAYOUT);
-    launch_layout(stream, E, a);
-    kend(K_LAYOUT, (double)E * 60);
-    // lastAncestors: fixed point from all -1
+    launch_layout(stream, E, a, C, seg);
+    kend(K_LAYOUT, (double)E * 64);
+    // lastAncestors: fixed point from all -1, dirty-tracked sweeps (k_la_sweep)
     HGX_TRY(hipMemsetAsync(LA.p, 0xFF, (size_t)E * n * 4, stream));
+    const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
+    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.alloc(2 * nunits));
     static const bool la_debug = getenv("HGX_DEBUG_LA") != nullptr;
-    static const int la_seg = getenv("HGX_LA_SEG") ? std::max(1, atoi(getenv("HGX_LA_SEG"))) : 16;
     la_sweeps = 0;
     la_rows = 0;
-    int32_t g_final = 0;   // rows with gid < g_final are final
     for (;;) {
-        HGX_TRY(hipMemsetD32Async((hipDeviceptr_t)(counters.p + 2), kMaxI32, 1, stream));
-        HGX_TRY(hipMemsetAsync(counters.p + 3, 0, 4, stream));
+        uint8_t* chg_prev = la_chg.p + (size_t)(la_sweeps & 1) * nunits;
+        uint8_t* chg_cur = la_chg.p + (size_t)((la_sweeps + 1) & 1) * nunits;
+        HGX_TRY(hipMemsetAsync(chg_cur, 0, nunits, stream));
+        HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 8, stream));
+        HGX_TRY(hipMemsetAsync(counters.p + 4, 0, 4, stream));
         kbeg(K_LA_SWEEP);
-        launch_la_sweep(stream, a, C, n, max_len, la_seg, g_final, counters.p + 2);
+        launch_la_sweep(stream, a, C, n, max_len, seg, la_sweeps == 0 ? 1 : 0, chg_prev, chg_cur, counters.p + 2);
         kend(K_LA_SWEEP, 0);
-        la_sweeps++;
-        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 8, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 12, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
-        // algorithmic bytes of the rows this sweep processed
-        la_rows += h_small[1];
-        kadd_bytes(K_LA_SWEEP, (double)h_small[1] * (12.0 * n + 8));
-        if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows %d, min gid written %d\n", la_sweeps, h_small[1], h_small[0]);
-        if (h_small[0] == kMaxI32) break;
-        g_final = h_small[0];
+        // algorithmic bytes of the rows this sweep recomputed: sweep 1
+        // reads the op row and writes the row (8n + 8); later sweeps also read the old row
+        la_rows += h_small[0];
+        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * ((la_sweeps == 0 ? 8.0 : 12.0) * n + 8));
+        la_sweeps++;
+        if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows recomputed %d, units written %d, rows written %d\n", la_sweeps, h_small[0], h_small[1], h_small[2]);
+        if (h_small[1] == 0) break;
         if (la_sweeps > 100000) return hipErrorUnknown;
     }
     kbeg(K_FD_BUILD);
@@ -301,7 +302,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int r = 0;
     if (n <= 256) {
-        // fused steps: kStepBatch step nodes (round = base + k) + one node advancing the
+        // kStepBatch step nodes (round = base + k) + one node advancing the
         // device-resident base, replayed as one hipGraph; batch i+1 is queued before
         // the host looks at batch i's "any candidate left" flag (pipelined check)
         HGX_TRY(hipMemsetAsync(d_round.p, 0, 4, stream));
@@ -313,9 +314,15 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 a = arrays();
             }
             if (!step_exec) {
+                RoundArgs A;
+                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = cap; A.d_base = d_round.p;
+                A.c_len = c_len.p; A.c_off = c_off.p; A.LA = LA.p; A.FDT = FDT.p; A.p_gid = p_gid.p;
+                A.g_coin = g_coin.p;
+                A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
+                A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                for (int k = 0; k < kStepBatch; k++) launch_round_step(stream, a, k, C, n, sm, cap);
-                launch_advance_round(stream, a, kStepBatch);
+                for (int k = 0; k < kStepBatch; k++) (void)launch_round_step(stream, A, k);
+                launch_advance_round(stream, d_round.p, kStepBatch);
                 HGX_TRY(hipStreamEndCapture(stream, &step_graph));
                 HGX_TRY(hipGraphInstantiate(&step_exec, step_graph, nullptr, nullptr, 0));
             }
@@ -369,6 +376,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     for (int g = 0; g < G; g++) mx = std::max(mx, out.last_round[g]);
     R = mx + 1;
     out.R = R;
+    launch_wcoin(stream, a, R, C);
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
     HGX_TRY(hipMemcpyAsync(out.bm.data(), Bm.p, out.bm.size() * 4, hipMemcpyDeviceToHost, stream));
@@ -449,7 +457,6 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
     launch_finish_order(stream, a, m, vals, R, n);
-    HGX_TRY(hipMemcpyAsync(h_order, order_gid.p, (size_t)m * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
@@ -459,6 +466,11 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[3] = ms;
     return collect_kernel_times();
+}
+
+hipError_t Engine::copy_order(int32_t* dst, int64_t first, int64_t count) {
+    if (count <= 0) return hipSuccess;
+    return hipMemcpyAsync(dst, order_gid.p + first, (size_t)count * 4, hipMemcpyDeviceToHost, stream);
 }
 
 hipError_t Engine::reset_received() {
@@ -499,6 +511,7 @@ hipError_t Engine::get_coords(int64_t gid, int32_t* la, int32_t* fd) {
 }
 
 }  // namespace hgx
+
 
 namespace hgx {
 void Engine::drop_step_graph() {

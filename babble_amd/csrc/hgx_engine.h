@@ -12,7 +12,8 @@
 
 namespace hgx {
 
-constexpr int kStepBatch = 16;   // fused round steps per hipGraph replay
+
+constexpr int kStepBatch = 16;   // round steps per hipGraph replay
 
 enum KernelId {
     K_LAYOUT = 0, K_LA_SWEEP, K_FD_BUILD, K_ROUND_GATHER, K_ROUND_SEARCH, K_FAME, K_THRESHOLD,
@@ -65,7 +66,9 @@ class Engine {
     hipError_t decide_fame(std::vector<int8_t>& fame_out);
     hipError_t find_order(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
                           const std::vector<uint8_t>& ur_empty, OrderHost& out);
-    const int32_t* pinned_order() const { return h_order; }
+    // D2H of order[first, first+count) of the last find_order (async; then sync())
+    hipError_t copy_order(int32_t* dst, int64_t first, int64_t count);
+    hipError_t sync() { return hipStreamSynchronize(stream); }
 
     hipError_t reset_received();
     hipError_t get_rounds(std::vector<int32_t>& round_by_gid);
@@ -76,7 +79,8 @@ class Engine {
     int64_t cap = 0, E = 0, E_div = 0;   // E_div: events laid out by the last divide_rounds
     int32_t R = 0;
     int la_sweeps = 0;
-    int64_t la_rows = 0;   // rows processed over all sweeps of the last divide_rounds
+    int64_t la_rows = 0;   // rows recomputed over all sweeps of the last divide_rounds
+    static constexpr int kLaSeg = 16;   // rows per lastAncestors unit
     hipStream_t stream = nullptr;
     double phase_ms[4] = {0, 0, 0, 0};   // coordinates, rounds, fame, order (last calls)
     KernelStat kstat[K_NUM];
@@ -100,7 +104,8 @@ class Engine {
     // chains
     DBuf<int32_t> c_off, c_len, c_base;
     // positions
-    DBuf<int32_t> p_gid, p_chain, p_op, p_round, p_rr;
+    DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_round, p_rr;
+    DBuf<uint8_t> la_chg;   // [2 x units] ping-pong dirty flags of the lastAncestors sweeps
     DBuf<int64_t> p_ts, p_cts;
     // coordinates
     DBuf<int32_t> LA, FDT;
@@ -108,10 +113,10 @@ class Engine {
     int32_t r_cap = 0;
     DBuf<int32_t> Bm, WLA, WFD, Tthr, active, lr, d_round;
     hipEvent_t flag_ev[2] = {nullptr, nullptr};
-    DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
-    hipGraph_t step_graph = nullptr;       // kStepBatch fused round steps, replayed per batch
+    hipGraph_t step_graph = nullptr;       // kStepBatch round steps, replayed per batch
     hipGraphExec_t step_exec = nullptr;
     void drop_step_graph();
+    DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<int8_t> fame;
     // order
@@ -121,7 +126,6 @@ class Engine {
     DBuf<uint64_t> key_a, key_b;
     DBuf<uint32_t> val_a, val_b, hist;
     DBuf<int64_t> minmax, blk_ntx;
-    int32_t* h_order = nullptr;   // pinned
     int32_t* h_small = nullptr;   // pinned scratch (flags)
     // timing
     hipEvent_t ph0 = nullptr, ph1 = nullptr;

@@ -20,14 +20,13 @@ struct DevArrays {
     // chains
     const int32_t *c_off, *c_len, *c_base;
     // positions
-    int32_t *p_gid, *p_chain, *p_op, *p_round, *p_rr;
+    int32_t *p_gid, *p_chain, *p_op, *p_opu, *p_round, *p_rr;
     int64_t *p_ts, *p_cts;
     // coordinates
     int32_t *LA, *FDT;
     // rounds
     int32_t* Bm;
     uint8_t *wflag, *wstat, *wcoin;   // wflag: candidate of round r exists; wstat: 2 witness, 1 jumped, 0 none
-    int32_t* d_round;     // device round base of the current step batch
     int32_t *WLA, *WFD;
     int32_t *active, *lr;
     // fame
@@ -50,19 +49,33 @@ struct DevArrays {
     int64_t* blk_ntx;
 };
 
+// arguments of the round step (hgx_rounds.hip)
+struct RoundArgs {
+    int n, C, sm, nw;
+    int64_t Pcap;
+    const int32_t* d_base;   // device-resident round of step 0 of the current graph batch
+    const int32_t *c_len, *c_off, *LA, *FDT, *p_gid;
+    const uint8_t* g_coin;
+    int32_t *Bm, *WLA, *WFD, *p_round, *active, *lr;
+    uint8_t *wflag, *wstat, *wcoin;
+    uint64_t* Smat;
+};
+
 int fd_tile_rows(int n);
-void launch_layout(hipStream_t s, int64_t E, const DevArrays& a);
-// one Gauss-Seidel sweep over units with a row of gid >= g_final; out[0] = atomicMin of
-// the gids written, out[1] += rows processed
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int32_t g_final,
-                     int32_t* out);
+// gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
+void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg);
+// one Gauss-Seidel sweep over the dirty units (all when `first`); out[0] += rows
+// recomputed, out[1] += units written (marked in chg_cur)
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int32_t* out);
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
+void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
 void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm);
-// fused step (n <= 256, hgx_rounds.hip): round = *a.d_round + kstep; false if n is unsupported
-bool launch_round_step(hipStream_t s, const DevArrays& a, int kstep, int C, int n, int sm, int64_t P);
+// one round step (n <= 256, hgx_rounds.hip): round = *A.d_base + kstep
+hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep);
+void launch_advance_round(hipStream_t s, int32_t* d_base, int by);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only
-void launch_advance_round(hipStream_t s, const DevArrays& a, int by);
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);

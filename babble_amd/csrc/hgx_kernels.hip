@@ -25,8 +25,8 @@ __global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const
                          const int32_t* __restrict__ g_rr, const int64_t* __restrict__ g_cts,
                          const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                          int32_t* __restrict__ g_pos, int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
-                         int32_t* __restrict__ p_op, int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
-                         int64_t* __restrict__ p_cts) {
+                         int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu, int64_t* __restrict__ p_ts,
+                         int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int seg) {
     int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= E) return;
     int c = g_creator[gid];
@@ -35,37 +35,42 @@ __global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const
     p_gid[p] = (int32_t)gid;
     p_chain[p] = c;
     int op = g_op[gid];
-    int opp = -1;
+    int opp = -1, opu = -1;
     if (op >= 0) {
         int oc = g_creator[op];
-        opp = c_off[oc] + g_index[op] - c_base[oc];
+        const int ok = g_index[op] - c_base[oc];
+        opp = c_off[oc] + ok;
+        opu = (ok / seg) * C + oc;   // lastAncestors unit of the op row (k_la_sweep)
     }
     p_op[p] = opp;
+    p_opu[p] = opu;
     p_ts[p] = g_ts[gid];
     p_rr[p] = g_rr[gid];
     p_cts[p] = g_cts[gid];
 }
 
 // ---------------------------------------------------------------------------------
-// lastAncestors: in-place monotone sweep (Gauss-Seidel) over chain segments.
+// lastAncestors: in-place monotone sweeps (Gauss-Seidel) over units, with dirty tracking.
 // LA[x] = max(LA[sp(x)], LA[op(x)]), LA[x][cr(x)] = Index(x)   (hashgraph.go:470-496)
-// A unit = (segment s of SEG rows, chain c); units are enumerated time-major so
+// A unit = (segment s of SEG rows, chain c), enumerated time-major (u = s*C + c) so
 // that earlier segments of every chain are usually finished before later ones read
-// them. Converges when a launch writes nothing (values only grow; stale reads are
-// lower bounds, and the register carry takes max(computed, stored) so it is one too).
-// Frontier: gids are topological (parents are inserted first), so if g is the
-// smallest gid written by sweep k, every row with gid < g is final after sweep k
-// (the smallest non-final one would have read only final inputs in sweep k). Sweep
-// k+1 therefore skips units whose last row has gid < g (SURVEY C.1 fixed point).
+// them. Values only grow and stale reads are lower bounds (the register carry takes
+// max(computed, stored)), so repeating sweeps until one writes nothing reaches the
+// fixed point. A unit's output can only change if one of its inputs
+// changed: the previous unit of its chain (the carry) or the unit of one of its
+// op rows. Sweep t+1 therefore recomputes only units whose input units wrote in
+// sweep t (chg_prev), and marks the units it writes (chg_cur); a unit whose input
+// changes later in the same sweep is caught by the next one. Sweep 1 computes every
+// unit and skips reading the old rows (LA starts at -1).
 template <int GS, int CPL>
 __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
-                           const int32_t* __restrict__ p_gid, const int32_t* __restrict__ c_off,
+                           const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
-                           int nseg, int seg, int32_t g_final, int32_t* __restrict__ out) {
+                           int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
+                           uint8_t* __restrict__ chg_cur, int32_t* __restrict__ out) {
     const int lane = lane_id();
     const int gl = lane % GS;
-    int first_w = kMaxI32;   // smallest gid this lane wrote
-    int rows = 0;
+    int rows = 0, nwr = 0;   // rows recomputed / units written (counted by group lane 0)
     // grid-stride over units in time-major order (one reduction + atomic per wave)
     const int64_t nunits = (int64_t)nseg * C;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x / GS;
@@ -75,59 +80,84 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
         const int s = (int)(unit / C), c = (int)(unit % C);
         const int len = c_len[c];
         const int k0 = s * seg;
+        if (k0 >= len) continue;
         const int off = c_off[c];
         const int k1 = min(len, k0 + seg);
-        if (k0 < len && p_gid[off + k1 - 1] >= g_final) {
-            if (gl == 0) rows += k1 - k0;
-            const int base = c_base[c], cl = c % n;
-            int32_t carry[CPL];
-#pragma unroll
-            for (int q = 0; q < CPL; q++) {
-                const int i = gl + GS * q;
-                carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
+        if (!first) {
+            // dirty iff the carry unit or an op unit of one of its rows wrote last sweep
+            bool d = (s > 0 && gl == 0) ? chg_prev[unit - C] != 0 : false;
+            for (int k = k0 + gl; k < k1; k += GS) {
+                const int u = p_opu[off + k];
+                d = d || (u >= 0 && chg_prev[u] != 0);
             }
-            int kw = kMaxI32;   // first chain offset written by this lane
-            for (int k = k0; k < k1; k += 4) {
-                int32_t opr[4][CPL], old[4][CPL];
-                int opp[4];
+            const uint64_t gm = group_mask(GS, lane / GS);
+            if ((__ballot(d) & gm) == 0) continue;
+        }
+        if (gl == 0) rows += k1 - k0;
+        const int base = c_base[c], cl = c % n;
+        int32_t carry[CPL];
 #pragma unroll
-                for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
+        for (int q = 0; q < CPL; q++) {
+            const int i = gl + GS * q;
+            carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
+        }
+        bool wrote = false;
+        uint32_t wrow = 0;   // rows of the unit written by this lane
+        for (int k = k0; k < k1; k += 4) {
+            int32_t opr[4][CPL], old[4][CPL];
+            int opp[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
 #pragma unroll
-                    for (int q = 0; q < CPL; q++) {
-                        const int i = gl + GS * q;
-                        opr[u][q] = (opp[u] >= 0 && i < n) ? LA[(size_t)opp[u] * n + i] : -1;
-                        old[u][q] = (k + u < k1 && i < n) ? LA[(size_t)(off + k + u) * n + i] : -1;
-                    }
-                }
+            for (int u = 0; u < 4; u++) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (k + u >= k1) break;
-#pragma unroll
-                    for (int q = 0; q < CPL; q++) {
-                        const int i = gl + GS * q;
-                        int32_t v = max(carry[q], opr[u][q]);
-                        if (i == cl) v = base + k + u;
-                        if (i < n && v > old[u][q]) {
-                            LA[(size_t)(off + k + u) * n + i] = v;
-                            kw = min(kw, k + u);
-                        }
-                        carry[q] = max(v, old[u][q]);
-                    }
+                for (int q = 0; q < CPL; q++) {
+                    const int i = gl + GS * q;
+                    opr[u][q] = (opp[u] >= 0 && i < n) ? LA[(size_t)opp[u] * n + i] : -1;
+                    old[u][q] = (!first && k + u < k1 && i < n) ? LA[(size_t)(off + k + u) * n + i] : -1;
                 }
             }
-            if (kw != kMaxI32) first_w = min(first_w, p_gid[off + kw]);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (k + u >= k1) break;
+#pragma unroll
+                for (int q = 0; q < CPL; q++) {
+                    const int i = gl + GS * q;
+                    int32_t v = max(carry[q], opr[u][q]);
+                    if (i == cl) v = base + k + u;
+                    if (i < n && v > old[u][q]) {
+                        LA[(size_t)(off + k + u) * n + i] = v;
+                        wrote = true;
+                        wrow |= 1u << (k + u - k0);
+                    }
+                    carry[q] = max(v, old[u][q]);
+                }
+            }
+        }
+        const uint64_t gm = group_mask(GS, lane / GS);
+        if ((__ballot(wrote) & gm) != 0) {
+            if (gl == 0) {
+                chg_cur[unit] = 1;
+                nwr++;
+            }
+        }
+#ifdef HGX_LA_ROWSTATS
+        {   // rows written (debug statistics)
+            uint32_t wr = wrow;
+            for (int o = 1; o < GS; o <<= 1) wr |= __shfl_xor(wr, o);
+            if (gl == 0) atomicAdd(out + 2, __popc(wr));
+        }
+#endif
+    }
+    if (GS < 64) {
+        for (int o = 32; o >= 1; o >>= 1) {
+            rows += __shfl_xor(rows, o);
+            nwr += __shfl_xor(nwr, o);
         }
     }
-    // wave reductions: smallest gid written -> out[0], rows processed -> out[1]
-    for (int o = 32; o >= 1; o >>= 1) first_w = min(first_w, __shfl_xor(first_w, o));
-    if (GS < 64) {
-        for (int o = 32; o >= GS; o >>= 1) rows += __shfl_xor(rows, o);
-    }
     if (lane == 0) {
-        if (first_w != kMaxI32) atomicMin(out, first_w);
-        if (rows) atomicAdd(out + 1, rows);
+        if (rows) atomicAdd(out, rows);
+        if (nwr) atomicAdd(out + 1, nwr);
     }
 }
 
@@ -236,6 +266,18 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
     } else if (i == 0) {
         wflag[(size_t)r * C + gc] = 0;
     }
+}
+
+// coin bit (middleBit, hashgraph.go:1039-1048: hash[16] != 0) of every round's
+// candidate, gathered once after the rounds (kept off the per-round critical path)
+__global__ void k_wcoin(int64_t RC, int C, const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
+                        const int32_t* __restrict__ c_len, const int32_t* __restrict__ p_gid,
+                        const uint8_t* __restrict__ g_coin, uint8_t* __restrict__ wcoin) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= RC) return;
+    const int gc = (int)(t % C);
+    const int b = Bm[t];
+    wcoin[t] = (b < c_len[gc]) ? g_coin[p_gid[c_off[gc] + b]] : 0;
 }
 
 // search: per chain, first offset k >= Bm[r] whose event strongly sees >= SM
@@ -955,23 +997,23 @@ __global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const i
 
 static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
 
-void launch_layout(hipStream_t s, int64_t E, const DevArrays& a) {
+void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg) {
     if (E <= 0) return;
     hipLaunchKernelGGL(k_layout, dim3(nblk(E, 256)), dim3(256), 0, s, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
-                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_ts, a.p_rr,
-                       a.p_cts);
+                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_ts,
+                       a.p_rr, a.p_cts, C, seg);
 }
 
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int32_t g_final,
-                     int32_t* out) {
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int32_t* out) {
     const int nseg = (max_len + seg - 1) / seg;
     if (nseg == 0) return;
 #define LA_LAUNCH(GS, CPL, NW)                                                                                \
     {                                                                                                         \
         const int64_t threads = (int64_t)nseg * C * GS;                                                       \
         hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, s,  \
-                           a.LA, a.p_op,                                                                     \
-                           a.p_gid, a.c_off, a.c_len, a.c_base, C, n, nseg, seg, g_final, out);              \
+                           a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nseg, seg, first, chg_prev,  \
+                           chg_cur, out);                                                                     \
     }
     HGX_DISPATCH_N(n, LA_LAUNCH);
 #undef LA_LAUNCH
@@ -995,6 +1037,13 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
     hipLaunchKernelGGL(k_round_gather, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm, a.c_off, a.c_len,
                        a.LA, a.FDT, a.p_gid, a.g_coin, a.WLA, a.WFD, a.wflag, a.wcoin, C, n, P);
+}
+
+void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
+    const int64_t RC = (int64_t)R * C;
+    if (RC <= 0) return;
+    hipLaunchKernelGGL(k_wcoin, dim3(nblk(RC, 256)), dim3(256), 0, s, RC, C, a.Bm, a.c_off, a.c_len, a.p_gid, a.g_coin,
+                       a.wcoin);
 }
 
 void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm) {

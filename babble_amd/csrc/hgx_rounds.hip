@@ -1,260 +1,315 @@
-// Round assignment for n <= 256: one fused launch per round.
+// Round assignment for n <= 256: one launch per round, kStepBatch launches replayed
+// as one hipGraph. Rounds are a sequential recurrence (round r+1's
+// candidates are the boundaries found in round r); a dependent kernel boundary costs
+// ~1.5 us on MI355X, less than an in-launch grid barrier (MI355X_MICROARCH.md price
+// list; a persistent variant measured 53 us/round against 34 for launches), so the
+// step is a plain launch and the work is in making its body short.
 //
-// Step r, one block per chain c, candidates W'_r = first event of every chain with
-// round >= r. The chain's boundary Bm[r+1][c] is the first offset k >= Bm[r][c]
-// whose event strongly sees >= SM candidates (RoundInc, hashgraph.go:285-305).
-// StronglySee(x_k, w) is monotone in k (lastAncestors only grow along a chain), so
-// for every candidate w the block binary-searches the first probe of a window of P
-// probes that strongly sees w (log2(P+1) ballot/popcount tests instead of P); a
-// histogram of those first hits gives the count per probe. Candidates are split
-// over the waves, each wave keeps its candidates' firstDescendants slices in
-// registers; the P probe rows (lastAncestors) are staged in LDS.
-// The same step records, for the new boundary event (the candidate of round r+1),
-// the bitmask of W'_r it strongly sees: DecideFame's S_{r+1} matrix for free.
+// Round r, chain c, candidates W'_r = first event of every chain with round >= r.
+// The chain's boundary Bm[r+1][c] is the first offset k >= Bm[r][c] whose event
+// strongly sees >= SM candidates (RoundInc, hashgraph.go:285-305; StronglySee
+// hashgraph.go:170-198). The count is monotone in k (lastAncestors only grow along a
+// chain), so a group of waves binary-searches k over a window of P probe rows staged
+// in LDS: each level tests ONE probe row against all candidates (each wave holds its
+// candidates' firstDescendants rows in registers; lane = coordinate, v_cmp -> 64-bit
+// ballot -> s_bcnt1), so the tests of a level are independent (ILP), and the group
+// sums the per-wave counts. The window's firstDescendants columns (FDT[i][p..p+P),
+// one 128-B line per coordinate) are staged beside it, so the new candidate's FD row
+// needs no dependent gather. The boundary event's bitmask of strongly-seen candidates
+// is DecideFame's S_{r+1} row (hashgraph.go:688-705) for free.
+//
+// Group = 16 waves (one chain per block) for 64 < n <= 256; one wave per chain for
+// n <= 64 (4 chains per 256-thread block).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
+#include <utility>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
 
 namespace hgx {
 
-// Optional phase timing of the round step (build with -DHGX_STEP_PROF): thread 0 of
-// every block adds clock deltas per phase into hgx_step_prof[8].
+// Optional phase timing (build with -DHGX_STEP_PROF, variant "prof"): thread 0 of
+// every block adds s_memtime deltas per phase into hgx_step_prof[8].
 #ifdef HGX_STEP_PROF
 __device__ unsigned long long hgx_step_prof[8];
 #define HGX_PROF_BEGIN() long long _pt = clock64()
-#define HGX_PROF(i)                                                  \
-    do {                                                             \
-        if (threadIdx.x == 0) {                                      \
-            const long long _t = clock64();                          \
+#define HGX_PROF(i)                                                       \
+    do {                                                                  \
+        if (threadIdx.x == 0) {                                           \
+            const long long _t = clock64();                               \
             atomicAdd(&hgx_step_prof[i], (unsigned long long)(_t - _pt)); \
-            _pt = _t;                                                \
-        }                                                            \
+            _pt = _t;                                                     \
+        }                                                                 \
     } while (0)
+#define HGX_PROF_COUNT(i) do { if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[i], 1ull); } while (0)
 #else
 #define HGX_PROF_BEGIN() (void)0
 #define HGX_PROF(i) (void)0
+#define HGX_PROF_COUNT(i) (void)0
 #endif
 
-template <int CPL>
-__device__ __forceinline__ bool ss_test(const int32_t* __restrict__ la_row, const int32_t (&fd)[CPL], int lane,
-                                        int n, int sm) {
+// total of candidate O goes to lane O of tv (v_writelane with an immediate lane: a
+// select on lane == O would make the compiler hoist OWN 64-bit lane masks and spill them)
+template <int O, int CPL, int OWN>
+__device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int& tv) {
     int tot = 0;
 #pragma unroll
-    for (int q = 0; q < CPL; q++) {
-        const int i = lane + 64 * q;
-        // unconditional LDS read (rows are staged with CPL*64 slack, see la_s), then a
-        // select: a guarded read becomes an exec branch + lgkmcnt(0) per read
-        const int32_t raw = la_row[i];
-        const int32_t la = (i < n) ? raw : -1;
-        tot += __popcll(__ballot(la >= fd[q]));
-    }
-    return tot >= sm;
+    for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(la[q] >= fd[O][q]));
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv) : "s"(tot), "i"(O));
 }
 
-template <int CPL, int OWN, int NWAVES, int P>
-__global__ void __launch_bounds__(NWAVES * 64) k_round_step2(
-    int kstep, const int32_t* __restrict__ d_base, int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
-    const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA, const int32_t* __restrict__ FDT,
-    const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
-    int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wstat, uint8_t* __restrict__ wcoin,
-    uint64_t* __restrict__ Smat, int32_t* __restrict__ p_round, int32_t* __restrict__ active, int32_t* __restrict__ lr,
-    int C, int n, int nw, int sm, int64_t Pcap) {
-    constexpr int NT = NWAVES * 64;
+template <int CPL, int OWN, int... O>
+__device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL],
+                                     std::integer_sequence<int, O...>) {
+    int tv = 0;
+    (tally_one<O, CPL, OWN>(la, fd, tv), ...);
+    return tv;
+}
+
+// bitmask (bit o = candidate o held by this wave) of the candidates that the probe row
+// strongly sees; candidate `excl` (own chain's candidate when the probe is that event)
+// never counts. Coordinates i >= n read past the row (slack / the next row), but
+// their fd is +inf (MaxInt32) and la is clamped below it, so they never count.
+template <int CPL, int OWN>
+__device__ __forceinline__ uint64_t seen_mask(const int32_t* __restrict__ row, const int32_t (&fd)[OWN][CPL],
+                                              int lane, int sm, int excl) {
+    int32_t la[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) la[q] = min(row[lane + 64 * q], kMaxI32 - 1);
+    const int tv = tally<CPL, OWN>(la, fd, std::make_integer_sequence<int, OWN>{});
+    return __ballot(lane < OWN && tv >= sm && lane != excl);
+}
+
+template <int CPL, int NWC, int OWN, int P, int GPB>
+__global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int kstep) {
+    constexpr int NT = NWC * 64;   // threads per group
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    __shared__ int32_t cand[256];
-    __shared__ int32_t kf_s[256];   // per candidate slot: first probe that strongly sees it
-    __shared__ int32_t hist[P + 1];
-    __shared__ int32_t s_ncand, s_first;
+    extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+    __shared__ int32_t s_cnt[2][NWC];
     __shared__ unsigned long long s_mask[4];
-    // P probe rows at stride n; + 64*CPL slack so ss_test may read a full CPL*64 row
-    __shared__ __attribute__((aligned(16))) int32_t la_s[P * 64 * CPL + 64 * CPL];
+
+    const int n = A.n, C = A.C, sm = A.sm;
+    const int r = *A.d_base + kstep;
+    // readfirstlane: the compiler does not know threadIdx.x >> 6 is wave-uniform, and
+    // everything derived from it (chain, window, search bounds) would go to VGPRs
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gslot = (NWC == 1) ? wave : 0;              // group within block
+    const int wg = (NWC == 1) ? 0 : wave;                 // wave within group
+    const int gt = (NWC == 1) ? lane : (int)threadIdx.x;  // thread within group
+    const int gc = blockIdx.x * GPB + gslot;
+    if (gc >= C) return;   // group-uniform; no block barrier is used when NWC == 1
+    // LDS per group: P LA rows (+ slack) | n FD columns of P
+    const int la_words = P * n + 64 * CPL;
+    int32_t* __restrict__ la_s = lds + gslot * (la_words + n * P);
+    int32_t* __restrict__ fd_s = la_s + la_words;
+
     HGX_PROF_BEGIN();
-#ifdef HGX_STEP_PROF
-    if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[0], 1ull);
-#endif
-    const int r = *d_base + kstep;
-    const int gc = blockIdx.x;
+    HGX_PROF_COUNT(0);
     const int g = gc / n, cl = gc % n;
-    const int len = c_len[gc];
-    const int off = c_off[gc];
-    const int b = Bm[(size_t)r * C + gc];
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
-    int kstar = len;
-    if (b < len) {
-        if (threadIdx.x == 0) s_ncand = 0;
-        if (threadIdx.x < 4) s_mask[threadIdx.x] = 0;
-        __syncthreads();
-        for (int j = threadIdx.x; j < n; j += NT)
-            if (wflag[(size_t)r * C + (size_t)g * n + j] == 1) cand[atomicAdd(&s_ncand, 1)] = j;
-        __syncthreads();
-        HGX_PROF(1);
-        const int ncand = s_ncand;
-        int32_t fd[OWN][CPL];
-        int own_c[OWN];   // wave-uniform (SGPRs)
-#pragma unroll
-        for (int o = 0; o < OWN; o++) {
-            const int wi = wave + NWAVES * o;
-            own_c[o] = __builtin_amdgcn_readfirstlane((wi < ncand) ? cand[wi] : -1);
-#pragma unroll
-            for (int q = 0; q < CPL; q++) {
-                const int i = lane + 64 * q;
-                fd[o][q] = (own_c[o] >= 0 && i < n)
-                               ? WFD[((size_t)r * C + (size_t)g * n + own_c[o]) * n + i] : kMaxI32;
-            }
+    const int len = A.c_len[gc], off = A.c_off[gc];
+    const int b = A.Bm[(size_t)r * C + gc];
+    if (b >= len) {
+        if (gt == 0) {
+            A.wstat[(size_t)r * C + gc] = 0;
+            A.wflag[(size_t)(r + 1) * C + gc] = 0;
+            A.Bm[(size_t)(r + 1) * C + gc] = len;
         }
-        int kbase = b;
-        for (;;) {
-#ifdef HGX_STEP_PROF
-            if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[6], 1ull);
-#endif
-            const int np = min(P, len - kbase);
-            const int nel = np * n;
-            const int32_t* __restrict__ src = LA + (size_t)(off + kbase) * n;
-            // stage the probe rows straight into LDS (global_load_lds): one wave
-            // instruction moves 64 lanes x 16 B (or x 4 B when rows are not 16-B aligned)
-            if ((n & 3) == 0) {
-                for (int c0 = wave * 256; c0 < nel; c0 += NWAVES * 256) {
-                    const int t = c0 + lane * 4;
-                    if (t < nel)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
-                }
-            } else {
-                for (int c0 = wave * 64; c0 < nel; c0 += NWAVES * 64) {
-                    const int t = c0 + lane;
-                    if (t < nel)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
-                }
-            }
-            for (int t = threadIdx.x; t <= P; t += NT) hist[t] = 0;
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
-            HGX_PROF(2);
-            // four candidates' searches interleaved (independent LDS/ballot chains)
-            static_assert(OWN % 4 == 0, "candidates are searched four at a time");
-#pragma unroll
-            for (int o0 = 0; o0 < OWN; o0 += 4) {
-                if (own_c[o0] < 0) break;                         // wave-uniform; own_c fills in order
-                int lo[4], hi[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) { lo[u] = 0; hi[u] = (own_c[o0 + u] >= 0) ? np : 0; }
-                for (;;) {
-                    bool open = false;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) open |= lo[u] < hi[u];
-                    if (!open) break;
-                    int mid[4];
-                    bool t[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) mid[u] = min((lo[u] + hi[u]) >> 1, np - 1);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) t[u] = ss_test<CPL>(la_s + mid[u] * n, fd[o0 + u], lane, n, sm);
-#pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (lo[u] < hi[u]) { if (t[u]) hi[u] = mid[u]; else lo[u] = mid[u] + 1; }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int o = o0 + u;
-                    if (own_c[o] < 0) continue;
-                    int l = lo[u];
-                    if (own_c[o] == cl && kbase + l == b && l < np) l++;   // x == w never counts (n == 1)
-                    if (lane == 0) {
-                        kf_s[wave + NWAVES * o] = l;
-                        atomicAdd(&hist[l], 1);
-                    }
-                }
-            }
-            __syncthreads();
-            HGX_PROF(3);
-            if (threadIdx.x == 0) {
-                int acc = 0, f = 0x7fffffff;
-                for (int pp = 0; pp < np; pp++) {
-                    acc += hist[pp];
-                    if (acc >= sm) { f = pp; break; }
-                }
-                s_first = f;
-            }
-            __syncthreads();
-            HGX_PROF(4);
-            const int f = s_first;
-            if (f != 0x7fffffff) {
-                kstar = kbase + f;
-                for (int j = threadIdx.x; j < ncand; j += NT)
-                    if (kf_s[j] <= f) atomicOr(&s_mask[cand[j] >> 6], 1ull << (cand[j] & 63));
-                break;
-            }
-            kbase += P;
-            if (kbase >= len) { kstar = len; break; }
-            __syncthreads();
-        }
-        __syncthreads();
-        HGX_PROF(5);
-        for (int k = b + (int)threadIdx.x; k < kstar; k += NT) p_round[off + k] = r;
-        if (threadIdx.x == 0) {
-            wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-            if (kstar < len) atomicOr(&active[r], 1);
-            if (kstar > b) atomicMax(&lr[g], r);
-        }
-        if (kstar < len && threadIdx.x < nw) Smat[((size_t)(r + 1) * C + gc) * nw + threadIdx.x] = s_mask[threadIdx.x];
-    } else if (threadIdx.x == 0) {
-        wstat[(size_t)r * C + gc] = 0;
+        return;
     }
-    if (threadIdx.x == 0) Bm[(size_t)(r + 1) * C + gc] = kstar;
-    // coordinate rows of this chain's candidate for round r+1 (offset kstar)
-    const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
+    // stage the probe window [kbase, kbase+np): LA rows (contiguous) and FD columns
+    // fd_s[i*P + p] = FDT[i][off+kbase+p] (one wave instruction = 64/P columns)
+    auto stage = [&](int kbase, int np) {
+        const int nel = np * n;
+        const int32_t* __restrict__ src = A.LA + (size_t)(off + kbase) * n;
+        if ((n & 3) == 0) {
+            for (int c0 = wg * 256; c0 < nel; c0 += NWC * 256) {
+                const int t = c0 + lane * 4;
+                if (t < nel)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
+            }
+        } else {
+            for (int c0 = wg * 64; c0 < nel; c0 += NWC * 64) {
+                const int t = c0 + lane;
+                if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
+            }
+        }
+        {
+            constexpr int CPI = 64 / P;
+            const int pcol = lane % P, icol = lane / P;
+            const int32_t* __restrict__ fsrc = A.FDT + off + kbase + pcol;
+            for (int i0 = wg * CPI; i0 < n; i0 += NWC * CPI) {
+                const int i = i0 + icol;
+                if (i < n && pcol < np)
+                    __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * A.Pcap),
+                                                     (lds_ptr_t)(fd_s + i0 * P), 4, 0, 0);
+            }
+        }
+    };
+    stage(b, min(P, len - b));   // in flight while the candidate rows load
+    // candidates of this wave: chains j = wg + NWC*o. Rows are loaded unconditionally
+    // (every slot of WFD exists) and masked by the candidate flag: no exec branches.
+    const size_t crow = (size_t)r * C + (size_t)g * n;
+    uint32_t fl[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int j = lane + 64 * q;
+        fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
+    }
+    int32_t fd[OWN][CPL];
+#pragma unroll
+    for (int o = 0; o < OWN; o++) {
+        const int j = wg + NWC * o;
+        const int jj = j < n ? j : 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int i = lane + 64 * q;
+            fd[o][q] = A.WFD[(crow + jj) * n + (i < n ? i : 0)];
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < OWN; o++) {
+        const int j = wg + NWC * o;
+        uint32_t f = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const uint32_t v = __shfl(fl[q], j & 63);
+            if (q == (j >> 6)) f = v;
+        }
+        const bool cand = (j < n) && f == 1u;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int i = lane + 64 * q;
+            fd[o][q] = (cand && i < n) ? fd[o][q] : kMaxI32;
+        }
+    }
+    HGX_PROF(1);
+    // own-chain candidate slot (never counts for the probe that is itself)
+    const int own_o = (cl >= wg && (cl - wg) % NWC == 0) ? (cl - wg) / NWC : -1;
+    int kbase = b, np = min(P, len - b), lo = 0, kstar = len, lv = 0;
+    bool staged = true;
+    for (;;) {
+        if (!staged) stage(kbase, np);
+        staged = false;
+        __builtin_amdgcn_s_waitcnt(0);
+        if (NWC == 1) wave_lds_fence(); else __syncthreads();
+        HGX_PROF(2);
+        HGX_PROF_COUNT(6);
+        lo = 0;
+        int hi = np;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int ex = (kbase + mid == b) ? own_o : -1;
+            int tot = __popcll(seen_mask<CPL, OWN>(la_s + mid * n, fd, lane, sm, ex));
+            if (NWC > 1) {
+                if (lane == 0) s_cnt[lv & 1][wave] = tot;
+                __syncthreads();
+                tot = 0;
+#pragma unroll
+                for (int w = 0; w < NWC; w++) tot += s_cnt[lv & 1][w];
+                lv++;
+            }
+            if (tot >= sm) hi = mid; else lo = mid + 1;
+        }
+        HGX_PROF(3);
+        if (lo < np) { kstar = kbase + lo; break; }
+        kbase += np;
+        if (kbase >= len) { kstar = len; break; }
+        np = min(P, len - kbase);
+        // everyone is done with the window before it is restaged
+        if (NWC == 1) wave_lds_fence(); else __syncthreads();
+    }
+    // outputs of round r for this chain
+    for (int k = b + gt; k < kstar; k += NT) A.p_round[off + k] = r;
+    if (gt == 0) {
+        A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
+        if (kstar < len) atomicOr(&A.active[r], 1);
+        if (kstar > b) atomicMax(&A.lr[g], r);
+        A.Bm[(size_t)(r + 1) * C + gc] = kstar;
+    }
     if (kstar < len) {
-        const int p = off + kstar;
-        for (int i = threadIdx.x; i < n; i += NT) {
-            const int32_t a = LA[(size_t)p * n + i];
-            const int32_t d = FDT[(size_t)i * Pcap + p];
-            WLA[nrow + i] = a;
-            WFD[nrow + i] = d;
+        // S row of the boundary event (the candidate of round r+1): W'_r members it strongly sees
+        const int pk = kstar - kbase;   // inside the staged window
+        const uint64_t bits = seen_mask<CPL, OWN>(la_s + pk * n, fd, lane, sm, (kstar == b) ? own_o : -1);
+        const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
+        if (NWC == 1) {
+            if (lane == 0) A.Smat[srow] = bits;
+        } else {
+            if (gt < 4) s_mask[gt] = 0;
+            __syncthreads();
+            if (lane == 0) {   // bit o of this wave = chain wg + NWC*o
+                uint64_t m[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int o = 0; o < OWN; o++) {
+                    const int j = wg + NWC * o;
+                    const uint64_t bit = ((bits >> o) & 1ull) << (j & 63);
+#pragma unroll
+                    for (int x = 0; x < 4; x++)
+                        if ((j >> 6) == x) m[x] |= bit;
+                }
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+                    if (m[x]) atomicOr(&s_mask[x], m[x]);
+            }
+            __syncthreads();
+            if (gt < A.nw) A.Smat[srow + gt] = s_mask[gt];
         }
-        if (threadIdx.x == 0) {
-            wflag[(size_t)(r + 1) * C + gc] = 1;
-            wcoin[(size_t)(r + 1) * C + gc] = g_coin[p_gid[p]];
+        // coordinate rows of the new candidate, both from the staged window
+        const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
+        for (int i = gt; i < n; i += NT) {
+            A.WLA[nrow + i] = la_s[pk * n + i];
+            A.WFD[nrow + i] = fd_s[i * P + pk];
         }
-    } else if (threadIdx.x == 0) {
-        wflag[(size_t)(r + 1) * C + gc] = 0;
+        if (gt == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
+    } else if (gt == 0) {
+        A.wflag[(size_t)(r + 1) * C + gc] = 0;
     }
-    HGX_PROF(7);
+    HGX_PROF(4);
+}
+
+template <int CPL, int NWC, int OWN, int P, int GPB>
+static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
+    const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB>;
+    const size_t lds = (size_t)GPB * (P * A.n + 64 * CPL + A.n * P) * sizeof(int32_t);
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
+    hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A, kstep);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
+    const int n = A.n;
+    if (n <= 16) return step_launch<1, 1, 16, 32, 4>(s, A, kstep);
+    if (n <= 32) return step_launch<1, 1, 32, 32, 4>(s, A, kstep);
+    if (n <= 64) return step_launch<1, 1, 64, 32, 4>(s, A, kstep);
+    if (n <= 128) return step_launch<2, 16, 8, 32, 1>(s, A, kstep);
+    if (n <= 256) return step_launch<4, 16, 16, 32, 1>(s, A, kstep);
+    return hipErrorInvalidValue;
 }
 
 __global__ void k_advance_round(int32_t* d_base, int by) { *d_base += by; }
 
-bool launch_round_step(hipStream_t s, const DevArrays& a, int kstep, int C, int n, int sm, int64_t P) {
-    const int nw = (n + 63) / 64;
-#define STEP2(CPL, OWN, NWAVES, PP)                                                                             \
-    hipLaunchKernelGGL((k_round_step2<CPL, OWN, NWAVES, PP>), dim3(C), dim3(NWAVES * 64), 0, s, kstep,         \
-                       a.d_round, a.Bm, a.c_off, a.c_len, a.LA, a.FDT, a.p_gid, a.g_coin, a.WLA, a.WFD, a.wflag, \
-                       a.wstat, a.wcoin, a.Smat, a.p_round, a.active, a.lr, C, n, nw, sm, P)
-    if (n <= 32) STEP2(1, 8, 4, 64);
-    else if (n <= 64) STEP2(1, 4, 16, 64);
-    else if (n <= 128) STEP2(2, 8, 16, 64);
-    else if (n <= 256) STEP2(4, 16, 16, 48);
-    else return false;
-#undef STEP2
-    return true;
+void launch_advance_round(hipStream_t s, int32_t* d_base, int by) {
+    hipLaunchKernelGGL(k_advance_round, dim3(1), dim3(1), 0, s, d_base, by);
 }
 
 #ifdef HGX_STEP_PROF
 void step_prof_dump() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_step_prof), sizeof(h)) != hipSuccess) return;
-    fprintf(stderr, "[hgx] step phases (clk sums):");
+    fprintf(stderr, "[hgx] round phases (clk sums; 0 = block-rounds, 6 = windows):");
     for (int i = 0; i < 8; i++) fprintf(stderr, " %d:%llu", i, h[i]);
     fprintf(stderr, "\n");
 }
 #else
 void step_prof_dump() {}
 #endif
-
-void launch_advance_round(hipStream_t s, const DevArrays& a, int by) {
-    hipLaunchKernelGGL(k_advance_round, dim3(1), dim3(1), 0, s, a.d_round, by);
-}
 
 }  // namespace hgx
