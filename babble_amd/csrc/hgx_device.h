@@ -113,4 +113,68 @@ __device__ uint64_t wave_select_kth(const uint64_t (&v)[CPL], const bool (&ok)[C
     return base;
 }
 
+// 32-bit variant for the common case (values already rebased): radix select with 8-bit
+// digits from the top set bit of the range, no per-pass range shrink. Requires
+// 0 <= K < #valid; every lane returns the result.
+template <int CPL>
+__device__ uint32_t wave_select_kth32(const uint32_t (&v)[CPL], const bool (&ok)[CPL], int K,
+                                      uint32_t* __restrict__ hist) {
+    const int lane = lane_id();
+    uint32_t lo = 0xffffffffu, hi = 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++)
+        if (ok[q]) { lo = min(lo, v[q]); hi = max(hi, v[q]); }
+    for (int o = 32; o >= 1; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor(lo, o));
+        hi = max(hi, (uint32_t)__shfl_xor(hi, o));
+    }
+    const uint32_t range = hi - lo;
+    if (range == 0) return lo;
+    const int bits = 32 - __clz((int)range);
+    uint32_t d[CPL];
+    bool act[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) { d[q] = v[q] - lo; act[q] = ok[q]; }
+    uint32_t prefix = 0;
+    int k = K;
+    for (int shift = ((bits - 1) / 8) * 8; shift >= 0; shift -= 8) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) hist[lane * 4 + t] = 0;
+        wave_lds_fence();
+#pragma unroll
+        for (int q = 0; q < CPL; q++)
+            if (act[q]) atomicAdd(&hist[(d[q] >> shift) & 255u], 1u);
+        wave_lds_fence();
+        uint32_t h[4], sum = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) { h[t] = hist[lane * 4 + t]; sum += h[t]; }
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t excl = incl - sum;
+        int bucket = -1;
+        uint32_t below = 0;
+        if ((uint32_t)k >= excl && (uint32_t)k < incl) {
+            uint32_t acc = excl;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if (bucket < 0 && (uint32_t)k < acc + h[t]) { bucket = lane * 4 + t; below = acc; }
+                acc += h[t];
+            }
+        }
+        const uint64_t bm = __ballot(bucket >= 0);
+        const int src = __ffsll((unsigned long long)bm) - 1;
+        bucket = __shfl(bucket, src);
+        below = __shfl(below, src);
+        wave_lds_fence();
+        k -= (int)below;
+        prefix |= (uint32_t)bucket << shift;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) act[q] = act[q] && ((d[q] >> shift) & 255u) == (uint32_t)bucket;
+    }
+    return lo + prefix;
+}
+
 }  // namespace hgx

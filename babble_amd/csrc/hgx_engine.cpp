@@ -121,7 +121,9 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
     // rounds: initial guess, grown on demand
     const int lg = std::max(1, bitlen((uint64_t)n));
-    int32_t guess = (int32_t)std::min<int64_t>(1 << 20, std::max<int64_t>(64, 2 * cap / std::max(1, n * lg) + 16));
+    // rounds of the largest graph: ~events per graph / (n log n) (SURVEY §8 estimate), x2
+    const int64_t per_graph = (cap + G - 1) / G;
+    int32_t guess = (int32_t)std::min<int64_t>(1 << 20, std::max<int64_t>(64, 2 * per_graph / std::max(1, n * lg) + 16));
     HGX_TRY(ensure_round_cap(guess));
     return hipSuccess;
 }
@@ -163,7 +165,7 @@ DevArrays Engine::arrays() {
     a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
     a.LA = LA.p; a.FDT = FDT.p;
-    a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p;
+    a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p; a.WLAT = WLAT.p;
     a.active = active.p; a.lr = lr.p;
     a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
     a.elig = elig.p; a.fw = fw.p; a.ur_empty = ur_empty.p; a.T = Tthr.p;
@@ -420,7 +422,12 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemcpyAsync(elig.p, el.data(), (size_t)G * R, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(fw.p, famous.data(), (size_t)R * C, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(ur_empty.p, ure.data(), (size_t)G, hipMemcpyHostToDevice, stream));
+    if (WLAT.n < (size_t)R * C * n) {
+        HGX_TRY(WLAT.alloc((size_t)R * C * n + (size_t)C * n));
+        a = arrays();
+    }
     kbeg(K_THRESHOLD);
+    launch_wla_transpose(stream, a, R, G, C, n);
     launch_threshold(stream, a, R, C, n);
     kend(K_THRESHOLD, 0);
     HGX_TRY(hipMemsetAsync(counters.p, 0, 8, stream));

@@ -111,7 +111,7 @@ class Engine {
     DBuf<int32_t> LA, FDT;
     // per round
     int32_t r_cap = 0;
-    DBuf<int32_t> Bm, WLA, WFD, Tthr, active, lr, d_round;
+    DBuf<int32_t> Bm, WLA, WFD, WLAT, Tthr, active, lr, d_round;
     hipEvent_t flag_ev[2] = {nullptr, nullptr};
     hipGraph_t step_graph = nullptr;       // kStepBatch round steps, replayed per batch
     hipGraphExec_t step_exec = nullptr;

@@ -27,7 +27,7 @@ struct DevArrays {
     // rounds
     int32_t* Bm;
     uint8_t *wflag, *wstat, *wcoin;   // wflag: candidate of round r exists; wstat: 2 witness, 1 jumped, 0 none
-    int32_t *WLA, *WFD;
+    int32_t *WLA, *WFD, *WLAT;
     int32_t *active, *lr;
     // fame
     uint64_t *Smat, *Vbuf;
@@ -77,6 +77,7 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep);
 void launch_advance_round(hipStream_t s, int32_t* d_base, int by);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
+void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
 void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P);

@@ -510,19 +510,42 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
 }
 
 // ---------------------------------------------------------------------------------
+// WLAT[i][g][d][c] = WLA[i][g][c][d]: per round, the lastAncestors of the candidates
+// transposed so that "which witnesses of round i see chain d up to index j" is one
+// contiguous row (k_threshold, k_cts_*). 64 x 64 tiles through LDS; eligible rounds only.
+__global__ void __launch_bounds__(256) k_wla_transpose(int R, int G, int C, int n, const uint8_t* __restrict__ elig,
+                                                       const int32_t* __restrict__ WLA, int32_t* __restrict__ WLAT) {
+    __shared__ int32_t t[64][65];
+    const int ig = blockIdx.y, i = ig / G, g = ig % G;
+    if (!elig[(size_t)g * R + i]) return;
+    const int nt = (n + 63) / 64, tc = blockIdx.x % nt, td = blockIdx.x / nt;
+    const size_t base = ((size_t)i * C + (size_t)g * n) * n;
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+        const int r = k >> 6, col = k & 63, c = tc * 64 + r, d = td * 64 + col;
+        t[r][col] = (c < n && d < n) ? WLA[base + (size_t)c * n + d] : 0;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+        const int r = k >> 6, col = k & 63, d = td * 64 + r, c = tc * 64 + col;
+        if (c < n && d < n) WLAT[base + (size_t)d * n + c] = t[col][r];
+    }
+}
+
 // round received: T[i][d] = (m/2+1)-th largest LA[w][d] over famous witnesses w of
-// round i (DecideRoundReceived hashgraph.go:767-775). One wave per (i, d).
+// round i (DecideRoundReceived hashgraph.go:767-775). One wave per (i, d),
+// reading the contiguous WLAT row.
 template <int CPL>
 __global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restrict__ elig, const uint8_t* __restrict__ fw,
-                            const int32_t* __restrict__ WLA, int32_t* __restrict__ T, int C, int n) {
+                            const int32_t* __restrict__ WLAT, int32_t* __restrict__ T, int C, int n) {
     const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (item >= (int64_t)R * C) return;
     const int i = (int)(item / C), gd = (int)(item % C);
-    const int g = gd / n, dl = gd % n;
+    const int g = gd / n;
     if (!elig[(size_t)g * R + i]) return;
     __shared__ uint32_t whist[4][256];
     const int lane = lane_id();
     const size_t base = (size_t)i * C + (size_t)g * n;
+    const size_t row = ((size_t)i * C + gd) * n;
     uint64_t v[CPL];
     bool ok[CPL];
     int m = 0;
@@ -530,7 +553,7 @@ __global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restr
     for (int q = 0; q < CPL; q++) {
         const int c = lane + 64 * q;
         ok[q] = c < n && fw[base + c];
-        const int32_t x = ok[q] ? WLA[(base + c) * n + dl] : 0;
+        const int32_t x = ok[q] ? WLAT[row + c] : 0;
         v[q] = (uint64_t)(int64_t)x ^ 0x8000000000000000ull;
         m += __popcll(__ballot(ok[q]));
     }
@@ -578,148 +601,182 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
     if (slot >= 0) recv_list[s_base + slot] = (int32_t)p;
 }
 
-// consensus timestamp: upper median of the timestamps of OldestSelfAncestorToSee(a, x)
-// = FD[x][cr(a)] over famous witnesses a of round rr(x) that see x
-// (hashgraph.go:780-787, 860-868). One wave per received event.
-template <int CPL>
-__global__ void __launch_bounds__(256) k_cts(int32_t m, const int32_t* __restrict__ recv_list, const int32_t* __restrict__ p_chain,
-                      const int32_t* __restrict__ p_rr, const int32_t* __restrict__ c_off,
-                      const int32_t* __restrict__ c_base, const uint8_t* __restrict__ fw,
-                      const int32_t* __restrict__ WLA, const int32_t* __restrict__ FDT,
-                      const int64_t* __restrict__ p_ts, int64_t* __restrict__ p_cts, int C, int n, int64_t P) {
-    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (item >= m) return;
-    const int p = recv_list[item];
-    const int gc = p_chain[p], g = gc / n, dl = gc % n;
-    const int j = c_base[gc] + (p - c_off[gc]);
+// consensus timestamp: upper median (ByTimestamp, index floor(|s|/2), event.go:227-237)
+// of the timestamps of OldestSelfAncestorToSee(a, x) = FD[x][cr(a)] over the famous
+// witnesses a of round rr(x) that see x (hashgraph.go:141-167, 780-787, 860-868).
+// "a sees x" is WLAT[rr][cr(x)][cr(a)] >= Index(x); the value is the timestamp of
+// event (cr(a), FD[x][cr(a)]). The median VALUE does not depend on how ties are ordered.
+
+// n <= 32: one lane per event; FDT[c][p] over consecutive p is coalesced, the
+// selection is a rank count over <= 32 values in registers.
+template <int NP>
+__global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __restrict__ p_new,
+                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+                                                   const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
+                                                   const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
+                                                   const int32_t* __restrict__ FDT, const int64_t* __restrict__ p_ts,
+                                                   int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Pn || !p_new[p]) return;
+    const int gc = p_chain[p], g = gc / n;
+    const int j = c_base[gc] + (int)(p - c_off[gc]);
     const int i = p_rr[p];
-    const int lane = lane_id();
-    const size_t base = (size_t)i * C + (size_t)g * n;
-    int64_t v[CPL];
-    bool ok[CPL];
-    int cnt = 0;
+    const size_t row = ((size_t)i * C + gc) * n;
+    const size_t fb = (size_t)i * C + (size_t)g * n;
+    int64_t v[NP];
+    uint32_t ok = 0;
 #pragma unroll
-    for (int q = 0; q < CPL; q++) {
-        const int c = lane + 64 * q;
-        ok[q] = c < n && fw[base + c] && WLA[(base + c) * n + dl] >= j;
-        v[q] = 0;
-        if (ok[q]) {
+    for (int c = 0; c < NP; c++) {
+        v[c] = 0;
+        if (c < n && fw[fb + c] && WLAT[row + c] >= j) {
             const int ch = g * n + c;
-            const int32_t fd = FDT[(size_t)c * P + p];
-            v[q] = p_ts[c_off[ch] + (fd - c_base[ch])];
+            v[c] = p_ts[c_off[ch] - c_base[ch] + FDT[(size_t)c * Pcap + p]];
+            ok |= 1u << c;
         }
-        cnt += __popcll(__ballot(ok[q]));
     }
-    const int K = cnt / 2;   // index in ascending order
+    const int K = __popc(ok) / 2;
     int64_t res = 0;
-    bool found = false;
 #pragma unroll
-    for (int q = 0; q < CPL; q++) {
+    for (int a = 0; a < NP; a++) {
         int rank = 0;
-        for (int q2 = 0; q2 < CPL; q2++) {
-            for (int src = 0; src < 64; src++) {
-                const int64_t u = __shfl(v[q2], src);
-                const bool uok = __shfl((int)ok[q2], src) != 0;
-                const int fi = src + 64 * q2, mi = lane + 64 * q;
-                if (uok && (u < v[q] || (u == v[q] && fi < mi))) rank++;
-            }
-        }
-        if (ok[q] && rank == K) { res = v[q]; found = true; }
+#pragma unroll
+        for (int b = 0; b < NP; b++)
+            rank += (((ok >> b) & 1u) && (v[b] < v[a] || (v[b] == v[a] && b < a))) ? 1 : 0;
+        if (((ok >> a) & 1u) && rank == K) res = v[a];
     }
-    const uint64_t b = __ballot(found);
-    const int src = b ? (__ffsll((unsigned long long)b) - 1) : 0;
-    res = __shfl(res, src);
-    if (lane == 0) p_cts[p] = res;
+    p_cts[p] = res;
 }
 
-// Tiled consensus timestamp. A block owns T consecutive positions (one chain
-// mostly). Phase A, lanes = events: for each witness chain c, FDT[c][p0..p0+T) is a
-// coalesced read and the timestamp gathers p_ts[pos(c, FD)] hit a few adjacent
-// lines (FD is monotone along a chain); values go to LDS as vals[e][c] (+inf when
-// the famous witness of chain c does not see the event). Phase B: one wave per
-// event bitonic-sorts its NPAD values in LDS and takes element floor(|s|/2).
-
-template <int NPAD, int T>
+// n > 32: a block owns T = 32 consecutive positions (mostly one chain, one round
+// received). Phase 1, lanes = events: for each witness chain c the 32 FD values
+// FDT[c][p0..p0+32) are one 128-B line, and since firstDescendants are monotone along
+// a chain the 32 timestamp gathers p_ts[pos(c, FD)] hit one or two lines. Values are
+// kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
+// do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
+// per event: radix select of element floor(m/2) in registers.
+template <int NPAD>
 __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
                                                   const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
-                                                  const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLA,
+                                                  const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                   const int32_t* __restrict__ FDT, const int64_t* __restrict__ p_ts,
-                                                  int64_t* __restrict__ p_cts, int C, int n, int64_t P) {
-    extern __shared__ __attribute__((aligned(16))) int64_t vals[];   // [T][NPAD+1]
-    __shared__ int32_t cnt[T];
+                                                  int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
+    constexpr int T = 32;
+    constexpr int LD = T + 1;                     // row stride of vals (bank spread)
+    constexpr int CPL = NPAD / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t vals[];   // [NPAD][LD] offsets + 2^31
+    __shared__ uint32_t mem[T][NPAD / 32];         // membership bits per event
+    __shared__ int32_t e_row[T], e_j[T], e_fb[T], e_g[T];
+    __shared__ int64_t e_ts[T];
+    __shared__ int32_t e_ovf[T];
+    __shared__ uint32_t whist[4][256];
     __shared__ int32_t s_any;
-    constexpr int LD = NPAD + 1;
-    constexpr int NCG = 256 / T;
     const int64_t p0 = (int64_t)blockIdx.x * T;
-    const int e = threadIdx.x % T, cg = threadIdx.x / T;
-    const int64_t p = p0 + e;
-    const bool valid = p < Pn && p_new[p];
     if (threadIdx.x == 0) s_any = 0;
-    if (threadIdx.x < T) cnt[threadIdx.x] = 0;
+    for (int k = threadIdx.x; k < T * (NPAD / 32); k += 256) mem[k / (NPAD / 32)][k % (NPAD / 32)] = 0;
     __syncthreads();
-    if (valid) s_any = 1;
+    if (threadIdx.x < T) {
+        const int e = threadIdx.x;
+        const int64_t p = p0 + e;
+        int row = -1;
+        if (p < Pn && p_new[p]) {
+            s_any = 1;
+            const int gc = p_chain[p], g = gc / n, i = p_rr[p];
+            row = i;
+            e_j[e] = c_base[gc] + (int)(p - c_off[gc]);
+            e_fb[e] = i * C + g * n;   // < 2^31: round tables are int32-indexed
+            e_g[e] = gc;
+            e_ts[e] = p_ts[p];
+        }
+        e_row[e] = row;
+        e_ovf[e] = 0;
+    }
     __syncthreads();
     if (!s_any) return;
-    int g = 0, dl = 0, j = 0, i = 0;
-    if (valid) {
-        const int gc = p_chain[p];
-        g = gc / n;
-        dl = gc % n;
-        j = c_base[gc] + (int)(p - c_off[gc]);
-        i = p_rr[p];
-    }
-    const size_t base = (size_t)i * C + (size_t)g * n;
-    int mycnt = 0;
-    constexpr int U = (NPAD / NCG) < 8 ? (NPAD / NCG > 0 ? NPAD / NCG : 1) : 8;   // chains per batch: issue
-                                   // all independent loads, then the dependent gathers
-    for (int c0 = cg; c0 < NPAD; c0 += NCG * U) {
-        bool mem[U];
-        int32_t fdv[U], pb[U];
+    // phase 1: lane = event e (32 per half-wave), 8 chain groups over the block
+    {
+        const int e = threadIdx.x & (T - 1), cg = threadIdx.x / T;   // cg in [0, 8)
+        const int i = e_row[e];
+        const int64_t p = p0 + e;
+        const int gc = (i >= 0) ? e_g[e] : 0;
+        const int g = gc / n;
+        const int j = (i >= 0) ? e_j[e] : 0;
+        const size_t fb = (i >= 0) ? (size_t)e_fb[e] : 0;
+        const size_t wrow = (size_t)(fb + (gc - g * n)) * n;   // WLAT row (i, g, d)
+        const int64_t base = (i >= 0) ? e_ts[e] : 0;
+        bool ovf = false;
+        // batches of U chains: all independent loads first, then the dependent gathers
+        // (branch-free: non-members gather a valid dummy index and are masked)
+        constexpr int U = 4;
+        for (int c0 = cg; c0 < n; c0 += 8 * U) {
+            bool ok[U];
+            int32_t idx[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int c = c0 + u * NCG;
-            mem[u] = false;
-            fdv[u] = 0;
-            pb[u] = 0;
-            if (valid && c < n) {
-                const int ch = g * n + c;
-                mem[u] = fw[base + c] && WLA[(base + c) * n + dl] >= j;
-                fdv[u] = FDT[(size_t)c * P + p];
-                pb[u] = c_off[ch] - c_base[ch];
+            for (int u = 0; u < U; u++) {
+                const int c = c0 + 8 * u;
+                const bool in = i >= 0 && c < n;
+                const int cc = in ? c : 0;
+                const int ch = g * n + cc;
+                const uint8_t f = fw[fb + cc];
+                const int32_t w = WLAT[wrow + cc];
+                ok[u] = in & (f != 0) & (w >= j);
+                idx[u] = c_off[ch] - c_base[ch] + FDT[(size_t)cc * Pcap + (in ? p : 0)];
+            }
+            int64_t x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) x[u] = p_ts[ok[u] ? idx[u] : 0];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int c = c0 + 8 * u;
+                const int64_t dlt = x[u] - base;
+                ovf |= ok[u] && (dlt < INT32_MIN || dlt > INT32_MAX);
+                if (c < n) vals[c * LD + e] = (uint32_t)(int32_t)dlt ^ 0x80000000u;
+                if (ok[u]) atomicOr(&mem[e][c >> 5], 1u << (c & 31));
             }
         }
-        int64_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) v[u] = mem[u] ? p_ts[pb[u] + fdv[u]] : 0x7fffffffffffffffLL;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int c = c0 + u * NCG;
-            if (c < NPAD) vals[e * LD + c] = v[u];
-            mycnt += mem[u] ? 1 : 0;
-        }
+        if (ovf) e_ovf[e] = 1;
     }
-    if (mycnt) atomicAdd(&cnt[e], mycnt);
     __syncthreads();
-    // phase B: one wave per event, exact radix select of element floor(|s|/2)
-    constexpr int SCPL = NPAD >= 64 ? NPAD / 64 : 1;
-    __shared__ uint32_t whist[4][256];
+    // phase 2: one wave per event
     const int lane = lane_id(), wave = threadIdx.x >> 6;
-    for (int ee = wave; ee < T; ee += 4) {
-        const int64_t pe = p0 + ee;
-        if (pe >= Pn || !p_new[pe]) continue;   // wave-uniform
-        const int64_t* col = vals + ee * LD;
-        uint64_t v[SCPL];
-        bool ok[SCPL];
+    for (int e = wave; e < T; e += 4) {
+        if (e_row[e] < 0) continue;   // wave-uniform
+        bool ok[CPL];
+        int m = 0;
 #pragma unroll
-        for (int q = 0; q < SCPL; q++) {
+        for (int q = 0; q < CPL; q++) {
             const int c = lane + 64 * q;
-            const int64_t x = (c < NPAD) ? col[c] : 0x7fffffffffffffffLL;
-            ok[q] = x != 0x7fffffffffffffffLL;
-            v[q] = (uint64_t)x ^ 0x8000000000000000ull;   // order-preserving signed -> unsigned
+            ok[q] = c < n && ((mem[e][c >> 5] >> (c & 31)) & 1u);
+            m += __popcll(__ballot(ok[q]));
         }
-        const uint64_t u = wave_select_kth<SCPL>(v, ok, cnt[ee] / 2, whist[wave]);
-        if (lane == 0) p_cts[pe] = (int64_t)(u ^ 0x8000000000000000ull);
+        int64_t res;
+        if (!e_ovf[e]) {
+            uint32_t v[CPL];
+#pragma unroll
+            for (int q = 0; q < CPL; q++) v[q] = vals[(lane + 64 * q) * LD + e];
+#ifdef HGX_CTS_NOSELECT
+            const uint32_t u = v[0] + (uint32_t)m;
+#else
+            const uint32_t u = wave_select_kth32<CPL>(v, ok, m / 2, whist[wave]);
+#endif
+            res = e_ts[e] + (int64_t)(int32_t)(u ^ 0x80000000u);
+        } else {   // rare: offsets beyond 32 bits -> regather and select in 64 bits
+            const int64_t p = p0 + e;
+            const int gc = e_g[e], g = gc / n;
+            uint64_t v[CPL];
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int c = lane + 64 * q;
+                int64_t x = 0;
+                if (ok[q]) {
+                    const int ch = g * n + c;
+                    x = p_ts[c_off[ch] - c_base[ch] + FDT[(size_t)c * Pcap + p]];
+                }
+                v[q] = (uint64_t)x ^ 0x8000000000000000ull;
+            }
+            res = (int64_t)(wave_select_kth<CPL>(v, ok, m / 2, whist[wave]) ^ 0x8000000000000000ull);
+        }
+        if (lane == 0) p_cts[p0 + e] = res;
     }
 }
 
@@ -1077,13 +1134,19 @@ void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw,
                        a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
 }
 
+void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n) {
+    if (R <= 0) return;
+    const int nt = (n + 63) / 64;
+    hipLaunchKernelGGL(k_wla_transpose, dim3(nt * nt, R * G), dim3(256), 0, s, R, G, C, n, a.elig, a.WLA, a.WLAT);
+}
+
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n) {
     if (R <= 0) return;
 #define TH_LAUNCH(GS, CPL, NW)                                                                                \
     {                                                                                                         \
         const int64_t threads = (int64_t)R * C * 64;                                                          \
         hipLaunchKernelGGL((k_threshold<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.elig, a.fw,   \
-                           a.WLA, a.T, C, n);                                                                 \
+                           a.WLAT, a.T, C, n);                                                                \
     }
     HGX_DISPATCH_N(n, TH_LAUNCH);
 #undef TH_LAUNCH
@@ -1095,30 +1158,36 @@ void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R,
                        a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.p_new, a.recv_list, a.counters, C, n);
 }
 
-template <int NPAD, int T>
+template <int NP>
+static void cts_small_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+    hipLaunchKernelGGL((k_cts_small<NP>), dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, a.p_new, a.p_chain, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLAT, a.FDT, a.p_ts, a.p_cts, C, n, P);
+}
+
+template <int NPAD>
 static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
-    const size_t lds = (size_t)T * (NPAD + 1) * sizeof(int64_t);
+    const size_t lds = (size_t)NPAD * 33 * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((k_cts_tile<NPAD, T>), dim3(nblk(Pn, T)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
-                       a.c_off, a.c_base, a.fw, a.WLA, a.FDT, a.p_ts, a.p_cts, C, n, P);
+    hipLaunchKernelGGL((k_cts_tile<NPAD>), dim3(nblk(Pn, 32)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLAT, a.FDT, a.p_ts, a.p_cts, C, n, P);
 }
 
 void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
     if (Pn <= 0) return;
-    if (n <= 4) cts_tile_launch<4, 64>(s, a, Pn, C, n, P);
-    else if (n <= 8) cts_tile_launch<8, 64>(s, a, Pn, C, n, P);
-    else if (n <= 16) cts_tile_launch<16, 64>(s, a, Pn, C, n, P);
-    else if (n <= 32) cts_tile_launch<32, 64>(s, a, Pn, C, n, P);
-    else if (n <= 64) cts_tile_launch<64, 64>(s, a, Pn, C, n, P);
-    else if (n <= 128) cts_tile_launch<128, 64>(s, a, Pn, C, n, P);
-    else if (n <= 256) cts_tile_launch<256, 16>(s, a, Pn, C, n, P);
-    else if (n <= 512) cts_tile_launch<512, 16>(s, a, Pn, C, n, P);
-    else cts_tile_launch<1024, 8>(s, a, Pn, C, n, P);
+    if (n <= 4) cts_small_launch<4>(s, a, Pn, C, n, P);
+    else if (n <= 8) cts_small_launch<8>(s, a, Pn, C, n, P);
+    else if (n <= 16) cts_small_launch<16>(s, a, Pn, C, n, P);
+    else if (n <= 32) cts_small_launch<32>(s, a, Pn, C, n, P);
+    else if (n <= 64) cts_tile_launch<64>(s, a, Pn, C, n, P);
+    else if (n <= 128) cts_tile_launch<128>(s, a, Pn, C, n, P);
+    else if (n <= 256) cts_tile_launch<256>(s, a, Pn, C, n, P);
+    else if (n <= 512) cts_tile_launch<512>(s, a, Pn, C, n, P);
+    else cts_tile_launch<1024>(s, a, Pn, C, n, P);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

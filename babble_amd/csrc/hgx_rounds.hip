@@ -286,6 +286,12 @@ static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
 
 hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
     const int n = A.n;
+    // many chains (batched graphs): one wave per chain; few chains: a 16-wave group per
+    // chain, so the candidates' tests of a level are spread over 16 waves
+    if (A.C < 1024 && n > 16) {
+        if (n <= 32) return step_launch<1, 16, 2, 32, 1>(s, A, kstep);
+        if (n <= 64) return step_launch<1, 16, 4, 32, 1>(s, A, kstep);
+    }
     if (n <= 16) return step_launch<1, 1, 16, 32, 4>(s, A, kstep);
     if (n <= 32) return step_launch<1, 1, 32, 32, 4>(s, A, kstep);
     if (n <= 64) return step_launch<1, 1, 64, 32, 4>(s, A, kstep);
