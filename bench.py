@@ -174,7 +174,8 @@ def main():
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
             try:
-                traffic = json.load(open(tf)).get(roof_k)
+                t = json.load(open(tf)).get(roof_k)
+                traffic = t["bytes_per_launch"] if isinstance(t, dict) else t
             except Exception:
                 traffic = None
         result = {
