@@ -262,6 +262,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemsetAsync(LA.p, 0xFF, (size_t)E * n * 4, stream));
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
     if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.alloc(2 * nunits));
+    if (la_usum.n < nunits) HGX_TRY(la_usum.alloc(nunits));
     static const bool la_debug = getenv("HGX_DEBUG_LA") != nullptr;
     la_sweeps = 0;
     la_rows = 0;
@@ -272,14 +273,15 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 8, stream));
         HGX_TRY(hipMemsetAsync(counters.p + 4, 0, 4, stream));
         kbeg(K_LA_SWEEP);
-        launch_la_sweep(stream, a, C, n, max_len, seg, la_sweeps == 0 ? 1 : 0, chg_prev, chg_cur, counters.p + 2);
+        launch_la_sweep(stream, a, C, n, max_len, seg, la_sweeps == 0 ? 1 : 0, chg_prev, chg_cur, la_usum.p,
+                        counters.p + 2);
         kend(K_LA_SWEEP, 0);
         HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 12, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
-        // algorithmic bytes of the rows this sweep recomputed: sweep 1
-        // reads the op row and writes the row (8n + 8); later sweeps also read the old row
+        // algorithmic bytes of the rows this sweep recomputed (read the two
+        // parent rows, write the row, 12n + 16; the self-parent row is the register carry)
         la_rows += h_small[0];
-        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * ((la_sweeps == 0 ? 8.0 : 12.0) * n + 8));
+        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * (12.0 * n + 16));
         la_sweeps++;
         if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows recomputed %d, units written %d, rows written %d\n", la_sweeps, h_small[0], h_small[1], h_small[2]);
         if (h_small[1] == 0) break;
@@ -302,8 +304,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kbeg(K_ROUND_GATHER);
     launch_round_gather(stream, a, 0, C, n, cap);   // W'_0 = first event of every chain
     kend(K_ROUND_GATHER, (double)C * n * 16);
-    int r = 0;
-    if (n <= 256) {
+    {   // n <= 1024 (hgx_create's limit)
         // kStepBatch step nodes (round = base + k) + one node advancing the
         // device-resident base, replayed as one hipGraph; batch i+1 is queued before
         // the host looks at batch i's "any candidate left" flag (pipelined check)
@@ -346,29 +347,6 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             checked++;
             if (!more) break;
             HGX_TRY(launch_batch());
-        }
-        r = launched * kStepBatch;
-    } else {
-        const int kBatch = 8;
-        for (;;) {
-            if (r + kBatch + 1 > r_cap) {
-                HGX_TRY(ensure_round_cap(r + kBatch + 1));
-                a = arrays();
-            }
-            for (int k = 0; k < kBatch; k++) {
-                if (r + k > 0) {
-                    kbeg(K_ROUND_GATHER);
-                    launch_round_gather(stream, a, r + k, C, n, cap);
-                    kend(K_ROUND_GATHER, (double)C * n * 16);
-                }
-                kbeg(K_ROUND_SEARCH);
-                launch_round_search(stream, a, r + k, C, n, sm);
-                kend(K_ROUND_SEARCH, 0);
-            }
-            r += kBatch;
-            HGX_TRY(hipMemcpyAsync(h_small, active.p + (r - 1), 4, hipMemcpyDeviceToHost, stream));
-            HGX_TRY(hipStreamSynchronize(stream));
-            if (h_small[0] == 0) break;
         }
     }
     out.last_round.assign(G, -1);

@@ -106,6 +106,7 @@ class Engine {
     // positions
     DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_round, p_rr;
     DBuf<uint8_t> la_chg;   // [2 x units] ping-pong dirty flags of the lastAncestors sweeps
+    DBuf<int64_t> la_usum;  // [units] sum of each unit's values (change detection)
     DBuf<int64_t> p_ts, p_cts;
     // coordinates
     DBuf<int32_t> LA, FDT;

@@ -65,13 +65,12 @@ int fd_tile_rows(int n);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
 void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg);
 // one Gauss-Seidel sweep over the dirty units (all when `first`); out[0] += rows
-// recomputed, out[1] += units written (marked in chg_cur)
+// recomputed, out[1] += units whose values changed (marked in chg_cur; usum = per-unit sums)
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int32_t* out);
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out);
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
 void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
-void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm);
 // one round step (n <= 256, hgx_rounds.hip): round = *A.d_base + kstep
 hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep);
 void launch_advance_round(hipStream_t s, int32_t* d_base, int by);

@@ -54,23 +54,23 @@ __global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const
 // LA[x] = max(LA[sp(x)], LA[op(x)]), LA[x][cr(x)] = Index(x)   (hashgraph.go:470-496)
 // A unit = (segment s of SEG rows, chain c), enumerated time-major (u = s*C + c) so
 // that earlier segments of every chain are usually finished before later ones read
-// them. Values only grow and stale reads are lower bounds (the register carry takes
-// max(computed, stored)), so repeating sweeps until one writes nothing reaches the
-// fixed point. A unit's output can only change if one of its inputs
-// changed: the previous unit of its chain (the carry) or the unit of one of its
-// op rows. Sweep t+1 therefore recomputes only units whose input units wrote in
-// sweep t (chg_prev), and marks the units it writes (chg_cur); a unit whose input
-// changes later in the same sweep is caught by the next one. Sweep 1 computes every
-// unit and skips reading the old rows (LA starts at -1).
+// them. Values only grow and stale reads are lower bounds, so a recomputed row is
+// never below its stored value and repeating sweeps until none changes anything
+// reaches the fixed point. A unit's rows can only change if one of its
+// inputs changed: the previous unit of its chain (the carry) or the unit of one of its
+// op rows; sweep t+1 recomputes only those (chg_prev), marking in chg_cur the units
+// whose values changed. "Changed" is detected without reading the old rows: a unit's
+// values only grow, so they are unchanged iff their sum equals the stored sum usum[u].
+// Per recomputed row: read the op row, write the row (8n bytes).
 template <int GS, int CPL>
 __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
                            const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
                            int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
-                           uint8_t* __restrict__ chg_cur, int32_t* __restrict__ out) {
+                           uint8_t* __restrict__ chg_cur, int64_t* __restrict__ usum, int32_t* __restrict__ out) {
     const int lane = lane_id();
     const int gl = lane % GS;
-    int rows = 0, nwr = 0;   // rows recomputed / units written (counted by group lane 0)
+    int rows = 0, nwr = 0;   // rows recomputed / units changed (counted by group lane 0)
     // grid-stride over units in time-major order (one reduction + atomic per wave)
     const int64_t nunits = (int64_t)nseg * C;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x / GS;
@@ -84,7 +84,7 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
         const int off = c_off[c];
         const int k1 = min(len, k0 + seg);
         if (!first) {
-            // dirty iff the carry unit or an op unit of one of its rows wrote last sweep
+            // dirty iff the carry unit or an op unit of one of its rows changed last sweep
             bool d = (s > 0 && gl == 0) ? chg_prev[unit - C] != 0 : false;
             for (int k = k0 + gl; k < k1; k += GS) {
                 const int u = p_opu[off + k];
@@ -101,10 +101,9 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
             const int i = gl + GS * q;
             carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
         }
-        bool wrote = false;
-        uint32_t wrow = 0;   // rows of the unit written by this lane
+        int64_t sum = 0;
         for (int k = k0; k < k1; k += 4) {
-            int32_t opr[4][CPL], old[4][CPL];
+            int32_t opr[4][CPL];
             int opp[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
@@ -114,7 +113,6 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
                 for (int q = 0; q < CPL; q++) {
                     const int i = gl + GS * q;
                     opr[u][q] = (opp[u] >= 0 && i < n) ? LA[(size_t)opp[u] * n + i] : -1;
-                    old[u][q] = (!first && k + u < k1 && i < n) ? LA[(size_t)(off + k + u) * n + i] : -1;
                 }
             }
 #pragma unroll
@@ -125,29 +123,23 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
                     const int i = gl + GS * q;
                     int32_t v = max(carry[q], opr[u][q]);
                     if (i == cl) v = base + k + u;
-                    if (i < n && v > old[u][q]) {
+                    if (i < n) {
                         LA[(size_t)(off + k + u) * n + i] = v;
-                        wrote = true;
-                        wrow |= 1u << (k + u - k0);
+                        sum += v;
                     }
-                    carry[q] = max(v, old[u][q]);
+                    carry[q] = v;
                 }
             }
         }
-        const uint64_t gm = group_mask(GS, lane / GS);
-        if ((__ballot(wrote) & gm) != 0) {
-            if (gl == 0) {
+        // group sum of the unit's values vs the stored one
+        for (int o = 1; o < GS; o <<= 1) sum += __shfl_xor(sum, o);
+        if (gl == 0) {
+            if (first || usum[unit] != sum) {
+                usum[unit] = sum;
                 chg_cur[unit] = 1;
                 nwr++;
             }
         }
-#ifdef HGX_LA_ROWSTATS
-        {   // rows written (debug statistics)
-            uint32_t wr = wrow;
-            for (int o = 1; o < GS; o <<= 1) wr |= __shfl_xor(wr, o);
-            if (gl == 0) atomicAdd(out + 2, __popc(wr));
-        }
-#endif
     }
     if (GS < 64) {
         for (int o = 32; o >= 1; o >>= 1) {
@@ -280,138 +272,9 @@ __global__ void k_wcoin(int64_t RC, int C, const int32_t* __restrict__ Bm, const
     wcoin[t] = (b < c_len[gc]) ? g_coin[p_gid[c_off[gc] + b]] : 0;
 }
 
-// search: per chain, first offset k >= Bm[r] whose event strongly sees >= SM
-// candidates of W'_r (RoundInc, hashgraph.go:285-305, with the witness set of the
-// parent round replaced by W'_r -- exact). One block per chain,
-// probes k = base + group in parallel; counts by ballot + popcount.
-template <int GS, int CPL, bool FD_LDS>
-__global__ void __launch_bounds__(256) k_round_search(int r, int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
-                               const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA,
-                               const int32_t* __restrict__ WFD, const uint8_t* __restrict__ wflag,
-                               uint8_t* __restrict__ wstat, int32_t* __restrict__ p_round,
-                               int32_t* __restrict__ active, int32_t* __restrict__ lr, int C, int n, int sm) {
-    extern __shared__ __attribute__((aligned(16))) int32_t fds[];  // [ncand x n] when FD_LDS
-    __shared__ int32_t cand[1024];
-    __shared__ int32_t s_ncand, s_first;
-    const int gc = blockIdx.x;
-    const int g = gc / n, cl = gc % n;
-    const int len = c_len[gc];
-    const int b = Bm[(size_t)r * C + gc];
-    if (b >= len) {
-        if (threadIdx.x == 0) {
-            Bm[(size_t)(r + 1) * C + gc] = len;
-            wstat[(size_t)r * C + gc] = 0;
-        }
-        return;
-    }
-    if (threadIdx.x == 0) { s_ncand = 0; s_first = 0x7fffffff; }
-    __syncthreads();
-    for (int j = threadIdx.x; j < n; j += blockDim.x)
-        if (wflag[(size_t)r * C + g * n + j] == 1) cand[atomicAdd(&s_ncand, 1)] = j;
-    __syncthreads();
-    const int ncand = s_ncand;
-    const int32_t* __restrict__ wfd_r = WFD + ((size_t)r * C + (size_t)g * n) * n;
-    if (FD_LDS) {
-        for (int idx = threadIdx.x; idx < ncand * n; idx += blockDim.x) {
-            const int w = idx / n, i = idx % n;
-            fds[idx] = wfd_r[(size_t)cand[w] * n + i];
-        }
-        __syncthreads();
-    }
-    const int lane = lane_id(), gl = lane % GS;
-    const int grp_w = lane / GS;                          // group within wave
-    const int grp = (threadIdx.x >> 6) * (64 / GS) + grp_w;  // group within block
-    const int ngroups = (blockDim.x >> 6) * (64 / GS);
-    const uint64_t gmask = group_mask(GS, grp_w);
-    const int off = c_off[gc];
-    int kbase = b, kstar = len;
-    for (;;) {
-        const int k = kbase + grp;
-        const bool valid = k < len;
-        int32_t la[CPL];
-#pragma unroll
-        for (int q = 0; q < CPL; q++) {
-            const int i = gl + GS * q;
-            la[q] = (valid && i < n) ? LA[(size_t)(off + k) * n + i] : -1;
-        }
-        int cnt = 0;
-        for (int w = 0; w < ncand; w++) {
-            const int wc = cand[w];
-            int tot = 0;
-#pragma unroll
-            for (int q = 0; q < CPL; q++) {
-                const int i = gl + GS * q;
-                int32_t f = kMaxI32;
-                if (i < n) f = FD_LDS ? fds[w * n + i] : wfd_r[(size_t)wc * n + i];
-                tot += __popcll(__ballot(la[q] >= f) & gmask);
-            }
-            if (tot >= sm && !(wc == cl && k == b)) cnt++;
-        }
-        if (valid && gl == 0 && cnt >= sm) atomicMin(&s_first, grp);
-        __syncthreads();
-        const int f = s_first;
-        if (f != 0x7fffffff) { kstar = kbase + f; break; }
-        kbase += ngroups;
-        if (kbase >= len) { kstar = len; break; }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        Bm[(size_t)(r + 1) * C + gc] = kstar;
-        wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) atomicOr(&active[r], 1);
-        if (kstar > b) atomicMax(&lr[g], r);
-    }
-    for (int k = b + (int)threadIdx.x; k < kstar; k += blockDim.x) p_round[off + k] = r;
-}
-
 // ---------------------------------------------------------------------------------
-// fame. S_j[y] = { w in W_{j-1} : StronglySee(y, w) } as bit masks (one wave per y).
-template <int GS, int CPL, int NW>
-__global__ void __launch_bounds__(256) k_fame_ss(int R, const uint8_t* __restrict__ wstat, const int32_t* __restrict__ WLA,
-                          const int32_t* __restrict__ WFD, uint64_t* __restrict__ Smat, int C, int n, int sm) {
-    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // (r-1)*C + gc
-    if (item >= (int64_t)(R - 1) * C) return;
-    const int r = (int)(item / C) + 1, gc = (int)(item % C);
-    if (wstat[(size_t)r * C + gc] != 2) return;
-    const int g = gc / n;
-    const int lane = lane_id(), gl = lane % GS, grp_w = lane / GS;
-    const int ngw = 64 / GS;
-    const uint64_t gmask = group_mask(GS, grp_w);
-    int32_t la[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; q++) {
-        const int i = gl + GS * q;
-        la[q] = (i < n) ? WLA[((size_t)r * C + gc) * n + i] : -1;
-    }
-    uint64_t mask[NW];
-#pragma unroll
-    for (int w = 0; w < NW; w++) mask[w] = 0;
-    const size_t prev = (size_t)(r - 1) * C + (size_t)g * n;
-    for (int wb = 0; wb < n; wb += ngw) {
-        const int w = wb + grp_w;
-        const bool ok = (w < n) && wstat[prev + w] == 2;
-        int tot = 0;
-#pragma unroll
-        for (int q = 0; q < CPL; q++) {
-            const int i = gl + GS * q;
-            const int32_t f = (ok && i < n) ? WFD[(prev + w) * n + i] : kMaxI32;
-            tot += __popcll(__ballot(la[q] >= f) & gmask);
-        }
-        const uint64_t bits = __ballot(ok && gl == 0 && tot >= sm);
-        for (int gg = 0; gg < ngw; gg++) {
-            if ((bits >> (gg * GS)) & 1ull) {
-                const int ww = wb + gg;
-#pragma unroll
-                for (int x = 0; x < NW; x++)
-                    if ((ww >> 6) == x) mask[x] |= 1ull << (ww & 63);
-            }
-        }
-    }
-#pragma unroll
-    for (int x = 0; x < NW; x++)
-        if (lane == x) Smat[((size_t)r * C + gc) * NW + x] = mask[x];
-}
-
+// fame. S_j[y] = { w in W_{j-1} : StronglySee(y, w) } as bit masks is produced by the
+// round step (hgx_rounds.hip) for the boundary event of every chain.
 // vote tally and decisions (DecideFame, hashgraph.go:649-730). One block per
 // (graph g, round i). Votes V[x] are bit masks over the witnesses of the previous
 // round; yays = popcount(S_j[y] & V[x]). Ties vote yes; coin rounds use middleBit.
@@ -1062,7 +925,7 @@ void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg)
 }
 
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int32_t* out) {
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out) {
     const int nseg = (max_len + seg - 1) / seg;
     if (nseg == 0) return;
 #define LA_LAUNCH(GS, CPL, NW)                                                                                \
@@ -1070,7 +933,7 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
         const int64_t threads = (int64_t)nseg * C * GS;                                                       \
         hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, s,  \
                            a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nseg, seg, first, chg_prev,  \
-                           chg_cur, out);                                                                     \
+                           chg_cur, usum, out);                                                               \
     }
     HGX_DISPATCH_N(n, LA_LAUNCH);
 #undef LA_LAUNCH
@@ -1103,33 +966,7 @@ void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
                        a.wcoin);
 }
 
-void launch_round_search(hipStream_t s, const DevArrays& a, int r, int C, int n, int sm) {
-#define RS_LAUNCH(GS, CPL, NW)                                                                                \
-    {                                                                                                         \
-        if (n <= 128) {                                                                                       \
-            const size_t lds = (size_t)n * n * sizeof(int32_t);                                               \
-            hipLaunchKernelGGL((k_round_search<GS, CPL, true>), dim3(C), dim3(256), lds, s, r, a.Bm, a.c_off, \
-                               a.c_len, a.LA, a.WFD, a.wflag, a.wstat, a.p_round, a.active, a.lr, C, n, sm);  \
-        } else {                                                                                              \
-            hipLaunchKernelGGL((k_round_search<GS, CPL, false>), dim3(C), dim3(256), 0, s, r, a.Bm, a.c_off,  \
-                               a.c_len, a.LA, a.WFD, a.wflag, a.wstat, a.p_round, a.active, a.lr, C, n, sm);  \
-        }                                                                                                     \
-    }
-    HGX_DISPATCH_N(n, RS_LAUNCH);
-#undef RS_LAUNCH
-}
-
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G) {
-    if (R > 1 && n > 256) {   // n <= 256: S rows were produced by the fused round step
-#define SS_LAUNCH(GS, CPL, NW)                                                                                \
-    {                                                                                                         \
-        const int64_t threads = (int64_t)(R - 1) * C * 64;                                                    \
-        hipLaunchKernelGGL((k_fame_ss<GS, CPL, NW>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.wstat,  \
-                           a.WLA, a.WFD, a.Smat, C, n, sm);                                                   \
-    }
-        HGX_DISPATCH_N(n, SS_LAUNCH);
-#undef SS_LAUNCH
-    }
     hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wstat, a.wcoin, a.Bm,
                        a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
 }

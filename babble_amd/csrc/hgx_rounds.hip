@@ -19,7 +19,7 @@
 // is DecideFame's S_{r+1} row (hashgraph.go:688-705) for free.
 //
 // Group = 16 waves (one chain per block) for 64 < n <= 256; one wave per chain for
-// n <= 64 (4 chains per 256-thread block).
+// n <= 64 (4 chains per 256-thread block); n > 256: k_round_step_big.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -269,6 +269,170 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     HGX_PROF(4);
 }
 
+// n in (256, 1024]: the candidates' firstDescendants rows (up to 4 MB per round) fit
+// neither in registers nor in LDS, so the search is per candidate: every wave streams
+// the FD rows of its candidates (shared by all chains of the round, so L2-resident).
+// A window of P probe rows is staged in LDS; each candidate is first tested against the
+// window's last probe (monotone: a candidate not seen there is not seen anywhere in the
+// window, and if fewer than SM are seen there the boundary is beyond the window), and
+// only the candidates seen there are binary-searched for their first seeing probe.
+// The count at probe p is the number of candidates first seen at or before p (an LDS
+// histogram). The own-chain candidate never counts at the probe that is itself.
+template <int CPL, int P>
+__global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep) {
+    constexpr int NWV = 16;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    extern __shared__ __attribute__((aligned(16))) int32_t la_s[];   // [P][n] probe rows (+ slack)
+    __shared__ int32_t hist[P + 1];
+    __shared__ uint8_t fhit[1024];               // first probe seeing candidate j (255: none / no candidate)
+    __shared__ unsigned long long s_mask[16];
+    __shared__ int32_t s_cnt[NWV];
+    __shared__ int32_t s_f;
+    const int n = A.n, C = A.C, sm = A.sm;
+    const int r = *A.d_base + kstep;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gc = blockIdx.x;
+    const int g = gc / n, cl = gc % n;
+    const int len = A.c_len[gc], off = A.c_off[gc];
+    const int b = A.Bm[(size_t)r * C + gc];
+    if (b >= len) {
+        if (threadIdx.x == 0) {
+            A.wstat[(size_t)r * C + gc] = 0;
+            A.wflag[(size_t)(r + 1) * C + gc] = 0;
+            A.Bm[(size_t)(r + 1) * C + gc] = len;
+        }
+        return;
+    }
+    const size_t crow = (size_t)r * C + (size_t)g * n;
+    auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(min(la_s[pp * n + lane + 64 * q], kMaxI32 - 1) >= fd[q]));
+        return tot >= sm && !(j == cl && kb + pp == b);
+    };
+    int kbase = b, np = 0, kstar = len, pk = 0;
+    for (;;) {
+        np = min(P, len - kbase);
+        {   // stage the window's LA rows (contiguous)
+            const int nel = np * n;
+            const int32_t* __restrict__ src = A.LA + (size_t)(off + kbase) * n;
+            if ((n & 3) == 0) {
+                for (int c0 = wave * 256; c0 < nel; c0 += NWV * 256) {
+                    const int t = c0 + lane * 4;
+                    if (t < nel)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
+                }
+            } else {
+                for (int c0 = wave * 64; c0 < nel; c0 += NWV * 64) {
+                    const int t = c0 + lane;
+                    if (t < nel)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
+                }
+            }
+        }
+        for (int t = threadIdx.x; t <= P; t += blockDim.x) hist[t] = 0;
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        // pass 1: every candidate against the window's last probe
+        int cnt = 0;
+        for (int j = wave; j < n; j += NWV) {
+            int32_t fd[CPL];
+            const bool cand = A.wflag[crow + j] == 1;
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int i = lane + 64 * q;
+                fd[q] = A.WFD[(crow + j) * n + (i < n ? i : 0)];
+                if (!cand || i >= n) fd[q] = kMaxI32;
+            }
+            const bool sl = cand && seen_at(fd, np - 1, j, kbase);
+            cnt += sl ? 1 : 0;
+            if (lane == 0) fhit[j] = sl ? (uint8_t)(np - 1) : (uint8_t)255;
+        }
+        if (lane == 0) s_cnt[wave] = cnt;
+        __syncthreads();
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < NWV; w++) tot += s_cnt[w];
+        if (tot >= sm) {
+            // pass 2: first seeing probe of the candidates seen at the last probe
+            for (int j = wave; j < n; j += NWV) {
+                if (fhit[j] == 255) continue;   // wave-uniform (written by this wave's lane 0)
+                int32_t fd[CPL];
+#pragma unroll
+                for (int q = 0; q < CPL; q++) {
+                    const int i = lane + 64 * q;
+                    fd[q] = (i < n) ? A.WFD[(crow + j) * n + i] : kMaxI32;
+                }
+                int lo = 0, hi = np - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (seen_at(fd, mid, j, kbase)) hi = mid; else lo = mid + 1;
+                }
+                if (lane == 0) {
+                    fhit[j] = (uint8_t)lo;
+                    atomicAdd(&hist[lo], 1);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int acc = 0, f = np - 1;
+                for (int pp = 0; pp < np; pp++) {
+                    acc += hist[pp];
+                    if (acc >= sm) { f = pp; break; }
+                }
+                s_f = f;
+            }
+            __syncthreads();
+            kstar = kbase + s_f;
+            pk = s_f;
+            break;
+        }
+        kbase += np;
+        if (kbase >= len) { kstar = len; break; }
+        __syncthreads();
+    }
+    for (int k = b + (int)threadIdx.x; k < kstar; k += blockDim.x) A.p_round[off + k] = r;
+    if (threadIdx.x == 0) {
+        A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
+        if (kstar < len) atomicOr(&A.active[r], 1);
+        if (kstar > b) atomicMax(&A.lr[g], r);
+        A.Bm[(size_t)(r + 1) * C + gc] = kstar;
+    }
+    if (kstar < len) {
+        // S row of the boundary event: candidates first seen at or before it
+        if (threadIdx.x < 16) s_mask[threadIdx.x] = 0;
+        __syncthreads();
+        for (int j = threadIdx.x; j < n; j += blockDim.x)
+            if (fhit[j] <= pk) atomicOr(&s_mask[j >> 6], 1ull << (j & 63));
+        __syncthreads();
+        const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
+        if ((int)threadIdx.x < A.nw) A.Smat[srow + threadIdx.x] = s_mask[threadIdx.x];
+        const int p = off + kstar;
+        const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            A.WLA[nrow + i] = la_s[pk * n + i];
+            A.WFD[nrow + i] = A.FDT[(size_t)i * A.Pcap + p];
+        }
+        if (threadIdx.x == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
+    } else if (threadIdx.x == 0) {
+        A.wflag[(size_t)(r + 1) * C + gc] = 0;
+    }
+}
+
+template <int CPL, int P>
+static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) {
+    const void* f = (const void*)k_round_step_big<CPL, P>;
+    const size_t lds = (size_t)(P * A.n + 64 * CPL) * sizeof(int32_t);
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_round_step_big<CPL, P>), dim3(A.C), dim3(1024), lds, s, A, kstep);
+    return hipGetLastError();
+}
+
 template <int CPL, int NWC, int OWN, int P, int GPB>
 static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
     const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB>;
@@ -297,6 +461,8 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
     if (n <= 64) return step_launch<1, 1, 64, 32, 4>(s, A, kstep);
     if (n <= 128) return step_launch<2, 16, 8, 32, 1>(s, A, kstep);
     if (n <= 256) return step_launch<4, 16, 16, 32, 1>(s, A, kstep);
+    if (n <= 512) return step_big_launch<8, 32>(s, A, kstep);
+    if (n <= 1024) return step_big_launch<16, 32>(s, A, kstep);
     return hipErrorInvalidValue;
 }
 

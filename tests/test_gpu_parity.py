@@ -101,7 +101,9 @@ GOSSIP = [
     (4, 1024, 1, 0, 0.0), (4, 1024, 2, 0, 0.0), (3, 600, 3, 0, 0.3), (5, 800, 4, 1, 0.0), (7, 1500, 5, 2, 0.4),
     (16, 4000, 6, 0, 0.0), (16, 4000, 7, 5, 0.5), (32, 6000, 8, 0, 0.0), (64, 12000, 9, 0, 0.0),
     (64, 12000, 10, 21, 0.2), (100, 15000, 11, 0, 0.0), (128, 20000, 12, 0, 0.0), (2, 300, 13, 0, 0.0),
-    (1, 64, 14, 0, 0.0), (200, 20000, 15, 60, 0.0), (256, 30000, 16, 0, 0.0)]
+    (1, 64, 14, 0, 0.0), (200, 20000, 15, 60, 0.0), (256, 30000, 16, 0, 0.0),
+    # n > 256: the per-candidate round step (k_round_step_big)
+    (300, 24000, 17, 0, 0.0), (512, 24000, 18, 100, 0.2), (1024, 16000, 19, 300, 0.0)]
 
 
 @pytest.mark.parametrize("n,E,seed,silent,stale", GOSSIP)
