@@ -95,6 +95,7 @@ def lib():
                                       C.POINTER(C.c_double)])
     _sig(L, "hgx_reset_stats", i32, [p])
     _sig(L, "hgx_set_kernel_timing", i32, [p, i32])
+    _sig(L, "hgx_set_coord_storage", i32, [p, i32])
     _L = L
     return L
 

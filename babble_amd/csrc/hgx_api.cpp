@@ -621,9 +621,9 @@ int32_t hgx_witness(hgx_ctx* c, int64_t x) {
 // ---- instrumentation ----------------------------------------------------------------
 int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
     if (!c || !out) return 0;
-    const int32_t m = std::min<int32_t>(cap, 6);
-    double v[6] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
-                   (double)c->eng.la_sweeps, (double)c->eng.R};
+    const int32_t m = std::min<int32_t>(cap, 7);
+    double v[7] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
+                   (double)c->eng.la_sweeps, (double)c->eng.R, (double)c->eng.compact};
     for (int32_t i = 0; i < m; i++) out[i] = v[i];
     return m;
 }
@@ -644,6 +644,12 @@ int32_t hgx_kernel_stats(hgx_ctx* c, int32_t k, char* name, int32_t name_cap, do
 int32_t hgx_reset_stats(hgx_ctx* c) {
     if (!c) return HGX_ERR_INVALID;
     for (auto& s : c->eng.kstat) s = hgx::KernelStat();
+    return HGX_OK;
+}
+
+int32_t hgx_set_coord_storage(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
+    c->eng.force_coord32 = mode == 1;
     return HGX_OK;
 }
 

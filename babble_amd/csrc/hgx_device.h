@@ -13,6 +13,30 @@ __device__ __forceinline__ uint64_t group_mask(int gs, int grp) {
     return (gs >= 64) ? ~0ull : (((1ull << gs) - 1ull) << (gs * grp));
 }
 
+// Storage of the coordinate arrays LA / FDT. int32_t: the raw values
+// (lastAncestors -1 = none, firstDescendants MaxInt32 = none). uint16_t ("compact",
+// every Index < 65534 and n even): LA stored as value + 1 (none = 0, so the encoding
+// is order-preserving and max() works on it directly), FD stored as is with
+// none = 0xFFFF. Kernels decode to int32 before comparing with raw values.
+template <typename CT>
+struct Coord;
+template <>
+struct Coord<int32_t> {
+    static constexpr int32_t kLaNone = -1;
+    __device__ __forceinline__ static int32_t la(int32_t v) { return v; }
+    __device__ __forceinline__ static int32_t enc_la(int32_t v) { return v; }
+    __device__ __forceinline__ static int32_t fd(int32_t v) { return v; }
+    __device__ __forceinline__ static int32_t enc_fd(int32_t v) { return v; }
+};
+template <>
+struct Coord<uint16_t> {
+    static constexpr int32_t kLaNone = 0;
+    __device__ __forceinline__ static int32_t la(uint32_t v) { return (int32_t)v - 1; }
+    __device__ __forceinline__ static uint16_t enc_la(int32_t v) { return (uint16_t)(v + 1); }
+    __device__ __forceinline__ static int32_t fd(uint32_t v) { return v == 0xFFFFu ? 2147483647 : (int32_t)v; }
+    __device__ __forceinline__ static uint16_t enc_fd(int32_t v) { return v >= 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)v; }
+};
+
 // order LDS accesses of one wave (lanes exchange data through LDS without a block barrier)
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -106,8 +106,9 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
     HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_opu.alloc(P)); HGX_TRY(p_round.alloc(P));
     HGX_TRY(p_rr.alloc(P)); HGX_TRY(p_ts.alloc(P)); HGX_TRY(p_cts.alloc(P));
+    fd_ld = (cap + 1) & ~(int64_t)1;
     HGX_TRY(LA.alloc(P * n));
-    HGX_TRY(FDT.alloc(P * n));
+    HGX_TRY(FDT.alloc((size_t)fd_ld * n + 128));   // slack: compact window staging reads past a column
     HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8)); HGX_TRY(order_gid.alloc(P));
     HGX_TRY(p_new.alloc(P));
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
@@ -164,7 +165,7 @@ DevArrays Engine::arrays() {
     a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
     a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
-    a.LA = LA.p; a.FDT = FDT.p;
+    a.LA = LA.p; a.FDT = FDT.p; a.compact = compact;
     a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p; a.WLAT = WLAT.p;
     a.active = active.p; a.lr = lr.p;
     a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
@@ -252,6 +253,14 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(c_len.p, chain_len.data(), C * 4, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
+    // compact (uint16) coordinates when every Index fits below the sentinels
+    // (Coord<uint16_t>, hgx_device.h) and rows are whole dwords
+    int32_t max_index = -1;
+    for (int c = 0; c < C; c++)
+        if (chain_len[c] > 0) max_index = std::max(max_index, chain_base[c] + chain_len[c] - 1);
+    static const bool force32 = getenv("HGX_COORD32") != nullptr;
+    compact = (!force32 && !force_coord32 && (n % 2) == 0 && max_index <= 65533) ? 1 : 0;
+    const size_t csz = compact ? 2 : 4;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
     const int seg = kLaSeg;
@@ -259,7 +268,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     launch_layout(stream, E, a, C, seg);
     kend(K_LAYOUT, (double)E * 64);
     // lastAncestors: fixed point from all -1, dirty-tracked sweeps (k_la_sweep)
-    HGX_TRY(hipMemsetAsync(LA.p, 0xFF, (size_t)E * n * 4, stream));
+    HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)E * n * csz, stream));
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
     if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.alloc(2 * nunits));
     if (la_usum.n < nunits) HGX_TRY(la_usum.alloc(nunits));
@@ -281,15 +290,15 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // algorithmic bytes of the rows this sweep recomputed (read the two
         // parent rows, write the row, 12n + 16; the self-parent row is the register carry)
         la_rows += h_small[0];
-        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * (12.0 * n + 16));
+        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * (3.0 * csz * n + 16));
         la_sweeps++;
         if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows recomputed %d, units written %d, rows written %d\n", la_sweeps, h_small[0], h_small[1], h_small[2]);
         if (h_small[1] == 0) break;
         if (la_sweeps > 100000) return hipErrorUnknown;
     }
     kbeg(K_FD_BUILD);
-    launch_fd_build(stream, a, C, n, max_len, cap);
-    kend(K_FD_BUILD, (double)E * 8.0 * n);
+    launch_fd_build(stream, a, C, n, max_len, fd_ld);
+    kend(K_FD_BUILD, (double)E * 2.0 * csz * n);
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     float ms = 0;
@@ -302,7 +311,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
     HGX_TRY(hipMemsetAsync(active.p, 0, (size_t)(r_cap + 1) * 4, stream));
     kbeg(K_ROUND_GATHER);
-    launch_round_gather(stream, a, 0, C, n, cap);   // W'_0 = first event of every chain
+    launch_round_gather(stream, a, 0, C, n, fd_ld);   // W'_0 = first event of every chain
     kend(K_ROUND_GATHER, (double)C * n * 16);
     {   // n <= 1024 (hgx_create's limit)
         // kStepBatch step nodes (round = base + k) + one node advancing the
@@ -318,8 +327,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             }
             if (!step_exec) {
                 RoundArgs A;
-                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = cap; A.d_base = d_round.p;
-                A.c_len = c_len.p; A.c_off = c_off.p; A.LA = LA.p; A.FDT = FDT.p; A.p_gid = p_gid.p;
+                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld; A.d_base = d_round.p;
+                A.c_len = c_len.p; A.c_off = c_off.p; A.LA = LA.p; A.FDT = FDT.p; A.compact = compact; A.p_gid = p_gid.p;
                 A.g_coin = g_coin.p;
                 A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
                 A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
@@ -420,7 +429,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     out.m = m;
     if (out.panic || m == 0) return collect_kernel_times();
     kbeg(K_CTS);
-    launch_cts(stream, a, E_div, C, n, cap);
+    launch_cts(stream, a, E_div, C, n, fd_ld);
     kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
     // sort keys: cts range, then (graph, rr)
     const unsigned long long init[2] = {~0ull, 0ull};
@@ -490,9 +499,22 @@ hipError_t Engine::get_coords(int64_t gid, int32_t* la, int32_t* fd) {
     int32_t pos = 0;
     HGX_TRY(hipMemcpyAsync(&pos, g_pos.p + gid, 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
-    HGX_TRY(hipMemcpyAsync(la, LA.p + (size_t)pos * n, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpy2DAsync(fd, 4, FDT.p + pos, (size_t)cap * 4, 4, (size_t)n, hipMemcpyDeviceToHost, stream));
-    return hipStreamSynchronize(stream);
+    if (!compact) {
+        HGX_TRY(hipMemcpyAsync(la, LA.p + (size_t)pos * n, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipMemcpy2DAsync(fd, 4, FDT.p + pos, (size_t)fd_ld * 4, 4, (size_t)n, hipMemcpyDeviceToHost, stream));
+        return hipStreamSynchronize(stream);
+    }
+    std::vector<uint16_t> l16(n), f16(n);
+    const uint16_t* la16 = (const uint16_t*)LA.p;
+    const uint16_t* fd16 = (const uint16_t*)FDT.p;
+    HGX_TRY(hipMemcpyAsync(l16.data(), la16 + (size_t)pos * n, (size_t)n * 2, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpy2DAsync(f16.data(), 2, fd16 + pos, (size_t)fd_ld * 2, 2, (size_t)n, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    for (int i = 0; i < n; i++) {   // Coord<uint16_t> decode
+        la[i] = (int32_t)l16[i] - 1;
+        fd[i] = f16[i] == 0xFFFF ? 2147483647 : (int32_t)f16[i];
+    }
+    return hipSuccess;
 }
 
 }  // namespace hgx

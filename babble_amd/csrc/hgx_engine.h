@@ -79,6 +79,8 @@ class Engine {
     int64_t cap = 0, E = 0, E_div = 0;   // E_div: events laid out by the last divide_rounds
     int32_t R = 0;
     int la_sweeps = 0;
+    int compact = 0;             // coordinates of the last DivideRounds stored as uint16
+    bool force_coord32 = false;  // hgx_set_coord_storage(1)
     int64_t la_rows = 0;   // rows recomputed over all sweeps of the last divide_rounds
     static constexpr int kLaSeg = 16;   // rows per lastAncestors unit
     hipStream_t stream = nullptr;
@@ -109,7 +111,8 @@ class Engine {
     DBuf<int64_t> la_usum;  // [units] sum of each unit's values (change detection)
     DBuf<int64_t> p_ts, p_cts;
     // coordinates
-    DBuf<int32_t> LA, FDT;
+    DBuf<int32_t> LA, FDT;   // int32 storage; uint16 views when `compact`
+    int64_t fd_ld = 0;       // FDT row stride (coordinates): cap rounded up to even
     // per round
     int32_t r_cap = 0;
     DBuf<int32_t> Bm, WLA, WFD, WLAT, Tthr, active, lr, d_round;

@@ -22,8 +22,9 @@ struct DevArrays {
     // positions
     int32_t *p_gid, *p_chain, *p_op, *p_opu, *p_round, *p_rr;
     int64_t *p_ts, *p_cts;
-    // coordinates
-    int32_t *LA, *FDT;
+    // coordinates: int32_t, or uint16_t when `compact` (Coord<CT> in hgx_device.h)
+    void *LA, *FDT;
+    int compact;
     // rounds
     int32_t* Bm;
     uint8_t *wflag, *wstat, *wcoin;   // wflag: candidate of round r exists; wstat: 2 witness, 1 jumped, 0 none
@@ -54,7 +55,9 @@ struct RoundArgs {
     int n, C, sm, nw;
     int64_t Pcap;
     const int32_t* d_base;   // device-resident round of step 0 of the current graph batch
-    const int32_t *c_len, *c_off, *LA, *FDT, *p_gid;
+    const int32_t *c_len, *c_off, *p_gid;
+    const void *LA, *FDT;   // int32_t or uint16_t (compact)
+    int compact;
     const uint8_t* g_coin;
     int32_t *Bm, *WLA, *WFD, *p_round, *active, *lr;
     uint8_t *wflag, *wstat, *wcoin;

@@ -62,12 +62,47 @@ __global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const
 // whose values changed. "Changed" is detected without reading the old rows: a unit's
 // values only grow, so they are unchanged iff their sum equals the stored sum usum[u].
 // Per recomputed row: read the op row, write the row (8n bytes).
-template <int GS, int CPL>
-__global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
+// Word view of an LA row: int32 storage = one coordinate per 32-bit word; compact
+// (uint16) storage = two coordinates per word, merged with packed 16-bit max
+// (v_pk_max_u16 on the value+1 encoding).
+template <typename CT>
+struct LaWord;
+template <>
+struct LaWord<int32_t> {
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;   // -1
+    __device__ __forceinline__ static uint32_t wmax(uint32_t a, uint32_t b) {
+        return (uint32_t)max((int32_t)a, (int32_t)b);
+    }
+    // word i holds coordinate i; the own coordinate cl gets `own`
+    __device__ __forceinline__ static uint32_t set_own(uint32_t v, int i, int cl, int32_t own) {
+        return i == cl ? (uint32_t)own : v;
+    }
+    __device__ __forceinline__ static int64_t wsum(uint32_t v) { return (int32_t)v; }
+};
+template <>
+struct LaWord<uint16_t> {
+    static constexpr uint32_t kNone = 0u;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    __device__ __forceinline__ static uint32_t wmax(uint32_t a, uint32_t b) {
+        const u16x2 m = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+        return __builtin_bit_cast(uint32_t, m);
+    }
+    __device__ __forceinline__ static uint32_t set_own(uint32_t v, int i, int cl, int32_t own) {
+        if (i != (cl >> 1)) return v;
+        const uint32_t e = (uint32_t)(own + 1) & 0xFFFFu;
+        return (cl & 1) ? ((v & 0xFFFFu) | (e << 16)) : ((v & 0xFFFF0000u) | e);
+    }
+    __device__ __forceinline__ static int64_t wsum(uint32_t v) { return (int64_t)((v & 0xFFFFu) + (v >> 16)); }
+};
+
+// LA rows as 32-bit words: nwd words per row (n for int32, n/2 for compact storage).
+template <int GS, int CPL, typename CT>
+__global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
                            const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
-                           int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
+                           int nwd, int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
                            uint8_t* __restrict__ chg_cur, int64_t* __restrict__ usum, int32_t* __restrict__ out) {
+    typedef LaWord<CT> W;
     const int lane = lane_id();
     const int gl = lane % GS;
     int rows = 0, nwr = 0;   // rows recomputed / units changed (counted by group lane 0)
@@ -95,15 +130,15 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
         }
         if (gl == 0) rows += k1 - k0;
         const int base = c_base[c], cl = c % n;
-        int32_t carry[CPL];
+        uint32_t carry[CPL];
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
             const int i = gl + GS * q;
-            carry[q] = (k0 > 0 && i < n) ? LA[(size_t)(off + k0 - 1) * n + i] : -1;
+            carry[q] = (k0 > 0 && i < nwd) ? LA[(size_t)(off + k0 - 1) * nwd + i] : W::kNone;
         }
         int64_t sum = 0;
         for (int k = k0; k < k1; k += 4) {
-            int32_t opr[4][CPL];
+            uint32_t opr[4][CPL];
             int opp[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
@@ -112,7 +147,7 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
 #pragma unroll
                 for (int q = 0; q < CPL; q++) {
                     const int i = gl + GS * q;
-                    opr[u][q] = (opp[u] >= 0 && i < n) ? LA[(size_t)opp[u] * n + i] : -1;
+                    opr[u][q] = (opp[u] >= 0 && i < nwd) ? LA[(size_t)opp[u] * nwd + i] : W::kNone;
                 }
             }
 #pragma unroll
@@ -121,11 +156,10 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
 #pragma unroll
                 for (int q = 0; q < CPL; q++) {
                     const int i = gl + GS * q;
-                    int32_t v = max(carry[q], opr[u][q]);
-                    if (i == cl) v = base + k + u;
-                    if (i < n) {
-                        LA[(size_t)(off + k + u) * n + i] = v;
-                        sum += v;
+                    const uint32_t v = W::set_own(W::wmax(carry[q], opr[u][q]), i, cl, base + k + u);
+                    if (i < nwd) {
+                        LA[(size_t)(off + k + u) * nwd + i] = v;
+                        sum += W::wsum(v);
                     }
                     carry[q] = v;
                 }
@@ -157,9 +191,11 @@ __global__ void k_la_sweep(int32_t* __restrict__ LA, const int32_t* __restrict__
 // firstDescendants: FD[(d,j)][c] = min{k : LA[(c,k)][d] >= j}, written
 // column-major FDT[c][pos(d,j)]. Block = (chain c, tile of FT rows). Each (d, j, c)
 // is written exactly once; j beyond the chain's last LA value gets MaxInt32.
-__global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__ FDT,
-                           const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
-                           const int32_t* __restrict__ c_base, int n, int FT, int64_t P) {
+template <typename CT>
+__global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT, const int32_t* __restrict__ c_off,
+                           const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int n, int nwd,
+                           int FT, int64_t P) {
+    typedef Coord<CT> K;
     extern __shared__ __attribute__((aligned(16))) int32_t sm[];
     const int c = blockIdx.x, t = blockIdx.y;
     const int len = c_len[c];
@@ -168,43 +204,49 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
     const int k0 = t * FT, k1 = min(len, k0 + FT), rows = k1 - k0;
     const int off = c_off[c], base_c = c_base[c];
     const int g = c / n, cl = c % n;
-    const int ld = n + 1;
-    // per target chain d of this graph, after the (FT+1) x ld tile
-    int32_t* m_len = sm + (FT + 1) * ld;
+    // per target chain d of this graph, then the (FT+1)-row tile (row 0 = row k0-1),
+    // rows padded to ldw words against bank conflicts of the per-d searches
+    int32_t* m_len = sm;
     int32_t* m_base = m_len + n;
     int32_t* m_off = m_base + n;
+    uint32_t* tw = (uint32_t*)(m_off + n);
+    const int ldw = nwd + 1;
+    const int ld = ldw * (int)(4 / sizeof(CT));   // in coordinates
+    const CT* __restrict__ tile = (const CT*)tw;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        sm[i] = (k0 > 0) ? LA[(size_t)(off + k0 - 1) * n + i] : -2147483647 - 1;
         m_len[i] = c_len[g * n + i];
         m_base[i] = c_base[g * n + i];
         m_off[i] = c_off[g * n + i];
     }
-    {   // the tile's rows are contiguous in LA
-        const int32_t* __restrict__ src = LA + (size_t)(off + k0) * n;
-        if ((n & 63) == 0) {
-            // straight into LDS (global_load_lds): one wave instruction = 64 ints of one row
+    {   // rows k0-1 .. k1-1 are contiguous in LA
+        const int r0 = (k0 > 0) ? 0 : 1;   // tile row 0 is unused when k0 == 0
+        const uint32_t* __restrict__ src = LA + (size_t)(off + k0 - 1) * nwd;
+        if (nwd >= 32) {
+            // straight into LDS (global_load_lds): one wave instruction = <= 64 words of one row
             typedef __attribute__((address_space(3))) void* lds_ptr_t;
             const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-            const int per_row = n >> 6;
-            for (int q = wave; q < rows * per_row; q += nwaves) {
+            const int per_row = (nwd + 63) >> 6;
+            for (int q = wave + r0 * per_row; q < (rows + 1) * per_row; q += nwaves) {
                 const int rr = q / per_row, cc = (q % per_row) << 6;
-                __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)rr * n + cc + lane),
-                                                 (lds_ptr_t)(sm + (rr + 1) * ld + cc), 4, 0, 0);
+                if (cc + lane < nwd)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)rr * nwd + cc + lane),
+                                                     (lds_ptr_t)(tw + rr * ldw + cc), 4, 0, 0);
             }
             __builtin_amdgcn_s_waitcnt(0);
         } else {
-            const int nel = rows * n;
+            const int nel = (rows + 1 - r0) * nwd;
+            const uint32_t* __restrict__ s0 = src + (size_t)r0 * nwd;
             for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * blockDim.x) {
-                int32_t v[4];
+                uint32_t v[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * blockDim.x;
-                    v[u] = (t < nel) ? src[t] : 0;
+                    const int tt = t0 + u * blockDim.x;
+                    v[u] = (tt < nel) ? s0[tt] : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * blockDim.x;
-                    if (t < nel) sm[(t / n + 1) * ld + (t % n)] = v[u];
+                    const int tt = t0 + u * blockDim.x;
+                    if (tt < nel) tw[(tt / nwd + r0) * ldw + (tt % nwd)] = v[u];
                 }
             }
         }
@@ -216,18 +258,18 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
         const int len_d = m_len[d];
         if (len_d == 0) continue;
         const int base_d = m_base[d], off_d = m_off[d];
-        int lo = (k0 > 0) ? sm[d] : base_d - 1;
+        int lo = (k0 > 0) ? K::la(tile[d]) : base_d - 1;
         if (lo < base_d - 1) lo = base_d - 1;
-        const int hi_val = (rows > 0) ? sm[rows * ld + d] : lo;
+        const int hi_val = (rows > 0) ? K::la(tile[rows * ld + d]) : lo;
         const int hi = last ? (base_d + len_d - 1) : min(hi_val, base_d + len_d - 1);
-        int32_t* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
+        CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
         for (int j = lo + 1 + lane; j <= hi; j += 64) {
             int a = 0, b = rows;
             while (a < b) {
                 const int m = (a + b) >> 1;
-                if (sm[(m + 1) * ld + d] >= j) b = m; else a = m + 1;
+                if (K::la(tile[(m + 1) * ld + d]) >= j) b = m; else a = m + 1;
             }
-            out[j] = (a < rows) ? (base_c + k0 + a) : kMaxI32;
+            out[j] = K::enc_fd((a < rows) ? (base_c + k0 + a) : kMaxI32);
         }
     }
 }
@@ -235,9 +277,10 @@ __global__ void k_fd_build(const int32_t* __restrict__ LA, int32_t* __restrict__
 // ---------------------------------------------------------------------------------
 // rounds. Step r: W'_r = {first event of each chain with round >= r}.
 // gather: copy the candidates' coordinate rows into compact per-round tables.
+template <typename CT>
 __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
-                               const int32_t* __restrict__ c_len, const int32_t* __restrict__ LA,
-                               const int32_t* __restrict__ FDT, const int32_t* __restrict__ p_gid,
+                               const int32_t* __restrict__ c_len, const CT* __restrict__ LA,
+                               const CT* __restrict__ FDT, const int32_t* __restrict__ p_gid,
                                const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
                                int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
                                int C, int n, int64_t P) {
@@ -249,8 +292,8 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
     const size_t wrow = ((size_t)r * C + gc) * n + i;
     if (b < len) {
         const int p = c_off[gc] + b;
-        WLA[wrow] = LA[(size_t)p * n + i];
-        WFD[wrow] = FDT[(size_t)i * P + p];
+        WLA[wrow] = Coord<CT>::la(LA[(size_t)p * n + i]);
+        WFD[wrow] = Coord<CT>::fd(FDT[(size_t)i * P + p]);
         if (i == 0) {
             wflag[(size_t)r * C + gc] = 1;
             wcoin[(size_t)r * C + gc] = g_coin[p_gid[p]];
@@ -472,12 +515,12 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
 
 // n <= 32: one lane per event; FDT[c][p] over consecutive p is coalesced, the
 // selection is a rank count over <= 32 values in registers.
-template <int NP>
+template <int NP, typename CT>
 __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __restrict__ p_new,
                                                    const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
                                                    const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                    const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
-                                                   const int32_t* __restrict__ FDT, const int64_t* __restrict__ p_ts,
+                                                   const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
                                                    int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= Pn || !p_new[p]) return;
@@ -493,7 +536,7 @@ __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __
         v[c] = 0;
         if (c < n && fw[fb + c] && WLAT[row + c] >= j) {
             const int ch = g * n + c;
-            v[c] = p_ts[c_off[ch] - c_base[ch] + FDT[(size_t)c * Pcap + p]];
+            v[c] = p_ts[c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)c * Pcap + p])];
             ok |= 1u << c;
         }
     }
@@ -517,12 +560,12 @@ __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __
 // kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
 // do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
 // per event: radix select of element floor(m/2) in registers.
-template <int NPAD>
+template <int NPAD, typename CT>
 __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
                                                   const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                   const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
-                                                  const int32_t* __restrict__ FDT, const int64_t* __restrict__ p_ts,
+                                                  const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
                                                   int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
     constexpr int T = 32;
     constexpr int LD = T + 1;                     // row stride of vals (bank spread)
@@ -583,7 +626,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
                 const uint8_t f = fw[fb + cc];
                 const int32_t w = WLAT[wrow + cc];
                 ok[u] = in & (f != 0) & (w >= j);
-                idx[u] = c_off[ch] - c_base[ch] + FDT[(size_t)cc * Pcap + (in ? p : 0)];
+                idx[u] = c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)cc * Pcap + (in ? p : 0)]);
             }
             int64_t x[U];
 #pragma unroll
@@ -633,7 +676,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
                 int64_t x = 0;
                 if (ok[q]) {
                     const int ch = g * n + c;
-                    x = p_ts[c_off[ch] - c_base[ch] + FDT[(size_t)c * Pcap + p]];
+                    x = p_ts[c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)c * Pcap + p])];
                 }
                 v[q] = (uint64_t)x ^ 0x8000000000000000ull;
             }
@@ -928,15 +971,21 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
                      const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out) {
     const int nseg = (max_len + seg - 1) / seg;
     if (nseg == 0) return;
-#define LA_LAUNCH(GS, CPL, NW)                                                                                \
+    const int nwd = a.compact ? n / 2 : n;
+#define LA_LAUNCH_T(GS, CPL, CT)                                                                              \
     {                                                                                                         \
         const int64_t threads = (int64_t)nseg * C * GS;                                                       \
-        hipLaunchKernelGGL((k_la_sweep<GS, CPL>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, s,  \
-                           a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nseg, seg, first, chg_prev,  \
-                           chg_cur, usum, out);                                                               \
+        hipLaunchKernelGGL((k_la_sweep<GS, CPL, CT>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, \
+                           s, (uint32_t*)a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nwd, nseg, seg, \
+                           first, chg_prev, chg_cur, usum, out);                                              \
     }
-    HGX_DISPATCH_N(n, LA_LAUNCH);
+#define LA_LAUNCH(GS, CPL, NW)                                        \
+    {                                                                 \
+        if (a.compact) LA_LAUNCH_T(GS, CPL, uint16_t) else LA_LAUNCH_T(GS, CPL, int32_t) \
+    }
+    HGX_DISPATCH_N(nwd, LA_LAUNCH);
 #undef LA_LAUNCH
+#undef LA_LAUNCH_T
 }
 
 int fd_tile_rows(int n) {
@@ -949,14 +998,25 @@ int fd_tile_rows(int n) {
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P) {
     const int ft = fd_tile_rows(n);
     const int tiles = max(1, (max_len + ft - 1) / ft);
-    const size_t lds = ((size_t)(ft + 1) * (n + 1) + 3 * (size_t)n) * sizeof(int32_t);
-    hipLaunchKernelGGL(k_fd_build, dim3(C, tiles), dim3(512), lds, s, a.LA, a.FDT, a.c_off, a.c_len, a.c_base, n,
-                       ft, P);
+    const int nwd = a.compact ? n / 2 : n;
+    const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n) * sizeof(int32_t);
+    if (a.compact)
+        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
+                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P);
+    else
+        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
+                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P);
 }
 
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
-    hipLaunchKernelGGL(k_round_gather, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm, a.c_off, a.c_len,
-                       a.LA, a.FDT, a.p_gid, a.g_coin, a.WLA, a.WFD, a.wflag, a.wcoin, C, n, P);
+    if (a.compact)
+        hipLaunchKernelGGL(k_round_gather<uint16_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
+                           a.c_off, a.c_len, (const uint16_t*)a.LA, (const uint16_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
+                           a.WFD, a.wflag, a.wcoin, C, n, P);
+    else
+        hipLaunchKernelGGL(k_round_gather<int32_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
+                           a.c_off, a.c_len, (const int32_t*)a.LA, (const int32_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
+                           a.WFD, a.wflag, a.wcoin, C, n, P);
 }
 
 void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
@@ -995,36 +1055,42 @@ void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R,
                        a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.p_new, a.recv_list, a.counters, C, n);
 }
 
-template <int NP>
+template <int NP, typename CT>
 static void cts_small_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
-    hipLaunchKernelGGL((k_cts_small<NP>), dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, a.p_new, a.p_chain, a.p_rr,
-                       a.c_off, a.c_base, a.fw, a.WLAT, a.FDT, a.p_ts, a.p_cts, C, n, P);
+    hipLaunchKernelGGL((k_cts_small<NP, CT>), dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, a.p_new, a.p_chain, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
 }
 
-template <int NPAD>
+template <int NPAD, typename CT>
 static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
     const size_t lds = (size_t)NPAD * 33 * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD, CT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((k_cts_tile<NPAD>), dim3(nblk(Pn, 32)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
-                       a.c_off, a.c_base, a.fw, a.WLAT, a.FDT, a.p_ts, a.p_cts, C, n, P);
+    hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(nblk(Pn, 32)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
+}
+
+template <typename CT>
+static void launch_cts_t(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+    if (n <= 4) cts_small_launch<4, CT>(s, a, Pn, C, n, P);
+    else if (n <= 8) cts_small_launch<8, CT>(s, a, Pn, C, n, P);
+    else if (n <= 16) cts_small_launch<16, CT>(s, a, Pn, C, n, P);
+    else if (n <= 32) cts_small_launch<32, CT>(s, a, Pn, C, n, P);
+    else if (n <= 64) cts_tile_launch<64, CT>(s, a, Pn, C, n, P);
+    else if (n <= 128) cts_tile_launch<128, CT>(s, a, Pn, C, n, P);
+    else if (n <= 256) cts_tile_launch<256, CT>(s, a, Pn, C, n, P);
+    else if (n <= 512) cts_tile_launch<512, CT>(s, a, Pn, C, n, P);
+    else cts_tile_launch<1024, CT>(s, a, Pn, C, n, P);
 }
 
 void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
     if (Pn <= 0) return;
-    if (n <= 4) cts_small_launch<4>(s, a, Pn, C, n, P);
-    else if (n <= 8) cts_small_launch<8>(s, a, Pn, C, n, P);
-    else if (n <= 16) cts_small_launch<16>(s, a, Pn, C, n, P);
-    else if (n <= 32) cts_small_launch<32>(s, a, Pn, C, n, P);
-    else if (n <= 64) cts_tile_launch<64>(s, a, Pn, C, n, P);
-    else if (n <= 128) cts_tile_launch<128>(s, a, Pn, C, n, P);
-    else if (n <= 256) cts_tile_launch<256>(s, a, Pn, C, n, P);
-    else if (n <= 512) cts_tile_launch<512>(s, a, Pn, C, n, P);
-    else cts_tile_launch<1024>(s, a, Pn, C, n, P);
+    if (a.compact) launch_cts_t<uint16_t>(s, a, Pn, C, n, P);
+    else launch_cts_t<int32_t>(s, a, Pn, C, n, P);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

@@ -73,21 +73,36 @@ __device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&f
 // strongly sees; candidate `excl` (own chain's candidate when the probe is that event)
 // never counts. Coordinates i >= n read past the row (slack / the next row), but
 // their fd is +inf (MaxInt32) and la is clamped below it, so they never count.
-template <int CPL, int OWN>
-__device__ __forceinline__ uint64_t seen_mask(const int32_t* __restrict__ row, const int32_t (&fd)[OWN][CPL],
+template <int CPL, int OWN, typename CT>
+__device__ __forceinline__ uint64_t seen_mask(const CT* __restrict__ row, const int32_t (&fd)[OWN][CPL],
                                               int lane, int sm, int excl) {
     int32_t la[CPL];
 #pragma unroll
-    for (int q = 0; q < CPL; q++) la[q] = min(row[lane + 64 * q], kMaxI32 - 1);
+    for (int q = 0; q < CPL; q++) la[q] = min(Coord<CT>::la(row[lane + 64 * q]), kMaxI32 - 1);
     const int tv = tally<CPL, OWN>(la, fd, std::make_integer_sequence<int, OWN>{});
     return __ballot(lane < OWN && tv >= sm && lane != excl);
 }
 
-template <int CPL, int NWC, int OWN, int P, int GPB>
+// LDS of one group: P LA rows (+ slack) | n FD columns of the window. Compact storage
+// stages each FD column as FDW aligned dwords (P + 2 coordinates: the window starts at
+// an odd or even position), so the staging stays dword LDS-DMA.
+template <int P, typename CT>
+struct StepLds {
+    static constexpr int FDW = P / 2 + 1;   // dwords per compact FD column
+    __host__ __device__ static constexpr size_t la_bytes(int n, int cpl) {
+        return ((size_t)(P * n + 64 * cpl) * sizeof(CT) + 15) & ~(size_t)15;
+    }
+    __host__ __device__ static constexpr size_t fd_bytes(int n) {
+        return sizeof(CT) == 4 ? (size_t)n * P * 4 : (((size_t)n * FDW * 4 + 15) & ~(size_t)15);
+    }
+    __host__ __device__ static constexpr size_t group_bytes(int n, int cpl) { return la_bytes(n, cpl) + fd_bytes(n); }
+};
+
+template <int CPL, int NWC, int OWN, int P, int GPB, typename CT>
 __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int kstep) {
     constexpr int NT = NWC * 64;   // threads per group
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ int32_t s_cnt[2][NWC];
     __shared__ unsigned long long s_mask[4];
 
@@ -101,10 +116,11 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     const int gt = (NWC == 1) ? lane : (int)threadIdx.x;  // thread within group
     const int gc = blockIdx.x * GPB + gslot;
     if (gc >= C) return;   // group-uniform; no block barrier is used when NWC == 1
-    // LDS per group: P LA rows (+ slack) | n FD columns of P
-    const int la_words = P * n + 64 * CPL;
-    int32_t* __restrict__ la_s = lds + gslot * (la_words + n * P);
-    int32_t* __restrict__ fd_s = la_s + la_words;
+    typedef StepLds<P, CT> L;
+    uint8_t* gl_lds = lds + gslot * L::group_bytes(n, CPL);
+    CT* __restrict__ la_s = (CT*)gl_lds;
+    CT* __restrict__ fd_s = (CT*)(gl_lds + L::la_bytes(n, CPL));
+    int fsh = 0;   // compact: parity of the staged window's first position
 
     HGX_PROF_BEGIN();
     HGX_PROF_COUNT(0);
@@ -122,29 +138,45 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     // stage the probe window [kbase, kbase+np): LA rows (contiguous) and FD columns
     // fd_s[i*P + p] = FDT[i][off+kbase+p] (one wave instruction = 64/P columns)
     auto stage = [&](int kbase, int np) {
-        const int nel = np * n;
-        const int32_t* __restrict__ src = A.LA + (size_t)(off + kbase) * n;
-        if ((n & 3) == 0) {
+        // LA rows [kbase, kbase+np) are contiguous: nel dwords
+        const int nel = (int)((size_t)np * n * sizeof(CT) / 4);
+        const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
+        uint32_t* la_w = (uint32_t*)la_s;
+        if (((n * (int)sizeof(CT)) & 15) == 0) {
             for (int c0 = wg * 256; c0 < nel; c0 += NWC * 256) {
                 const int t = c0 + lane * 4;
                 if (t < nel)
-                    __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_w + c0), 16, 0, 0);
             }
         } else {
             for (int c0 = wg * 64; c0 < nel; c0 += NWC * 64) {
                 const int t = c0 + lane;
-                if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
+                if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_w + c0), 4, 0, 0);
             }
         }
-        {
+        if (sizeof(CT) == 4) {
             constexpr int CPI = 64 / P;
             const int pcol = lane % P, icol = lane / P;
-            const int32_t* __restrict__ fsrc = A.FDT + off + kbase + pcol;
+            const CT* __restrict__ fsrc = (const CT*)A.FDT + off + kbase + pcol;
             for (int i0 = wg * CPI; i0 < n; i0 += NWC * CPI) {
                 const int i = i0 + icol;
                 if (i < n && pcol < np)
                     __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * A.Pcap),
                                                      (lds_ptr_t)(fd_s + i0 * P), 4, 0, 0);
+            }
+        } else {
+            // column i: dwords covering positions [p0, p0 + 2*FDW), p0 = even start
+            constexpr int FDW = L::FDW, CPI = 64 / FDW;
+            const int64_t p0 = (off + kbase) & ~1;
+            fsh = (off + kbase) & 1;
+            const int pcol = lane % FDW, icol = lane / FDW;
+            const uint32_t* __restrict__ fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
+            uint32_t* fd_w = (uint32_t*)fd_s;
+            for (int i0 = wg * CPI; i0 < n; i0 += NWC * CPI) {
+                const int i = i0 + icol;
+                if (i < n && icol < CPI)
+                    __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * (A.Pcap / 2)),
+                                                     (lds_ptr_t)(fd_w + i0 * FDW), 4, 0, 0);
             }
         }
     };
@@ -202,7 +234,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             const int ex = (kbase + mid == b) ? own_o : -1;
-            int tot = __popcll(seen_mask<CPL, OWN>(la_s + mid * n, fd, lane, sm, ex));
+            int tot = __popcll(seen_mask<CPL, OWN, CT>(la_s + mid * n, fd, lane, sm, ex));
             if (NWC > 1) {
                 if (lane == 0) s_cnt[lv & 1][wave] = tot;
                 __syncthreads();
@@ -232,7 +264,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     if (kstar < len) {
         // S row of the boundary event (the candidate of round r+1): W'_r members it strongly sees
         const int pk = kstar - kbase;   // inside the staged window
-        const uint64_t bits = seen_mask<CPL, OWN>(la_s + pk * n, fd, lane, sm, (kstar == b) ? own_o : -1);
+        const uint64_t bits = seen_mask<CPL, OWN, CT>(la_s + pk * n, fd, lane, sm, (kstar == b) ? own_o : -1);
         const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
         if (NWC == 1) {
             if (lane == 0) A.Smat[srow] = bits;
@@ -259,8 +291,9 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         // coordinate rows of the new candidate, both from the staged window
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
-            A.WLA[nrow + i] = la_s[pk * n + i];
-            A.WFD[nrow + i] = fd_s[i * P + pk];
+            A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
+            A.WFD[nrow + i] = (sizeof(CT) == 4) ? Coord<CT>::fd(fd_s[i * P + pk])
+                                                : Coord<CT>::fd(fd_s[i * 2 * L::FDW + fsh + pk]);
         }
         if (gt == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (gt == 0) {
@@ -278,11 +311,12 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 // only the candidates seen there are binary-searched for their first seeing probe.
 // The count at probe p is the number of candidates first seen at or before p (an LDS
 // histogram). The own-chain candidate never counts at the probe that is itself.
-template <int CPL, int P>
+template <int CPL, int P, typename CT>
 __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep) {
     constexpr int NWV = 16;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    extern __shared__ __attribute__((aligned(16))) int32_t la_s[];   // [P][n] probe rows (+ slack)
+    extern __shared__ __attribute__((aligned(16))) uint8_t big_lds[];
+    CT* __restrict__ la_s = (CT*)big_lds;   // [P][n] probe rows (+ slack)
     __shared__ int32_t hist[P + 1];
     __shared__ uint8_t fhit[1024];               // first probe seeing candidate j (255: none / no candidate)
     __shared__ unsigned long long s_mask[16];
@@ -307,26 +341,28 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
     auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
         int tot = 0;
 #pragma unroll
-        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(min(la_s[pp * n + lane + 64 * q], kMaxI32 - 1) >= fd[q]));
+        for (int q = 0; q < CPL; q++)
+            tot += __popcll(__ballot(min(Coord<CT>::la(la_s[pp * n + lane + 64 * q]), kMaxI32 - 1) >= fd[q]));
         return tot >= sm && !(j == cl && kb + pp == b);
     };
     int kbase = b, np = 0, kstar = len, pk = 0;
     for (;;) {
         np = min(P, len - kbase);
-        {   // stage the window's LA rows (contiguous)
-            const int nel = np * n;
-            const int32_t* __restrict__ src = A.LA + (size_t)(off + kbase) * n;
-            if ((n & 3) == 0) {
+        {   // stage the window's LA rows (contiguous, nel dwords)
+            const int nel = (int)((size_t)np * n * sizeof(CT) / 4);
+            const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
+            uint32_t* la_w = (uint32_t*)la_s;
+            if (((n * (int)sizeof(CT)) & 15) == 0) {
                 for (int c0 = wave * 256; c0 < nel; c0 += NWV * 256) {
                     const int t = c0 + lane * 4;
                     if (t < nel)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 16, 0, 0);
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_w + c0), 16, 0, 0);
                 }
             } else {
                 for (int c0 = wave * 64; c0 < nel; c0 += NWV * 64) {
                     const int t = c0 + lane;
                     if (t < nel)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_s + c0), 4, 0, 0);
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(la_w + c0), 4, 0, 0);
                 }
             }
         }
@@ -410,8 +446,8 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         const int p = off + kstar;
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            A.WLA[nrow + i] = la_s[pk * n + i];
-            A.WFD[nrow + i] = A.FDT[(size_t)i * A.Pcap + p];
+            A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
+            A.WFD[nrow + i] = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + p]);
         }
         if (threadIdx.x == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (threadIdx.x == 0) {
@@ -419,24 +455,24 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
     }
 }
 
-template <int CPL, int P>
+template <int CPL, int P, typename CT>
 static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) {
-    const void* f = (const void*)k_round_step_big<CPL, P>;
-    const size_t lds = (size_t)(P * A.n + 64 * CPL) * sizeof(int32_t);
+    const void* f = (const void*)k_round_step_big<CPL, P, CT>;
+    const size_t lds = (size_t)(P * A.n + 64 * CPL) * sizeof(CT);
     static bool attr = false;
     if (!attr) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_round_step_big<CPL, P>), dim3(A.C), dim3(1024), lds, s, A, kstep);
+    hipLaunchKernelGGL((k_round_step_big<CPL, P, CT>), dim3(A.C), dim3(1024), lds, s, A, kstep);
     return hipGetLastError();
 }
 
-template <int CPL, int NWC, int OWN, int P, int GPB>
+template <int CPL, int NWC, int OWN, int P, int GPB, typename CT>
 static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
-    const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB>;
-    const size_t lds = (size_t)GPB * (P * A.n + 64 * CPL + A.n * P) * sizeof(int32_t);
+    const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB, CT>;
+    const size_t lds = (size_t)GPB * StepLds<P, CT>::group_bytes(A.n, CPL);
     static bool attr = false;
     if (!attr) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
@@ -444,26 +480,31 @@ static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
         attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
-    hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A, kstep);
+    hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB, CT>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A, kstep);
     return hipGetLastError();
 }
 
-hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
+template <typename CT>
+static hipError_t launch_round_step_t(hipStream_t s, const RoundArgs& A, int kstep) {
     const int n = A.n;
     // many chains (batched graphs): one wave per chain; few chains: a 16-wave group per
     // chain, so the candidates' tests of a level are spread over 16 waves
     if (A.C < 1024 && n > 16) {
-        if (n <= 32) return step_launch<1, 16, 2, 32, 1>(s, A, kstep);
-        if (n <= 64) return step_launch<1, 16, 4, 32, 1>(s, A, kstep);
+        if (n <= 32) return step_launch<1, 16, 2, 32, 1, CT>(s, A, kstep);
+        if (n <= 64) return step_launch<1, 16, 4, 32, 1, CT>(s, A, kstep);
     }
-    if (n <= 16) return step_launch<1, 1, 16, 32, 4>(s, A, kstep);
-    if (n <= 32) return step_launch<1, 1, 32, 32, 4>(s, A, kstep);
-    if (n <= 64) return step_launch<1, 1, 64, 32, 4>(s, A, kstep);
-    if (n <= 128) return step_launch<2, 16, 8, 32, 1>(s, A, kstep);
-    if (n <= 256) return step_launch<4, 16, 16, 32, 1>(s, A, kstep);
-    if (n <= 512) return step_big_launch<8, 32>(s, A, kstep);
-    if (n <= 1024) return step_big_launch<16, 32>(s, A, kstep);
+    if (n <= 16) return step_launch<1, 1, 16, 32, 4, CT>(s, A, kstep);
+    if (n <= 32) return step_launch<1, 1, 32, 32, 4, CT>(s, A, kstep);
+    if (n <= 64) return step_launch<1, 1, 64, 32, 4, CT>(s, A, kstep);
+    if (n <= 128) return step_launch<2, 16, 8, 32, 1, CT>(s, A, kstep);
+    if (n <= 256) return step_launch<4, 16, 16, 32, 1, CT>(s, A, kstep);
+    if (n <= 512) return step_big_launch<8, 32, CT>(s, A, kstep);
+    if (n <= 1024) return step_big_launch<16, 32, CT>(s, A, kstep);
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
+    return A.compact ? launch_round_step_t<uint16_t>(s, A, kstep) : launch_round_step_t<int32_t>(s, A, kstep);
 }
 
 __global__ void k_advance_round(int32_t* d_base, int by) { *d_base += by; }

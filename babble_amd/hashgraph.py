@@ -232,10 +232,15 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(6, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 6)
+        out = np.zeros(7, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 7)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
-                    la_sweeps=int(out[4]), rounds=int(out[5]))
+                    la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]))
+
+    def set_coord_storage(self, mode):
+        """0 = auto (uint16 coordinates when every Index fits), 1 = always int32."""
+        if self.L.hgx_set_coord_storage(self.ctx, int(mode)) != 0:
+            raise ValueError(f"invalid coordinate storage mode {mode}")
 
     def kernel_stats(self):
         res = {}

@@ -151,7 +151,8 @@ int32_t hgx_block_hash(int64_t round_received, int32_t ntx, const uint8_t* const
                        int32_t tx_nil, uint8_t* out32);
 
 /* ---- timing / instrumentation --------------------------------------------- */
-/* per-phase device times (ms) of the last calls: coords, rounds, fame, order */
+/* per-phase device times (ms) of the last calls: coords, rounds, fame, order; then
+ * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16) */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
  * name of the kernel, summed device ms, launches, algorithmic bytes moved */
@@ -160,6 +161,10 @@ int32_t hgx_kernel_stats(hgx_ctx* ctx, int32_t k, char* name, int32_t name_cap, 
 int32_t hgx_reset_stats(hgx_ctx* ctx);
 /* time the kernels in bitmask `mask` (bit k = kernel id of hgx_kernel_stats; -1 = all) with HIP events on the context stream (bench.py roofline) */
 int32_t hgx_set_kernel_timing(hgx_ctx* ctx, int32_t mask);
+
+/* coordinate storage of later DivideRounds calls: 0 = auto (uint16 when every Index
+ * <= 65533 and n is even, else int32), 1 = always int32. Same results either way. */
+int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
 
 /* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
 /* Seeded random gossip modelled on node/core_test.go:514-537: every active peer

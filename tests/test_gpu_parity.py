@@ -17,8 +17,10 @@ def _hg(n, cap=1 << 14, graphs=1):
     return Hashgraph(n, capacity=cap, n_graphs=graphs)
 
 
-def run_gpu(t, chunk=None, cap=None):
+def run_gpu(t, chunk=None, cap=None, coord32=False):
     h = _hg(t.n, cap or max(64, t.E))
+    if coord32:
+        h.set_coord_storage(1)
     if chunk is None:
         h.insert_trace(t)
         h.RunConsensus()
@@ -110,6 +112,42 @@ GOSSIP = [
 def test_gossip_batch(n, E, seed, silent, stale):
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
     compare(run_gpu(t), hgref.oracle_run(t), t, hashes=(E <= 6000))
+
+
+def _expect_compact(t):
+    """Coordinate storage rule of DivideRounds (hgx_engine.cpp): uint16 iff n is even and
+    every Index <= 65533."""
+    return t.n % 2 == 0 and int(t.index.max(initial=0)) <= 65533
+
+
+@pytest.mark.parametrize("n,E,seed,silent,stale", [(4, 1024, 1, 0, 0.0), (16, 4000, 7, 5, 0.5), (64, 12000, 10, 21, 0.2),
+                                                   (128, 20000, 12, 0, 0.0), (256, 30000, 16, 0, 0.0),
+                                                   (512, 24000, 18, 100, 0.2)])
+def test_gossip_int32_coordinates(n, E, seed, silent, stale):
+    """The int32 coordinate path (forced) gives the same results as the oracle."""
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
+    h = run_gpu(t, coord32=True)
+    assert h.phase_times()["compact"] == 0
+    compare(h, hgref.oracle_run(t), t, hashes=False)
+
+
+@pytest.mark.parametrize("E,seed", [(120000, 31), (140000, 32)])
+def test_compact_coordinate_threshold(E, seed):
+    """Two peers with chains around the uint16 limit: the mode follows the rule and
+    both paths match the oracle."""
+    t = gtrace.gossip(2, E, seed)
+    h = run_gpu(t)
+    assert h.phase_times()["compact"] == int(_expect_compact(t))
+    compare(h, hgref.oracle_run(t), t, hashes=False)
+
+
+def test_gossip_batch_uses_compact_coordinates():
+    t = gtrace.gossip(64, 12000, 9)
+    h = run_gpu(t)
+    assert h.phase_times()["compact"] == 1
+    t = gtrace.gossip(7, 1500, 5)
+    h = run_gpu(t)
+    assert h.phase_times()["compact"] == 0
 
 
 @pytest.mark.parametrize("n,E,seed,chunk", [(4, 1024, 21, 64), (4, 600, 22, 7), (5, 700, 23, 13), (16, 2000, 24, 100),
