@@ -313,12 +313,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kbeg(K_ROUND_GATHER);
     launch_round_gather(stream, a, 0, C, n, fd_ld);   // W'_0 = first event of every chain
     kend(K_ROUND_GATHER, (double)C * n * 16);
+    int launched = 0, checked = 0;
     {   // n <= 1024 (hgx_create's limit)
         // kStepBatch step nodes (round = base + k) + one node advancing the
         // device-resident base, replayed as one hipGraph; batch i+1 is queued before
         // the host looks at batch i's "any candidate left" flag (pipelined check)
         HGX_TRY(hipMemsetAsync(d_round.p, 0, 4, stream));
-        int launched = 0, checked = 0;
         auto launch_batch = [&]() -> hipError_t {
             const int need = (launched + 2) * kStepBatch + 2;
             if (need > r_cap) {
@@ -358,6 +358,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_batch());
         }
     }
+    launch_last_round(stream, launched * kStepBatch, G, C, n, wstat.p, lr.p);
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));

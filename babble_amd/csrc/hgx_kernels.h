@@ -77,6 +77,8 @@ void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
 // one round step (n <= 256, hgx_rounds.hip): round = *A.d_base + kstep
 hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep);
 void launch_advance_round(hipStream_t s, int32_t* d_base, int by);
+// lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
+void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
 void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);

@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ int32_t s_cnt[2][NWC];
-    __shared__ unsigned long long s_mask[4];
+    __shared__ uint32_t s_wbits[NWC];
 
     const int n = A.n, C = A.C, sm = A.sm;
     const int r = *A.d_base + kstep;
@@ -215,12 +215,18 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         for (int q = 0; q < CPL; q++) {
             const int i = lane + 64 * q;
             fd[o][q] = (cand && i < n) ? fd[o][q] : kMaxI32;
+            // opaque from here on: otherwise the compiler keeps (cand && i < n) as a lane
+            // mask per candidate and ANDs it into every compare (SGPR pressure, spills)
+            asm volatile("" : "+v"(fd[o][q]));
         }
     }
     HGX_PROF(1);
     // own-chain candidate slot (never counts for the probe that is itself)
     const int own_o = (cl >= wg && (cl - wg) % NWC == 0) ? (cl - wg) / NWC : -1;
     int kbase = b, np = min(P, len - b), lo = 0, kstar = len, lv = 0;
+    // this wave's strongly-seen bits at the last probe that reached SM: the search ends on
+    // such a probe when the boundary is in the window, so it is the boundary's S row
+    uint64_t hit_bits = 0;
     bool staged = true;
     for (;;) {
         if (!staged) stage(kbase, np);
@@ -234,7 +240,8 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             const int ex = (kbase + mid == b) ? own_o : -1;
-            int tot = __popcll(seen_mask<CPL, OWN, CT>(la_s + mid * n, fd, lane, sm, ex));
+            const uint64_t bits = seen_mask<CPL, OWN, CT>(la_s + mid * n, fd, lane, sm, ex);
+            int tot = __popcll(bits);
             if (NWC > 1) {
                 if (lane == 0) s_cnt[lv & 1][wave] = tot;
                 __syncthreads();
@@ -243,7 +250,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
                 for (int w = 0; w < NWC; w++) tot += s_cnt[lv & 1][w];
                 lv++;
             }
-            if (tot >= sm) hi = mid; else lo = mid + 1;
+            if (tot >= sm) { hi = mid; hit_bits = bits; } else lo = mid + 1;
         }
         HGX_PROF(3);
         if (lo < np) { kstar = kbase + lo; break; }
@@ -257,37 +264,28 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     for (int k = b + gt; k < kstar; k += NT) A.p_round[off + k] = r;
     if (gt == 0) {
         A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) atomicOr(&A.active[r], 1);
-        if (kstar > b) atomicMax(&A.lr[g], r);
+        if (kstar < len) A.active[r] = 1;   // same value from every writer: a plain store
         A.Bm[(size_t)(r + 1) * C + gc] = kstar;
     }
+    HGX_PROF(4);
     if (kstar < len) {
-        // S row of the boundary event (the candidate of round r+1): W'_r members it strongly sees
+        // S row of the boundary event (the candidate of round r+1): W'_r members it
+        // strongly sees, bit o of wave wg = candidate j = wg + NWC*o
         const int pk = kstar - kbase;   // inside the staged window
-        const uint64_t bits = seen_mask<CPL, OWN, CT>(la_s + pk * n, fd, lane, sm, (kstar == b) ? own_o : -1);
         const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
         if (NWC == 1) {
-            if (lane == 0) A.Smat[srow] = bits;
+            if (lane == 0) A.Smat[srow] = hit_bits;
         } else {
-            if (gt < 4) s_mask[gt] = 0;
+            if (lane == 0) s_wbits[wave] = (uint32_t)hit_bits;
             __syncthreads();
-            if (lane == 0) {   // bit o of this wave = chain wg + NWC*o
-                uint64_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int o = 0; o < OWN; o++) {
-                    const int j = wg + NWC * o;
-                    const uint64_t bit = ((bits >> o) & 1ull) << (j & 63);
-#pragma unroll
-                    for (int x = 0; x < 4; x++)
-                        if ((j >> 6) == x) m[x] |= bit;
-                }
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-                    if (m[x]) atomicOr(&s_mask[x], m[x]);
+            if (wg < A.nw) {   // wave x assembles word x: candidate j = 64x + lane
+                const int j = 64 * wg + lane;
+                const bool bit = j < n && ((s_wbits[j % NWC] >> (j / NWC)) & 1u);
+                const uint64_t word = __ballot(bit);
+                if (lane == 0) A.Smat[srow + wg] = word;
             }
-            __syncthreads();
-            if (gt < A.nw) A.Smat[srow + gt] = s_mask[gt];
         }
+        HGX_PROF(5);
         // coordinate rows of the new candidate, both from the staged window
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
@@ -299,7 +297,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     } else if (gt == 0) {
         A.wflag[(size_t)(r + 1) * C + gc] = 0;
     }
-    HGX_PROF(4);
+    HGX_PROF(7);
 }
 
 // n in (256, 1024]: the candidates' firstDescendants rows (up to 4 MB per round) fit
@@ -430,8 +428,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
     for (int k = b + (int)threadIdx.x; k < kstar; k += blockDim.x) A.p_round[off + k] = r;
     if (threadIdx.x == 0) {
         A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) atomicOr(&A.active[r], 1);
-        if (kstar > b) atomicMax(&A.lr[g], r);
+        if (kstar < len) A.active[r] = 1;   // same value from every writer: a plain store
         A.Bm[(size_t)(r + 1) * C + gc] = kstar;
     }
     if (kstar < len) {
@@ -508,6 +505,32 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
 }
 
 __global__ void k_advance_round(int32_t* d_base, int by) { *d_base += by; }
+
+// lastRound per graph after the round steps: the largest r < R with a witness
+// (wstat 2) in any chain of graph g. Grid (G, ceil(R / 64)).
+__global__ void __launch_bounds__(256) k_last_round(int R, int C, int n, const uint8_t* __restrict__ wstat,
+                                                    int32_t* __restrict__ lr) {
+    __shared__ int32_t s_max[4];
+    const int g = blockIdx.x;
+    const int r0 = blockIdx.y * 64;
+    int m = -1;
+    for (int t = threadIdx.x; t < 64 * n; t += blockDim.x) {
+        const int r = r0 + t / n, i = t % n;
+        if (r < R && wstat[(size_t)r * C + (size_t)g * n + i] == 2) m = max(m, r);
+    }
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+        if (m >= 0) atomicMax(&lr[g], m);
+    }
+}
+
+void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr) {
+    if (R <= 0) return;
+    hipLaunchKernelGGL(k_last_round, dim3(G, (R + 63) / 64), dim3(256), 0, s, R, C, n, wstat, lr);
+}
 
 void launch_advance_round(hipStream_t s, int32_t* d_base, int by) {
     hipLaunchKernelGGL(k_advance_round, dim3(1), dim3(1), 0, s, d_base, by);
