@@ -282,7 +282,7 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
                                const int32_t* __restrict__ c_len, const CT* __restrict__ LA,
                                const CT* __restrict__ FDT, const int32_t* __restrict__ p_gid,
                                const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
-                               int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
+                               CT* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
                                int C, int n, int64_t P) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)C * n) return;
@@ -293,7 +293,7 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
     if (b < len) {
         const int p = c_off[gc] + b;
         WLA[wrow] = Coord<CT>::la(LA[(size_t)p * n + i]);
-        WFD[wrow] = Coord<CT>::fd(FDT[(size_t)i * P + p]);
+        WFD[wrow] = FDT[(size_t)i * P + p];   // stored form (Coord<CT>)
         if (i == 0) {
             wflag[(size_t)r * C + gc] = 1;
             wcoin[(size_t)r * C + gc] = g_coin[p_gid[p]];
@@ -1012,7 +1012,7 @@ void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n,
     if (a.compact)
         hipLaunchKernelGGL(k_round_gather<uint16_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const uint16_t*)a.LA, (const uint16_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
-                           a.WFD, a.wflag, a.wcoin, C, n, P);
+                           (uint16_t*)a.WFD, a.wflag, a.wcoin, C, n, P);
     else
         hipLaunchKernelGGL(k_round_gather<int32_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const int32_t*)a.LA, (const int32_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,

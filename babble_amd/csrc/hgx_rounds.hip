@@ -35,52 +35,95 @@ namespace hgx {
 // every block adds s_memtime deltas per phase into hgx_step_prof[8].
 #ifdef HGX_STEP_PROF
 __device__ unsigned long long hgx_step_prof[8];
-#define HGX_PROF_BEGIN() long long _pt = clock64()
-#define HGX_PROF(i)                                                       \
-    do {                                                                  \
-        if (threadIdx.x == 0) {                                           \
-            const long long _t = clock64();                               \
-            atomicAdd(&hgx_step_prof[i], (unsigned long long)(_t - _pt)); \
-            _pt = _t;                                                     \
-        }                                                                 \
+// deltas accumulate in thread 0's registers and are added to the global counters once,
+// at HGX_PROF_END (atomics inside the step would be waited for at every barrier)
+#define HGX_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define HGX_PROF(i)                            \
+    do {                                       \
+        if (threadIdx.x == 0) {                \
+            const long long _t = clock64();    \
+            _pa[i] += (unsigned long long)(_t - _pt); \
+            _pt = _t;                          \
+        }                                      \
     } while (0)
-#define HGX_PROF_COUNT(i) do { if (threadIdx.x == 0) atomicAdd(&hgx_step_prof[i], 1ull); } while (0)
+#define HGX_PROF_COUNT(i) do { if (threadIdx.x == 0) _pa[i] += 1ull; } while (0)
+#define HGX_PROF_END()                                                            \
+    do {                                                                          \
+        if (threadIdx.x == 0)                                                     \
+            for (int _i = 0; _i < 8; _i++)                                        \
+                if (_pa[_i]) atomicAdd(&hgx_step_prof[_i], _pa[_i]);              \
+    } while (0)
 #else
 #define HGX_PROF_BEGIN() (void)0
 #define HGX_PROF(i) (void)0
 #define HGX_PROF_COUNT(i) (void)0
+#define HGX_PROF_END() (void)0
 #endif
 
 // total of candidate O goes to lane O of tv (v_writelane with an immediate lane: a
 // select on lane == O would make the compiler hoist OWN 64-bit lane masks and spill them)
+// Candidates whose bit is clear in `test` are skipped (wave-uniform branch).
 template <int O, int CPL, int OWN>
-__device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int& tv) {
-    int tot = 0;
+__device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int& tv,
+                                          uint64_t test) {
+    if ((test >> O) & 1ull) {
+        int tot = 0;
 #pragma unroll
-    for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(la[q] >= fd[O][q]));
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv) : "s"(tot), "i"(O));
+        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(la[q] >= fd[O][q]));
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv) : "s"(tot), "i"(O));
+    }
 }
 
 template <int CPL, int OWN, int... O>
-__device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL],
+__device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], uint64_t test,
                                      std::integer_sequence<int, O...>) {
     int tv = 0;
-    (tally_one<O, CPL, OWN>(la, fd, tv), ...);
+    (tally_one<O, CPL, OWN>(la, fd, tv, test), ...);
     return tv;
+}
+
+// CPL consecutive coordinates of type CT as one load (VEC: n % CPL == 0, so the
+// lane's slice is aligned) or CPL scalar loads
+template <typename CT, int CPL, bool VEC>
+__device__ __forceinline__ void load_slice(const CT* __restrict__ p, uint32_t (&v)[CPL]) {
+    constexpr int B = CPL * (int)sizeof(CT);
+    if constexpr (VEC && B == 16) {
+        const uint4 x = *(const uint4*)p;
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else if constexpr (VEC && B == 8 && sizeof(CT) == 4) {
+        const uint2 x = *(const uint2*)p;
+        v[0] = x.x; v[1] = x.y;
+    } else if constexpr (VEC && B == 8) {   // 4 x uint16
+        const uint2 x = *(const uint2*)p;
+        v[0] = x.x & 0xFFFFu; v[1] = x.x >> 16; v[2] = x.y & 0xFFFFu; v[3] = x.y >> 16;
+    } else if constexpr (VEC && B == 4 && sizeof(CT) == 2) {   // 2 x uint16
+        const uint32_t x = *(const uint32_t*)p;
+        v[0] = x & 0xFFFFu; v[1] = x >> 16;
+    } else {
+#pragma unroll
+        for (int q = 0; q < CPL; q++) v[q] = (uint32_t)p[q];
+    }
 }
 
 // bitmask (bit o = candidate o held by this wave) of the candidates that the probe row
 // strongly sees; candidate `excl` (own chain's candidate when the probe is that event)
-// never counts. Coordinates i >= n read past the row (slack / the next row), but
-// their fd is +inf (MaxInt32) and la is clamped below it, so they never count.
-template <int CPL, int OWN, typename CT>
+// never counts. Only the candidates in `test` are tallied; `known` (seen at an earlier
+// probe, hence seen here) are added without a tally. Lane l holds coordinates [CPL*l, CPL*l + CPL). Coordinates i >= n read
+// past the row (slack / the next row), but their fd is +inf (MaxInt32) and la is
+// clamped below it, so they never count.
+template <int CPL, int OWN, typename CT, bool VEC>
 __device__ __forceinline__ uint64_t seen_mask(const CT* __restrict__ row, const int32_t (&fd)[OWN][CPL],
-                                              int lane, int sm, int excl) {
+                                              int lane, int sm, int excl, uint64_t test, uint64_t known) {
+    uint32_t raw[CPL];
+    load_slice<CT, CPL, VEC>(row + CPL * lane, raw);
     int32_t la[CPL];
 #pragma unroll
-    for (int q = 0; q < CPL; q++) la[q] = min(Coord<CT>::la(row[lane + 64 * q]), kMaxI32 - 1);
-    const int tv = tally<CPL, OWN>(la, fd, std::make_integer_sequence<int, OWN>{});
-    return __ballot(lane < OWN && tv >= sm && lane != excl);
+    for (int q = 0; q < CPL; q++) la[q] = min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
+    // the masks are wave-uniform: keep them in SGPRs so the skips are scalar branches
+    test = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(test >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)test);
+    const int tv = tally<CPL, OWN>(la, fd, test, std::make_integer_sequence<int, OWN>{});
+    return (__ballot(lane < OWN && tv >= sm && lane != excl) & test) | known;
 }
 
 // LDS of one group: P LA rows (+ slack) | n FD columns of the window. Compact storage
@@ -98,7 +141,7 @@ struct StepLds {
     __host__ __device__ static constexpr size_t group_bytes(int n, int cpl) { return la_bytes(n, cpl) + fd_bytes(n); }
 };
 
-template <int CPL, int NWC, int OWN, int P, int GPB, typename CT>
+template <int CPL, int NWC, int OWN, int P, int GPB, typename CT, bool VEC>
 __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int kstep) {
     constexpr int NT = NWC * 64;   // threads per group
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -190,16 +233,19 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const int j = lane + 64 * q;
         fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
     }
+    // WFD rows are stored as CT (compact: uint16 with 0xFFFF = none); lane l loads
+    // coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
     int32_t fd[OWN][CPL];
+    uint64_t cmask = 0;   // this wave's slots that hold a candidate
+    const int lc = (CPL * lane < n) ? CPL * lane : 0;
 #pragma unroll
     for (int o = 0; o < OWN; o++) {
         const int j = wg + NWC * o;
         const int jj = j < n ? j : 0;
+        uint32_t raw[CPL];
+        load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + jj) * n + lc, raw);
 #pragma unroll
-        for (int q = 0; q < CPL; q++) {
-            const int i = lane + 64 * q;
-            fd[o][q] = A.WFD[(crow + jj) * n + (i < n ? i : 0)];
-        }
+        for (int q = 0; q < CPL; q++) fd[o][q] = Coord<CT>::fd(raw[q]);
     }
 #pragma unroll
     for (int o = 0; o < OWN; o++) {
@@ -211,9 +257,10 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
             if (q == (j >> 6)) f = v;
         }
         const bool cand = (j < n) && f == 1u;
+        cmask |= (uint64_t)cand << o;
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
-            const int i = lane + 64 * q;
+            const int i = CPL * lane + q;
             fd[o][q] = (cand && i < n) ? fd[o][q] : kMaxI32;
             // opaque from here on: otherwise the compiler keeps (cand && i < n) as a lane
             // mask per candidate and ANDs it into every compare (SGPR pressure, spills)
@@ -227,6 +274,10 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     // this wave's strongly-seen bits at the last probe that reached SM: the search ends on
     // such a probe when the boundary is in the window, so it is the boundary's S row
     uint64_t hit_bits = 0;
+    // monotone along the chain: candidates seen at the last probe below the boundary
+    // (s_lo) are seen at every later probe; candidates not seen at the first probe
+    // that reached SM (s_hi) are not seen below it. Only s_hi & ~s_lo are tallied.
+    uint64_t s_lo = 0;
     bool staged = true;
     for (;;) {
         if (!staged) stage(kbase, np);
@@ -237,10 +288,12 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         HGX_PROF_COUNT(6);
         lo = 0;
         int hi = np;
+        uint64_t s_hi = cmask;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             const int ex = (kbase + mid == b) ? own_o : -1;
-            const uint64_t bits = seen_mask<CPL, OWN, CT>(la_s + mid * n, fd, lane, sm, ex);
+            const uint64_t bits =
+                seen_mask<CPL, OWN, CT, VEC>(la_s + mid * n, fd, lane, sm, ex, s_hi & ~s_lo, s_lo);
             int tot = __popcll(bits);
             if (NWC > 1) {
                 if (lane == 0) s_cnt[lv & 1][wave] = tot;
@@ -250,7 +303,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
                 for (int w = 0; w < NWC; w++) tot += s_cnt[lv & 1][w];
                 lv++;
             }
-            if (tot >= sm) { hi = mid; hit_bits = bits; } else lo = mid + 1;
+            if (tot >= sm) { hi = mid; hit_bits = bits; s_hi = bits; } else { lo = mid + 1; s_lo = bits; }
         }
         HGX_PROF(3);
         if (lo < np) { kstar = kbase + lo; break; }
@@ -290,14 +343,14 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            A.WFD[nrow + i] = (sizeof(CT) == 4) ? Coord<CT>::fd(fd_s[i * P + pk])
-                                                : Coord<CT>::fd(fd_s[i * 2 * L::FDW + fsh + pk]);
+            ((CT*)A.WFD)[nrow + i] = (sizeof(CT) == 4) ? fd_s[i * P + pk] : fd_s[i * 2 * L::FDW + fsh + pk];
         }
         if (gt == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (gt == 0) {
         A.wflag[(size_t)(r + 1) * C + gc] = 0;
     }
     HGX_PROF(7);
+    HGX_PROF_END();
 }
 
 // n in (256, 1024]: the candidates' firstDescendants rows (up to 4 MB per round) fit
@@ -375,7 +428,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
 #pragma unroll
             for (int q = 0; q < CPL; q++) {
                 const int i = lane + 64 * q;
-                fd[q] = A.WFD[(crow + j) * n + (i < n ? i : 0)];
+                fd[q] = Coord<CT>::fd(((const CT*)A.WFD)[(crow + j) * n + (i < n ? i : 0)]);
                 if (!cand || i >= n) fd[q] = kMaxI32;
             }
             const bool sl = cand && seen_at(fd, np - 1, j, kbase);
@@ -395,7 +448,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
 #pragma unroll
                 for (int q = 0; q < CPL; q++) {
                     const int i = lane + 64 * q;
-                    fd[q] = (i < n) ? A.WFD[(crow + j) * n + i] : kMaxI32;
+                    fd[q] = (i < n) ? Coord<CT>::fd(((const CT*)A.WFD)[(crow + j) * n + i]) : kMaxI32;
                 }
                 int lo = 0, hi = np - 1;
                 while (lo < hi) {
@@ -444,7 +497,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            A.WFD[nrow + i] = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + p]);
+            ((CT*)A.WFD)[nrow + i] = ((const CT*)A.FDT)[(size_t)i * A.Pcap + p];
         }
         if (threadIdx.x == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (threadIdx.x == 0) {
@@ -466,9 +519,9 @@ static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) 
     return hipGetLastError();
 }
 
-template <int CPL, int NWC, int OWN, int P, int GPB, typename CT>
-static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
-    const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB, CT>;
+template <int CPL, int NWC, int OWN, int P, int GPB, typename CT, bool VEC>
+static hipError_t step_launch_v(hipStream_t s, const RoundArgs& A, int kstep) {
+    const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB, CT, VEC>;
     const size_t lds = (size_t)GPB * StepLds<P, CT>::group_bytes(A.n, CPL);
     static bool attr = false;
     if (!attr) {
@@ -477,8 +530,15 @@ static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
         attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
-    hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB, CT>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A, kstep);
+    hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB, CT, VEC>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A,
+                       kstep);
     return hipGetLastError();
+}
+
+template <int CPL, int NWC, int OWN, int P, int GPB, typename CT>
+static hipError_t step_launch(hipStream_t s, const RoundArgs& A, int kstep) {
+    if (CPL == 1 || A.n % CPL == 0) return step_launch_v<CPL, NWC, OWN, P, GPB, CT, true>(s, A, kstep);
+    return step_launch_v<CPL, NWC, OWN, P, GPB, CT, false>(s, A, kstep);
 }
 
 template <typename CT>
