@@ -64,7 +64,7 @@ struct RoundArgs {
     uint64_t* Smat;
 };
 
-int fd_tile_rows(int n);
+int fd_tile_rows(int n, int compact);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
 void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg);
 // one Gauss-Seidel sweep over the dirty units (all when `first`); out[0] += rows

@@ -263,13 +263,29 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
         const int hi_val = (rows > 0) ? K::la(tile[rows * ld + d]) : lo;
         const int hi = last ? (base_d + len_d - 1) : min(hi_val, base_d + len_d - 1);
         CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
-        for (int j = lo + 1 + lane; j <= hi; j += 64) {
-            int a = 0, b = rows;
-            while (a < b) {
-                const int m = (a + b) >> 1;
-                if (K::la(tile[(m + 1) * ld + d]) >= j) b = m; else a = m + 1;
+        // lane k = tile row k: the row is the first descendant of d's events j in
+        // (v[k-1], v[k]] (v = LA[(c, k0+k)][d], monotone in k) -- one LDS read per lane and
+        // a short range of coalesced writes, instead of a binary search per j
+        const int vmax = base_d + len_d - 1;
+        int v = (lane < rows) ? min(max(K::la(tile[(lane + 1) * ld + d]), lo), vmax) : hi_val;
+        int prev = __shfl_up(v, 1);
+        if (lane == 0) prev = lo;
+        const int L = (lane < rows) ? v - prev : 0;
+        if (__ballot(L > 16) == 0) {
+            const CT val = K::enc_fd(base_c + k0 + lane);
+            for (int t = 0; __ballot(t < L) != 0; t++)
+                if (t < L) out[prev + 1 + t] = val;
+            if (last)
+                for (int j = max(lo, min(hi_val, vmax)) + 1 + lane; j <= hi; j += 64) out[j] = K::enc_fd(kMaxI32);
+        } else {   // long ranges (a fast chain d seen by a slow chain c): per-j search
+            for (int j = lo + 1 + lane; j <= hi; j += 64) {
+                int a = 0, b = rows;
+                while (a < b) {
+                    const int m = (a + b) >> 1;
+                    if (K::la(tile[(m + 1) * ld + d]) >= j) b = m; else a = m + 1;
+                }
+                out[j] = K::enc_fd((a < rows) ? (base_c + k0 + a) : kMaxI32);
             }
-            out[j] = K::enc_fd((a < rows) ? (base_c + k0 + a) : kMaxI32);
         }
     }
 }
@@ -988,15 +1004,16 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 #undef LA_LAUNCH_T
 }
 
-int fd_tile_rows(int n) {
-    int ft = 8192 / n;   // ~33 KB of LDS per block: 4 blocks (32 waves) per CU
+int fd_tile_rows(int n, int compact) {
+    // <= 64 rows (one per lane), ~33 KB of LDS per block: 4 blocks (32 waves) per CU
+    int ft = (compact ? 16384 : 8192) / n;
     if (ft > 64) ft = 64;
     if (ft < 4) ft = 4;
     return ft;
 }
 
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P) {
-    const int ft = fd_tile_rows(n);
+    const int ft = fd_tile_rows(n, a.compact);
     const int tiles = max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
     const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n) * sizeof(int32_t);
