@@ -116,7 +116,6 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
     HGX_TRY(minmax.alloc(2));
     HGX_TRY(lr.alloc(G));
-    HGX_TRY(d_round.alloc(1));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[1], hipEventDisableTiming));
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
@@ -315,10 +314,10 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int launched = 0, checked = 0;
     {   // n <= 1024 (hgx_create's limit)
-        // kStepBatch step nodes (round = base + k) + one node advancing the
-        // device-resident base, replayed as one hipGraph; batch i+1 is queued before
-        // the host looks at batch i's "any candidate left" flag (pipelined check)
-        HGX_TRY(hipMemsetAsync(d_round.p, 0, 4, stream));
+        // kStepBatch step nodes replayed as one hipGraph; before each replay the nodes'
+        // round arguments are rewritten (hipGraphExecKernelNodeSetParams), so a step
+        // knows its round without a dependent device load. Batch i+1 is queued before
+        // the host looks at batch i's "any candidate left" flag (pipelined check).
         auto launch_batch = [&]() -> hipError_t {
             const int need = (launched + 2) * kStepBatch + 2;
             if (need > r_cap) {
@@ -326,17 +325,50 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 a = arrays();
             }
             if (!step_exec) {
-                RoundArgs A;
-                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld; A.d_base = d_round.p;
+                RoundArgs& A = step_args;
+                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld;
                 A.c_len = c_len.p; A.c_off = c_off.p; A.LA = LA.p; A.FDT = FDT.p; A.compact = compact; A.p_gid = p_gid.p;
                 A.g_coin = g_coin.p;
                 A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
                 A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
                 for (int k = 0; k < kStepBatch; k++) (void)launch_round_step(stream, A, k);
-                launch_advance_round(stream, d_round.p, kStepBatch);
                 HGX_TRY(hipStreamEndCapture(stream, &step_graph));
                 HGX_TRY(hipGraphInstantiate(&step_exec, step_graph, nullptr, nullptr, 0));
+                // the step nodes in launch order (a linear chain)
+                size_t nn = 0;
+                HGX_TRY(hipGraphGetNodes(step_graph, nullptr, &nn));
+                std::vector<hipGraphNode_t> nodes(nn);
+                HGX_TRY(hipGraphGetNodes(step_graph, nodes.data(), &nn));
+                step_nodes.clear();
+                step_params.clear();
+                hipGraphNode_t cur = nullptr;
+                for (auto nd : nodes) {
+                    size_t nd_deps = 0;
+                    HGX_TRY(hipGraphNodeGetDependencies(nd, nullptr, &nd_deps));
+                    if (nd_deps == 0) cur = nd;
+                }
+                while (cur) {
+                    hipKernelNodeParams kp;
+                    HGX_TRY(hipGraphKernelNodeGetParams(cur, &kp));
+                    step_nodes.push_back(cur);
+                    step_params.push_back(kp);
+                    size_t nd_out = 0;
+                    HGX_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd_out));
+                    if (nd_out == 0) break;
+                    std::vector<hipGraphNode_t> outs(nd_out);
+                    HGX_TRY(hipGraphNodeGetDependentNodes(cur, outs.data(), &nd_out));
+                    cur = outs[0];
+                }
+                if ((int)step_nodes.size() != kStepBatch) return hipErrorUnknown;
+            }
+            for (int k = 0; k < kStepBatch; k++) {
+                step_round[k] = launched * kStepBatch + k;
+                void* args[2] = {(void*)&step_args, (void*)&step_round[k]};
+                hipKernelNodeParams kp = step_params[k];
+                kp.kernelParams = args;
+                kp.extra = nullptr;
+                HGX_TRY(hipGraphExecKernelNodeSetParams(step_exec, step_nodes[k], &kp));
             }
             kbeg(K_ROUND_SEARCH);
             HGX_TRY(hipGraphLaunch(step_exec, stream));

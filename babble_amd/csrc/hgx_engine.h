@@ -115,10 +115,14 @@ class Engine {
     int64_t fd_ld = 0;       // FDT row stride (coordinates): cap rounded up to even
     // per round
     int32_t r_cap = 0;
-    DBuf<int32_t> Bm, WLA, WFD, WLAT, Tthr, active, lr, d_round;
+    DBuf<int32_t> Bm, WLA, WFD, WLAT, Tthr, active, lr;
     hipEvent_t flag_ev[2] = {nullptr, nullptr};
     hipGraph_t step_graph = nullptr;       // kStepBatch round steps, replayed per batch
     hipGraphExec_t step_exec = nullptr;
+    std::vector<hipGraphNode_t> step_nodes;      // the kStepBatch step nodes, in order
+    std::vector<hipKernelNodeParams> step_params;
+    RoundArgs step_args{};
+    int32_t step_round[64] = {};
     void drop_step_graph();
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;

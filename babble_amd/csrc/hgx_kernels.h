@@ -54,7 +54,6 @@ struct DevArrays {
 struct RoundArgs {
     int n, C, sm, nw;
     int64_t Pcap;
-    const int32_t* d_base;   // device-resident round of step 0 of the current graph batch
     const int32_t *c_len, *c_off, *p_gid;
     const void *LA, *FDT;   // int32_t or uint16_t (compact)
     int compact;
@@ -74,9 +73,8 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
 void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
-// one round step (n <= 256, hgx_rounds.hip): round = *A.d_base + kstep
-hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep);
-void launch_advance_round(hipStream_t s, int32_t* d_base, int by);
+// one round step (hgx_rounds.hip) of round r
+hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only

@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     __shared__ uint32_t s_wbits[NWC];
 
     const int n = A.n, C = A.C, sm = A.sm;
-    const int r = *A.d_base + kstep;
+    const int r = kstep;   // the round (graph node argument, rewritten per batch)
     // readfirstlane: the compiler does not know threadIdx.x >> 6 is wave-uniform, and
     // everything derived from it (chain, window, search bounds) would go to VGPRs
     const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -168,6 +168,38 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     HGX_PROF_BEGIN();
     HGX_PROF_COUNT(0);
     const int g = gc / n, cl = gc % n;
+    constexpr int rot = 0;   // slot o of wave wg holds candidate j = wg + NWC*((o + rot) % OWN)
+    // candidates of this wave: chains j = wg + NWC*o. Their rows do not depend on this
+    // chain's boundary, so they are loaded first (their latency overlaps the boundary
+    // load and the window staging); unconditionally (every slot of WFD exists), masked
+    // by the candidate flag after the window wait.
+    const size_t crow = (size_t)r * C + (size_t)g * n;
+    uint32_t fl[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int j = lane + 64 * q;
+        fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
+    }
+    // WFD rows are stored as CT (compact: uint16 with 0xFFFF = none); lane l loads
+    // coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
+    uint32_t fdr[OWN][CPL];
+    const int lc = (CPL * lane < n) ? CPL * lane : 0;
+#pragma unroll
+    for (int o = 0; o < OWN; o++) {
+        const int j = wg + NWC * ((o + rot) % OWN);
+        const int jj = j < n ? j : 0;
+        load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + jj) * n + lc, fdr[o]);
+#ifdef HGX_EXP_WFD2   // experiment: the candidate rows loaded twice (bandwidth vs latency)
+        {
+            uint32_t t2[CPL];
+            load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + ((jj + 5) % n)) * n + lc, t2);
+            uint32_t z = 0;
+            asm volatile("" : "+v"(z));
+#pragma unroll
+            for (int q = 0; q < CPL; q++) fdr[o][q] |= t2[q] & z;
+        }
+#endif
+    }
     const int len = A.c_len[gc], off = A.c_off[gc];
     const int b = A.Bm[(size_t)r * C + gc];
     if (b >= len) {
@@ -223,33 +255,20 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
             }
         }
     };
+    HGX_PROF(4);
     stage(b, min(P, len - b));   // in flight while the candidate rows load
-    // candidates of this wave: chains j = wg + NWC*o. Rows are loaded unconditionally
-    // (every slot of WFD exists) and masked by the candidate flag: no exec branches.
-    const size_t crow = (size_t)r * C + (size_t)g * n;
-    uint32_t fl[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; q++) {
-        const int j = lane + 64 * q;
-        fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
-    }
-    // WFD rows are stored as CT (compact: uint16 with 0xFFFF = none); lane l loads
-    // coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
+#ifdef HGX_EXP_STAGE2   // experiment: the window staged twice
+    stage(b, min(P, len - b));
+#endif
+    HGX_PROF(5);
+    // window landed (and the candidate rows with it): everyone may read the LDS window
+    __builtin_amdgcn_s_waitcnt(0);
+    if (NWC == 1) wave_lds_fence(); else __syncthreads();
     int32_t fd[OWN][CPL];
     uint64_t cmask = 0;   // this wave's slots that hold a candidate
-    const int lc = (CPL * lane < n) ? CPL * lane : 0;
 #pragma unroll
     for (int o = 0; o < OWN; o++) {
-        const int j = wg + NWC * o;
-        const int jj = j < n ? j : 0;
-        uint32_t raw[CPL];
-        load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + jj) * n + lc, raw);
-#pragma unroll
-        for (int q = 0; q < CPL; q++) fd[o][q] = Coord<CT>::fd(raw[q]);
-    }
-#pragma unroll
-    for (int o = 0; o < OWN; o++) {
-        const int j = wg + NWC * o;
+        const int j = wg + NWC * ((o + rot) % OWN);
         uint32_t f = 0;
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
@@ -261,7 +280,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
             const int i = CPL * lane + q;
-            fd[o][q] = (cand && i < n) ? fd[o][q] : kMaxI32;
+            fd[o][q] = (cand && i < n) ? Coord<CT>::fd(fdr[o][q]) : kMaxI32;
             // opaque from here on: otherwise the compiler keeps (cand && i < n) as a lane
             // mask per candidate and ANDs it into every compare (SGPR pressure, spills)
             asm volatile("" : "+v"(fd[o][q]));
@@ -269,7 +288,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     }
     HGX_PROF(1);
     // own-chain candidate slot (never counts for the probe that is itself)
-    const int own_o = (cl >= wg && (cl - wg) % NWC == 0) ? (cl - wg) / NWC : -1;
+    const int own_o = (cl >= wg && (cl - wg) % NWC == 0) ? ((cl - wg) / NWC - rot + OWN) % OWN : -1;
     int kbase = b, np = min(P, len - b), lo = 0, kstar = len, lv = 0;
     // this wave's strongly-seen bits at the last probe that reached SM: the search ends on
     // such a probe when the boundary is in the window, so it is the boundary's S row
@@ -280,18 +299,22 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     uint64_t s_lo = 0;
     bool staged = true;
     for (;;) {
-        if (!staged) stage(kbase, np);
+        if (!staged) {
+            stage(kbase, np);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (NWC == 1) wave_lds_fence(); else __syncthreads();
+        }
         staged = false;
-        __builtin_amdgcn_s_waitcnt(0);
-        if (NWC == 1) wave_lds_fence(); else __syncthreads();
         HGX_PROF(2);
-        HGX_PROF_COUNT(6);
         lo = 0;
         int hi = np;
         uint64_t s_hi = cmask;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             const int ex = (kbase + mid == b) ? own_o : -1;
+#ifdef HGX_STEP_PROF
+            if (threadIdx.x == 0) _pa[6] += (unsigned long long)__popcll(s_hi & ~s_lo) * 1000ull + 1ull;
+#endif
             const uint64_t bits =
                 seen_mask<CPL, OWN, CT, VEC>(la_s + mid * n, fd, lane, sm, ex, s_hi & ~s_lo, s_lo);
             int tot = __popcll(bits);
@@ -320,25 +343,28 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         if (kstar < len) A.active[r] = 1;   // same value from every writer: a plain store
         A.Bm[(size_t)(r + 1) * C + gc] = kstar;
     }
-    HGX_PROF(4);
+    HGX_PROF(7);
     if (kstar < len) {
         // S row of the boundary event (the candidate of round r+1): W'_r members it
-        // strongly sees, bit o of wave wg = candidate j = wg + NWC*o
+        // strongly sees, bit o of wave wg = candidate j = wg + NWC*((o + rot) % OWN)
         const int pk = kstar - kbase;   // inside the staged window
         const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
-        if (NWC == 1) {
-            if (lane == 0) A.Smat[srow] = hit_bits;
+        if (NWC == 1) {   // j = (o + rot) % OWN: rotate left by rot within OWN bits
+            const uint64_t msk = (OWN >= 64) ? ~0ull : ((1ull << OWN) - 1ull);
+            const uint64_t hb = hit_bits & msk;
+            const uint64_t rb = rot ? (((hb << rot) | (hb >> (OWN - rot))) & msk) : hb;
+            if (lane == 0) A.Smat[srow] = rb;
         } else {
             if (lane == 0) s_wbits[wave] = (uint32_t)hit_bits;
             __syncthreads();
             if (wg < A.nw) {   // wave x assembles word x: candidate j = 64x + lane
                 const int j = 64 * wg + lane;
-                const bool bit = j < n && ((s_wbits[j % NWC] >> (j / NWC)) & 1u);
+                const bool bit = j < n && ((s_wbits[j % NWC] >> ((j / NWC - rot + OWN) % OWN)) & 1u);
                 const uint64_t word = __ballot(bit);
                 if (lane == 0) A.Smat[srow + wg] = word;
             }
         }
-        HGX_PROF(5);
+        HGX_PROF(7);
         // coordinate rows of the new candidate, both from the staged window
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
@@ -374,7 +400,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
     __shared__ int32_t s_cnt[NWV];
     __shared__ int32_t s_f;
     const int n = A.n, C = A.C, sm = A.sm;
-    const int r = *A.d_base + kstep;
+    const int r = kstep;   // the round (graph node argument, rewritten per batch)
     const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gc = blockIdx.x;
     const int g = gc / n, cl = gc % n;
@@ -564,7 +590,7 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep) {
     return A.compact ? launch_round_step_t<uint16_t>(s, A, kstep) : launch_round_step_t<int32_t>(s, A, kstep);
 }
 
-__global__ void k_advance_round(int32_t* d_base, int by) { *d_base += by; }
+
 
 // lastRound per graph after the round steps: the largest r < R with a witness
 // (wstat 2) in any chain of graph g. Grid (G, ceil(R / 64)).
@@ -592,15 +618,12 @@ void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t*
     hipLaunchKernelGGL(k_last_round, dim3(G, (R + 63) / 64), dim3(256), 0, s, R, C, n, wstat, lr);
 }
 
-void launch_advance_round(hipStream_t s, int32_t* d_base, int by) {
-    hipLaunchKernelGGL(k_advance_round, dim3(1), dim3(1), 0, s, d_base, by);
-}
 
 #ifdef HGX_STEP_PROF
 void step_prof_dump() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_step_prof), sizeof(h)) != hipSuccess) return;
-    fprintf(stderr, "[hgx] round phases (clk sums; 0 = block-rounds, 6 = windows):");
+    fprintf(stderr, "[hgx] round phases (clk sums; 0 = block-rounds, 6 = wave-0 tallies*1000 + levels):");
     for (int i = 0; i < 8; i++) fprintf(stderr, " %d:%llu", i, h[i]);
     fprintf(stderr, "\n");
 }
