@@ -77,6 +77,43 @@ def cpu_baseline(cfg, budget_s=20.0):
                        f"ordered in {dt:.2f}s on {platform.processor() or platform.machine()}")
 
 
+class Reducer:
+    """Timing/count reductions over the ranks of a multi-GPU run (one replica per rank,
+    DESIGN.md §6: no data-path collective). backend "nccl" (RCCL) on GPUs; "gloo" keeps
+    the same code testable on CPU (tests/test_dist.py)."""
+
+    def __init__(self, world, local_rank=0, backend="nccl"):
+        self.world, self.dist, self.device = world, None, "cpu"
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend == "nccl":
+                torch.cuda.set_device(local_rank)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                self.device = f"cuda:{local_rank}"
+            elif not dist.is_initialized():
+                dist.init_process_group(backend)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def _reduce(self, x, op):
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, x):
+        return x if self.dist is None else self._reduce(x, self.dist.ReduceOp.MAX)
+
+    def sum(self, x):
+        return x if self.dist is None else self._reduce(x, self.dist.ReduceOp.SUM)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,32 +126,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def max_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+    red = Reducer(world, local_rank)
+    barrier, max_over_ranks, sum_over_ranks = red.barrier, red.max, red.sum
+    dist = red.dist
 
     from babble_amd.hashgraph import Hashgraph
     n, E, G, *_ = CONFIGS[args.config]
