@@ -462,7 +462,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     out.m = m;
     if (out.panic || m == 0) return collect_kernel_times();
     kbeg(K_CTS);
-    launch_cts(stream, a, E_div, C, n, fd_ld);
+    launch_cts(stream, a, E_div, C, n, fd_ld, max_len);
     kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
     // sort keys: cts range, then (graph, rr)
     const unsigned long long init[2] = {~0ull, 0ull};

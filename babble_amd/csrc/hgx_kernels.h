@@ -82,7 +82,8 @@ void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw,
 void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
-void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P);
+// time-major tiles of 32 positions per chain (max_len = longest chain)
+void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len);
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);

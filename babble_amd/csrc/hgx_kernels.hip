@@ -298,7 +298,7 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
                                const int32_t* __restrict__ c_len, const CT* __restrict__ LA,
                                const CT* __restrict__ FDT, const int32_t* __restrict__ p_gid,
                                const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
-                               CT* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
+                               int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
                                int C, int n, int64_t P) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)C * n) return;
@@ -309,7 +309,7 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
     if (b < len) {
         const int p = c_off[gc] + b;
         WLA[wrow] = Coord<CT>::la(LA[(size_t)p * n + i]);
-        WFD[wrow] = FDT[(size_t)i * P + p];   // stored form (Coord<CT>)
+        WFD[wrow] = Coord<CT>::fd(FDT[(size_t)i * P + p]);
         if (i == 0) {
             wflag[(size_t)r * C + gc] = 1;
             wcoin[(size_t)r * C + gc] = g_coin[p_gid[p]];
@@ -593,7 +593,12 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     __shared__ int32_t e_ovf[T];
     __shared__ uint32_t whist[4][256];
     __shared__ int32_t s_any;
-    const int64_t p0 = (int64_t)blockIdx.x * T;
+    // time-major tiles: block i = tile i / C of chain i % C, so the blocks in flight cover
+    // every chain at about the same time and their timestamp gathers (events of other
+    // chains at that time) share lines in L2
+    const int tc = (int)(blockIdx.x % (unsigned)C), tt = (int)(blockIdx.x / (unsigned)C);
+    const int64_t p0 = (int64_t)c_off[tc] + (int64_t)tt * T;
+    const int64_t pend = min((int64_t)c_off[tc + 1], Pn);
     if (threadIdx.x == 0) s_any = 0;
     for (int k = threadIdx.x; k < T * (NPAD / 32); k += 256) mem[k / (NPAD / 32)][k % (NPAD / 32)] = 0;
     __syncthreads();
@@ -601,7 +606,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
         const int e = threadIdx.x;
         const int64_t p = p0 + e;
         int row = -1;
-        if (p < Pn && p_new[p]) {
+        if (p < pend && p_new[p]) {
             s_any = 1;
             const int gc = p_chain[p], g = gc / n, i = p_rr[p];
             row = i;
@@ -1029,7 +1034,7 @@ void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n,
     if (a.compact)
         hipLaunchKernelGGL(k_round_gather<uint16_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const uint16_t*)a.LA, (const uint16_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
-                           (uint16_t*)a.WFD, a.wflag, a.wcoin, C, n, P);
+                           a.WFD, a.wflag, a.wcoin, C, n, P);
     else
         hipLaunchKernelGGL(k_round_gather<int32_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const int32_t*)a.LA, (const int32_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
@@ -1079,7 +1084,7 @@ static void cts_small_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int 
 }
 
 template <int NPAD, typename CT>
-static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
     const size_t lds = (size_t)NPAD * 33 * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
@@ -1087,27 +1092,29 @@ static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C
                                   (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(nblk(Pn, 32)), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
+    const unsigned grid = (unsigned)((int64_t)C * ((max_len + 31) / 32));
+    if (grid == 0) return;
+    hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
                        a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
 }
 
 template <typename CT>
-static void launch_cts_t(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+static void launch_cts_t(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
     if (n <= 4) cts_small_launch<4, CT>(s, a, Pn, C, n, P);
     else if (n <= 8) cts_small_launch<8, CT>(s, a, Pn, C, n, P);
     else if (n <= 16) cts_small_launch<16, CT>(s, a, Pn, C, n, P);
     else if (n <= 32) cts_small_launch<32, CT>(s, a, Pn, C, n, P);
-    else if (n <= 64) cts_tile_launch<64, CT>(s, a, Pn, C, n, P);
-    else if (n <= 128) cts_tile_launch<128, CT>(s, a, Pn, C, n, P);
-    else if (n <= 256) cts_tile_launch<256, CT>(s, a, Pn, C, n, P);
-    else if (n <= 512) cts_tile_launch<512, CT>(s, a, Pn, C, n, P);
-    else cts_tile_launch<1024, CT>(s, a, Pn, C, n, P);
+    else if (n <= 64) cts_tile_launch<64, CT>(s, a, Pn, C, n, P, max_len);
+    else if (n <= 128) cts_tile_launch<128, CT>(s, a, Pn, C, n, P, max_len);
+    else if (n <= 256) cts_tile_launch<256, CT>(s, a, Pn, C, n, P, max_len);
+    else if (n <= 512) cts_tile_launch<512, CT>(s, a, Pn, C, n, P, max_len);
+    else cts_tile_launch<1024, CT>(s, a, Pn, C, n, P, max_len);
 }
 
-void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
+void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
     if (Pn <= 0) return;
-    if (a.compact) launch_cts_t<uint16_t>(s, a, Pn, C, n, P);
-    else launch_cts_t<int32_t>(s, a, Pn, C, n, P);
+    if (a.compact) launch_cts_t<uint16_t>(s, a, Pn, C, n, P, max_len);
+    else launch_cts_t<int32_t>(s, a, Pn, C, n, P, max_len);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

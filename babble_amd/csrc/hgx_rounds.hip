@@ -87,7 +87,31 @@ __device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&f
 template <typename CT, int CPL, bool VEC>
 __device__ __forceinline__ void load_slice(const CT* __restrict__ p, uint32_t (&v)[CPL]) {
     constexpr int B = CPL * (int)sizeof(CT);
-    if constexpr (VEC && B == 16) {
+    if constexpr (VEC && B > 16 && B % 16 == 0) {   // several 16-byte pieces
+        constexpr int PER = 16 / (int)sizeof(CT);   // coordinates per piece
+#pragma unroll
+        for (int k = 0; k < B / 16; k++) {
+            const uint4 x = ((const uint4*)p)[k];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if constexpr (sizeof(CT) == 4) {
+                    v[k * PER + u] = w[u];
+                } else {
+                    v[k * PER + 2 * u] = w[u] & 0xFFFFu;
+                    v[k * PER + 2 * u + 1] = w[u] >> 16;
+                }
+            }
+        }
+    } else if constexpr (VEC && B == 16 && sizeof(CT) == 2) {   // 8 x uint16
+        const uint4 x = *(const uint4*)p;
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            v[2 * u] = w[u] & 0xFFFFu;
+            v[2 * u + 1] = w[u] >> 16;
+        }
+    } else if constexpr (VEC && B == 16) {
         const uint4 x = *(const uint4*)p;
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
     } else if constexpr (VEC && B == 8 && sizeof(CT) == 4) {
@@ -180,7 +204,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const int j = lane + 64 * q;
         fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
     }
-    // WFD rows are stored as CT (compact: uint16 with 0xFFFF = none); lane l loads
+    // WFD rows hold the decoded firstDescendants (int32, MaxInt32 = none); lane l loads
     // coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
     uint32_t fdr[OWN][CPL];
     const int lc = (CPL * lane < n) ? CPL * lane : 0;
@@ -188,11 +212,11 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     for (int o = 0; o < OWN; o++) {
         const int j = wg + NWC * ((o + rot) % OWN);
         const int jj = j < n ? j : 0;
-        load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + jj) * n + lc, fdr[o]);
+        load_slice<int32_t, CPL, VEC>(A.WFD + (crow + jj) * n + lc, fdr[o]);
 #ifdef HGX_EXP_WFD2   // experiment: the candidate rows loaded twice (bandwidth vs latency)
         {
             uint32_t t2[CPL];
-            load_slice<CT, CPL, VEC>((const CT*)A.WFD + (crow + ((jj + 5) % n)) * n + lc, t2);
+            load_slice<int32_t, CPL, VEC>(A.WFD + (crow + ((jj + 5) % n)) * n + lc, t2);
             uint32_t z = 0;
             asm volatile("" : "+v"(z));
 #pragma unroll
@@ -280,7 +304,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
             const int i = CPL * lane + q;
-            fd[o][q] = (cand && i < n) ? Coord<CT>::fd(fdr[o][q]) : kMaxI32;
+            fd[o][q] = (cand && i < n) ? (int32_t)fdr[o][q] : kMaxI32;
             // opaque from here on: otherwise the compiler keeps (cand && i < n) as a lane
             // mask per candidate and ANDs it into every compare (SGPR pressure, spills)
             asm volatile("" : "+v"(fd[o][q]));
@@ -369,7 +393,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            ((CT*)A.WFD)[nrow + i] = (sizeof(CT) == 4) ? fd_s[i * P + pk] : fd_s[i * 2 * L::FDW + fsh + pk];
+            A.WFD[nrow + i] = Coord<CT>::fd((sizeof(CT) == 4) ? fd_s[i * P + pk] : fd_s[i * 2 * L::FDW + fsh + pk]);
         }
         if (gt == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (gt == 0) {
@@ -388,7 +412,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 // only the candidates seen there are binary-searched for their first seeing probe.
 // The count at probe p is the number of candidates first seen at or before p (an LDS
 // histogram). The own-chain candidate never counts at the probe that is itself.
-template <int CPL, int P, typename CT>
+template <int CPL, int P, typename CT, bool VEC>
 __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep) {
     constexpr int NWV = 16;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -415,12 +439,43 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         return;
     }
     const size_t crow = (size_t)r * C + (size_t)g * n;
+    // coordinates of lane l, slot q: int32 i = l + 64q; compact i = 2l + (q & 1) + 128(q >> 1)
+    // (pairs as one dword): coalesced row loads and conflict-free LDS reads
+    auto coord = [&](int q) -> int {
+        return sizeof(CT) == 4 ? lane + 64 * q : 2 * lane + (q & 1) + 128 * (q >> 1);
+    };
+    auto load_row = [&](const CT* __restrict__ row, uint32_t (&raw)[CPL], bool clamp) {
+        if constexpr (sizeof(CT) == 4) {
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int i = lane + 64 * q;
+                raw[q] = (uint32_t)row[(clamp && i >= n) ? 0 : i];
+            }
+        } else {
+#pragma unroll
+            for (int q2 = 0; q2 < CPL / 2; q2++) {
+                const int i = 2 * lane + 128 * q2;
+                const uint32_t w = *(const uint32_t*)(row + ((clamp && i >= n) ? 0 : i));
+                raw[2 * q2] = w & 0xFFFFu;
+                raw[2 * q2 + 1] = w >> 16;
+            }
+        }
+    };
     auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
+        uint32_t raw[CPL];
+        load_row(la_s + pp * n, raw, false);
         int tot = 0;
 #pragma unroll
-        for (int q = 0; q < CPL; q++)
-            tot += __popcll(__ballot(min(Coord<CT>::la(la_s[pp * n + lane + 64 * q]), kMaxI32 - 1) >= fd[q]));
+        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(min(Coord<CT>::la(raw[q]), kMaxI32 - 1) >= fd[q]));
         return tot >= sm && !(j == cl && kb + pp == b);
+    };
+    auto load_fd = [&](int j, bool cand, int32_t (&fd)[CPL]) {
+        const int32_t* __restrict__ row = A.WFD + (crow + j) * n;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int i = coord(q);
+            fd[q] = (cand && i < n) ? row[i] : kMaxI32;
+        }
     };
     int kbase = b, np = 0, kstar = len, pk = 0;
     for (;;) {
@@ -451,12 +506,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         for (int j = wave; j < n; j += NWV) {
             int32_t fd[CPL];
             const bool cand = A.wflag[crow + j] == 1;
-#pragma unroll
-            for (int q = 0; q < CPL; q++) {
-                const int i = lane + 64 * q;
-                fd[q] = Coord<CT>::fd(((const CT*)A.WFD)[(crow + j) * n + (i < n ? i : 0)]);
-                if (!cand || i >= n) fd[q] = kMaxI32;
-            }
+            load_fd(j, cand, fd);
             const bool sl = cand && seen_at(fd, np - 1, j, kbase);
             cnt += sl ? 1 : 0;
             if (lane == 0) fhit[j] = sl ? (uint8_t)(np - 1) : (uint8_t)255;
@@ -471,11 +521,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
             for (int j = wave; j < n; j += NWV) {
                 if (fhit[j] == 255) continue;   // wave-uniform (written by this wave's lane 0)
                 int32_t fd[CPL];
-#pragma unroll
-                for (int q = 0; q < CPL; q++) {
-                    const int i = lane + 64 * q;
-                    fd[q] = (i < n) ? Coord<CT>::fd(((const CT*)A.WFD)[(crow + j) * n + i]) : kMaxI32;
-                }
+                load_fd(j, true, fd);
                 int lo = 0, hi = np - 1;
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
@@ -523,7 +569,7 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            ((CT*)A.WFD)[nrow + i] = ((const CT*)A.FDT)[(size_t)i * A.Pcap + p];
+            A.WFD[nrow + i] = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + p]);
         }
         if (threadIdx.x == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (threadIdx.x == 0) {
@@ -531,9 +577,9 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
     }
 }
 
-template <int CPL, int P, typename CT>
-static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) {
-    const void* f = (const void*)k_round_step_big<CPL, P, CT>;
+template <int CPL, int P, typename CT, bool VEC>
+static hipError_t step_big_launch_v(hipStream_t s, const RoundArgs& A, int kstep) {
+    const void* f = (const void*)k_round_step_big<CPL, P, CT, VEC>;
     const size_t lds = (size_t)(P * A.n + 64 * CPL) * sizeof(CT);
     static bool attr = false;
     if (!attr) {
@@ -541,8 +587,13 @@ static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) 
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_round_step_big<CPL, P, CT>), dim3(A.C), dim3(1024), lds, s, A, kstep);
+    hipLaunchKernelGGL((k_round_step_big<CPL, P, CT, VEC>), dim3(A.C), dim3(1024), lds, s, A, kstep);
     return hipGetLastError();
+}
+
+template <int CPL, int P, typename CT>
+static hipError_t step_big_launch(hipStream_t s, const RoundArgs& A, int kstep) {
+    return step_big_launch_v<CPL, P, CT, false>(s, A, kstep);
 }
 
 template <int CPL, int NWC, int OWN, int P, int GPB, typename CT, bool VEC>
