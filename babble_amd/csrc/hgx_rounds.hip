@@ -63,13 +63,43 @@ __device__ unsigned long long hgx_step_prof[8];
 // total of candidate O goes to lane O of tv (v_writelane with an immediate lane: a
 // select on lane == O would make the compiler hoist OWN 64-bit lane masks and spill them)
 // Candidates whose bit is clear in `test` are skipped (wave-uniform branch).
+// The CPL compares of one candidate go to distinct SGPR pairs in one asm block, so they
+// issue back to back; left to itself the compiler (at this SGPR pressure) funnels every
+// compare through one pair and each v_cmp -> s_bcnt1 round trip serialises the tally.
+template <int CPL>
+__device__ __forceinline__ int count_seen(const int32_t (&la)[CPL], const int32_t (&fd)[CPL]) {
+    if constexpr (CPL == 4) {
+        uint64_t m0, m1, m2, m3;
+        asm volatile(
+            "v_cmp_ge_i32_e64 %0, %4, %8\n\t"
+            "v_cmp_ge_i32_e64 %1, %5, %9\n\t"
+            "v_cmp_ge_i32_e64 %2, %6, %10\n\t"
+            "v_cmp_ge_i32_e64 %3, %7, %11"
+            : "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3)
+            : "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(fd[0]), "v"(fd[1]), "v"(fd[2]), "v"(fd[3]));
+        return (__popcll(m0) + __popcll(m1)) + (__popcll(m2) + __popcll(m3));
+    } else if constexpr (CPL == 2) {
+        uint64_t m0, m1;
+        asm volatile(
+            "v_cmp_ge_i32_e64 %0, %2, %4\n\t"
+            "v_cmp_ge_i32_e64 %1, %3, %5"
+            : "=s"(m0), "=s"(m1)
+            : "v"(la[0]), "v"(la[1]), "v"(fd[0]), "v"(fd[1]));
+        return __popcll(m0) + __popcll(m1);
+    } else {
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(la[q] >= fd[q]));
+        return tot;
+    }
+}
+
+// Candidates whose bit is clear in `test` are skipped (wave-uniform branch).
 template <int O, int CPL, int OWN>
 __device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int& tv,
                                           uint64_t test) {
     if ((test >> O) & 1ull) {
-        int tot = 0;
-#pragma unroll
-        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(la[q] >= fd[O][q]));
+        const int tot = count_seen<CPL>(la, fd[O]);
         asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv) : "s"(tot), "i"(O));
     }
 }
