@@ -137,13 +137,16 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
             carry[q] = (k0 > 0 && i < nwd) ? LA[(size_t)(off + k0 - 1) * nwd + i] : W::kNone;
         }
         int64_t sum = 0;
-        for (int k = k0; k < k1; k += 4) {
-            uint32_t opr[4][CPL];
-            int opp[4];
+        // UB rows per batch: all their op-row loads are issued before the first use (one
+        // memory round trip per batch; a whole 16-row unit when the rows are narrow)
+        constexpr int UB = (CPL <= 2) ? 16 : (CPL <= 4 ? 8 : 4);
+        for (int k = k0; k < k1; k += UB) {
+            uint32_t opr[UB][CPL];
+            int opp[UB];
 #pragma unroll
-            for (int u = 0; u < 4; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
+            for (int u = 0; u < UB; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < UB; u++) {
 #pragma unroll
                 for (int q = 0; q < CPL; q++) {
                     const int i = gl + GS * q;
@@ -151,17 +154,18 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (k + u >= k1) break;
+            for (int u = 0; u < UB; u++) {
+                if (k + u < k1) {
 #pragma unroll
-                for (int q = 0; q < CPL; q++) {
-                    const int i = gl + GS * q;
-                    const uint32_t v = W::set_own(W::wmax(carry[q], opr[u][q]), i, cl, base + k + u);
-                    if (i < nwd) {
-                        LA[(size_t)(off + k + u) * nwd + i] = v;
-                        sum += W::wsum(v);
+                    for (int q = 0; q < CPL; q++) {
+                        const int i = gl + GS * q;
+                        const uint32_t v = W::set_own(W::wmax(carry[q], opr[u][q]), i, cl, base + k + u);
+                        if (i < nwd) {
+                            LA[(size_t)(off + k + u) * nwd + i] = v;
+                            sum += W::wsum(v);
+                        }
+                        carry[q] = v;
                     }
-                    carry[q] = v;
                 }
             }
         }
