@@ -6,6 +6,7 @@
 // quirk, per-witness fame frozen once decided, LastConsensusRound /
 // LastCommitedRoundEvents, received events, blocks, counters.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -27,26 +28,34 @@ struct Block {
 };
 
 // growable pinned host array: the consensus order is copied D2H straight into it
-struct PinnedOrder {
+// Pinned host arena holding the consensus orders of all graphs: every FindOrder appends
+// the device order (graph-major) with ONE copy, and each graph's order is the list of
+// its segments in the arena (one per FindOrder call that ordered events of the graph).
+struct OrderArena {
     int32_t* p = nullptr;
-    size_t n = 0, cap = 0;
-    PinnedOrder() = default;
-    PinnedOrder(const PinnedOrder&) = delete;
-    PinnedOrder& operator=(const PinnedOrder&) = delete;
-    ~PinnedOrder() { if (p) (void)hipHostFree(p); }
+    size_t used = 0, cap = 0;
+    OrderArena() = default;
+    OrderArena(const OrderArena&) = delete;
+    OrderArena& operator=(const OrderArena&) = delete;
+    ~OrderArena() { if (p) (void)hipHostFree(p); }
     bool reserve(size_t want) {
         if (want <= cap) return true;
         size_t nc = std::max<size_t>(want, cap * 2 + 1024);
         int32_t* q = nullptr;
         if (hipHostMalloc((void**)&q, nc * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) return false;
-        if (n) std::memcpy(q, p, n * sizeof(int32_t));
+        if (used) std::memcpy(q, p, used * sizeof(int32_t));
         if (p) (void)hipHostFree(p);
         p = q;
         cap = nc;
         return true;
     }
+};
+
+struct GraphOrder {
+    struct Seg { size_t off, len; };
+    std::vector<Seg> segs;
+    size_t n = 0;
     size_t size() const { return n; }
-    int32_t operator[](size_t i) const { return p[i]; }
 };
 
 struct GraphState {
@@ -90,7 +99,8 @@ struct hgx_ctx {
     bool divided = false;
     hgx::RoundsHost rh;
     std::vector<GraphState> gs;
-    std::vector<PinnedOrder> order;          // [G] consensus order (gids) per graph
+    OrderArena arena;                        // consensus orders (gids) of all graphs
+    std::vector<GraphOrder> order;           // [G] segments of each graph's order in the arena
     std::vector<int64_t> g_events, g_loaded;  // [G] inserted events / loaded events per graph
     // getter caches
     bool rounds_cached = false;
@@ -153,7 +163,7 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->last_index.assign(c->C, -1);
     c->chain_gids.assign(c->C, {});
     c->gs.assign(n_graphs, GraphState());
-    c->order = std::vector<PinnedOrder>(n_graphs);
+    c->order = std::vector<GraphOrder>(n_graphs);
     c->g_events.assign(n_graphs, 0);
     c->g_loaded.assign(n_graphs, 0);
     const size_t rsv = (size_t)std::min<int64_t>(capacity_events, 1 << 22);
@@ -347,59 +357,78 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
     if (!c->divided) { if (err) set_err(err, HGX_OK, ""); return HGX_OK; }
     const int n = c->n, C = c->C, G = c->G;
     const int32_t R = c->rh.R;
+    static const bool dbg = getenv("HGX_DEBUG_HOST") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!dbg) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        fprintf(stderr, "[hgx] find_order %s: %.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    };
     std::vector<uint8_t> elig((size_t)G * std::max(R, 1), 0), fw((size_t)std::max(R, 1) * C, 0), ure(G, 0);
     for (int g = 0; g < G; g++) {
         const GraphState& s = c->gs[g];
         ure[g] = s.undecided.empty() ? 1 : 0;
         const int32_t U0 = s.undecided.empty() ? -1 : s.undecided[0];
         for (int32_t i = 0; i <= s.last_round; i++) {
-            // DecideRoundReceived skip rule (hashgraph.go:763)
-            elig[(size_t)g * R + i] = (U0 >= 0 && i < U0 && witnesses_decided(c, g, i)) ? 1 : 0;
-            for (int cl = 0; cl < n; cl++)
-                if (is_witness(c, i, g * n + cl) && s.fame[(size_t)i * n + cl] == 1) fw[(size_t)i * C + g * n + cl] = 1;
+            // one pass over the round's chains: famous witnesses, and WitnessesDecided
+            // (roundInfo.go:64-71) for the DecideRoundReceived skip rule (hashgraph.go:763)
+            bool decided = true;
+            const uint8_t* ws = c->rh.wflag.data() + (size_t)i * C + (size_t)g * n;
+            const int8_t* fm = s.fame.data() + (size_t)i * n;
+            uint8_t* fwr = fw.data() + (size_t)i * C + (size_t)g * n;
+            for (int cl = 0; cl < n; cl++) {
+                if (ws[cl] != 2) continue;
+                if (fm[cl] == 0) decided = false;
+                if (fm[cl] == 1) fwr[cl] = 1;
+            }
+            elig[(size_t)g * R + i] = (U0 >= 0 && i < U0 && decided) ? 1 : 0;
         }
     }
+    lap("eligibility");
     hgx::OrderHost oh;
     hipError_t e = c->eng.find_order(elig, fw, ure, oh);
+    lap("device");
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     if (oh.panic) {
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
         return HGX_ERR_PANIC;
     }
     c->recv_cached = false;
-    // per-graph segments of the device order (graph-major), copied D2H straight into
-    // each graph's pinned order array
+    // the device order is graph-major: one D2H copy appends it to the arena and every
+    // graph gets its segment
     std::vector<int64_t> seg_at(G, 0), seg_len(G, 0);
-    {
-        int64_t at = 0;
-        for (int g = 0; g < G; g++) {
-            int64_t mg = 0;
-            for (int32_t rr = 0; rr < R; rr++) mg += oh.blk_cnt[(size_t)g * R + rr];
-            seg_at[g] = at;
-            seg_len[g] = mg;
-            at += mg;
+    int64_t total = 0;
+    for (int g = 0; g < G; g++) {
+        int64_t mg = 0;
+        for (int32_t rr = 0; rr < R; rr++) mg += oh.blk_cnt[(size_t)g * R + rr];
+        seg_at[g] = total;
+        seg_len[g] = mg;
+        total += mg;
+    }
+    const size_t base_off = c->arena.used;
+    if (total > 0) {
+        if (!c->arena.reserve(base_off + (size_t)total)) {
+            set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
+            return HGX_ERR_CAPACITY;
         }
-        for (int g = 0; g < G; g++) {
-            if (!seg_len[g]) continue;
-            PinnedOrder& o = c->order[g];
-            if (!o.reserve(o.n + (size_t)seg_len[g])) {
-                set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
-                return HGX_ERR_CAPACITY;
-            }
-            e = c->eng.copy_order(o.p + o.n, seg_at[g], seg_len[g]);
-            if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
-        }
+        e = c->eng.copy_order(c->arena.p + base_off, 0, total);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
         e = c->eng.sync();
         if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
+        c->arena.used = base_off + (size_t)total;
     }
+    lap("order D2H");
     for (int g = 0; g < G; g++) {
         const int64_t mg = seg_len[g];
         if (mg == 0) continue;
         GraphState& s = c->gs[g];
-        PinnedOrder& o = c->order[g];
+        GraphOrder& o = c->order[g];
         const int64_t base_pos = (int64_t)o.n;
-        const int32_t* order = o.p + o.n;
+        const int32_t* order = c->arena.p + base_off + seg_at[g];
+        o.segs.push_back({base_off + (size_t)seg_at[g], (size_t)mg});
         o.n += (size_t)mg;
+        s.blocks.reserve(s.blocks.size() + (size_t)R);
         int64_t off = 0;
         for (int32_t rr = 0; rr < R; rr++) {    // one Block per rr, ascending (blockOrder)
             const int32_t cnt = oh.blk_cnt[(size_t)g * R + rr];
@@ -420,6 +449,7 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
         }
         s.undetermined -= mg;
     }
+    lap("blocks");
     if (err) set_err(err, HGX_OK, "");
     return HGX_OK;
 }
@@ -439,8 +469,9 @@ int32_t hgx_reset_consensus(hgx_ctx* c) {
         s.reset();
         s.undetermined = c->g_events[g];
         s.pending_loaded = c->g_loaded[g];
-        c->order[g].n = 0;
+        c->order[g] = GraphOrder();
     }
+    c->arena.used = 0;
     c->divided = false;
     c->E_div = 0;
     c->rounds_cached = c->recv_cached = false;
@@ -497,8 +528,13 @@ int32_t hgx_known(hgx_ctx* c, int32_t g, int32_t* out) {
 int64_t hgx_consensus_events_count(hgx_ctx* c, int32_t g) { return graph(c, g) ? (int64_t)c->order[g].size() : 0; }
 int32_t hgx_consensus_events(hgx_ctx* c, int32_t g, int64_t first, int64_t count, int64_t* gids) {
     if (!graph(c, g) || first < 0 || count < 0 || first + count > (int64_t)c->order[g].size()) return HGX_ERR_INVALID;
-    const int32_t* o = c->order[g].p;
-    for (int64_t i = 0; i < count; i++) gids[i] = o[first + i];
+    int64_t pos = 0, k = 0;   // walk the graph's segments
+    for (const GraphOrder::Seg& sg : c->order[g].segs) {
+        const int64_t a = std::max<int64_t>(first, pos), b = std::min<int64_t>(first + count, pos + (int64_t)sg.len);
+        for (int64_t i = a; i < b; i++) gids[k++] = c->arena.p[sg.off + (size_t)(i - pos)];
+        pos += (int64_t)sg.len;
+        if (pos >= first + count) break;
+    }
     return HGX_OK;
 }
 int64_t hgx_num_blocks(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->blocks.size() : 0; }
