@@ -19,34 +19,120 @@ namespace hgx {
 
 
 // ---------------------------------------------------------------------------------
-// layout: gid order -> chain-major positions
-__global__ void k_layout(int64_t E, const int32_t* __restrict__ g_creator, const int32_t* __restrict__ g_index,
-                         const int32_t* __restrict__ g_op, const int64_t* __restrict__ g_ts,
-                         const int32_t* __restrict__ g_rr, const int64_t* __restrict__ g_cts,
-                         const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
-                         int32_t* __restrict__ g_pos, int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
-                         int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu, int64_t* __restrict__ p_ts,
-                         int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int seg) {
-    int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= E) return;
-    int c = g_creator[gid];
-    int p = c_off[c] + g_index[gid] - c_base[c];
-    g_pos[gid] = p;
-    p_gid[p] = (int32_t)gid;
-    p_chain[p] = c;
-    int op = g_op[gid];
+// layout: gid order -> chain-major positions. Consecutive gids belong to different
+// chains, so a direct per-gid scatter writes every output array 4-8 bytes at a time at
+// random positions. A block instead takes kLayoutB consecutive gids, groups them by chain
+// in LDS (a chain's events in the block have consecutive indices, hence consecutive
+// positions) and writes each chain's run contiguously.
+constexpr int kLayoutB = 4096;   // gids per block
+constexpr int kLayoutH = 1024;   // chain-id range a block can group (else direct scatter)
+
+__device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __restrict__ g_creator,
+                                           const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                           const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
+                                           const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
+                                           const int32_t* __restrict__ c_base, int32_t* __restrict__ p_gid,
+                                           int32_t* __restrict__ p_chain, int32_t* __restrict__ p_op,
+                                           int32_t* __restrict__ p_opu, int64_t* __restrict__ p_ts,
+                                           int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int seg) {
+    const int c = g_creator[gid];
+    const int op = g_op[gid];
     int opp = -1, opu = -1;
     if (op >= 0) {
-        int oc = g_creator[op];
+        const int oc = g_creator[op];
         const int ok = g_index[op] - c_base[oc];
         opp = c_off[oc] + ok;
         opu = (ok / seg) * C + oc;   // lastAncestors unit of the op row (k_la_sweep)
     }
+    p_gid[p] = (int32_t)gid;
+    p_chain[p] = c;
     p_op[p] = opp;
     p_opu[p] = opu;
     p_ts[p] = g_ts[gid];
     p_rr[p] = g_rr[gid];
     p_cts[p] = g_cts[gid];
+}
+
+__global__ void __launch_bounds__(256) k_layout(int64_t E, const int32_t* __restrict__ g_creator,
+                                                const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                                const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
+                                                const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
+                                                const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
+                                                int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
+                                                int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu,
+                                                int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
+                                                int64_t* __restrict__ p_cts, int C, int seg) {
+    __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
+    __shared__ int32_t s_slot[kLayoutB];   // slot -> gid offset in the block
+    __shared__ int32_t s_lo, s_hi;
+    const int64_t g0 = (int64_t)blockIdx.x * kLayoutB;
+    const int nb = (int)min<int64_t>(kLayoutB, E - g0);
+    if (threadIdx.x == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
+    for (int h = threadIdx.x; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
+    __syncthreads();
+    int lo = 0x7FFFFFFF, hi = -1;
+    for (int t = threadIdx.x; t < nb; t += 256) {
+        const int c = g_creator[g0 + t];
+        lo = min(lo, c);
+        hi = max(hi, c);
+    }
+    for (int o = 32; o >= 1; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
+    if ((threadIdx.x & 63) == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    __syncthreads();
+    const int clo = s_lo;
+    if (s_hi - clo >= kLayoutH) {   // block-uniform: too many chains to group, direct scatter
+        for (int t = threadIdx.x; t < nb; t += 256) {
+            const int64_t gid = g0 + t;
+            const int c = g_creator[gid];
+            const int p = c_off[c] + g_index[gid] - c_base[c];
+            g_pos[gid] = p;
+            layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
+                       p_opu, p_ts, p_rr, p_cts, C, seg);
+        }
+        return;
+    }
+    // per chain: events in the block and their smallest index
+    for (int t = threadIdx.x; t < nb; t += 256) {
+        const int64_t gid = g0 + t;
+        const int h = g_creator[gid] - clo;
+        atomicAdd(&s_cnt[h], 1);
+        atomicMin(&s_min[h], g_index[gid]);
+    }
+    __syncthreads();
+    // exclusive scan of the counts (one wave)
+    if (threadIdx.x < 64) {
+        constexpr int PER = kLayoutH / 64;
+        int v[PER], sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) { v[k] = s_cnt[threadIdx.x * PER + k]; sum += v[k]; }
+        int incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if ((int)threadIdx.x >= o) incl += y;
+        }
+        int run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < PER; k++) { s_cnt[threadIdx.x * PER + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    // slot of an event = run start of its chain + (index - smallest index of the chain in the block)
+    for (int t = threadIdx.x; t < nb; t += 256) {
+        const int64_t gid = g0 + t;
+        const int c = g_creator[gid];
+        const int h = c - clo;
+        const int idx = g_index[gid];
+        s_slot[s_cnt[h] + idx - s_min[h]] = t;
+        g_pos[gid] = c_off[c] + idx - c_base[c];
+    }
+    __syncthreads();
+    // consecutive slots = consecutive positions within a chain's run
+    for (int sl = threadIdx.x; sl < nb; sl += 256) {
+        const int64_t gid = g0 + s_slot[sl];
+        const int c = g_creator[gid];
+        const int p = c_off[c] + g_index[gid] - c_base[c];
+        layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu,
+                   p_ts, p_rr, p_cts, C, seg);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -987,7 +1073,7 @@ static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs
 
 void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg) {
     if (E <= 0) return;
-    hipLaunchKernelGGL(k_layout, dim3(nblk(E, 256)), dim3(256), 0, s, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
+    hipLaunchKernelGGL(k_layout, dim3(nblk(E, kLayoutB)), dim3(256), 0, s, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
                        a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_ts,
                        a.p_rr, a.p_cts, C, seg);
 }
