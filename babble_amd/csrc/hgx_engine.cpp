@@ -479,7 +479,8 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     uint64_t* keys = nullptr;
     kbeg(K_SORT);
     launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
-    kend(K_SORT, (double)m * 24.0 * ((cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+    kend(K_SORT, (double)m * 24.0 *
+                     (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8 : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
     HGX_TRY(hipMemsetAsync(blk_cnt.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));

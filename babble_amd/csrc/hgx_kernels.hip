@@ -938,6 +938,18 @@ __global__ void k_keys_cts(int32_t m, const int32_t* __restrict__ list, const in
     vals[i] = (uint32_t)p;
 }
 
+// one key (graph, rr, cts - min) when it fits in 64 bits: a single LSD sort over it
+__global__ void k_keys_comb(int32_t m, const int32_t* __restrict__ list, const int64_t* __restrict__ p_cts,
+                            const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr, int64_t cmin,
+                            int cts_bits, int R, int n, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int p = list[i];
+    const uint64_t seg = (uint64_t)(p_chain[p] / n) * (uint64_t)R + (uint64_t)p_rr[p];
+    keys[i] = (seg << cts_bits) | (uint64_t)(p_cts[p] - cmin);
+    vals[i] = (uint32_t)p;
+}
+
 __global__ void k_keys_seg(int32_t m, const uint32_t* __restrict__ vals, const int32_t* __restrict__ p_chain,
                            const int32_t* __restrict__ p_rr, int R, int n, uint64_t* __restrict__ keys) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -978,6 +990,28 @@ __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
     for (int k = 0; k < 32; k++)
         if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
     return 0;
+}
+
+// runs of equal combined keys (same graph, rr and timestamp) ordered by S
+__global__ void k_tiefix_comb(int32_t m, uint32_t* __restrict__ vals, const uint64_t* __restrict__ keys,
+                              const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = keys[i];
+    if (i > 0 && keys[i - 1] == k) return;   // not a run start
+    if (i + 1 >= m || keys[i + 1] != k) return;
+    int e = i + 2;
+    while (e < m && keys[e] == k) e++;
+    for (int a = i + 1; a < e; a++) {   // insertion sort by S (run owned by this thread)
+        const uint32_t va = vals[a];
+        const uint8_t* sa = g_S + (size_t)p_gid[va] * 32;
+        int b = a - 1;
+        while (b >= i && cmp_s(g_S + (size_t)p_gid[vals[b]] * 32, sa) > 0) {
+            vals[b + 1] = vals[b];
+            b--;
+        }
+        vals[b + 1] = va;
+    }
 }
 
 __global__ void k_tiefix(int32_t m, uint32_t* __restrict__ vals, const uint64_t* __restrict__ segk,
@@ -1234,6 +1268,19 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys) {
     uint64_t *ka = a.key_a, *kb = a.key_b;
     uint32_t *va = a.val_a, *vb = a.val_b;
+    if (cts_bits + seg_bits <= 64) {   // one key, one sort, ties found on the keys
+        hipLaunchKernelGGL(k_keys_comb, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain,
+                           a.p_rr, cmin, cts_bits, R, n, ka, va);
+        for (int sh = 0; sh < cts_bits + seg_bits; sh += 8) {
+            radix_pass(s, a, m, sh, ka, va, kb, vb);
+            uint64_t* tk = ka; ka = kb; kb = tk;
+            uint32_t* tv = va; va = vb; vb = tv;
+        }
+        hipLaunchKernelGGL(k_tiefix_comb, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_gid, a.g_S);
+        *final_vals = va;
+        *final_keys = ka;
+        return;
+    }
     hipLaunchKernelGGL(k_keys_cts, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, cmin, ka, va);
     for (int sh = 0; sh < cts_bits; sh += 8) {
         radix_pass(s, a, m, sh, ka, va, kb, vb);
