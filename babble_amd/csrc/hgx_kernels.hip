@@ -11,6 +11,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
@@ -519,6 +521,209 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
         uint64_t* tmp = Vc; Vc = Vn; Vn = tmp;
     }
     for (int x = threadIdx.x; x < nx; x += blockDim.x) fame[(size_t)i * C + gi + xs[x]] = (int8_t)dec[x];
+}
+
+// ---------------------------------------------------------------------------------
+// fame for n >= 128 (same decisions as k_fame_vote, DecideFame hashgraph.go:649-730).
+// The decision of a witness x depends on x's own votes only, so a block takes one
+// (graph g, round i, tile of 64 witnesses x of round i) and walks j = i+1.. on its own:
+// G*R*ceil(n/64) independent blocks instead of G*R. Per step j the tally
+//   yays[y][x] = sum_w S_j[y][w] * wm_{j-1}[w] * V_{j-1}[x][w]      (y voter of round j)
+// is a 0/1 matrix product (K = n witnesses of round j-1, bit-packed, 64 per word).
+//   kMfma:  v_mfma_i32_16x16x64_i8. A = S rows expanded bit->byte in registers (one
+//           64-bit word is one K step: lane group h takes bits [16h, 16h+16)), B = the
+//           tile's votes expanded once per step into an int8 LDS image [x][w].
+//   !kMfma: AND + popcount, lane = x, S words wave-uniform.
+// tot[y] = popcount(S_j[y] & wm); votes of the step are OR-ed into LDS bit rows.
+typedef int int4v __attribute__((ext_vector_type(4)));
+constexpr int kFameTile = 64;     // witnesses x per block
+constexpr int kFameMaxW = 16;     // words per bit row (n <= 1024)
+
+// 16 bits -> 16 bytes of 0/1 (bit q of b -> byte q): nibble * 0x00204081 puts bits
+// 0..3 at 0, 8, 16, 24 with no overlapping partial products.
+__device__ __forceinline__ int4v expand16(uint32_t b) {
+    int4v r;
+    r[0] = (int)(((b & 0xFu) * 0x00204081u) & 0x01010101u);
+    r[1] = (int)((((b >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r[2] = (int)((((b >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
+    r[3] = (int)((((b >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+    return r;
+}
+
+// wave 0 compacts { c < n : st[c] == 2 } into out (ascending; count to *cnt) and/or
+// writes it as a bit mask (word k = chains [64k, 64k+64))
+__device__ __forceinline__ void compact_witnesses(const uint8_t* __restrict__ st, int n, int32_t* out, int* cnt,
+                                                  uint64_t* mask) {
+    if (threadIdx.x >= 64) return;
+    const int lane = lane_id();
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int c = c0 + lane;
+        const bool w = c < n && st[c] == 2;
+        const uint64_t m = __ballot(w);
+        if (out && w) out[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
+        if (mask && lane == 0) mask[c0 >> 6] = m;
+        base += __popcll(m);
+    }
+    if (cnt && lane == 0) *cnt = base;
+}
+
+template <bool kMfma>
+__global__ void __launch_bounds__(256) k_fame_tile(int R, int XT, const int32_t* __restrict__ lr,
+                            const uint8_t* __restrict__ wstat, const uint8_t* __restrict__ wcoin,
+                            const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
+                            const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
+                            int8_t* __restrict__ fame, int C, int n, int nw, int sm) {
+    extern __shared__ __align__(16) unsigned char fsm[];   // kMfma: int8 vote image [64][nw*64+16]
+    __shared__ int32_t xs[kFameTile], dec[kFameTile];
+    __shared__ int32_t ys[1024], ytot[1024];
+    __shared__ int32_t s_ny, s_und;
+    __shared__ uint64_t wmask[2][kFameMaxW];   // witness masks of rounds j-1 / j (by parity)
+    __shared__ uint64_t Vb[2][kFameTile][kFameMaxW];   // vote bit rows V[x][w] (current / next)
+    const int xt = blockIdx.x % XT;
+    const int i = (blockIdx.x / XT) % R;
+    const int g = blockIdx.x / (XT * R);
+    const int LR = lr[g];
+    if (i > LR) return;
+    const size_t gi = (size_t)g * n;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    // witnesses of round i, this block's slice
+    compact_witnesses(wstat + (size_t)i * C + gi, n, ys, &s_ny, nullptr);
+    __syncthreads();
+    const int nxt = min(kFameTile, s_ny - xt * kFameTile);
+    if (nxt <= 0) return;
+    if (threadIdx.x < kFameTile) {
+        xs[threadIdx.x] = threadIdx.x < nxt ? ys[xt * kFameTile + threadIdx.x] : 0;
+        dec[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    if (i + 2 > LR) {   // no round can decide: fame stays undefined
+        if ((int)threadIdx.x < nxt) fame[(size_t)i * C + gi + xs[threadIdx.x]] = 0;
+        return;
+    }
+    // j = i+1: vote(y, x) = See(y, x) = LA[y][cr(x)] >= Index(x)
+    {
+        const size_t jr = (size_t)(i + 1) * C + gi;
+        for (int t = threadIdx.x; t < kFameTile * nw; t += blockDim.x) {
+            const int x = t % kFameTile, wd = t / kFameTile;
+            uint64_t bits = 0;
+            if (x < nxt) {
+                const int xc = xs[x];
+                const int32_t xidx = c_base[gi + xc] + Bm[(size_t)i * C + gi + xc];
+                for (int bb = 0; bb < 64; bb++) {
+                    const int y = wd * 64 + bb;
+                    if (y >= n) break;
+                    if (wstat[jr + y] != 2) continue;
+                    if (WLA[(jr + y) * n + xc] >= xidx) bits |= 1ull << bb;
+                }
+            }
+            Vb[0][x][wd] = bits;
+        }
+    }
+    compact_witnesses(wstat + (size_t)(i + 1) * C + gi, n, nullptr, nullptr, wmask[(i + 1) & 1]);
+    const int KB = nw * 64 + 16;   // int8 image row stride (16-B pad: 16 lanes of one x-group hit distinct banks)
+    int cur = 0;
+    for (int j = i + 2; j <= LR; j++) {
+        const bool normal = ((j - i) % n) != 0;
+        const size_t jr = (size_t)j * C + gi;
+        const uint64_t* wm = wmask[(j - 1) & 1];   // witnesses of round j-1 (S rows may cover jumped candidates)
+        for (int t = threadIdx.x; t < kFameTile * nw; t += blockDim.x) Vb[cur ^ 1][t / nw][t % nw] = 0;
+        compact_witnesses(wstat + jr, n, ys, &s_ny, wmask[j & 1]);
+        __syncthreads();
+        const int ny = s_ny;
+        // tot[y] = #{w witness of j-1 : S_j[y][w]}
+        for (int t = threadIdx.x; t < ny; t += blockDim.x) {
+            const uint64_t* srow = Smat + (jr + ys[t]) * nw;
+            int tot = 0;
+            for (int k = 0; k < nw; k++) tot += __popcll(srow[k] & wm[k]);
+            ytot[t] = tot;
+        }
+        if constexpr (kMfma) {
+            // int8 image of the current votes: byte [x][w] = bit w of V[x]
+            int* img = reinterpret_cast<int*>(fsm);
+            for (int t = threadIdx.x; t < kFameTile * nw * 16; t += blockDim.x) {
+                const int x = t / (nw * 16), q = t % (nw * 16);   // q: 4-byte group of the row
+                const uint32_t nib = (uint32_t)(Vb[cur][x][q >> 4] >> ((q & 15) * 4)) & 0xFu;
+                img[(x * KB >> 2) + q] = (int)((nib * 0x00204081u) & 0x01010101u);
+            }
+        }
+        __syncthreads();
+        auto vote = [&](int yi, int x, int yays) {
+            const int y = ys[yi];
+            const int nays = ytot[yi] - yays;
+            const bool v = yays >= nays;
+            const int tt = v ? yays : nays;
+            bool bit;
+            if (normal) {
+                if (tt >= sm) atomicCAS(&dec[x], 0, v ? 1 : 2);
+                bit = v;
+            } else {
+                bit = (tt >= sm) ? v : (wcoin[jr + y] != 0);
+            }
+            if (bit) atomicOr((unsigned long long*)&Vb[cur ^ 1][x][y >> 6], 1ull << (y & 63));
+        };
+        if constexpr (kMfma) {
+            // wave: 32 voter rows (2 row tiles) x 64 witnesses (4 column tiles) per pass
+            const int h = lane >> 4, r16 = lane & 15;
+            const signed char* img = reinterpret_cast<const signed char*>(fsm);
+            for (int rp = wave; rp * 32 < ny; rp += 4) {
+                int4v acc[2][4];
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++) acc[a][b] = int4v{0, 0, 0, 0};
+                const int yi0 = rp * 32 + r16, yi1 = yi0 + 16;
+                const uint64_t* s0 = yi0 < ny ? Smat + (jr + ys[yi0]) * nw : nullptr;
+                const uint64_t* s1 = yi1 < ny ? Smat + (jr + ys[yi1]) * nw : nullptr;
+                for (int k = 0; k < nw; k++) {
+                    const uint64_t w0 = s0 ? (s0[k] & wm[k]) : 0ull;
+                    const uint64_t w1 = s1 ? (s1[k] & wm[k]) : 0ull;
+                    const int4v a0 = expand16((uint32_t)(w0 >> (16 * h)) & 0xFFFFu);
+                    const int4v a1 = expand16((uint32_t)(w1 >> (16 * h)) & 0xFFFFu);
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const int4v bf = *reinterpret_cast<const int4v*>(img + (b * 16 + r16) * KB + k * 64 + 16 * h);
+                        acc[0][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf, acc[0][b], 0, 0, 0);
+                        acc[1][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf, acc[1][b], 0, 0, 0);
+                    }
+                }
+                // C/D: column x = 16b + (lane & 15), row = 4 (lane >> 4) + q
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int yi = rp * 32 + a * 16 + 4 * h + q, x = b * 16 + r16;
+                            if (yi < ny && x < nxt) vote(yi, x, acc[a][b][q]);
+                        }
+            }
+        } else {
+            // lane = witness x; S words are wave-uniform
+            const int x = lane;
+            uint64_t vx[kFameMaxW];
+#pragma unroll
+            for (int k = 0; k < kFameMaxW; k++) vx[k] = k < nw ? Vb[cur][x][k] : 0ull;
+            for (int yi = wave; yi < ny; yi += 4) {
+                const uint64_t* srow = Smat + (jr + ys[yi]) * nw;
+                int yays = 0;
+#pragma unroll
+                for (int k = 0; k < kFameMaxW; k++)
+                    if (k < nw) yays += __popcll(srow[k] & wm[k] & vx[k]);
+                if (x < nxt) vote(yi, x, yays);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const bool u = (int)threadIdx.x < nxt && dec[threadIdx.x] == 0;
+            const uint64_t m = __ballot(u);
+            if (threadIdx.x == 0) s_und = __popcll(m);
+        }
+        __syncthreads();
+        if (s_und == 0) break;
+        cur ^= 1;
+    }
+    if ((int)threadIdx.x < nxt) fame[(size_t)i * C + gi + xs[threadIdx.x]] = (int8_t)dec[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------------
@@ -1172,7 +1377,33 @@ void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
                        a.wcoin);
 }
 
+// fame kernel choice: n >= 128 takes the witness-tiled kernel with the popcount tally
+// (measured faster than the MFMA tally), smaller n the per-round kernel. HGX_FAME=vote|popc|mfma forces one (measurement).
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G) {
+    const char* force = getenv("HGX_FAME");   // read per call: tests switch it in-process
+    int mode = 1;
+    if (force && !strcmp(force, "vote")) mode = 0;
+    if (force && !strcmp(force, "popc")) mode = 1;
+    if (force && !strcmp(force, "mfma")) mode = 2;
+    if (mode != 0 && n <= kFameMaxW * 64) {
+        const int XT = (n + kFameTile - 1) / kFameTile;
+        const dim3 grid((unsigned)((int64_t)G * R * XT));
+        if (mode == 2) {
+            const int shm = kFameTile * (nw * 64 + 16);
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)k_fame_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          kFameTile * (kFameMaxW * 64 + 16));
+                attr = true;
+            }
+            hipLaunchKernelGGL(k_fame_tile<true>, grid, dim3(256), shm, s, R, XT, a.lr, a.wstat, a.wcoin, a.Bm,
+                               a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
+        } else {
+            hipLaunchKernelGGL(k_fame_tile<false>, grid, dim3(256), 0, s, R, XT, a.lr, a.wstat, a.wcoin, a.Bm,
+                               a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
+        }
+        return;
+    }
     hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wstat, a.wcoin, a.Bm,
                        a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
 }

@@ -248,3 +248,48 @@ def test_empty_decide_fame_error_like_go():
     with pytest.raises(HgxError) as ei:
         h.DecideFame()
     assert ei.value.msg == "0, Not Found"
+
+
+FAME_CASES = [(4, 1024, 2, 0, 0.0), (7, 1500, 5, 2, 0.4), (16, 4000, 7, 5, 0.5), (128, 20000, 12, 0, 0.0),
+              (200, 20000, 15, 60, 0.0), (256, 30000, 16, 0, 0.3), (512, 24000, 18, 100, 0.2),
+              (1024, 16000, 19, 300, 0.0)]
+
+
+@pytest.mark.parametrize("mode", ["vote", "popc", "mfma"])
+@pytest.mark.parametrize("n,E,seed,silent,stale", FAME_CASES)
+def test_fame_kernels_agree_with_oracle(monkeypatch, mode, n, E, seed, silent, stale):
+    """Every DecideFame kernel (per-round popcount k_fame_vote, witness-tiled k_fame_tile with
+    the popcount or the int8 MFMA tally; HGX_FAME forces one) gives the oracle's fame, at every
+    n (small n reaches the coin rounds, (j-i) % n == 0)."""
+    monkeypatch.setenv("HGX_FAME", mode)
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
+    compare(run_gpu(t), hgref.oracle_run(t), t, hashes=False)
+
+
+@pytest.mark.parametrize("mode", ["vote", "popc", "mfma"])
+@pytest.mark.parametrize("name", ["funky_hashgraph", "consensus_hashgraph"])
+def test_fame_kernels_on_fixtures(monkeypatch, mode, name):
+    """The reference fixtures (funky_hashgraph has a coin round, hashgraph_test.go:1407-1462)
+    through each fame kernel."""
+    monkeypatch.setenv("HGX_FAME", mode)
+    t = hgref.fixture_trace(name)
+    compare(run_gpu(t), hgref.oracle_run(t), t)
+
+
+@pytest.mark.parametrize("mode", ["popc", "mfma"])
+def test_fame_tile_batched_graphs(monkeypatch, mode):
+    """k_fame_tile's (graph, round, witness tile) block mapping over a batched context."""
+    monkeypatch.setenv("HGX_FAME", mode)
+    G, n, Es = 3, 128, 12000
+    traces = [gtrace.gossip(n, Es, 300 + g, n_silent=10 * g, stale_prob=0.15 * g, stale_depth=3) for g in range(G)]
+    cat = gtrace.concat_graphs(traces)
+    h = _hg(n, cap=cat.E, graphs=G)
+    h.insert_trace(cat)
+    h.RunConsensus()
+    off = 0
+    for g, t in enumerate(traces):
+        o = hgref.oracle_run(t).results()
+        assert list(h.ConsensusEvents(g) - off) == list(o["order"]), g
+        assert h.UndecidedRounds(g) == o["undecided"]
+        assert h.LastConsensusRound(g) == o["lcr"]
+        off += t.E
