@@ -1197,26 +1197,69 @@ __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
     return 0;
 }
 
-// runs of equal combined keys (same graph, rr and timestamp) ordered by S
-__global__ void k_tiefix_comb(int32_t m, uint32_t* __restrict__ vals, const uint64_t* __restrict__ keys,
+// runs of equal combined keys (same graph, rr and timestamp) ordered by S (256-bit
+// big-endian, consensus_sorter.go:36-51 with the zero whitening).
+// k_tie_prefix: pre[i] = S's first 8 bytes as a big-endian u64, for members of runs.
+// k_tiefix_rank: element i of a run [s, e) goes to s + #{j in run : S_j < S_i} (prefix
+// compare, full compare on equal prefixes), so each run is placed in parallel; runs longer
+// than kTieRankMax are insertion-sorted by their first thread (degenerate traces only).
+constexpr int kTieRankMax = 8192;
+
+__global__ void k_tie_prefix(int32_t m, const uint32_t* __restrict__ vals, const uint64_t* __restrict__ keys,
+                             const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S,
+                             uint64_t* __restrict__ pre) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = keys[i];
+    const bool tie = (i > 0 && keys[i - 1] == k) || (i + 1 < m && keys[i + 1] == k);
+    if (!tie) return;
+    const uint8_t* sp = g_S + (size_t)p_gid[vals[i]] * 32;
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) v = (v << 8) | sp[b];
+    pre[i] = v;
+}
+
+__global__ void k_tiefix_rank(int32_t m, const uint32_t* __restrict__ vals, uint32_t* __restrict__ out,
+                              const uint64_t* __restrict__ keys, const uint64_t* __restrict__ pre,
                               const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint64_t k = keys[i];
-    if (i > 0 && keys[i - 1] == k) return;   // not a run start
-    if (i + 1 >= m || keys[i + 1] != k) return;
-    int e = i + 2;
-    while (e < m && keys[e] == k) e++;
-    for (int a = i + 1; a < e; a++) {   // insertion sort by S (run owned by this thread)
-        const uint32_t va = vals[a];
-        const uint8_t* sa = g_S + (size_t)p_gid[va] * 32;
-        int b = a - 1;
-        while (b >= i && cmp_s(g_S + (size_t)p_gid[vals[b]] * 32, sa) > 0) {
-            vals[b + 1] = vals[b];
-            b--;
-        }
-        vals[b + 1] = va;
+    const uint32_t vi = vals[i];
+    if (!((i > 0 && keys[i - 1] == k) || (i + 1 < m && keys[i + 1] == k))) {
+        out[i] = vi;
+        return;
     }
+    int s = i, e = i + 1;
+    while (s > 0 && keys[s - 1] == k && i - s <= kTieRankMax) s--;
+    while (e < m && keys[e] == k && e - s <= kTieRankMax) e++;
+    if (e - s > kTieRankMax) {   // long run: first element's thread insertion-sorts it
+        if (i > 0 && keys[i - 1] == k) return;
+        e = i + 1;
+        while (e < m && keys[e] == k) e++;
+        for (int a = i; a < e; a++) out[a] = vals[a];
+        for (int a = i + 1; a < e; a++) {
+            const uint32_t va = out[a];
+            const uint8_t* sa = g_S + (size_t)p_gid[va] * 32;
+            int b = a - 1;
+            while (b >= i && cmp_s(g_S + (size_t)p_gid[out[b]] * 32, sa) > 0) {
+                out[b + 1] = out[b];
+                b--;
+            }
+            out[b + 1] = va;
+        }
+        return;
+    }
+    const uint64_t my = pre[i];
+    const uint8_t* si = g_S + (size_t)p_gid[vi] * 32;
+    int rank = 0;
+    for (int j = s; j < e; j++) {
+        const uint64_t pj = pre[j];
+        const int c = (pj != my) ? (pj < my ? -1 : 1) : (j == i ? 0 : cmp_s(g_S + (size_t)p_gid[vals[j]] * 32, si));
+        rank += c < 0 || (c == 0 && j < i);   // equal S (never in a valid trace): stable
+    }
+    out[s + rank] = vi;
 }
 
 __global__ void k_tiefix(int32_t m, uint32_t* __restrict__ vals, const uint64_t* __restrict__ segk,
@@ -1507,7 +1550,10 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
             uint64_t* tk = ka; ka = kb; kb = tk;
             uint32_t* tv = va; va = vb; vb = tv;
         }
-        hipLaunchKernelGGL(k_tiefix_comb, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_gid, a.g_S);
+        // kb / vb are free after the passes: prefixes and the placed values
+        hipLaunchKernelGGL(k_tie_prefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_gid, a.g_S, kb);
+        hipLaunchKernelGGL(k_tiefix_rank, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, vb, ka, kb, a.p_gid, a.g_S);
+        va = vb;
         *final_vals = va;
         *final_keys = ka;
         return;
