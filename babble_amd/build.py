@@ -28,8 +28,9 @@ def _newer(target, deps):
 def build_lib(force: bool = False, verbose: bool = True, variant: str = "") -> str:
     """variant "prof": -DHGX_STEP_PROF build into libhgx_prof.so (phase timing of the round step)."""
     out = OUT if not variant else os.path.join(HERE, f"libhgx_{variant}.so")
-    extra = {"prof": ["-DHGX_STEP_PROF", "-DHGX_LA_ROWSTATS"],
-             "exp": [f"-D{d}" for d in os.environ.get("HGX_EXP_DEFS", "").split(",") if d]}.get(variant, [])
+    # variant "exp*": experiment build with the macros listed in HGX_EXP_DEFS (comma separated)
+    extra = ["-DHGX_STEP_PROF", "-DHGX_LA_ROWSTATS"] if variant == "prof" else \
+        [f"-D{d}" for d in os.environ.get("HGX_EXP_DEFS", "").split(",") if d] if variant.startswith("exp") else []
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
         [os.path.join(ROOT, "include", "hgx.h")]

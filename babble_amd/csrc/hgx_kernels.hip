@@ -864,13 +864,20 @@ __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __
     p_cts[p] = res;
 }
 
-// n > 32: a block owns T = 32 consecutive positions (mostly one chain, one round
-// received). Phase 1, lanes = events: for each witness chain c the 32 FD values
-// FDT[c][p0..p0+32) are one 128-B line, and since firstDescendants are monotone along
-// a chain the 32 timestamp gathers p_ts[pos(c, FD)] hit one or two lines. Values are
+// n > 32: a block owns T = kCtsTile consecutive positions of one chain (mostly one round
+// received). Phase 1, lanes = events: for each witness chain c the T FD values
+// FDT[c][p0..p0+T) are one segment, and since firstDescendants are monotone along
+// a chain the T timestamp gathers p_ts[pos(c, FD)] hit one or two lines. The kernel is
+// bound by the dependent FD -> timestamp latency per tile, not by bytes: smaller tiles
+// keep more blocks (and tiles) in flight per CU. Values are
 // kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
 // do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
 // per event: radix select of element floor(m/2) in registers.
+#ifdef HGX_CTS_T   // experiment: tile size
+constexpr int kCtsTile = HGX_CTS_T;
+#else
+constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8
+#endif
 template <int NPAD, typename CT>
 __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
@@ -878,7 +885,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
                                                   const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                   const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
                                                   int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
-    constexpr int T = 32;
+    constexpr int T = kCtsTile;
     constexpr int LD = T + 1;                     // row stride of vals (bank spread)
     constexpr int CPL = NPAD / 64;
     extern __shared__ __attribute__((aligned(16))) uint32_t vals[];   // [NPAD][LD] offsets + 2^31
@@ -917,7 +924,8 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     if (!s_any) return;
     // phase 1: lane = event e (32 per half-wave), 8 chain groups over the block
     {
-        const int e = threadIdx.x & (T - 1), cg = threadIdx.x / T;   // cg in [0, 8)
+        constexpr int NG = 256 / T;                                  // chain groups
+        const int e = threadIdx.x & (T - 1), cg = threadIdx.x / T;   // cg in [0, NG)
         const int i = e_row[e];
         const int64_t p = p0 + e;
         const int gc = (i >= 0) ? e_g[e] : 0;
@@ -928,28 +936,34 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
         const int64_t base = (i >= 0) ? e_ts[e] : 0;
         bool ovf = false;
         // batches of U chains: all independent loads first, then the dependent gathers
-        // (branch-free: non-members gather a valid dummy index and are masked)
-        constexpr int U = 4;
-        for (int c0 = cg; c0 < n; c0 += 8 * U) {
-            bool ok[U];
+        // (branch-free: non-members gather a valid dummy index and are masked). Up to
+        // 32 chains per batch (every gather of the tile in one batch at n = 256, T = 32)
+        // measured 11.45 -> 10.66 ms at c3 against 4; a per-tile LDS table of the per-chain terms
+        // (thresholds, chain bases) measured slower (14.3 ms: one more dependent round
+        // trip per tile, and the LDS cost a resident block).
+        constexpr int U = (NPAD / NG < 32) ? NPAD / NG : 32;
+        for (int c0 = cg; c0 < n; c0 += NG * U) {
+            // idx < 0 marks a non-member (kept in VGPRs: 32 lane masks would spill SGPRs)
             int32_t idx[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int c = c0 + 8 * u;
+                const int c = c0 + NG * u;
                 const bool in = i >= 0 && c < n;
                 const int cc = in ? c : 0;
                 const int ch = g * n + cc;
                 const uint8_t f = fw[fb + cc];
                 const int32_t w = WLAT[wrow + cc];
-                ok[u] = in & (f != 0) & (w >= j);
-                idx[u] = c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)cc * Pcap + (in ? p : 0)]);
+                const int32_t k = c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)cc * Pcap + (in ? p : 0)]);
+                idx[u] = (in & (f != 0) & (w >= j)) ? k : -1;
             }
             int64_t x[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) x[u] = p_ts[ok[u] ? idx[u] : 0];
+            for (int u = 0; u < U; u++) x[u] = p_ts[max(idx[u], 0)];
+            bool ok[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int c = c0 + 8 * u;
+                const int c = c0 + NG * u;
+                ok[u] = idx[u] >= 0;
                 const int64_t dlt = x[u] - base;
                 ovf |= ok[u] && (dlt < INT32_MIN || dlt > INT32_MAX);
                 if (c < n) vals[c * LD + e] = (uint32_t)(int32_t)dlt ^ 0x80000000u;
@@ -1483,14 +1497,14 @@ static void cts_small_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int 
 
 template <int NPAD, typename CT>
 static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
-    const size_t lds = (size_t)NPAD * 33 * sizeof(uint32_t);
+    const size_t lds = (size_t)NPAD * (kCtsTile + 1) * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD, CT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         attr = true;
     }
-    const unsigned grid = (unsigned)((int64_t)C * ((max_len + 31) / 32));
+    const unsigned grid = (unsigned)((int64_t)C * ((max_len + kCtsTile - 1) / kCtsTile));
     if (grid == 0) return;
     hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
                        a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
