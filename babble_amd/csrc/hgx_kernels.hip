@@ -385,13 +385,15 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
 // ---------------------------------------------------------------------------------
 // rounds. Step r: W'_r = {first event of each chain with round >= r}.
 // gather: copy the candidates' coordinate rows into compact per-round tables.
+// wfd16: the WFD rows are kept as raw uint16 firstDescendants (compact coordinates, the
+// k_round_step path for n <= 256), otherwise as decoded int32.
 template <typename CT>
 __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
                                const int32_t* __restrict__ c_len, const CT* __restrict__ LA,
                                const CT* __restrict__ FDT, const int32_t* __restrict__ p_gid,
                                const uint8_t* __restrict__ g_coin, int32_t* __restrict__ WLA,
                                int32_t* __restrict__ WFD, uint8_t* __restrict__ wflag, uint8_t* __restrict__ wcoin,
-                               int C, int n, int64_t P) {
+                               int C, int n, int64_t P, int wfd16) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)C * n) return;
     const int gc = (int)(t / n), i = (int)(t % n);
@@ -401,7 +403,8 @@ __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int3
     if (b < len) {
         const int p = c_off[gc] + b;
         WLA[wrow] = Coord<CT>::la(LA[(size_t)p * n + i]);
-        WFD[wrow] = Coord<CT>::fd(FDT[(size_t)i * P + p]);
+        if (wfd16) ((uint16_t*)WFD)[wrow] = (uint16_t)FDT[(size_t)i * P + p];
+        else WFD[wrow] = Coord<CT>::fd(FDT[(size_t)i * P + p]);
         if (i == 0) {
             wflag[(size_t)r * C + gc] = 1;
             wcoin[(size_t)r * C + gc] = g_coin[p_gid[p]];
@@ -1397,6 +1400,9 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 
 int fd_tile_rows(int n, int compact) {
     // <= 64 rows (one per lane), ~33 KB of LDS per block: 4 blocks (32 waves) per CU
+    // (measured at c3: 16 rows 17.2 ms, 32 rows 10.0, 64 rows 6.8; 128 rows in 64-row
+    // chunks 8.9 and 256 rows 14.9 -- fewer resident blocks. The kernel is bound by the
+    // per-(tile, target chain) latency chain, not by bytes.)
     int ft = (compact ? 16384 : 8192) / n;
     if (ft > 64) ft = 64;
     if (ft < 4) ft = 4;
@@ -1420,11 +1426,11 @@ void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n,
     if (a.compact)
         hipLaunchKernelGGL(k_round_gather<uint16_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const uint16_t*)a.LA, (const uint16_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
-                           a.WFD, a.wflag, a.wcoin, C, n, P);
+                           a.WFD, a.wflag, a.wcoin, C, n, P, n <= 256 ? 1 : 0);
     else
         hipLaunchKernelGGL(k_round_gather<int32_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const int32_t*)a.LA, (const int32_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
-                           a.WFD, a.wflag, a.wcoin, C, n, P);
+                           a.WFD, a.wflag, a.wcoin, C, n, P, 0);
 }
 
 void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {

@@ -171,8 +171,10 @@ __device__ __forceinline__ uint64_t seen_mask(const CT* __restrict__ row, const 
     uint32_t raw[CPL];
     load_slice<CT, CPL, VEC>(row + CPL * lane, raw);
     int32_t la[CPL];
+    // compact: raw LA (value + 1, none = 0) against fd + 1 (none = 0x10000): raw >= fd + 1
+    // iff LA >= FD, without decoding; int32: LA clamped below the none value MaxInt32
 #pragma unroll
-    for (int q = 0; q < CPL; q++) la[q] = min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
+    for (int q = 0; q < CPL; q++) la[q] = (sizeof(CT) == 2) ? (int32_t)raw[q] : min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
     // the masks are wave-uniform: keep them in SGPRs so the skips are scalar branches
     test = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(test >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)test);
@@ -234,25 +236,19 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const int j = lane + 64 * q;
         fl[q] = (j < n) ? A.wflag[crow + j] : 0u;
     }
-    // WFD rows hold the decoded firstDescendants (int32, MaxInt32 = none); lane l loads
-    // coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
+    // WFD rows hold the firstDescendants: raw uint16 for compact coordinates (half the
+    // bytes every block loads per round), decoded int32 (MaxInt32 = none) otherwise; lane
+    // l loads coordinates [CPL*l, CPL*l + CPL) of each row in one load when VEC
     uint32_t fdr[OWN][CPL];
     const int lc = (CPL * lane < n) ? CPL * lane : 0;
 #pragma unroll
     for (int o = 0; o < OWN; o++) {
         const int j = wg + NWC * ((o + rot) % OWN);
         const int jj = j < n ? j : 0;
-        load_slice<int32_t, CPL, VEC>(A.WFD + (crow + jj) * n + lc, fdr[o]);
-#ifdef HGX_EXP_WFD2   // experiment: the candidate rows loaded twice (bandwidth vs latency)
-        {
-            uint32_t t2[CPL];
-            load_slice<int32_t, CPL, VEC>(A.WFD + (crow + ((jj + 5) % n)) * n + lc, t2);
-            uint32_t z = 0;
-            asm volatile("" : "+v"(z));
-#pragma unroll
-            for (int q = 0; q < CPL; q++) fdr[o][q] |= t2[q] & z;
-        }
-#endif
+        if constexpr (sizeof(CT) == 2)
+            load_slice<uint16_t, CPL, VEC>((const uint16_t*)A.WFD + (crow + jj) * n + lc, fdr[o]);
+        else
+            load_slice<int32_t, CPL, VEC>(A.WFD + (crow + jj) * n + lc, fdr[o]);
     }
     const int len = A.c_len[gc], off = A.c_off[gc];
     const int b = A.Bm[(size_t)r * C + gc];
@@ -334,7 +330,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
             const int i = CPL * lane + q;
-            fd[o][q] = (cand && i < n) ? (int32_t)fdr[o][q] : kMaxI32;
+            fd[o][q] = (cand && i < n) ? ((sizeof(CT) == 2) ? (int32_t)fdr[o][q] + 1 : (int32_t)fdr[o][q]) : kMaxI32;
             // opaque from here on: otherwise the compiler keeps (cand && i < n) as a lane
             // mask per candidate and ANDs it into every compare (SGPR pressure, spills)
             asm volatile("" : "+v"(fd[o][q]));
@@ -423,7 +419,8 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = gt; i < n; i += NT) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            A.WFD[nrow + i] = Coord<CT>::fd((sizeof(CT) == 4) ? fd_s[i * P + pk] : fd_s[i * 2 * L::FDW + fsh + pk]);
+            if constexpr (sizeof(CT) == 2) ((uint16_t*)A.WFD)[nrow + i] = fd_s[i * 2 * L::FDW + fsh + pk];
+            else A.WFD[nrow + i] = fd_s[i * P + pk];
         }
         if (gt == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (gt == 0) {
