@@ -279,6 +279,17 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
     }
 }
 
+// inclusive max-scan over the 64 lanes (DPP row shifts, then row broadcasts 15 / 31)
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return x;
+}
+
 // ---------------------------------------------------------------------------------
 // firstDescendants: FD[(d,j)][c] = min{k : LA[(c,k)][d] >= j}, written
 // column-major FDT[c][pos(d,j)]. Block = (chain c, tile of FT rows). Each (d, j, c)
@@ -346,38 +357,43 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     __syncthreads();
     const bool last = (k1 == len);
     const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    // per target chain d: lane k = tile row k owns d's events j in (v[k-1], v[k]]
+    // (v = LA[(c, k0+k)][d], monotone in k; FD[(d,j)][c] = row k). The owner of every
+    // position is found without per-lane loops: each non-empty range marks its first
+    // position in a wave-private LDS slot array, and an inclusive max-scan over the 64
+    // positions of a chunk carries the owner forward; then one coalesced store per 64
+    // positions. (A per-lane store loop measured 9 stores and ~76 VALU per (tile, d),
+    // VALU-issue-bound at 6.2 ms for c3.)
+    // Per-d values are wave-uniform: readfirstlane keeps them (and the chunk loop) in SGPRs.
+    int32_t* slot = (int32_t*)(tw + (FT + 1) * ldw) + 64 * wave;
+    const int ownv = base_c + k0;
     for (int d = wave; d < n; d += nwaves) {
-        const int len_d = m_len[d];
+        const int len_d = __builtin_amdgcn_readfirstlane(m_len[d]);
         if (len_d == 0) continue;
-        const int base_d = m_base[d], off_d = m_off[d];
-        int lo = (k0 > 0) ? K::la(tile[d]) : base_d - 1;
+        const int base_d = __builtin_amdgcn_readfirstlane(m_base[d]);
+        const int off_d = __builtin_amdgcn_readfirstlane(m_off[d]);
+        int lo = (k0 > 0) ? __builtin_amdgcn_readfirstlane(K::la(tile[d])) : base_d - 1;
         if (lo < base_d - 1) lo = base_d - 1;
-        const int hi_val = (rows > 0) ? K::la(tile[rows * ld + d]) : lo;
-        const int hi = last ? (base_d + len_d - 1) : min(hi_val, base_d + len_d - 1);
-        CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
-        // lane k = tile row k: the row is the first descendant of d's events j in
-        // (v[k-1], v[k]] (v = LA[(c, k0+k)][d], monotone in k) -- one LDS read per lane and
-        // a short range of coalesced writes, instead of a binary search per j
         const int vmax = base_d + len_d - 1;
-        int v = (lane < rows) ? min(max(K::la(tile[(lane + 1) * ld + d]), lo), vmax) : hi_val;
-        int prev = __shfl_up(v, 1);
-        if (lane == 0) prev = lo;
-        const int L = (lane < rows) ? v - prev : 0;
-        if (__ballot(L > 16) == 0) {
-            const CT val = K::enc_fd(base_c + k0 + lane);
-            for (int t = 0; __ballot(t < L) != 0; t++)
-                if (t < L) out[prev + 1 + t] = val;
-            if (last)
-                for (int j = max(lo, min(hi_val, vmax)) + 1 + lane; j <= hi; j += 64) out[j] = K::enc_fd(kMaxI32);
-        } else {   // long ranges (a fast chain d seen by a slow chain c): per-j search
-            for (int j = lo + 1 + lane; j <= hi; j += 64) {
-                int a = 0, b = rows;
-                while (a < b) {
-                    const int m = (a + b) >> 1;
-                    if (K::la(tile[(m + 1) * ld + d]) >= j) b = m; else a = m + 1;
-                }
-                out[j] = K::enc_fd((a < rows) ? (base_c + k0 + a) : kMaxI32);
-            }
+        const int hi_val = (rows > 0) ? __builtin_amdgcn_readfirstlane(K::la(tile[rows * ld + d])) : lo;
+        const int hi = last ? vmax : min(hi_val, vmax);
+        CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
+        const int v = (lane < rows) ? min(max(K::la(tile[(lane + 1) * ld + d]), lo), vmax) : hi_val;
+        // first position of this lane's range = previous lane's v + 1 (lane 0: lo + 1)
+        const int start = __builtin_amdgcn_update_dpp(lo, v, 0x138, 0xf, 0xf, false) + 1;   // wave_shr:1
+        const bool own = lane < rows && v >= start;
+        const int vlast = max(lo, min(hi_val, vmax));   // end of the tile's last range
+        int carry = -1;
+        for (int j0 = lo + 1; j0 <= hi; j0 += 64) {   // scalar loop
+            slot[lane] = -1;
+            wave_lds_fence();
+            if (own && (unsigned)(start - j0) < 64u) slot[start - j0] = lane;
+            // past the last row (last tile only): none = MaxInt32, sentinel owner 64
+            if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 64;
+            wave_lds_fence();
+            const int o = max(wave_incl_max(slot[lane]), carry);
+            carry = __builtin_amdgcn_readlane(o, 63);
+            if (j0 + lane <= hi) out[j0 + lane] = K::enc_fd(o < rows ? ownv + o : kMaxI32);
         }
     }
 }
@@ -1413,7 +1429,8 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     const int ft = fd_tile_rows(n, a.compact);
     const int tiles = max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
-    const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n) * sizeof(int32_t);
+    // + 8 waves x 64 owner slots
+    const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n + 8 * 64) * sizeof(int32_t);
     if (a.compact)
         hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
                            (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P);
