@@ -137,9 +137,38 @@ __device__ uint64_t wave_select_kth(const uint64_t (&v)[CPL], const bool (&ok)[C
     return base;
 }
 
-// 32-bit variant for the common case (values already rebased): radix select with 8-bit
-// digits from the top set bit of the range, no per-pass range shrink. Requires
-// 0 <= K < #valid; every lane returns the result.
+// Inclusive wave scans in lane order on DPP (GFX9 row_shr 1/2/4/8 within rows of 16,
+// then row_bcast 15 / 31 across rows): a few VALU ops instead of ds_bpermute shuffles.
+// Lanes without a DPP source keep the identity `id`.
+#define HGX_DPP_SCAN(x, id, OP)                                                                  \
+    do {                                                                                         \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x111, 0xf, 0xf, false)); \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x112, 0xf, 0xf, false)); \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x114, 0xf, 0xf, false)); \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x118, 0xf, 0xf, false)); \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x142, 0xa, 0xf, false)); \
+        x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(x), 0x143, 0xc, 0xf, false)); \
+    } while (0)
+#define HGX_OP_ADD(a, b) ((a) + (b))
+#define HGX_OP_MIN(a, b) min((a), (b))
+#define HGX_OP_MAX(a, b) max((a), (b))
+
+__device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t x) { HGX_DPP_SCAN(x, 0u, HGX_OP_ADD); return x; }
+// wave-wide min / max of a u32, returned in an SGPR (lane 63 of the inclusive scan)
+__device__ __forceinline__ uint32_t wave_reduce_min_u32(uint32_t x) {
+    HGX_DPP_SCAN(x, 0xffffffffu, HGX_OP_MIN);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_reduce_max_u32(uint32_t x) {
+    HGX_DPP_SCAN(x, 0u, HGX_OP_MAX);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// 32-bit k-th smallest for the common case (values already rebased): radix select with
+// 8-bit digits from the top set bit of the range. Reductions and the bucket scan run on
+// DPP, the chosen bucket is read from the owning lane with readlane, and the wave's
+// 256-bin histogram (16-B aligned, lane l owns bins 4l..4l+3) is zeroed and read as one
+// 16-B access per lane. Requires 0 <= K < #valid; every lane returns the result.
 template <int CPL>
 __device__ uint32_t wave_select_kth32(const uint32_t (&v)[CPL], const bool (&ok)[CPL], int K,
                                       uint32_t* __restrict__ hist) {
@@ -148,10 +177,8 @@ __device__ uint32_t wave_select_kth32(const uint32_t (&v)[CPL], const bool (&ok)
 #pragma unroll
     for (int q = 0; q < CPL; q++)
         if (ok[q]) { lo = min(lo, v[q]); hi = max(hi, v[q]); }
-    for (int o = 32; o >= 1; o >>= 1) {
-        lo = min(lo, (uint32_t)__shfl_xor(lo, o));
-        hi = max(hi, (uint32_t)__shfl_xor(hi, o));
-    }
+    lo = wave_reduce_min_u32(lo);
+    hi = wave_reduce_max_u32(hi);
     const uint32_t range = hi - lo;
     if (range == 0) return lo;
     const int bits = 32 - __clz((int)range);
@@ -159,44 +186,32 @@ __device__ uint32_t wave_select_kth32(const uint32_t (&v)[CPL], const bool (&ok)
     bool act[CPL];
 #pragma unroll
     for (int q = 0; q < CPL; q++) { d[q] = v[q] - lo; act[q] = ok[q]; }
+    uint4* __restrict__ h4 = (uint4*)hist;
     uint32_t prefix = 0;
-    int k = K;
+    uint32_t k = (uint32_t)K;
     for (int shift = ((bits - 1) / 8) * 8; shift >= 0; shift -= 8) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) hist[lane * 4 + t] = 0;
+        h4[lane] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
 #pragma unroll
         for (int q = 0; q < CPL; q++)
             if (act[q]) atomicAdd(&hist[(d[q] >> shift) & 255u], 1u);
         wave_lds_fence();
-        uint32_t h[4], sum = 0;
-#pragma unroll
-        for (int t = 0; t < 4; t++) { h[t] = hist[lane * 4 + t]; sum += h[t]; }
-        uint32_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        const uint4 h = h4[lane];
+        const uint32_t sum = h.x + h.y + h.z + h.w;
+        const uint32_t incl = wave_scan_add_u32(sum);
         const uint32_t excl = incl - sum;
-        int bucket = -1;
-        uint32_t below = 0;
-        if ((uint32_t)k >= excl && (uint32_t)k < incl) {
-            uint32_t acc = excl;
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                if (bucket < 0 && (uint32_t)k < acc + h[t]) { bucket = lane * 4 + t; below = acc; }
-                acc += h[t];
-            }
-        }
-        const uint64_t bm = __ballot(bucket >= 0);
-        const int src = __ffsll((unsigned long long)bm) - 1;
-        bucket = __shfl(bucket, src);
-        below = __shfl(below, src);
+        // bucket of the k-th value inside this lane's 4 bins (meaningful in one lane)
+        const uint32_t a1 = excl + h.x, a2 = a1 + h.y, a3 = a2 + h.z;
+        const int bt = (k < a1) ? 0 : (k < a2) ? 1 : (k < a3) ? 2 : 3;
+        const uint32_t below = (k < a1) ? excl : (k < a2) ? a1 : (k < a3) ? a2 : a3;
+        const uint64_t bm = __ballot(k >= excl && k < incl);
+        const int src = (int)__builtin_ctzll(bm);
+        const uint32_t bucket = (uint32_t)__builtin_amdgcn_readlane(lane * 4 + bt, src);
+        k -= (uint32_t)__builtin_amdgcn_readlane((int)below, src);
         wave_lds_fence();
-        k -= (int)below;
-        prefix |= (uint32_t)bucket << shift;
+        prefix |= bucket << shift;
 #pragma unroll
-        for (int q = 0; q < CPL; q++) act[q] = act[q] && ((d[q] >> shift) & 255u) == (uint32_t)bucket;
+        for (int q = 0; q < CPL; q++) act[q] = act[q] && ((d[q] >> shift) & 255u) == bucket;
     }
     return lo + prefix;
 }

@@ -912,7 +912,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     __shared__ int32_t e_row[T], e_j[T], e_fb[T], e_g[T];
     __shared__ int64_t e_ts[T];
     __shared__ int32_t e_ovf[T];
-    __shared__ uint32_t whist[4][256];
+    __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
     __shared__ int32_t s_any;
     // time-major tiles: block i = tile i / C of chain i % C, so the blocks in flight cover
     // every chain at about the same time and their timestamp gathers (events of other
