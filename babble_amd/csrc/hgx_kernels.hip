@@ -401,8 +401,8 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
 // ---------------------------------------------------------------------------------
 // rounds. Step r: W'_r = {first event of each chain with round >= r}.
 // gather: copy the candidates' coordinate rows into compact per-round tables.
-// wfd16: the WFD rows are kept as raw uint16 firstDescendants (compact coordinates, the
-// k_round_step path for n <= 256), otherwise as decoded int32.
+// wfd16: the WFD rows are kept as raw uint16 firstDescendants (compact coordinates),
+// otherwise as decoded int32.
 template <typename CT>
 __global__ void k_round_gather(int r, const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_off,
                                const int32_t* __restrict__ c_len, const CT* __restrict__ LA,
@@ -1443,7 +1443,7 @@ void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n,
     if (a.compact)
         hipLaunchKernelGGL(k_round_gather<uint16_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const uint16_t*)a.LA, (const uint16_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,
-                           a.WFD, a.wflag, a.wcoin, C, n, P, n <= 256 ? 1 : 0);
+                           a.WFD, a.wflag, a.wcoin, C, n, P, 1);
     else
         hipLaunchKernelGGL(k_round_gather<int32_t>, dim3(nblk((int64_t)C * n, 256)), dim3(256), 0, s, r, a.Bm,
                            a.c_off, a.c_len, (const int32_t*)a.LA, (const int32_t*)a.FDT, a.p_gid, a.g_coin, a.WLA,

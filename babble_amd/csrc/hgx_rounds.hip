@@ -439,9 +439,16 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 // only the candidates seen there are binary-searched for their first seeing probe.
 // The count at probe p is the number of candidates first seen at or before p (an LDS
 // histogram). The own-chain candidate never counts at the probe that is itself.
+// waves per block: the candidates of a chain are walked per wave, so more waves per block
+// wins over more resident blocks (c5 step: 16 waves 470 us, 8 waves 539 us, 4 waves 854 us)
+#ifdef HGX_BIG_NWV   // experiment
+constexpr int kBigWaves = HGX_BIG_NWV;
+#else
+constexpr int kBigWaves = 16;
+#endif
 template <int CPL, int P, typename CT, bool VEC>
-__global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep) {
-    constexpr int NWV = 16;
+__global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, int kstep) {
+    constexpr int NWV = kBigWaves;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     extern __shared__ __attribute__((aligned(16))) uint8_t big_lds[];
     CT* __restrict__ la_s = (CT*)big_lds;   // [P][n] probe rows (+ slack)
@@ -488,20 +495,39 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
             }
         }
     };
+    // compact: raw LA (value + 1, none = 0) against the raw WFD value + 1 (none = 0x10000),
+    // no decode; int32: LA clamped below the none value MaxInt32
     auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
         uint32_t raw[CPL];
         load_row(la_s + pp * n, raw, false);
         int tot = 0;
 #pragma unroll
-        for (int q = 0; q < CPL; q++) tot += __popcll(__ballot(min(Coord<CT>::la(raw[q]), kMaxI32 - 1) >= fd[q]));
+        for (int q = 0; q < CPL; q++) {
+            const int32_t la = (sizeof(CT) == 2) ? (int32_t)raw[q] : min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
+            tot += __popcll(__ballot(la >= fd[q]));
+        }
         return tot >= sm && !(j == cl && kb + pp == b);
     };
-    auto load_fd = [&](int j, bool cand, int32_t (&fd)[CPL]) {
-        const int32_t* __restrict__ row = A.WFD + (crow + j) * n;
+    // WFD row of candidate j in the lane's coordinate order (compact rows are raw uint16,
+    // read as coordinate pairs); j >= n loads nothing. Issued one candidate ahead of use.
+    auto load_fd = [&](int j, int32_t (&fd)[CPL]) {
+        if (j >= n) return;
+        if constexpr (sizeof(CT) == 2) {
+            const uint16_t* __restrict__ row = (const uint16_t*)A.WFD + (crow + j) * n;
 #pragma unroll
-        for (int q = 0; q < CPL; q++) {
-            const int i = coord(q);
-            fd[q] = (cand && i < n) ? row[i] : kMaxI32;
+            for (int q2 = 0; q2 < CPL / 2; q2++) {
+                const int i = 2 * lane + 128 * q2;
+                const uint32_t w = (i < n) ? *(const uint32_t*)(row + i) : 0u;
+                fd[2 * q2] = (i < n) ? (int32_t)(w & 0xFFFFu) + 1 : kMaxI32;
+                fd[2 * q2 + 1] = (i < n) ? (int32_t)(w >> 16) + 1 : kMaxI32;
+            }
+        } else {
+            const int32_t* __restrict__ row = A.WFD + (crow + j) * n;
+#pragma unroll
+            for (int q = 0; q < CPL; q++) {
+                const int i = coord(q);
+                fd[q] = (i < n) ? row[i] : kMaxI32;
+            }
         }
     };
     int kbase = b, np = 0, kstar = len, pk = 0;
@@ -530,10 +556,14 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         __syncthreads();
         // pass 1: every candidate against the window's last probe
         int cnt = 0;
+        int32_t fdn[CPL];
+        load_fd(wave, fdn);
         for (int j = wave; j < n; j += NWV) {
             int32_t fd[CPL];
+#pragma unroll
+            for (int q = 0; q < CPL; q++) fd[q] = fdn[q];
+            load_fd(j + NWV, fdn);   // next candidate's row in flight during this test
             const bool cand = A.wflag[crow + j] == 1;
-            load_fd(j, cand, fd);
             const bool sl = cand && seen_at(fd, np - 1, j, kbase);
             cnt += sl ? 1 : 0;
             if (lane == 0) fhit[j] = sl ? (uint8_t)(np - 1) : (uint8_t)255;
@@ -545,10 +575,22 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         for (int w = 0; w < NWV; w++) tot += s_cnt[w];
         if (tot >= sm) {
             // pass 2: first seeing probe of the candidates seen at the last probe
-            for (int j = wave; j < n; j += NWV) {
-                if (fhit[j] == 255) continue;   // wave-uniform (written by this wave's lane 0)
+            // this wave's candidates seen at the last probe (fhit written by this wave's
+            // lane 0, so the walk is wave-uniform), rows loaded one candidate ahead
+            auto next_seen = [&](int j) {
+                while (j < n && fhit[j] == 255) j += NWV;
+                return j;
+            };
+            int jn = next_seen(wave);
+            int32_t fdn2[CPL];
+            load_fd(jn, fdn2);
+            while (jn < n) {
+                const int j = jn;
                 int32_t fd[CPL];
-                load_fd(j, true, fd);
+#pragma unroll
+                for (int q = 0; q < CPL; q++) fd[q] = fdn2[q];
+                jn = next_seen(j + NWV);
+                load_fd(jn, fdn2);
                 int lo = 0, hi = np - 1;
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
@@ -596,7 +638,8 @@ __global__ void __launch_bounds__(1024) k_round_step_big(RoundArgs A, int kstep)
         const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             A.WLA[nrow + i] = Coord<CT>::la(la_s[pk * n + i]);
-            A.WFD[nrow + i] = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + p]);
+            if constexpr (sizeof(CT) == 2) ((uint16_t*)A.WFD)[nrow + i] = ((const CT*)A.FDT)[(size_t)i * A.Pcap + p];
+            else A.WFD[nrow + i] = ((const CT*)A.FDT)[(size_t)i * A.Pcap + p];
         }
         if (threadIdx.x == 0) A.wflag[(size_t)(r + 1) * C + gc] = 1;
     } else if (threadIdx.x == 0) {
@@ -614,7 +657,7 @@ static hipError_t step_big_launch_v(hipStream_t s, const RoundArgs& A, int kstep
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_round_step_big<CPL, P, CT, VEC>), dim3(A.C), dim3(1024), lds, s, A, kstep);
+    hipLaunchKernelGGL((k_round_step_big<CPL, P, CT, VEC>), dim3(A.C), dim3(kBigWaves * 64), lds, s, A, kstep);
     return hipGetLastError();
 }
 
