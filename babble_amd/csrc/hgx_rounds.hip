@@ -24,6 +24,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <type_traits>
 #include <utility>
 
 #include "hgx_device.h"
@@ -94,22 +95,64 @@ __device__ __forceinline__ int count_seen(const int32_t (&la)[CPL], const int32_
     }
 }
 
-// Candidates whose bit is clear in `test` are skipped (wave-uniform branch).
+#ifndef HGX_TALLY_FUSED
+#define HGX_TALLY_SPLIT 1
+#endif
+// Candidates whose bit is clear in `test` are skipped (wave-uniform branch; a 32-bit mask
+// when OWN <= 32, so the skip is one scalar bit test). HGX_TALLY_SPLIT: the popcount of
+// each of the CPL compare masks goes to lane O of its own partial register tv[q] and the
+// partials are added once per probe in VALU, instead of CPL - 1 scalar adds per candidate
+// (the tally is scalar-issue-bound: 4 s_bcnt1 + 3 s_add + skip test per candidate).
+template <int OWN>
+using TallyMask = typename std::conditional<(OWN <= 32), uint32_t, uint64_t>::type;
 template <int O, int CPL, int OWN>
-__device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int& tv,
-                                          uint64_t test) {
-    if ((test >> O) & 1ull) {
-        const int tot = count_seen<CPL>(la, fd[O]);
-        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv) : "s"(tot), "i"(O));
+__device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int (&tv)[CPL],
+                                          TallyMask<OWN> test) {
+    if ((test >> O) & 1u) {
+#ifdef HGX_TALLY_SPLIT
+        if constexpr (CPL == 4) {
+            uint64_t m0, m1, m2, m3;
+            asm volatile(
+                "v_cmp_ge_i32_e64 %0, %4, %8\n\t"
+                "v_cmp_ge_i32_e64 %1, %5, %9\n\t"
+                "v_cmp_ge_i32_e64 %2, %6, %10\n\t"
+                "v_cmp_ge_i32_e64 %3, %7, %11"
+                : "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3)
+                : "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(fd[O][0]), "v"(fd[O][1]), "v"(fd[O][2]),
+                  "v"(fd[O][3]));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[0]) : "s"(__popcll(m0)), "i"(O));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[1]) : "s"(__popcll(m1)), "i"(O));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[2]) : "s"(__popcll(m2)), "i"(O));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[3]) : "s"(__popcll(m3)), "i"(O));
+        } else if constexpr (CPL == 2) {
+            uint64_t m0, m1;
+            asm volatile(
+                "v_cmp_ge_i32_e64 %0, %2, %4\n\t"
+                "v_cmp_ge_i32_e64 %1, %3, %5"
+                : "=s"(m0), "=s"(m1)
+                : "v"(la[0]), "v"(la[1]), "v"(fd[O][0]), "v"(fd[O][1]));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[0]) : "s"(__popcll(m0)), "i"(O));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[1]) : "s"(__popcll(m1)), "i"(O));
+        } else
+#endif
+        {
+            const int tot = count_seen<CPL>(la, fd[O]);
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[0]) : "s"(tot), "i"(O));
+        }
     }
 }
 
 template <int CPL, int OWN, int... O>
-__device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], uint64_t test,
+__device__ __forceinline__ int tally(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], TallyMask<OWN> test,
                                      std::integer_sequence<int, O...>) {
-    int tv = 0;
+    int tv[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) tv[q] = 0;
     (tally_one<O, CPL, OWN>(la, fd, tv, test), ...);
-    return tv;
+    int t = tv[0];
+#pragma unroll
+    for (int q = 1; q < CPL; q++) t += tv[q];
+    return t;
 }
 
 // CPL consecutive coordinates of type CT as one load (VEC: n % CPL == 0, so the
@@ -178,7 +221,7 @@ __device__ __forceinline__ uint64_t seen_mask(const CT* __restrict__ row, const 
     // the masks are wave-uniform: keep them in SGPRs so the skips are scalar branches
     test = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(test >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)test);
-    const int tv = tally<CPL, OWN>(la, fd, test, std::make_integer_sequence<int, OWN>{});
+    const int tv = tally<CPL, OWN>(la, fd, (TallyMask<OWN>)test, std::make_integer_sequence<int, OWN>{});
     return (__ballot(lane < OWN && tv >= sm && lane != excl) & test) | known;
 }
 
