@@ -497,6 +497,7 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
     CT* __restrict__ la_s = (CT*)big_lds;   // [P][n] probe rows (+ slack)
     __shared__ int32_t hist[P + 1];
     __shared__ uint8_t fhit[1024];               // first probe seeing candidate j (255: none / no candidate)
+    __shared__ uint8_t s_cand[1024];             // candidate flags of the round (staged once)
     __shared__ unsigned long long s_mask[16];
     __shared__ int32_t s_cnt[NWV];
     __shared__ int32_t s_f;
@@ -543,12 +544,24 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
     auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
         uint32_t raw[CPL];
         load_row(la_s + pp * n, raw, false);
+#ifdef HGX_BIG_BALLOT   // experiment: one ballot + scalar popcount per coordinate slot
         int tot = 0;
 #pragma unroll
         for (int q = 0; q < CPL; q++) {
             const int32_t la = (sizeof(CT) == 2) ? (int32_t)raw[q] : min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
             tot += __popcll(__ballot(la >= fd[q]));
         }
+#else
+        // per-lane count over the CPL slots in VALU, one DPP wave sum: CPL scalar popcounts
+        // and adds per test would make the walk scalar-issue-bound
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int32_t la = (sizeof(CT) == 2) ? (int32_t)raw[q] : min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
+            c += (la >= fd[q]) ? 1u : 0u;
+        }
+        const int tot = (int)__builtin_amdgcn_readlane((int)wave_scan_add_u32(c), 63);
+#endif
         return tot >= sm && !(j == cl && kb + pp == b);
     };
     // WFD row of candidate j in the lane's coordinate order (compact rows are raw uint16,
@@ -573,6 +586,7 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
             }
         }
     };
+    for (int t = threadIdx.x; t < n; t += blockDim.x) s_cand[t] = A.wflag[crow + t];   // before the first barrier
     int kbase = b, np = 0, kstar = len, pk = 0;
     for (;;) {
         np = min(P, len - kbase);
@@ -606,7 +620,7 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
 #pragma unroll
             for (int q = 0; q < CPL; q++) fd[q] = fdn[q];
             load_fd(j + NWV, fdn);   // next candidate's row in flight during this test
-            const bool cand = A.wflag[crow + j] == 1;
+            const bool cand = s_cand[j] == 1;
             const bool sl = cand && seen_at(fd, np - 1, j, kbase);
             cnt += sl ? 1 : 0;
             if (lane == 0) fhit[j] = sl ? (uint8_t)(np - 1) : (uint8_t)255;
