@@ -90,6 +90,10 @@ def lib():
         _sig(L, nm, i32, [p, i64, i64] if nm not in ("hgx_round", "hgx_witness") else [p, i64])
     _sig(L, "hgx_oldest_self_ancestor_to_see", i64, [p, i64, i64])
     _sig(L, "hgx_block_hash", i32, [i64, i32, p, p, i32, p])
+    _sig(L, "hgx_sha256_batch", i32, [i32, p, p, i64, p, p])
+    _sig(L, "hgx_sha256_batch_device", i32, [p, p, i64, p, p])
+    _sig(L, "hgx_sha256_bench", i32, [i32, i64, i32, i32, C.c_uint64, i32, i32, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int64), i64, p])
     _sig(L, "hgx_phase_times", i32, [p, p, i32])
     _sig(L, "hgx_kernel_stats", i32, [p, i32, C.c_char_p, i32, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_double)])

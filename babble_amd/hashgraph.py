@@ -281,3 +281,62 @@ def block_hash(rr: int, txs: List[bytes], tx_nil: bool) -> bytes:
     if rc:
         raise HgxError(rc, "hgx_block_hash failed")
     return out.raw
+
+
+def sha256_batch(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
+    """crypto.SHA256 (crypto/utils.go:11-16) of every message data[offsets[i]:offsets[i+1]]
+    in one device launch (hgx_sha256_batch). Returns a (count, 32) uint8 array.
+    Raises HgxError (code HGX_ERR_DEVICE) without a gfx950 GPU: there is no CPU path."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    count = max(len(offsets) - 1, 0)
+    out = np.zeros((count, 32), dtype=np.uint8)
+    err = hgx_error()
+    rc = _lib.lib().hgx_sha256_batch(device, ptr(data) if data.size else None, ptr(offsets) if count else None,
+                                     count, ptr(out) if count else None, C.byref(err))
+    _lib.check(rc, err)
+    return out
+
+
+def event_ids(bodies: Sequence[bytes], device: int = 0) -> List[bytes]:
+    """Event.Hash for a batch of json.Encoder(Event) encodings (hashgraph/event.go:171-180),
+    hashed on the GPU; Hex() is "0x%X" of each (event.go:183-188)."""
+    lens = np.fromiter((len(b) for b in bodies), dtype=np.int64, count=len(bodies))
+    offsets = np.zeros(len(bodies) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.frombuffer(b"".join(bodies), dtype=np.uint8)
+    return [bytes(r) for r in sha256_batch(data, offsets, device)]
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def sha256_bench_messages(n: int, min_len: int, max_len: int, seed: int) -> List[bytes]:
+    """The first n synthetic messages hgx_sha256_bench hashes (include/hgx.h), rebuilt on the host."""
+    i = np.arange(n, dtype=np.uint64)
+    lens = min_len + (_splitmix64(~np.uint64(seed) + i) % np.uint64(max_len - min_len + 1)).astype(np.int64)
+    total = int(lens.sum())
+    words = _splitmix64(np.uint64(seed) + np.arange((total + 7) // 8, dtype=np.uint64))
+    blob = words.astype("<u8").tobytes()
+    out, o = [], 0
+    for ln in lens:
+        out.append(blob[o:o + int(ln)])
+        o += int(ln)
+    return out
+
+
+def sha256_bench(count: int, min_len: int, max_len: int, seed: int = 5, warmup: int = 1, iters: int = 3,
+                 n_sample: int = 64, device: int = 0) -> dict:
+    """Device-resident SHA-256 throughput (hgx_sha256_bench) + digests of the first n_sample messages."""
+    ms, tot, nb = C.c_double(), C.c_int64(), C.c_int64()
+    sample = np.zeros((n_sample, 32), dtype=np.uint8)
+    rc = _lib.lib().hgx_sha256_bench(device, count, min_len, max_len, seed, warmup, iters, C.byref(ms),
+                                     C.byref(tot), C.byref(nb), n_sample, ptr(sample))
+    if rc:
+        raise HgxError(rc, "hgx_sha256_bench failed")
+    return {"ms_per_launch": ms.value, "bytes": tot.value, "blocks": nb.value, "sample": sample}

@@ -116,6 +116,33 @@ class Reducer:
         return x if self.dist is None else self._reduce(x, self.dist.ReduceOp.SUM)
 
 
+# SHA-256 compression in gfx950 lane instructions per 64-byte block (3-input v_bitop3/v_add3):
+# 64 rounds x (6 rotates + 2 xor3 + Ch + Maj + 4 adds) + 48 schedule words x (4 rotates + 2 shifts
+# + 2 xor3 + 3 adds); VALU peak = 32 lanes/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz (MI355X_MICROARCH.md)
+SHA_OPS_PER_BLOCK = 64 * 14 + 48 * 11
+VALU_PEAK_TOPS = 32 * 4 * 256 * 2.4e9 / 1e12
+
+
+def ingest_leg(count, steps, warmup, device):
+    """Side leg: Event.Hash ids (hashgraph/event.go:171-180) of `count` synthetic
+    event bodies of Go-JSON event size (400..560 B, PRNG bytes), HBM-resident, hashed by
+    k_sha256_batch; device time per launch from HIP events on the launch stream (hgx_sha256_bench)."""
+    import hashlib
+    from babble_amd.hashgraph import sha256_bench, sha256_bench_messages
+    lo, hi, seed = 400, 560, 5
+    r = sha256_bench(count, lo, hi, seed, warmup=max(1, warmup), iters=steps, n_sample=64, device=device)
+    # sanity sample against the host digest (tests/test_gpu_sha256.py covers the kernel in full)
+    msgs = sha256_bench_messages(64, lo, hi, seed)
+    assert all(hashlib.sha256(m).digest() == bytes(d) for m, d in zip(msgs, r["sample"])), "SHA-256 mismatch"
+    ms = r["ms_per_launch"]
+    achieved = r["blocks"] * SHA_OPS_PER_BLOCK / (ms * 1e-3) / 1e12
+    return {"kernel": "k_sha256_batch", "events": count, "bytes": r["bytes"], "ms_per_launch": ms,
+            "event_ids_per_s": count / (ms * 1e-3), "input_GB_per_s": r["bytes"] / (ms * 1e-3) / 1e9,
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                         "frac": achieved / VALU_PEAK_TOPS, "ops_per_block": SHA_OPS_PER_BLOCK,
+                         "blocks_per_launch": r["blocks"]}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +150,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the batched event-id SHA-256 side leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,6 +245,11 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
         }
+        if not args.no_ingest:
+            try:
+                result["ingest_sha256"] = ingest_leg(int(tr.E), args.steps, args.warmup, local_rank)
+            except Exception as e:  # reported, never fatal
+                result["ingest_sha256"] = {"error": str(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(args.config)

@@ -150,6 +150,27 @@ int32_t hgx_witness(hgx_ctx* ctx, int64_t x);
 int32_t hgx_block_hash(int64_t round_received, int32_t ntx, const uint8_t* const* tx, const int64_t* tx_len,
                        int32_t tx_nil, uint8_t* out32);
 
+/* ---- ingest front end: batched SHA-256 ----------------- */
+/* crypto.SHA256 (crypto/utils.go:11-16) of `count` messages in one launch, message i =
+ * data[offsets[i], offsets[i+1]) (offsets has count+1 non-decreasing entries). Replaces the
+ * per-event calls Event.Hash (hashgraph/event.go:171-180; the event id of Hex() :183-188),
+ * EventBody.Hash (:48-54, the bytes Verify checks :142-152) and Block.Hash (block.go:44-53)
+ * over a whole sync batch (node/core.go:199-211). Host buffers, copied to HBM; out32 gets
+ * 32 bytes per message. HGX_ERR_DEVICE without a gfx950 device (no CPU fallback). */
+int32_t hgx_sha256_batch(int32_t device, const uint8_t* data, const int64_t* offsets, int64_t count,
+                         uint8_t* out32, hgx_error* err);
+/* The same on device-resident buffers, enqueued on `stream` (a hipStream_t; NULL = null
+ * stream) without synchronising. d_out32 must be 4-byte aligned. */
+int32_t hgx_sha256_batch_device(const uint8_t* d_data, const int64_t* d_offsets, int64_t count,
+                                uint8_t* d_out32, void* stream);
+/* Measurement: `count` synthetic messages resident in HBM (message i has length
+ * min_len + splitmix64(~seed + i) % (max_len - min_len + 1); packed 8-byte word j of the
+ * data is splitmix64(seed + j)), hashed warmup + iters times; *ms_per_launch from HIP
+ * events on the launch stream; digests of the first n_sample messages to sample32. */
+int32_t hgx_sha256_bench(int32_t device, int64_t count, int32_t min_len, int32_t max_len, uint64_t seed,
+                         int32_t warmup, int32_t iters, double* ms_per_launch, int64_t* total_bytes,
+                         int64_t* n_blocks, int64_t n_sample, uint8_t* sample32);
+
 /* ---- timing / instrumentation --------------------------------------------- */
 /* per-phase device times (ms) of the last calls: coords, rounds, fame, order; then
  * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16) */

@@ -64,3 +64,16 @@ def test_trace_generator_deterministic():
         assert a.index[idx].tolist() == list(range(len(idx)))
         assert a.sp[idx[1:]].tolist() == idx[:-1].tolist()
     assert trace.payload(3, 17) == b"p003 tx 00000017"
+
+
+def test_sha256_batch_validates_then_fails_loudly_without_gpu():
+    import torch
+    from babble_amd.hashgraph import sha256_batch
+    with pytest.raises(_lib.HgxError) as ei:
+        sha256_batch(np.zeros(4, np.uint8), np.array([0, 3, 2], np.int64))
+    assert ei.value.code == 102 and "non-decreasing" in str(ei.value)
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.HgxError) as ei:
+        sha256_batch(np.zeros(4, np.uint8), np.array([0, 2, 4], np.int64))
+    assert "no CPU fallback" in str(ei.value)
