@@ -73,7 +73,7 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 #undef HGX_SHA_R
 
 // One lane per message i = data[offsets[i], offsets[i+1]); digest to out + 32 i.
-__global__ __launch_bounds__(256) void k_sha256_batch(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sha256_batch(const uint8_t* __restrict__ data,
                                                       const int64_t* __restrict__ offsets, int64_t count,
                                                       uint8_t* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -105,17 +105,18 @@ __global__ __launch_bounds__(256) void k_sha256_batch(const uint8_t* __restrict_
 #pragma unroll
         for (int j = 0; j < 17; j++) d[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
         uint32_t w[16];
+        const int r = (int)(rem < 64 ? rem : 64);   // valid bytes in this block, 32-bit math below
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const uint32_t x = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh));
-            const int64_t v = rem - 4 * k;   // valid bytes of word k
+            const int v = r - 4 * k;   // valid bytes of word k
             uint32_t y;
             if (v >= 4) y = x;
             else if (v > 0) y = (x & (0xFFFFFFFFu << (32 - 8 * v))) | (0x80u << (24 - 8 * v));
             else y = (v == 0) ? 0x80000000u : 0u;
             w[k] = y;
         }
-        if (b == nb - 1) {
+        if (b == nb - 1) {   // the last block (rem <= 55) carries the bit length
             w[14] = (uint32_t)(bits >> 32);
             w[15] = (uint32_t)bits;
         }
