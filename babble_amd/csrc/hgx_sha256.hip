@@ -20,6 +20,13 @@
 
 #include "hgx.h"
 
+#ifndef HGX_SHA_WAVES
+#define HGX_SHA_WAVES 4
+#endif
+#ifndef HGX_SHA_PREFETCH
+#define HGX_SHA_PREFETCH 1
+#endif
+
 namespace hgx {
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
@@ -73,7 +80,7 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 #undef HGX_SHA_R
 
 // One lane per message i = data[offsets[i], offsets[i+1]); digest to out + 32 i.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sha256_batch(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGX_SHA_WAVES))) void k_sha256_batch(const uint8_t* __restrict__ data,
                                                       const int64_t* __restrict__ offsets, int64_t count,
                                                       uint8_t* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -94,13 +101,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         for (int t = 0; t < 5; t++) E[t] = (16 * t - sh16 < rem) ? vp[4 * b + t] : make_uint4(0, 0, 0, 0);
     };
     uint4 E[5];
-    load_block(0, E);
+    if (HGX_SHA_PREFETCH) load_block(0, E);
     for (int64_t b = 0; b < nb; b++) {
+        if (!HGX_SHA_PREFETCH) load_block(b, E);
         const int64_t rem = len - 64 * b;   // message bytes from this block's first byte on
         uint32_t D[20];
 #pragma unroll
         for (int t = 0; t < 5; t++) { D[4 * t] = E[t].x; D[4 * t + 1] = E[t].y; D[4 * t + 2] = E[t].z; D[4 * t + 3] = E[t].w; }
-        if (b + 1 < nb) load_block(b + 1, E);   // next block in flight during this compression
+        if (HGX_SHA_PREFETCH && b + 1 < nb) load_block(b + 1, E);   // next block in flight during this compression
         uint32_t d[17];
 #pragma unroll
         for (int j = 0; j < 17; j++) d[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
