@@ -64,7 +64,9 @@ def lib():
     _sig(L, "hgx_create_batch", p, [i32, i32, i64, i32, E])
     _sig(L, "hgx_destroy", None, [p])
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
+    _sig(L, "hgx_insert_events_device", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_reset_consensus", i32, [p])
+    _sig(L, "hgx_clear", i32, [p])
     for nm in ("hgx_divide_rounds", "hgx_decide_fame", "hgx_find_order", "hgx_run_consensus"):
         _sig(L, nm, i32, [p, E])
     _sig(L, "hgx_num_events", i64, [p])
@@ -83,6 +85,15 @@ def lib():
     _sig(L, "hgx_consensus_events", i32, [p, i32, i64, i64, p])
     _sig(L, "hgx_num_blocks", i64, [p, i32])
     _sig(L, "hgx_block_info", i32, [p, i32, i64, p, p, p, p, p, p])
+    _sig(L, "hgx_get_block", i32, [p, i32, i32, p, E])
+    _sig(L, "hgx_consensus_received", i32, [p, i32, i64, i64, p, p, p])
+    _sig(L, "hgx_last_from", i32, [p, i32, p, p, E])
+    _sig(L, "hgx_participant_events", i32, [p, i32, i64, p, i64, p, E])
+    _sig(L, "hgx_participant_event", i32, [p, i32, i64, p, E])
+    _sig(L, "hgx_get_root", i32, [p, i32, p, p, p, p, E])
+    _sig(L, "hgx_get_event", i32, [p, i64, p, p, p, p, p, p, p, E])
+    _sig(L, "hgx_wire_info", i32, [p, i64, i64, p, p, p])
+    _sig(L, "hgx_read_wire_info", i32, [p, i32, i64, i32, i64, p, p, E])
     _sig(L, "hgx_get_rounds", i32, [p, i64, i64, p, p, p])
     _sig(L, "hgx_get_received", i32, [p, i64, i64, p, p])
     _sig(L, "hgx_get_coords", i32, [p, i64, p, p])
@@ -100,6 +111,8 @@ def lib():
     _sig(L, "hgx_reset_stats", i32, [p])
     _sig(L, "hgx_set_kernel_timing", i32, [p, i32])
     _sig(L, "hgx_set_coord_storage", i32, [p, i32])
+    _sig(L, "hgx_set_fame_tally", i32, [p, i32])
+    _sig(L, "hgx_reserve_rounds", i32, [p, i32])
     _L = L
     return L
 

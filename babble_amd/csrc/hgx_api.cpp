@@ -88,13 +88,8 @@ struct hgx_ctx {
     hgx::Engine eng;
     int G = 1, n = 0, C = 0, sm = 0;
     int64_t cap = 0;
-    // host event mirror (gid order)
-    std::vector<int32_t> creator, index32, sp, op, ntx;
-    std::vector<int64_t> ts;
-    std::vector<uint8_t> S, coin, loaded, txnil;
-    std::vector<int32_t> chain_len, chain_base;
-    std::vector<int64_t> last_gid, last_index;
-    std::vector<std::vector<int32_t>> chain_gids;
+    // per-creator state after the last insert ([C], copied back from the device)
+    std::vector<int32_t> chain_len, chain_base, last_gid, last_index;
     int64_t E = 0, E_div = 0;
     bool divided = false;
     hgx::RoundsHost rh;
@@ -102,6 +97,11 @@ struct hgx_ctx {
     OrderArena arena;                        // consensus orders (gids) of all graphs
     std::vector<GraphOrder> order;           // [G] segments of each graph's order in the arena
     std::vector<int64_t> g_events, g_loaded;  // [G] inserted events / loaded events per graph
+    // per-event columns (gid order), mirrored from the device when a getter needs them
+    bool mirror_ok = false;
+    std::vector<int32_t> creator, index32, sp, op;
+    bool chains_ok = false;
+    std::vector<std::vector<int32_t>> chain_gids;   // [C] gids of each creator's events in Index order
     // getter caches
     bool rounds_cached = false;
     std::vector<int32_t> round_cache;
@@ -114,6 +114,11 @@ static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
     if (!err) return;
     err->code = code;
     std::snprintf(err->msg, sizeof(err->msg), "%s", msg.c_str());
+}
+
+static int32_t ok(hgx_error* err) {
+    if (err) set_err(err, HGX_OK, "");
+    return HGX_OK;
 }
 
 static int32_t dev_err(hgx_error* err, hipError_t e, const char* where) {
@@ -131,6 +136,51 @@ static std::string go_rune(int64_t v) {
     else { s += (char)(0xF0 | (r >> 18)); s += (char)(0x80 | ((r >> 12) & 63)); s += (char)(0x80 | ((r >> 6) & 63)); s += (char)(0x80 | (r & 63)); }
     return s;
 }
+
+// Every entry point that touches the engine runs on the context's device and restores the
+// caller's current device on return (cgo moves goroutines between OS threads; a thread
+// starts on device 0).
+struct DeviceGuard {
+    int prev = -1, want = 0;
+    explicit DeviceGuard(const hgx_ctx* c) : want(c ? c->eng.dev : 0) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (c && prev != want) (void)hipSetDevice(want);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+    }
+};
+
+static int32_t ensure_mirror(hgx_ctx* c) {
+    if (c->mirror_ok) return HGX_OK;
+    if (c->eng.get_events(c->creator, c->index32, c->sp, c->op) != hipSuccess) return HGX_ERR_DEVICE;
+    c->mirror_ok = true;
+    return HGX_OK;
+}
+
+static int32_t ensure_chains(hgx_ctx* c) {
+    if (c->chains_ok) return HGX_OK;
+    if (ensure_mirror(c)) return HGX_ERR_DEVICE;
+    for (auto& v : c->chain_gids) v.clear();
+    for (int64_t g = 0; g < c->E; g++) c->chain_gids[(size_t)c->creator[(size_t)g]].push_back((int32_t)g);
+    c->chains_ok = true;
+    return HGX_OK;
+}
+
+static int graph_of(const hgx_ctx* c, int64_t x) { return c->creator[(size_t)x] / c->n; }
+
+// walk the graph's order segments over positions [first, first + count)
+template <typename F>
+static void walk_order(hgx_ctx* c, int32_t g, int64_t first, int64_t count, F&& f) {
+    int64_t pos = 0, k = 0;
+    for (const GraphOrder::Seg& sg : c->order[g].segs) {
+        const int64_t a = std::max<int64_t>(first, pos), b = std::min<int64_t>(first + count, pos + (int64_t)sg.len);
+        for (int64_t i = a; i < b; i++) f(k++, (int64_t)c->arena.p[sg.off + (size_t)(i - pos)]);
+        pos += (int64_t)sg.len;
+        if (pos >= first + count) break;
+    }
+}
+
 
 extern "C" {
 
@@ -150,8 +200,11 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->C = n_graphs * n_participants;
     c->sm = 2 * n_participants / 3 + 1;
     c->cap = capacity_events;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
     std::string why;
     hipError_t e = c->eng.init(device, n_graphs, n_participants, capacity_events, why);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         set_err(err, HGX_ERR_DEVICE, "hgx_create: " + (why.empty() ? std::string(hipGetErrorString(e)) : why));
         delete c;
@@ -166,9 +219,7 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->order = std::vector<GraphOrder>(n_graphs);
     c->g_events.assign(n_graphs, 0);
     c->g_loaded.assign(n_graphs, 0);
-    const size_t rsv = (size_t)std::min<int64_t>(capacity_events, 1 << 22);
-    c->creator.reserve(rsv);
-    if (err) set_err(err, HGX_OK, "");
+    ok(err);
     return c;
 }
 
@@ -176,89 +227,142 @@ hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t dev
     return hgx_create_batch(1, n_participants, capacity_events, device, err);
 }
 
-void hgx_destroy(hgx_ctx* ctx) { delete ctx; }
+void hgx_destroy(hgx_ctx* ctx) {
+    if (!ctx) return;
+    DeviceGuard dg(ctx);
+    delete ctx;
+}
 
 // ---- InsertEvent (hashgraph.go:356-401) ------------------------------------------
-int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
-    if (n_inserted) *n_inserted = 0;
-    if (!c || !ev || count < 0) { set_err(err, HGX_ERR_INVALID, "hgx_insert_events: bad arguments"); return HGX_ERR_INVALID; }
-    const int64_t first = c->E;
-    int32_t rc = HGX_OK;
-    std::string msg;
-    int64_t k = 0;
-    for (; k < count; k++) {
-        const int32_t cr = ev->creator[k];
-        const int64_t sp = ev->self_parent[k], op = ev->other_parent[k], idx = ev->index[k];
-        // event.Verify(): signature verification stays on the Go side
-        if (cr < 0 || cr >= c->C) {   // Store.LastFrom -> KeyNotFound (inmem_store.go:85-90)
-            rc = HGX_ERR_KEY_NOT_FOUND;
-            msg = "CheckSelfParent: " + std::to_string(cr) + ", Not Found";
-            break;
+// Both entry points validate and append on the device (hgx_insert.hip), then mirror the
+// per-creator state and the Hashgraph counters (UndeterminedEvents, PendingLoadedEvents).
+static int32_t finish_insert(hgx_ctx* c, const hgx::InsertOut& out, int64_t* n_inserted, hgx_error* err) {
+    for (int cl = 0; cl < c->C; cl++) {
+        const int32_t nl = out.last_gid[cl] >= 0 ? out.last_index[cl] - out.chain_base[cl] + 1 : 0;
+        const int32_t d = nl - c->chain_len[cl];
+        if (d) {
+            c->g_events[cl / c->n] += d;
+            c->gs[cl / c->n].undetermined += d;
         }
-        if (sp != c->last_gid[cr]) {   // CheckSelfParent (hashgraph.go:404-420)
+        c->chain_len[cl] = nl;
+    }
+    c->last_gid = out.last_gid;
+    c->last_index = out.last_index;
+    c->chain_base = out.chain_base;
+    for (int g = 0; g < c->G; g++) {
+        const int64_t l = (int64_t)out.graph_loaded[g];
+        c->gs[g].pending_loaded += l - c->g_loaded[g];
+        c->g_loaded[g] = l;
+    }
+    c->E = c->eng.E;
+    if (out.accepted > 0) {
+        c->mirror_ok = c->chains_ok = false;
+        c->rounds_cached = c->recv_cached = false;
+    }
+    if (n_inserted) *n_inserted = out.accepted;
+    std::string msg;
+    int32_t rc = HGX_OK;
+    switch (out.code) {
+        case hgx::INS_OK: return ok(err);
+        case hgx::INS_KEY_NOT_FOUND:   // Store.LastFrom of an unknown creator (inmem_store.go:85-90)
+            rc = HGX_ERR_KEY_NOT_FOUND;
+            msg = "CheckSelfParent: " + std::to_string(out.fail_creator) + ", Not Found";
+            break;
+        case hgx::INS_SELF_PARENT:
             rc = HGX_ERR_SELF_PARENT;
             msg = "CheckSelfParent: Self-parent not last known event by creator";
             break;
-        }
-        if (op != -1) {                // CheckOtherParent (hashgraph.go:423-445), genesis Root only
-            const bool known = op >= 0 && op < c->E && c->creator[op] / c->n == cr / c->n;
-            if (!known) {
-                rc = HGX_ERR_OTHER_PARENT;
-                msg = "CheckOtherParent: Other-parent not known";
-                break;
-            }
-        }
-        if (c->E >= c->cap) {
+        case hgx::INS_OTHER_PARENT:
+            rc = HGX_ERR_OTHER_PARENT;
+            msg = "CheckOtherParent: Other-parent not known";
+            break;
+        case hgx::INS_CAPACITY:
             rc = HGX_ERR_CAPACITY;
             msg = "hgx_insert_events: context capacity exceeded";
             break;
-        }
-        const int64_t li = c->last_index[cr];   // RollingIndex.Add (common/rolling_index.go:54-68)
-        if (idx <= li) { rc = HGX_ERR_PASSED_INDEX; msg = "SetEvent: " + go_rune(idx) + ", Passed Index"; break; }
-        if (li >= 0 && idx > li + 1) { rc = HGX_ERR_SKIPPED_INDEX; msg = "SetEvent: " + go_rune(idx) + ", Skipped Index"; break; }
-        if (idx > 2147483646) { rc = HGX_ERR_INVALID; msg = "hgx_insert_events: index out of int32 range"; break; }
-        const int64_t gid = c->E++;
-        c->creator.push_back(cr);
-        c->index32.push_back((int32_t)idx);
-        c->sp.push_back((int32_t)sp);
-        c->op.push_back((int32_t)op);
-        c->ts.push_back(ev->timestamp_ns[k]);
-        c->S.insert(c->S.end(), ev->sig_s + 32 * k, ev->sig_s + 32 * k + 32);
-        c->coin.push_back(ev->hash[32 * k + 16] != 0 ? 1 : 0);   // middleBit (hashgraph.go:1039-1048)
-        const int32_t nt = ev->ntx[k];
-        const int32_t nil = ev->tx_nil[k] ? 1 : 0;
-        c->ntx.push_back(nt);
-        c->txnil.push_back((uint8_t)nil);
-        const bool ld = idx == 0 || (!nil && nt > 0);          // IsLoaded (event.go:119-126)
-        c->loaded.push_back(ld ? 1 : 0);
-        if (c->chain_len[cr] == 0) c->chain_base[cr] = (int32_t)idx;
-        c->chain_len[cr]++;
-        c->chain_gids[cr].push_back((int32_t)gid);
-        c->last_gid[cr] = gid;
-        c->last_index[cr] = idx;
-        GraphState& g = c->gs[cr / c->n];
-        if (ld) { g.pending_loaded++; c->g_loaded[cr / c->n]++; }
-        g.undetermined++;
-        c->g_events[cr / c->n]++;
+        case hgx::INS_PASSED_INDEX:
+            rc = HGX_ERR_PASSED_INDEX;
+            msg = "SetEvent: " + go_rune(out.fail_index) + ", Passed Index";
+            break;
+        case hgx::INS_SKIPPED_INDEX:
+            rc = HGX_ERR_SKIPPED_INDEX;
+            msg = "SetEvent: " + go_rune(out.fail_index) + ", Skipped Index";
+            break;
+        default:
+            rc = HGX_ERR_INVALID;
+            msg = "hgx_insert_events: index out of int32 range";
     }
-    const int64_t added = c->E - first;
-    if (added > 0) {
-        hipError_t e = c->eng.upload_events(first, added, c->creator.data() + first, c->index32.data() + first,
-                                            c->op.data() + first, c->ts.data() + first, c->S.data() + 32 * first,
-                                            c->coin.data() + first, c->ntx.data() + first, c->loaded.data() + first);
+    set_err(err, rc, msg);
+    return rc;
+}
+
+int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !ev || count < 0 ||
+        (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
+                       !ev->hash || !ev->sig_s || !ev->ntx || !ev->tx_nil))) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    hgx::InsertIn in{};
+    if (count > 0) {
+        hipError_t e = c->eng.stage_host(ev->creator, ev->index, ev->self_parent, ev->other_parent, ev->timestamp_ns,
+                                         ev->hash, ev->sig_s, ev->ntx, ev->tx_nil, count, in);
         if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events");
-        c->rounds_cached = c->recv_cached = false;
     }
-    if (n_inserted) *n_inserted = added;
-    if (rc != HGX_OK) { set_err(err, rc, msg); return rc; }
-    if (err) set_err(err, HGX_OK, "");
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert(in, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events");
+    return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_insert_events_device(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted,
+                                 hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !ev || count < 0 ||
+        (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
+                       !ev->hash || !ev->sig_s || !ev->ntx || !ev->tx_nil)) ||
+        ((uintptr_t)ev->sig_s & 15) || ((uintptr_t)ev->hash & 15)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events_device: bad arguments (hash / sig_s must be 16-byte aligned)");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    hgx::InsertIn in{ev->creator, ev->index, ev->self_parent, ev->other_parent, ev->timestamp_ns,
+                     ev->hash, ev->sig_s, ev->ntx, ev->tx_nil};
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert(in, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events_device");
+    return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_clear(hgx_ctx* c) {
+    if (!c) return HGX_ERR_INVALID;
+    DeviceGuard dg(c);
+    if (c->eng.clear() != hipSuccess) return HGX_ERR_DEVICE;
+    std::fill(c->chain_len.begin(), c->chain_len.end(), 0);
+    std::fill(c->chain_base.begin(), c->chain_base.end(), 0);
+    std::fill(c->last_gid.begin(), c->last_gid.end(), -1);
+    std::fill(c->last_index.begin(), c->last_index.end(), -1);
+    for (int g = 0; g < c->G; g++) {
+        c->gs[g].reset();
+        c->order[g] = GraphOrder();
+    }
+    std::fill(c->g_events.begin(), c->g_events.end(), 0);
+    std::fill(c->g_loaded.begin(), c->g_loaded.end(), 0);
+    c->arena.used = 0;
+    c->E = c->E_div = 0;
+    c->divided = false;
+    c->mirror_ok = c->chains_ok = false;
+    c->rounds_cached = c->recv_cached = false;
     return HGX_OK;
 }
 
 // ---- DivideRounds (hashgraph.go:616-646) -----------------------------------------
 int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
-    if (c->divided && c->E_div == c->E) return HGX_OK;   // nothing new: AddEvent is idempotent
+    if (c->divided && c->E_div == c->E) return ok(err);   // nothing new: AddEvent is idempotent
+    DeviceGuard dg(c);
     hipError_t e = c->eng.divide_rounds(c->E, c->chain_len, c->chain_base, c->rh);
     if (e != hipSuccess) return dev_err(err, e, "hgx_divide_rounds");
     c->divided = true;
@@ -283,8 +387,7 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
             s.round_events[r] = (int32_t)cnt;
         }
     }
-    if (err) set_err(err, HGX_OK, "");
-    return HGX_OK;
+    return ok(err);
 }
 
 static bool is_witness(const hgx_ctx* c, int32_t r, int gc) {
@@ -303,6 +406,7 @@ static bool witnesses_decided(const hgx_ctx* c, int g, int32_t r) {
 // ---- DecideFame (hashgraph.go:649-750) -------------------------------------------
 int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    DeviceGuard dg(c);
     std::vector<int8_t> dev;
     if (c->divided) {
         hipError_t e = c->eng.decide_fame(dev);
@@ -314,12 +418,10 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
     for (int g = 0; g < c->G; g++) {
         GraphState& s = c->gs[g];
         std::vector<int32_t> decided;
-        int32_t grc = HGX_OK;
         for (size_t pos = 0; pos < s.undecided.size(); pos++) {
             const int32_t i = s.undecided[pos];
             if (i < 0 || i > s.last_round) {          // Store.GetRound miss -> error
-                grc = HGX_ERR_KEY_NOT_FOUND;
-                if (rc == HGX_OK) { rc = grc; msg = std::to_string(i) + ", Not Found"; }
+                if (rc == HGX_OK) { rc = HGX_ERR_KEY_NOT_FOUND; msg = std::to_string(i) + ", Not Found"; }
                 break;
             }
             for (int cl = 0; cl < n; cl++) {
@@ -347,24 +449,16 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
         s.undecided.swap(keep);
     }
     if (rc != HGX_OK) { set_err(err, rc, msg); return rc; }
-    if (err) set_err(err, HGX_OK, "");
-    return HGX_OK;
+    return ok(err);
 }
 
 // ---- FindOrder (hashgraph.go:801-858) --------------------------------------------
 int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
-    if (!c->divided) { if (err) set_err(err, HGX_OK, ""); return HGX_OK; }
+    if (!c->divided) return ok(err);
+    DeviceGuard dg(c);
     const int n = c->n, C = c->C, G = c->G;
     const int32_t R = c->rh.R;
-    static const bool dbg = getenv("HGX_DEBUG_HOST") != nullptr;
-    auto t0 = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!dbg) return;
-        const auto t1 = std::chrono::steady_clock::now();
-        fprintf(stderr, "[hgx] find_order %s: %.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
-        t0 = t1;
-    };
     std::vector<uint8_t> elig((size_t)G * std::max(R, 1), 0), fw((size_t)std::max(R, 1) * C, 0), ure(G, 0);
     for (int g = 0; g < G; g++) {
         const GraphState& s = c->gs[g];
@@ -385,10 +479,8 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
             elig[(size_t)g * R + i] = (U0 >= 0 && i < U0 && decided) ? 1 : 0;
         }
     }
-    lap("eligibility");
     hgx::OrderHost oh;
     hipError_t e = c->eng.find_order(elig, fw, ure, oh);
-    lap("device");
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     if (oh.panic) {
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
@@ -418,40 +510,36 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
         if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
         c->arena.used = base_off + (size_t)total;
     }
-    lap("order D2H");
     for (int g = 0; g < G; g++) {
         const int64_t mg = seg_len[g];
         if (mg == 0) continue;
         GraphState& s = c->gs[g];
         GraphOrder& o = c->order[g];
         const int64_t base_pos = (int64_t)o.n;
-        const int32_t* order = c->arena.p + base_off + seg_at[g];
         o.segs.push_back({base_off + (size_t)seg_at[g], (size_t)mg});
         o.n += (size_t)mg;
         s.blocks.reserve(s.blocks.size() + (size_t)R);
         int64_t off = 0;
         for (int32_t rr = 0; rr < R; rr++) {    // one Block per rr, ascending (blockOrder)
-            const int32_t cnt = oh.blk_cnt[(size_t)g * R + rr];
+            const size_t bi = (size_t)g * R + rr;
+            const int32_t cnt = oh.blk_cnt[bi];
             if (!cnt) continue;
             Block b;
             b.rr = rr;
             b.first = base_pos + off;
             b.nev = cnt;
-            b.ntx = oh.blk_ntx[(size_t)g * R + rr];
-            const int32_t first_gid = order[off];
+            b.ntx = oh.blk_ntx[bi];
             // NewBlock(rr, first.Transactions()) then append(...): nil iff first nil and nothing appended
-            b.tx_nil = (c->txnil[first_gid] && b.ntx == 0) ? 1 : 0;
+            b.tx_nil = (oh.blk_nil[bi] && b.ntx == 0) ? 1 : 0;
             b.committed = b.ntx > 0 ? 1 : 0;   // commitCh only if len(Transactions) > 0
             s.blocks.push_back(b);
             s.consensus_tx += b.ntx;
-            s.pending_loaded -= oh.blk_loaded[(size_t)g * R + rr];
+            s.pending_loaded -= oh.blk_loaded[bi];
             off += cnt;
         }
         s.undetermined -= mg;
     }
-    lap("blocks");
-    if (err) set_err(err, HGX_OK, "");
-    return HGX_OK;
+    return ok(err);
 }
 
 int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
@@ -464,6 +552,7 @@ int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
 
 int32_t hgx_reset_consensus(hgx_ctx* c) {
     if (!c) return HGX_ERR_INVALID;
+    DeviceGuard dg(c);
     for (int g = 0; g < c->G; g++) {
         GraphState& s = c->gs[g];
         s.reset();
@@ -511,6 +600,8 @@ int32_t hgx_round_event_count(hgx_ctx* c, int32_t g, int32_t r) {
 int32_t hgx_round_witnesses(hgx_ctx* c, int32_t g, int32_t r, int64_t* out, int32_t cap) {
     GraphState* s = graph(c, g);
     if (!s || r < 0 || r > s->last_round) return 0;
+    DeviceGuard dg(c);
+    if (ensure_chains(c)) return 0;
     int32_t m = 0;
     for (int cl = 0; cl < c->n; cl++) {
         const int gc = g * c->n + cl;
@@ -526,17 +617,33 @@ int32_t hgx_known(hgx_ctx* c, int32_t g, int32_t* out) {
     return HGX_OK;
 }
 int64_t hgx_consensus_events_count(hgx_ctx* c, int32_t g) { return graph(c, g) ? (int64_t)c->order[g].size() : 0; }
+
 int32_t hgx_consensus_events(hgx_ctx* c, int32_t g, int64_t first, int64_t count, int64_t* gids) {
     if (!graph(c, g) || first < 0 || count < 0 || first + count > (int64_t)c->order[g].size()) return HGX_ERR_INVALID;
-    int64_t pos = 0, k = 0;   // walk the graph's segments
-    for (const GraphOrder::Seg& sg : c->order[g].segs) {
-        const int64_t a = std::max<int64_t>(first, pos), b = std::min<int64_t>(first + count, pos + (int64_t)sg.len);
-        for (int64_t i = a; i < b; i++) gids[k++] = c->arena.p[sg.off + (size_t)(i - pos)];
-        pos += (int64_t)sg.len;
-        if (pos >= first + count) break;
-    }
+    walk_order(c, g, first, count, [&](int64_t k, int64_t gid) { gids[k] = gid; });
     return HGX_OK;
 }
+
+static int32_t ensure_received(hgx_ctx* c) {
+    if (c->recv_cached) return HGX_OK;
+    if (c->eng.get_received(c->rr_cache, c->cts_cache) != hipSuccess) return HGX_ERR_DEVICE;
+    c->recv_cached = true;
+    return HGX_OK;
+}
+
+int32_t hgx_consensus_received(hgx_ctx* c, int32_t g, int64_t first, int64_t count, int64_t* gids, int32_t* rr,
+                               int64_t* cts) {
+    if (!graph(c, g) || first < 0 || count < 0 || first + count > (int64_t)c->order[g].size()) return HGX_ERR_INVALID;
+    DeviceGuard dg(c);
+    if (ensure_received(c)) return HGX_ERR_DEVICE;
+    walk_order(c, g, first, count, [&](int64_t k, int64_t gid) {
+        if (gids) gids[k] = gid;
+        if (rr) rr[k] = c->rr_cache[(size_t)gid];
+        if (cts) cts[k] = c->cts_cache[(size_t)gid];
+    });
+    return HGX_OK;
+}
+
 int64_t hgx_num_blocks(hgx_ctx* c, int32_t g) { GraphState* s = graph(c, g); return s ? (int64_t)s->blocks.size() : 0; }
 int32_t hgx_block_info(hgx_ctx* c, int32_t g, int64_t b, int32_t* rr, int64_t* first, int32_t* nev, int64_t* ntx,
                        int32_t* tx_nil, int32_t* committed) {
@@ -552,6 +659,150 @@ int32_t hgx_block_info(hgx_ctx* c, int32_t g, int64_t b, int32_t* rr, int64_t* f
     return HGX_OK;
 }
 
+// Store.GetBlock(rr) (inmem_store.go:163-169)
+int32_t hgx_get_block(hgx_ctx* c, int32_t g, int32_t round_received, int64_t* block, hgx_error* err) {
+    GraphState* s = graph(c, g);
+    if (!s) { set_err(err, HGX_ERR_INVALID, "hgx_get_block: bad graph"); return HGX_ERR_INVALID; }
+    for (size_t b = 0; b < s->blocks.size(); b++)
+        if (s->blocks[b].rr == round_received) {
+            if (block) *block = (int64_t)b;
+            return ok(err);
+        }
+    set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(round_received) + ", Not Found");
+    return HGX_ERR_KEY_NOT_FOUND;
+}
+
+// ---- Store: events by participant (inmem_store.go:48-102, caches.go:30-114) -----------
+// No eviction (cacheSize >= events): a participant's RollingIndex holds all its
+// events, oldest cached Index = its first Index.
+static bool valid_participant(const hgx_ctx* c, int32_t p) { return c && p >= 0 && p < c->C; }
+
+int32_t hgx_last_from(hgx_ctx* c, int32_t p, int64_t* gid, int32_t* is_root, hgx_error* err) {
+    if (!valid_participant(c, p)) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(p) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    const bool none = c->last_gid[p] < 0;   // no event: the Root's X (genesis: "")
+    if (gid) *gid = none ? -1 : c->last_gid[p];
+    if (is_root) *is_root = none ? 1 : 0;
+    return ok(err);
+}
+
+int32_t hgx_participant_events(hgx_ctx* c, int32_t p, int64_t skip, int64_t* gids, int64_t cap, int64_t* count,
+                               hgx_error* err) {
+    if (count) *count = 0;
+    if (!valid_participant(c, p)) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(p) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    const int64_t last = c->last_index[p];
+    if (skip > last) return ok(err);   // RollingIndex.Get (common/rolling_index.go:21-38)
+    const int64_t items = c->chain_len[p];
+    const int64_t oldest = last - items + 1;
+    if (skip + 1 < oldest) {
+        set_err(err, HGX_ERR_TOO_LATE, go_rune(4 - 1) + ", Too Late");   // NewStoreErr(TooLate, string(SkippedIndex))
+        return HGX_ERR_TOO_LATE;
+    }
+    DeviceGuard dg(c);
+    if (ensure_chains(c)) return dev_err(err, hipErrorUnknown, "hgx_participant_events");
+    const int64_t start = skip - oldest + 1, m = items - start;
+    if (count) *count = m;
+    for (int64_t k = 0; k < m && k < cap; k++) gids[k] = c->chain_gids[p][(size_t)(start + k)];
+    return ok(err);
+}
+
+int32_t hgx_participant_event(hgx_ctx* c, int32_t p, int64_t index, int64_t* gid, hgx_error* err) {
+    if (!valid_participant(c, p)) {   // participantEvents[participant] is nil: Go panics
+        set_err(err, HGX_ERR_PANIC, "runtime error: invalid memory address or nil pointer dereference");
+        return HGX_ERR_PANIC;
+    }
+    const int64_t last = c->last_index[p], items = c->chain_len[p];
+    const int64_t oldest = last - items + 1;   // RollingIndex.GetItem (common/rolling_index.go:40-50)
+    if (index < oldest) {
+        set_err(err, HGX_ERR_TOO_LATE, go_rune(index) + ", Too Late");
+        return HGX_ERR_TOO_LATE;
+    }
+    if (index - oldest >= items) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, go_rune(index) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    DeviceGuard dg(c);
+    if (ensure_chains(c)) return dev_err(err, hipErrorUnknown, "hgx_participant_event");
+    if (gid) *gid = c->chain_gids[p][(size_t)(index - oldest)];
+    return ok(err);
+}
+
+// Store.GetRoot (inmem_store.go:155-161): the genesis Root (root.go:70-77) of every participant
+int32_t hgx_get_root(hgx_ctx* c, int32_t p, int64_t* x, int64_t* y, int32_t* index, int32_t* round, hgx_error* err) {
+    if (!valid_participant(c, p)) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(p) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    if (x) *x = -1;
+    if (y) *y = -1;
+    if (index) *index = -1;
+    if (round) *round = -1;
+    return ok(err);
+}
+
+// Store.GetEvent (inmem_store.go:48-55): the DAG fields of one event
+int32_t hgx_get_event(hgx_ctx* c, int64_t gid, int32_t* creator, int64_t* index, int64_t* self_parent,
+                      int64_t* other_parent, int64_t* timestamp_ns, int32_t* ntx, int32_t* tx_nil, hgx_error* err) {
+    if (!c || gid < 0 || gid >= c->E) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(gid) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    DeviceGuard dg(c);
+    if (ensure_mirror(c)) return dev_err(err, hipErrorUnknown, "hgx_get_event");
+    int64_t ts = 0;
+    int32_t nt = 0, nil = 0;
+    hipError_t e = c->eng.get_event_fields(gid, &ts, &nt, &nil);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_get_event");
+    const size_t x = (size_t)gid;
+    if (creator) *creator = c->creator[x];
+    if (index) *index = c->index32[x];
+    if (self_parent) *self_parent = c->sp[x];
+    if (other_parent) *other_parent = c->op[x];
+    if (timestamp_ns) *timestamp_ns = ts;
+    if (ntx) *ntx = nt;
+    if (tx_nil) *tx_nil = nil;
+    return ok(err);
+}
+
+// SetWireInfo (hashgraph.go:532-567): self-parent Index (Root.Index = -1 for a first event),
+// other-parent creator id and Index (-1 when ""), per event
+int32_t hgx_wire_info(hgx_ctx* c, int64_t first, int64_t count, int32_t* self_parent_index,
+                      int32_t* other_parent_creator, int32_t* other_parent_index) {
+    if (!c || first < 0 || count < 0 || first + count > c->E) return HGX_ERR_INVALID;
+    DeviceGuard dg(c);
+    if (ensure_mirror(c)) return HGX_ERR_DEVICE;
+    for (int64_t k = 0; k < count; k++) {
+        const size_t x = (size_t)(first + k);
+        const int32_t sp = c->sp[x], op = c->op[x];
+        if (self_parent_index) self_parent_index[k] = sp >= 0 ? c->index32[(size_t)sp] : -1;
+        if (other_parent_creator) other_parent_creator[k] = op >= 0 ? c->creator[(size_t)op] : -1;
+        if (other_parent_index) other_parent_index[k] = op >= 0 ? c->index32[(size_t)op] : -1;
+    }
+    return HGX_OK;
+}
+
+// ReadWireInfo (hashgraph.go:569-614): the parents of a wire event resolved through
+// Store.ParticipantEvent
+int32_t hgx_read_wire_info(hgx_ctx* c, int32_t creator, int64_t self_parent_index, int32_t other_parent_creator,
+                           int64_t other_parent_index, int64_t* self_parent, int64_t* other_parent, hgx_error* err) {
+    if (self_parent) *self_parent = -1;
+    if (other_parent) *other_parent = -1;
+    if (self_parent_index >= 0) {
+        const int32_t rc = hgx_participant_event(c, creator, self_parent_index, self_parent, err);
+        if (rc) return rc;
+    }
+    if (other_parent_index >= 0) {
+        const int32_t rc = hgx_participant_event(c, other_parent_creator, other_parent_index, other_parent, err);
+        if (rc) return rc;
+    }
+    return ok(err);
+}
+
 // ---- per-event results -------------------------------------------------------------
 static int32_t ensure_rounds(hgx_ctx* c) {
     if (c->rounds_cached) return HGX_OK;
@@ -565,13 +816,14 @@ static int32_t round_of(hgx_ctx* c, int64_t x) {
 }
 static int32_t witness_of(hgx_ctx* c, int64_t x) {   // Witness (hashgraph.go:265-282)
     if (x < 0 || x >= (int64_t)c->round_cache.size()) return 0;
-    if (c->sp[x] == -1 && c->op[x] == -1) return 1;
-    return round_of(c, x) > round_of(c, c->sp[x]) ? 1 : 0;
+    if (c->sp[(size_t)x] == -1 && c->op[(size_t)x] == -1) return 1;
+    return round_of(c, x) > round_of(c, c->sp[(size_t)x]) ? 1 : 0;
 }
 
 int32_t hgx_get_rounds(hgx_ctx* c, int64_t first, int64_t count, int32_t* round, int8_t* witness, int8_t* famous) {
     if (!c || first < 0 || count < 0 || first + count > c->E) return HGX_ERR_INVALID;
-    if (ensure_rounds(c)) return HGX_ERR_DEVICE;
+    DeviceGuard dg(c);
+    if (ensure_rounds(c) || ensure_mirror(c)) return HGX_ERR_DEVICE;
     for (int64_t k = 0; k < count; k++) {
         const int64_t x = first + k;
         const int32_t r = round_of(c, x);
@@ -581,7 +833,7 @@ int32_t hgx_get_rounds(hgx_ctx* c, int64_t first, int64_t count, int32_t* round,
         if (famous) {
             int8_t f = 0;
             if (w && r >= 0) {
-                const int gc = c->creator[x];
+                const int gc = c->creator[(size_t)x];
                 const GraphState& s = c->gs[gc / c->n];
                 if (r <= s.last_round) f = s.fame[(size_t)r * c->n + gc % c->n];
             }
@@ -593,10 +845,8 @@ int32_t hgx_get_rounds(hgx_ctx* c, int64_t first, int64_t count, int32_t* round,
 
 int32_t hgx_get_received(hgx_ctx* c, int64_t first, int64_t count, int32_t* rr, int64_t* cts) {
     if (!c || first < 0 || count < 0 || first + count > c->E) return HGX_ERR_INVALID;
-    if (!c->recv_cached) {
-        if (c->eng.get_received(c->rr_cache, c->cts_cache) != hipSuccess) return HGX_ERR_DEVICE;
-        c->recv_cached = true;
-    }
+    DeviceGuard dg(c);
+    if (ensure_received(c)) return HGX_ERR_DEVICE;
     for (int64_t k = 0; k < count; k++) {
         const size_t x = (size_t)(first + k);
         const bool have = x < c->rr_cache.size();
@@ -608,27 +858,36 @@ int32_t hgx_get_received(hgx_ctx* c, int64_t first, int64_t count, int32_t* rr, 
 
 int32_t hgx_get_coords(hgx_ctx* c, int64_t gid, int32_t* la, int32_t* fd) {
     if (!c || gid < 0 || gid >= c->E_div || !c->divided) return HGX_ERR_INVALID;
+    DeviceGuard dg(c);
     return c->eng.get_coords(gid, la, fd) == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
 }
 
 // ---- primitives (hashgraph.go:73-339) ----------------------------------------------
+// Events of different graphs of a batched context never see each other.
 static bool known_div(hgx_ctx* c, int64_t x) { return c && x >= 0 && x < c->E_div && c->divided; }
+static bool same_graph(hgx_ctx* c, int64_t x, int64_t y) { return graph_of(c, x) == graph_of(c, y); }
 
 int32_t hgx_ancestor(hgx_ctx* c, int64_t x, int64_t y) {
     if (x == y) return 1;
     if (!known_div(c, x) || !known_div(c, y)) return 0;
+    DeviceGuard dg(c);
+    if (ensure_mirror(c) || !same_graph(c, x, y)) return 0;
     std::vector<int32_t> la(c->n), fd(c->n);
     if (c->eng.get_coords(x, la.data(), fd.data()) != hipSuccess) return 0;
-    return la[c->creator[y] % c->n] >= c->index32[y] ? 1 : 0;
+    return la[c->creator[(size_t)y] % c->n] >= c->index32[(size_t)y] ? 1 : 0;
 }
 int32_t hgx_self_ancestor(hgx_ctx* c, int64_t x, int64_t y) {
     if (x == y) return 1;
     if (!c || x < 0 || y < 0 || x >= c->E || y >= c->E) return 0;
-    return (c->creator[x] == c->creator[y] && c->index32[x] >= c->index32[y]) ? 1 : 0;
+    DeviceGuard dg(c);
+    if (ensure_mirror(c)) return 0;
+    return (c->creator[(size_t)x] == c->creator[(size_t)y] && c->index32[(size_t)x] >= c->index32[(size_t)y]) ? 1 : 0;
 }
 int32_t hgx_see(hgx_ctx* c, int64_t x, int64_t y) { return hgx_ancestor(c, x, y); }
 int32_t hgx_strongly_see(hgx_ctx* c, int64_t x, int64_t y) {
     if (!known_div(c, x) || !known_div(c, y)) return 0;
+    DeviceGuard dg(c);
+    if (ensure_mirror(c) || !same_graph(c, x, y)) return 0;
     std::vector<int32_t> lx(c->n), fx(c->n), ly(c->n), fy(c->n);
     if (c->eng.get_coords(x, lx.data(), fx.data()) != hipSuccess) return 0;
     if (c->eng.get_coords(y, ly.data(), fy.data()) != hipSuccess) return 0;
@@ -638,23 +897,29 @@ int32_t hgx_strongly_see(hgx_ctx* c, int64_t x, int64_t y) {
 }
 int64_t hgx_oldest_self_ancestor_to_see(hgx_ctx* c, int64_t x, int64_t y) {
     if (!known_div(c, x) || !known_div(c, y)) return -1;
+    DeviceGuard dg(c);
+    if (ensure_chains(c) || !same_graph(c, x, y)) return -1;
     std::vector<int32_t> la(c->n), fd(c->n);
     if (c->eng.get_coords(y, la.data(), fd.data()) != hipSuccess) return -1;
-    const int cx = c->creator[x];
+    const int cx = c->creator[(size_t)x];
     const int32_t a = fd[cx % c->n];
-    if (a <= c->index32[x]) return c->chain_gids[cx][(size_t)(a - c->chain_base[cx])];
+    if (a <= c->index32[(size_t)x]) return c->chain_gids[cx][(size_t)(a - c->chain_base[cx])];
     return -1;
 }
 int32_t hgx_round(hgx_ctx* c, int64_t x) {
-    if (!c || ensure_rounds(c)) return -1;
+    if (!c) return -1;
+    DeviceGuard dg(c);
+    if (ensure_rounds(c)) return -1;
     return round_of(c, x);
 }
 int32_t hgx_witness(hgx_ctx* c, int64_t x) {
-    if (!c || ensure_rounds(c)) return 0;
+    if (!c) return 0;
+    DeviceGuard dg(c);
+    if (ensure_rounds(c) || ensure_mirror(c)) return 0;
     return witness_of(c, x);
 }
 
-// ---- instrumentation ----------------------------------------------------------------
+// ---- instrumentation / knobs ----------------------------------------------------------
 int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
     if (!c || !out) return 0;
     const int32_t m = std::min<int32_t>(cap, 7);
@@ -692,6 +957,20 @@ int32_t hgx_set_coord_storage(hgx_ctx* c, int32_t mode) {
 int32_t hgx_set_kernel_timing(hgx_ctx* c, int32_t on) {
     if (!c) return HGX_ERR_INVALID;
     c->eng.time_mask = (uint32_t)on;
+    return HGX_OK;
+}
+
+int32_t hgx_set_fame_tally(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
+    c->eng.fame_tally = mode;
+    return HGX_OK;
+}
+
+int32_t hgx_reserve_rounds(hgx_ctx* c, int32_t rounds) {
+    if (!c || rounds < 1 || c->divided) return HGX_ERR_INVALID;   // before the first DivideRounds only
+    DeviceGuard dg(c);
+    if (c->eng.reserve_rounds(rounds) != hipSuccess) return HGX_ERR_DEVICE;
+    c->rounds_cached = c->recv_cached = false;
     return HGX_OK;
 }
 

@@ -52,6 +52,7 @@ template struct DBuf<uint8_t>;
 template struct DBuf<int8_t>;
 template struct DBuf<uint32_t>;
 template struct DBuf<uint64_t>;
+template struct DBuf<unsigned long long>;
 
 static int bitlen(uint64_t v) {
     int b = 0;
@@ -100,9 +101,20 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     nw = (n + 63) / 64;
     cap = std::max<int64_t>(cap_events, 1);
     const size_t P = (size_t)cap;
-    HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_op.alloc(P)); HGX_TRY(g_ntx.alloc(P));
-    HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P)); HGX_TRY(g_cts.alloc(P));
-    HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
+    HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_sp.alloc(P)); HGX_TRY(g_op.alloc(P));
+    HGX_TRY(g_ntx.alloc(P)); HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P));
+    HGX_TRY(g_cts.alloc(P)); HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
+    HGX_TRY(g_txnil.alloc(P));
+    // insert state: no claims, no events per creator
+    HGX_TRY(succ.alloc(P)); HGX_TRY(first_none.alloc(C));
+    HGX_TRY(last_gid_d.alloc(C)); HGX_TRY(last_index_d.alloc(C)); HGX_TRY(chain_base_d.alloc(C));
+    HGX_TRY(ins_fail.alloc(1)); HGX_TRY(graph_loaded_d.alloc(G));
+    HGX_TRY(hipMemsetAsync(succ.p, 0xFF, P * 4, stream));
+    HGX_TRY(hipMemsetAsync(first_none.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(last_index_d.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
     HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
     HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_opu.alloc(P)); HGX_TRY(p_round.alloc(P));
     HGX_TRY(p_rr.alloc(P)); HGX_TRY(p_ts.alloc(P)); HGX_TRY(p_cts.alloc(P));
@@ -125,7 +137,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     const int64_t per_graph = (cap + G - 1) / G;
     int32_t guess = (int32_t)std::min<int64_t>(1 << 20, std::max<int64_t>(64, 2 * per_graph / std::max(1, n * lg) + 16));
     HGX_TRY(ensure_round_cap(guess));
-    return hipSuccess;
+    return hipStreamSynchronize(stream);
 }
 
 hipError_t Engine::ensure_round_cap(int32_t need) {
@@ -145,12 +157,15 @@ hipError_t Engine::ensure_round_cap(int32_t need) {
     HGX_TRY(fw.grow_copy((size_t)nc * Cz, 0, stream));
     HGX_TRY(elig.grow_copy((size_t)nc * G, 0, stream));
     HGX_TRY(ur_empty.grow_copy((size_t)G, 0, stream));
-    HGX_TRY(Smat.grow_copy((size_t)nc * Cz * nw, 0, stream));
+    // S rows of earlier rounds were written by the round steps of this DivideRounds (the
+    // growth happens between step batches) and are read by DecideFame: keep them
+    HGX_TRY(Smat.grow_copy((size_t)nc * Cz * nw, (size_t)old * Cz * nw, stream));
     HGX_TRY(Vbuf.grow_copy((size_t)nc * 2 * Cz * nw, 0, stream));
     HGX_TRY(fame.grow_copy((size_t)nc * Cz, 0, stream));
     HGX_TRY(blk_cnt.grow_copy((size_t)nc * G, 0, stream));
     HGX_TRY(blk_loaded.grow_copy((size_t)nc * G, 0, stream));
     HGX_TRY(blk_ntx.grow_copy((size_t)nc * G, 0, stream));
+    HGX_TRY(blk_nil.grow_copy((size_t)nc * G, 0, stream));
     if (old < nc) HGX_TRY(hipMemsetAsync(active.p + old + 1, 0, (size_t)(nc - old) * sizeof(int32_t), stream));
     r_cap = nc;
     return hipSuccess;
@@ -159,7 +174,7 @@ hipError_t Engine::ensure_round_cap(int32_t need) {
 DevArrays Engine::arrays() {
     DevArrays a;
     a.g_creator = g_creator.p; a.g_index = g_index.p; a.g_op = g_op.p; a.g_ntx = g_ntx.p;
-    a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p;
+    a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p; a.g_txnil = g_txnil.p;
     a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p;
     a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
     a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
@@ -172,7 +187,7 @@ DevArrays Engine::arrays() {
     a.recv_list = recv_list.p; a.counters = counters.p; a.p_new = p_new.p; a.scan_part = scan_part.p;
     a.key_a = key_a.p; a.key_b = key_b.p; a.val_a = val_a.p; a.val_b = val_b.p; a.hist = hist.p;
     a.minmax = minmax.p; a.order_gid = order_gid.p;
-    a.blk_cnt = blk_cnt.p; a.blk_loaded = blk_loaded.p; a.blk_ntx = blk_ntx.p;
+    a.blk_cnt = blk_cnt.p; a.blk_loaded = blk_loaded.p; a.blk_ntx = blk_ntx.p; a.blk_nil = blk_nil.p;
     return a;
 }
 
@@ -217,25 +232,125 @@ hipError_t Engine::collect_kernel_times() {
     return hipSuccess;
 }
 
-// ---- inputs ---------------------------------------------------------------------
-hipError_t Engine::upload_events(int64_t first, int64_t count, const int32_t* creator, const int32_t* index,
-                                 const int32_t* op, const int64_t* ts, const uint8_t* S, const uint8_t* coin,
-                                 const int32_t* ntx, const uint8_t* loaded) {
-    if (count <= 0) return hipSuccess;
-    const size_t f = (size_t)first, c = (size_t)count;
-    HGX_TRY(hipMemcpyAsync(g_creator.p + f, creator, c * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_index.p + f, index, c * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_op.p + f, op, c * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_ts.p + f, ts, c * 8, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_S.p + 32 * f, S, c * 32, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_coin.p + f, coin, c, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_ntx.p + f, ntx, c * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(g_loaded.p + f, loaded, c, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemsetAsync(g_rr.p + f, 0xFF, c * 4, stream));   // roundReceived = nil
-    HGX_TRY(hipMemsetAsync(g_cts.p + f, 0, c * 8, stream));
-    HGX_TRY(hipStreamSynchronize(stream));
-    E = std::max<int64_t>(E, first + count);
+// ---- inputs: InsertEvent batches (hgx_insert.hip) ----------------------------------
+InsertState Engine::insert_state() {
+    InsertState st;
+    st.g_creator = g_creator.p; st.g_index = g_index.p; st.g_sp = g_sp.p; st.g_op = g_op.p; st.g_ntx = g_ntx.p;
+    st.g_rr = g_rr.p; st.g_ts = g_ts.p; st.g_cts = g_cts.p; st.g_S = g_S.p; st.g_coin = g_coin.p;
+    st.g_loaded = g_loaded.p; st.g_txnil = g_txnil.p;
+    st.succ = succ.p; st.first_none = first_none.p;
+    st.last_gid = last_gid_d.p; st.last_index = last_index_d.p; st.chain_base = chain_base_d.p;
+    st.fail = ins_fail.p; st.graph_loaded = graph_loaded_d.p;
+    return st;
+}
+
+template <typename T>
+static hipError_t stage_col(DBuf<T>& b, const T* src, size_t count, size_t per, hipStream_t s) {
+    if (b.n < count * per) HGX_TRY(b.alloc(count * per));
+    return hipMemcpyAsync(b.p, src, count * per * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+hipError_t Engine::stage_host(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
+                              const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
+                              const int32_t* nil, int64_t count, InsertIn& in) {
+    const size_t c = (size_t)count;
+    HGX_TRY(stage_col(st_creator, creator, c, 1, stream));
+    HGX_TRY(stage_col(st_index, index, c, 1, stream));
+    HGX_TRY(stage_col(st_sp, sp, c, 1, stream));
+    HGX_TRY(stage_col(st_op, op, c, 1, stream));
+    HGX_TRY(stage_col(st_ts, ts, c, 1, stream));
+    HGX_TRY(stage_col(st_hash, hash, c, 32, stream));
+    HGX_TRY(stage_col(st_S, S, c, 32, stream));
+    HGX_TRY(stage_col(st_ntx, ntx, c, 1, stream));
+    HGX_TRY(stage_col(st_nil, nil, c, 1, stream));
+    in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p; in.ts = st_ts.p;
+    in.hash = st_hash.p; in.S = st_S.p; in.ntx = st_ntx.p; in.nil = st_nil.p;
     return hipSuccess;
+}
+
+hipError_t Engine::insert(const InsertIn& in, int64_t count, InsertOut& out) {
+    out = InsertOut();
+    const int64_t E0 = E;
+    InsertState st = insert_state();
+    if (count > 0) {
+        HGX_TRY(hipMemsetAsync(ins_fail.p, 0xFF, 8, stream));
+        launch_insert_claim(stream, count, E0, cap, C, in, st);
+        launch_insert_check(stream, count, E0, cap, C, n, in, st);
+        unsigned long long fail = 0;
+        HGX_TRY(hipMemcpyAsync(h_small, ins_fail.p, 8, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipStreamSynchronize(stream));
+        std::memcpy(&fail, h_small, 8);
+        const int64_t m_ok = (fail == ~0ull) ? count : (int64_t)(fail >> 8);
+        out.accepted = m_ok;
+        out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
+        launch_insert_commit(stream, m_ok, E0, n, in, st);
+        launch_insert_unclaim(stream, count, m_ok, E0, cap, C, in, st);
+        if (out.code) {
+            HGX_TRY(hipMemcpyAsync(&out.fail_creator, in.creator + m_ok, 4, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipMemcpyAsync(&out.fail_index, in.index + m_ok, 8, hipMemcpyDeviceToHost, stream));
+        }
+        E = E0 + m_ok;
+    }
+    out.last_gid.resize(C);
+    out.last_index.resize(C);
+    out.chain_base.resize(C);
+    out.graph_loaded.resize(G);
+    HGX_TRY(hipMemcpyAsync(out.last_gid.data(), last_gid_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.last_index.data(), last_index_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.chain_base.data(), chain_base_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.graph_loaded.data(), graph_loaded_d.p, (size_t)G * 8, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::clear() {
+    if (E > 0) HGX_TRY(hipMemsetAsync(succ.p, 0xFF, (size_t)E * 4, stream));
+    HGX_TRY(hipMemsetAsync(first_none.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(last_index_d.p, 0xFF, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
+    E = 0;
+    E_div = 0;
+    R = 0;
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_events(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
+                              std::vector<int32_t>& op) {
+    creator.resize((size_t)E);
+    index.resize((size_t)E);
+    sp.resize((size_t)E);
+    op.resize((size_t)E);
+    if (E == 0) return hipSuccess;
+    HGX_TRY(hipMemcpyAsync(creator.data(), g_creator.p, (size_t)E * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(index.data(), g_index.p, (size_t)E * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(sp.data(), g_sp.p, (size_t)E * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(op.data(), g_op.p, (size_t)E * 4, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil) {
+    uint8_t nil = 0;
+    HGX_TRY(hipMemcpyAsync(ts, g_ts.p + gid, 8, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(ntx, g_ntx.p + gid, 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(&nil, g_txnil.p + gid, 1, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    *tx_nil = nil;
+    return hipSuccess;
+}
+
+hipError_t Engine::reserve_rounds(int32_t rounds) {
+    rounds = std::max<int32_t>(rounds, 1);
+    drop_step_graph();
+    Bm.release(); WLA.release(); WFD.release(); wflag.release(); wstat.release(); wcoin.release();
+    active.release(); Tthr.release(); fw.release(); elig.release(); ur_empty.release(); Smat.release();
+    Vbuf.release(); fame.release(); blk_cnt.release(); blk_loaded.release(); blk_ntx.release(); blk_nil.release();
+    WLAT.release();
+    r_cap = 0;
+    R = 0;
+    E_div = 0;
+    HGX_TRY(ensure_round_cap(rounds));
+    return hipStreamSynchronize(stream);
 }
 
 // ---- DivideRounds ---------------------------------------------------------------
@@ -257,8 +372,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     int32_t max_index = -1;
     for (int c = 0; c < C; c++)
         if (chain_len[c] > 0) max_index = std::max(max_index, chain_base[c] + chain_len[c] - 1);
-    static const bool force32 = getenv("HGX_COORD32") != nullptr;
-    compact = (!force32 && !force_coord32 && (n % 2) == 0 && max_index <= 65533) ? 1 : 0;
+    compact = (!force_coord32 && (n % 2) == 0 && max_index <= 65533) ? 1 : 0;
     const size_t csz = compact ? 2 : 4;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
@@ -271,7 +385,6 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
     if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.alloc(2 * nunits));
     if (la_usum.n < nunits) HGX_TRY(la_usum.alloc(nunits));
-    static const bool la_debug = getenv("HGX_DEBUG_LA") != nullptr;
     la_sweeps = 0;
     la_rows = 0;
     for (;;) {
@@ -291,7 +404,6 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         la_rows += h_small[0];
         kadd_bytes(K_LA_SWEEP, (double)h_small[0] * (3.0 * csz * n + 16));
         la_sweeps++;
-        if (la_debug) fprintf(stderr, "[hgx] la sweep %d: rows recomputed %d, units written %d, rows written %d\n", la_sweeps, h_small[0], h_small[1], h_small[2]);
         if (h_small[1] == 0) break;
         if (la_sweeps > 100000) return hipErrorUnknown;
     }
@@ -407,7 +519,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipEventSynchronize(ph1));
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[1] = ms;
-    if (la_debug) step_prof_dump();
+    step_prof_dump();   // -DHGX_STEP_PROF builds only
     return collect_kernel_times();
 }
 
@@ -418,7 +530,7 @@ hipError_t Engine::decide_fame(std::vector<int8_t>& fame_out) {
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
     kbeg(K_FAME);
-    launch_fame(stream, a, R, C, n, nw, sm, G);
+    launch_fame(stream, a, R, C, n, nw, sm, G, fame_tally);
     kend(K_FAME, 0);
     HGX_TRY(hipMemcpyAsync(fame_out.data(), fame.p, fame_out.size(), hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipEventRecord(ph1, stream));
@@ -436,6 +548,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
     out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
     out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_nil.assign((size_t)G * std::max(R, 1), 0);
     if (R == 0 || E_div == 0) return hipSuccess;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
@@ -484,10 +597,12 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemsetAsync(blk_cnt.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
+    HGX_TRY(hipMemsetAsync(blk_nil.p, 0, (size_t)G * R, stream));
     launch_finish_order(stream, a, m, vals, R, n);
     HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(out.blk_nil.data(), blk_nil.p, (size_t)G * R, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     float ms = 0;

@@ -50,7 +50,19 @@ struct OrderHost {
     std::vector<int32_t> blk_cnt;     // [G x R]
     std::vector<int64_t> blk_ntx;     // [G x R]
     std::vector<int32_t> blk_loaded;  // [G x R]
+    std::vector<uint8_t> blk_nil;     // [G x R] the block's first event has nil Transactions
     bool panic = false;
+};
+
+// Outcome of one insert batch (Engine::insert)
+struct InsertOut {
+    int64_t accepted = 0;          // events appended (the prefix before the first failure)
+    int code = 0;                  // InsertCode of the first failing event (0: none)
+    int32_t fail_creator = 0;      // its creator and Index (error messages)
+    int64_t fail_index = 0;
+    // per-creator state after the batch ([C]) and loaded events per graph ([G], cumulative)
+    std::vector<int32_t> last_gid, last_index, chain_base;
+    std::vector<unsigned long long> graph_loaded;
 };
 
 class Engine {
@@ -58,9 +70,18 @@ class Engine {
     ~Engine();
     hipError_t init(int device, int n_graphs, int n_part, int64_t cap_events, std::string& why);
 
-    hipError_t upload_events(int64_t first, int64_t count, const int32_t* creator, const int32_t* index,
-                             const int32_t* op, const int64_t* ts, const uint8_t* S, const uint8_t* coin,
-                             const int32_t* ntx, const uint8_t* loaded);
+    // InsertEvent for `count` events whose columns are device pointers (hgx_insert_events_device)
+    // or host pointers staged to HBM first (hgx_insert_events); validation and append on the GPU.
+    hipError_t insert(const InsertIn& in, int64_t count, InsertOut& out);
+    hipError_t stage_host(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
+                          const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
+                          const int32_t* nil, int64_t count, InsertIn& in);
+    // forget every event (a fresh NewHashgraph); allocations are kept
+    hipError_t clear();
+    // per-event columns (gid order) for the host-side getters
+    hipError_t get_events(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
+                          std::vector<int32_t>& op);
+    hipError_t get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil);
     hipError_t divide_rounds(int64_t E, const std::vector<int32_t>& chain_len,
                              const std::vector<int32_t>& chain_base, RoundsHost& out);
     hipError_t decide_fame(std::vector<int8_t>& fame_out);
@@ -71,6 +92,8 @@ class Engine {
     hipError_t sync() { return hipStreamSynchronize(stream); }
 
     hipError_t reset_received();
+    // per-round tables reserved for `rounds` rounds (testing: a small value forces the growth path)
+    hipError_t reserve_rounds(int32_t rounds);
     hipError_t get_rounds(std::vector<int32_t>& round_by_gid);
     hipError_t get_received(std::vector<int32_t>& rr, std::vector<int64_t>& cts);
     hipError_t get_coords(int64_t gid, int32_t* la, int32_t* fd);
@@ -87,22 +110,32 @@ class Engine {
     double phase_ms[4] = {0, 0, 0, 0};   // coordinates, rounds, fame, order (last calls)
     KernelStat kstat[K_NUM];
     uint32_t time_mask = 0;   // kernels (bit = KernelId) timed with HIP events
+    int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
+    int dev = 0;
 
    private:
     hipError_t ensure_round_cap(int32_t need);
+    InsertState insert_state();
     void kbeg(int k);
     void kend(int k, double bytes);
     void kadd_bytes(int k, double bytes);
     hipError_t collect_kernel_times();
     DevArrays arrays();
 
-    int dev = 0;
     int max_len = 0;
     std::vector<int32_t> h_off;
     // gid order
-    DBuf<int32_t> g_creator, g_index, g_op, g_ntx, g_rr, g_pos;
+    DBuf<int32_t> g_creator, g_index, g_sp, g_op, g_ntx, g_rr, g_pos;
     DBuf<int64_t> g_ts, g_cts;
-    DBuf<uint8_t> g_S, g_coin, g_loaded;
+    DBuf<uint8_t> g_S, g_coin, g_loaded, g_txnil;
+    // insert state (hgx_insert.hip)
+    DBuf<uint32_t> succ, first_none;
+    DBuf<int32_t> last_gid_d, last_index_d, chain_base_d;
+    DBuf<unsigned long long> ins_fail, graph_loaded_d;
+    // host-batch staging (hgx_insert_events)
+    DBuf<int32_t> st_creator, st_ntx, st_nil;
+    DBuf<int64_t> st_index, st_sp, st_op, st_ts;
+    DBuf<uint8_t> st_hash, st_S;
     // chains
     DBuf<int32_t> c_off, c_len, c_base;
     // positions
@@ -129,7 +162,7 @@ class Engine {
     DBuf<int8_t> fame;
     // order
     DBuf<int32_t> recv_list, counters, order_gid, blk_cnt, blk_loaded;
-    DBuf<uint8_t> p_new;
+    DBuf<uint8_t> p_new, blk_nil;
     DBuf<uint32_t> scan_part;
     DBuf<uint64_t> key_a, key_b;
     DBuf<uint32_t> val_a, val_b, hist;

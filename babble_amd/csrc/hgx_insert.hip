@@ -1,0 +1,174 @@
+// InsertEvent (hashgraph/hashgraph.go:356-401) for a whole batch, on the device.
+//
+// The reference inserts one event at a time: CheckSelfParent (:404-420; the self-parent
+// must be Store.LastFrom(creator), inmem_store.go:85-102), CheckOtherParent (:423-445;
+// the other-parent must be known), then Store.SetEvent -> RollingIndex.Add
+// (common/rolling_index.go:54-68; PassedIndex / SkippedIndex), and it stops at the first
+// event that fails (Core.Sync, node/core.go:199-211). A batch of m events is checked here
+// in parallel with the first-failure rule made data-parallel:
+//
+//   Event k's checks are evaluated as if every earlier event of the batch was accepted.
+//   For k below the first true failure k* that assumption holds, so the first k whose
+//   check fails is exactly k*; events >= k* are discarded.
+//
+// "As if accepted" makes the self-parent rule local: the events of creator c accepted
+// before k form a chain linked by self-parents, so k's self-parent sp is the last of
+// them iff sp is an event of c earlier than k that no earlier event names as its
+// self-parent. Claims record, per event, the smallest gid naming it as self-parent
+// (succ) and per creator the smallest gid with self-parent "" (first_none); event k
+// passes iff its own claim is the smallest. Claims of discarded events are withdrawn.
+// The index rule then compares Index with the self-parent's Index (its creator's last).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hgx_device.h"
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(256) k_insert_claim(int64_t m, int64_t E0, int64_t cap, int C, InsertIn in,
+                                                      InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const int64_t gid = E0 + k;
+    const int cr = in.creator[k];
+    const int64_t sp = in.sp[k];
+    if (sp == -1) {
+        if (cr >= 0 && cr < C) atomicMin(&st.first_none[cr], (uint32_t)gid);
+    } else if (sp >= 0 && sp < gid && sp < cap) {
+        atomicMin(&st.succ[sp], (uint32_t)gid);
+    }
+}
+
+__device__ __forceinline__ int creator_of(int64_t x, int64_t E0, const InsertIn& in, const InsertState& st) {
+    return x < E0 ? st.g_creator[x] : in.creator[x - E0];
+}
+
+__device__ __forceinline__ int64_t index_of(int64_t x, int64_t E0, const InsertIn& in, const InsertState& st) {
+    return x < E0 ? (int64_t)st.g_index[x] : in.index[x - E0];
+}
+
+// Checks in the reference's order: creator known (LastFrom -> KeyNotFound), self-parent,
+// other-parent (genesis Root only: "" or a known event of the same graph), capacity,
+// then the RollingIndex rules of SetEvent.
+__global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int64_t cap, int C, int n, InsertIn in,
+                                                      InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const int64_t gid = E0 + k;
+    const int cr = in.creator[k];
+    const int64_t sp = in.sp[k], op = in.op[k], idx = in.index[k];
+    int code = INS_OK;
+    if (cr < 0 || cr >= C) {
+        code = INS_KEY_NOT_FOUND;
+    } else if (sp == -1) {
+        if (!(st.last_gid[cr] == -1 && st.first_none[cr] == (uint32_t)gid)) code = INS_SELF_PARENT;
+    } else {
+        const bool ok = sp >= 0 && sp < gid && sp < cap && creator_of(sp, E0, in, st) == cr &&
+                        st.succ[sp] == (uint32_t)gid && (sp >= E0 || sp == (int64_t)st.last_gid[cr]);
+        if (!ok) code = INS_SELF_PARENT;
+    }
+    if (code == INS_OK && op != -1) {
+        bool ok = op >= 0 && op < gid && op < cap;
+        if (ok) {
+            const int oc = creator_of(op, E0, in, st);
+            ok = oc >= 0 && oc < C && oc / n == cr / n;
+        }
+        if (!ok) code = INS_OTHER_PARENT;
+    }
+    if (code == INS_OK && gid >= cap) code = INS_CAPACITY;
+    if (code == INS_OK) {
+        const int64_t li = sp < 0 ? -1 : index_of(sp, E0, in, st);
+        if (idx <= li) code = INS_PASSED_INDEX;
+        else if (li >= 0 && idx > li + 1) code = INS_SKIPPED_INDEX;
+        else if (idx > 2147483646) code = INS_INDEX_RANGE;
+    }
+    if (code != INS_OK) atomicMin(st.fail, ((unsigned long long)k << 8) | (unsigned long long)code);
+}
+
+// Append the accepted events [0, m_ok) to the context's arrays (gid order) and move the
+// per-creator state (last event, last Index, first Index) forward.
+__global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0, int n, InsertIn in, InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool ld = false;
+    int g = -1;
+    if (k < m_ok) {
+        const int64_t gid = E0 + k;
+        const int cr = in.creator[k];
+        const int64_t idx = in.index[k], sp = in.sp[k];
+        const int nt = in.ntx[k];
+        const int nil = in.nil[k] ? 1 : 0;
+        st.g_creator[gid] = cr;
+        st.g_index[gid] = (int32_t)idx;
+        st.g_sp[gid] = (int32_t)sp;
+        st.g_op[gid] = (int32_t)in.op[k];
+        st.g_ts[gid] = in.ts[k];
+        const uint4* s4 = (const uint4*)(in.S + 32 * k);
+        uint4* d4 = (uint4*)(st.g_S + 32 * gid);
+        d4[0] = s4[0];
+        d4[1] = s4[1];
+        st.g_coin[gid] = in.hash[32 * k + 16] != 0 ? 1 : 0;   // middleBit (hashgraph.go:1039-1048)
+        st.g_ntx[gid] = nt;
+        st.g_txnil[gid] = (uint8_t)nil;
+        ld = idx == 0 || (!nil && nt > 0);   // IsLoaded (event.go:119-126)
+        st.g_loaded[gid] = ld ? 1 : 0;
+        st.g_rr[gid] = -1;                   // roundReceived = nil
+        st.g_cts[gid] = 0;
+        if (sp == -1) st.chain_base[cr] = (int32_t)idx;
+        if (st.succ[gid] >= (uint32_t)(E0 + m_ok)) {   // no accepted event follows it on its chain
+            st.last_gid[cr] = (int32_t)gid;
+            st.last_index[cr] = (int32_t)idx;
+        }
+        g = cr / n;
+    }
+    // loaded events per graph: one atomic per wave when the wave's events share a graph
+    const int g0 = __shfl(g, 0);
+    const uint64_t lm = __ballot(ld);
+    if (__all(g == g0 || g < 0)) {
+        if (lane_id() == 0 && lm && g0 >= 0) atomicAdd(&st.graph_loaded[g0], (unsigned long long)__popcll(lm));
+    } else if (ld) {
+        atomicAdd(&st.graph_loaded[g], 1ull);
+    }
+}
+
+// withdraw the claims of the discarded events [m_ok, m)
+__global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C,
+                                                        InsertIn in, InsertState st) {
+    const int64_t k = m_ok + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const int64_t gid = E0 + k;
+    const int cr = in.creator[k];
+    const int64_t sp = in.sp[k];
+    if (sp == -1) {
+        if (cr >= 0 && cr < C && st.first_none[cr] == (uint32_t)gid) st.first_none[cr] = kNone32;
+    } else if (sp >= 0 && sp < gid && sp < cap) {
+        if (st.succ[sp] == (uint32_t)gid) st.succ[sp] = kNone32;
+    }
+}
+
+static inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
+
+void launch_insert_claim(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                         const InsertState& st) {
+    if (m > 0) hipLaunchKernelGGL(k_insert_claim, dim3(nblocks(m)), dim3(256), 0, s, m, E0, cap, C, in, st);
+}
+
+void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, int n, const InsertIn& in,
+                         const InsertState& st) {
+    if (m > 0) hipLaunchKernelGGL(k_insert_check, dim3(nblocks(m)), dim3(256), 0, s, m, E0, cap, C, n, in, st);
+}
+
+void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st) {
+    if (m_ok > 0) hipLaunchKernelGGL(k_insert_commit, dim3(nblocks(m_ok)), dim3(256), 0, s, m_ok, E0, n, in, st);
+}
+
+void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                           const InsertState& st) {
+    if (m > m_ok)
+        hipLaunchKernelGGL(k_insert_unclaim, dim3(nblocks(m - m_ok)), dim3(256), 0, s, m, m_ok, E0, cap, C, in, st);
+}
+
+}  // namespace hgx

@@ -14,7 +14,7 @@ struct DevArrays {
     // gid order
     const int32_t *g_creator, *g_index, *g_op, *g_ntx;
     const int64_t* g_ts;
-    const uint8_t *g_S, *g_coin, *g_loaded;
+    const uint8_t *g_S, *g_coin, *g_loaded, *g_txnil;
     int32_t *g_rr, *g_pos;
     int64_t* g_cts;
     // chains
@@ -48,6 +48,33 @@ struct DevArrays {
     int32_t* order_gid;
     int32_t *blk_cnt, *blk_loaded;
     int64_t* blk_ntx;
+    uint8_t* blk_nil;   // [G x R] Transactions of the block's first event are nil
+};
+
+// One batch of events to insert, device pointers (the hgx_events columns, include/hgx.h)
+struct InsertIn {
+    const int32_t* creator;
+    const int64_t *index, *sp, *op, *ts;
+    const uint8_t *hash, *S;
+    const int32_t *ntx, *nil;
+};
+
+// Device state the insert path reads and writes (hgx_engine.h owns the buffers)
+struct InsertState {
+    int32_t *g_creator, *g_index, *g_sp, *g_op, *g_ntx, *g_rr;
+    int64_t *g_ts, *g_cts;
+    uint8_t *g_S, *g_coin, *g_loaded, *g_txnil;
+    uint32_t* succ;         // [cap] smallest gid whose self-parent is this event (UINT32_MAX none)
+    uint32_t* first_none;   // [C] smallest gid of the chain with self-parent "" (UINT32_MAX none)
+    int32_t *last_gid, *last_index, *chain_base;   // [C] per-chain state before / after the batch
+    unsigned long long* fail;           // min over failing events of (k << 8 | code)
+    unsigned long long* graph_loaded;   // [G] loaded events inserted (IsLoaded, event.go:119-126)
+};
+
+// first-failure codes of the insert check (hgx_insert_events, hashgraph.go:356-401)
+enum InsertCode {
+    INS_OK = 0, INS_KEY_NOT_FOUND = 1, INS_SELF_PARENT = 2, INS_OTHER_PARENT = 3, INS_CAPACITY = 4,
+    INS_PASSED_INDEX = 5, INS_SKIPPED_INDEX = 6, INS_INDEX_RANGE = 7
 };
 
 // arguments of the round step (hgx_rounds.hip)
@@ -78,7 +105,8 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only
-void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G);
+// tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
+void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G, int tally);
 void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);
 void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
 void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
@@ -89,5 +117,14 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);
 void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n);
 void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst);
+
+// insert path (hgx_insert.hip): events k in [0, m) get gid E0 + k
+void launch_insert_claim(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                         const InsertState& st);
+void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, int n, const InsertIn& in,
+                         const InsertState& st);
+void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st);
+void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                           const InsertState& st);
 
 }  // namespace hgx

@@ -892,11 +892,7 @@ __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __
 // kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
 // do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
 // per event: radix select of element floor(m/2) in registers.
-#ifdef HGX_CTS_T   // experiment: tile size
-constexpr int kCtsTile = HGX_CTS_T;
-#else
 constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8
-#endif
 template <int NPAD, typename CT>
 __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
@@ -1009,11 +1005,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
             uint32_t v[CPL];
 #pragma unroll
             for (int q = 0; q < CPL; q++) v[q] = vals[(lane + 64 * q) * LD + e];
-#ifdef HGX_CTS_NOSELECT
-            const uint32_t u = v[0] + (uint32_t)m;
-#else
             const uint32_t u = wave_select_kth32<CPL>(v, ok, m / 2, whist[wave]);
-#endif
             res = e_ts[e] + (int64_t)(int32_t)(u ^ 0x80000000u);
         } else {   // rare: offsets beyond 32 bits -> regather and select in 64 bits
             const int64_t p = p0 + e;
@@ -1324,10 +1316,10 @@ __global__ void k_tiefix(int32_t m, uint32_t* __restrict__ vals, const uint64_t*
 __global__ void k_finish_order(int32_t m, const uint32_t* __restrict__ vals, const int32_t* __restrict__ p_gid,
                                const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
                                const int64_t* __restrict__ p_cts, const int32_t* __restrict__ g_ntx,
-                               const uint8_t* __restrict__ g_loaded, int R, int n, int32_t* __restrict__ order_gid,
-                               int32_t* __restrict__ g_rr, int64_t* __restrict__ g_cts,
+                               const uint8_t* __restrict__ g_loaded, const uint8_t* __restrict__ g_txnil, int R, int n,
+                               int32_t* __restrict__ order_gid, int32_t* __restrict__ g_rr, int64_t* __restrict__ g_cts,
                                int32_t* __restrict__ blk_cnt, int64_t* __restrict__ blk_ntx,
-                               int32_t* __restrict__ blk_loaded) {
+                               int32_t* __restrict__ blk_loaded, uint8_t* __restrict__ blk_nil) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool ok = i < m;
     int64_t b = -1;
@@ -1342,6 +1334,10 @@ __global__ void k_finish_order(int32_t m, const uint32_t* __restrict__ vals, con
         cnt = 1;
         ntx = g_ntx[gid];
         ld = g_loaded[gid] ? 1 : 0;
+        // NewBlock(rr, first.Transactions()) (hashgraph.go:838-845): the block's nil-ness
+        // starts from its first event's slice
+        const int pp = i > 0 ? (int)vals[i - 1] : -1;
+        if (pp < 0 || (int64_t)(p_chain[pp] / n) * R + p_rr[pp] != b) blk_nil[b] = g_txnil[gid];
     }
     // the order is sorted by (graph, rr): most waves hit one block -> one atomic per wave
     const int64_t b0 = __shfl(b, 0);
@@ -1457,14 +1453,11 @@ void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
                        a.wcoin);
 }
 
-// fame kernel choice: n >= 128 takes the witness-tiled kernel with the popcount tally
-// (measured faster than the MFMA tally), smaller n the per-round kernel. HGX_FAME=vote|popc|mfma forces one (measurement).
-void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G) {
-    const char* force = getenv("HGX_FAME");   // read per call: tests switch it in-process
-    int mode = 1;
-    if (force && !strcmp(force, "vote")) mode = 0;
-    if (force && !strcmp(force, "popc")) mode = 1;
-    if (force && !strcmp(force, "mfma")) mode = 2;
+// fame kernel choice (hgx_set_fame_tally): the witness-tiled kernel with the popcount tally
+// by default (measured faster than the int8 MFMA tally at every n); the
+// per-round popcount kernel and the MFMA tally stay selectable for measurement.
+void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G, int tally) {
+    const int mode = tally == 1 ? 0 : tally == 2 ? 2 : 1;
     if (mode != 0 && n <= kFameMaxW * 64) {
         const int XT = (n + kFameTile - 1) / kFameTile;
         const dim3 grid((unsigned)((int64_t)G * R * XT));
@@ -1614,8 +1607,8 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
 
 void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n) {
     hipLaunchKernelGGL(k_finish_order, dim3(nblk(m, 256)), dim3(256), 0, s, m, vals, a.p_gid, a.p_chain, a.p_rr,
-                       a.p_cts, a.g_ntx, a.g_loaded, R, n, a.order_gid, a.g_rr, a.g_cts, a.blk_cnt, a.blk_ntx,
-                       a.blk_loaded);
+                       a.p_cts, a.g_ntx, a.g_loaded, a.g_txnil, R, n, a.order_gid, a.g_rr, a.g_cts, a.blk_cnt,
+                       a.blk_ntx, a.blk_loaded, a.blk_nil);
 }
 
 void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst) {

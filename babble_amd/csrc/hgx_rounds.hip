@@ -95,11 +95,8 @@ __device__ __forceinline__ int count_seen(const int32_t (&la)[CPL], const int32_
     }
 }
 
-#ifndef HGX_TALLY_FUSED
-#define HGX_TALLY_SPLIT 1
-#endif
 // Candidates whose bit is clear in `test` are skipped (wave-uniform branch; a 32-bit mask
-// when OWN <= 32, so the skip is one scalar bit test). HGX_TALLY_SPLIT: the popcount of
+// when OWN <= 32, so the skip is one scalar bit test). The popcount of
 // each of the CPL compare masks goes to lane O of its own partial register tv[q] and the
 // partials are added once per probe in VALU, instead of CPL - 1 scalar adds per candidate
 // (the tally is scalar-issue-bound: 4 s_bcnt1 + 3 s_add + skip test per candidate).
@@ -109,7 +106,6 @@ template <int O, int CPL, int OWN>
 __device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_t (&fd)[OWN][CPL], int (&tv)[CPL],
                                           TallyMask<OWN> test) {
     if ((test >> O) & 1u) {
-#ifdef HGX_TALLY_SPLIT
         if constexpr (CPL == 4) {
             uint64_t m0, m1, m2, m3;
             asm volatile(
@@ -133,9 +129,7 @@ __device__ __forceinline__ void tally_one(const int32_t (&la)[CPL], const int32_
                 : "v"(la[0]), "v"(la[1]), "v"(fd[O][0]), "v"(fd[O][1]));
             asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[0]) : "s"(__popcll(m0)), "i"(O));
             asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[1]) : "s"(__popcll(m1)), "i"(O));
-        } else
-#endif
-        {
+        } else {
             const int tot = count_seen<CPL>(la, fd[O]);
             asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(tv[0]) : "s"(tot), "i"(O));
         }
@@ -350,9 +344,6 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     };
     HGX_PROF(4);
     stage(b, min(P, len - b));   // in flight while the candidate rows load
-#ifdef HGX_EXP_STAGE2   // experiment: the window staged twice
-    stage(b, min(P, len - b));
-#endif
     HGX_PROF(5);
     // window landed (and the candidate rows with it): everyone may read the LDS window
     __builtin_amdgcn_s_waitcnt(0);
@@ -484,11 +475,7 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
 // histogram). The own-chain candidate never counts at the probe that is itself.
 // waves per block: the candidates of a chain are walked per wave, so more waves per block
 // wins over more resident blocks (c5 step: 16 waves 470 us, 8 waves 539 us, 4 waves 854 us)
-#ifdef HGX_BIG_NWV   // experiment
-constexpr int kBigWaves = HGX_BIG_NWV;
-#else
 constexpr int kBigWaves = 16;
-#endif
 template <int CPL, int P, typename CT, bool VEC>
 __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, int kstep) {
     constexpr int NWV = kBigWaves;
@@ -544,14 +531,6 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
     auto seen_at = [&](const int32_t (&fd)[CPL], int pp, int j, int kb) -> bool {
         uint32_t raw[CPL];
         load_row(la_s + pp * n, raw, false);
-#ifdef HGX_BIG_BALLOT   // experiment: one ballot + scalar popcount per coordinate slot
-        int tot = 0;
-#pragma unroll
-        for (int q = 0; q < CPL; q++) {
-            const int32_t la = (sizeof(CT) == 2) ? (int32_t)raw[q] : min(Coord<CT>::la(raw[q]), kMaxI32 - 1);
-            tot += __popcll(__ballot(la >= fd[q]));
-        }
-#else
         // per-lane count over the CPL slots in VALU, one DPP wave sum: CPL scalar popcounts
         // and adds per test would make the walk scalar-issue-bound
         uint32_t c = 0;
@@ -561,7 +540,6 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
             c += (la >= fd[q]) ? 1u : 0u;
         }
         const int tot = (int)__builtin_amdgcn_readlane((int)wave_scan_add_u32(c), 63);
-#endif
         return tot >= sm && !(j == cl && kb + pp == b);
     };
     // WFD row of candidate j in the lane's coordinate order (compact rows are raw uint16,

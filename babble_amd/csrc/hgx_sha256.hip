@@ -7,10 +7,13 @@
 //   Block.Hash                    hashgraph/block.go:44-53
 // Here a whole batch of already-encoded messages is hashed in one launch: one lane per
 // message, the 64-round compression fully unrolled in VGPRs (rotates are v_alignbit,
-// Ch/Maj v_bfi). The work is VALU-bound (~1.5 k lane instructions per 64-byte block
-// against ~68 bytes read), so there is no LDS staging: each lane streams its own
-// message with guarded dword loads that never touch a byte past the message's last
-// aligned dword, and the Merkle-Damgard padding is built in registers.
+// Sigma/Ch/Maj v_bitop3). The work is VALU-bound (~1.5 k lane instructions per 64-byte
+// block against ~68 bytes read), so there is no LDS staging: each lane streams its own
+// message with 16-byte loads from the 16-byte-aligned address below each block (guarded:
+// a 16-byte slice holding no message byte is not read), so a load may touch up to 15
+// bytes before the message's first byte and up to 15 bytes past its last byte, always
+// inside the 16-byte-aligned span of the message (include/hgx.h states this for the
+// device entry). The Merkle-Damgard padding is built in registers.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -19,16 +22,6 @@
 #include <vector>
 
 #include "hgx.h"
-
-#ifndef HGX_SHA_WAVES
-#define HGX_SHA_WAVES 4
-#endif
-#ifndef HGX_SHA_MSGS
-#define HGX_SHA_MSGS 1
-#endif
-#ifndef HGX_SHA_PREFETCH
-#define HGX_SHA_PREFETCH 1
-#endif
 
 namespace hgx {
 
@@ -83,7 +76,7 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 #undef HGX_SHA_R
 
 // One lane per message i = data[offsets[i], offsets[i+1]); digest to out + 32 i.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGX_SHA_WAVES))) void k_sha256_batch(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sha256_batch(const uint8_t* __restrict__ data,
                                                       const int64_t* __restrict__ offsets, int64_t count,
                                                       uint8_t* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -104,14 +97,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGX_SHA_WAV
         for (int t = 0; t < 5; t++) E[t] = (16 * t - sh16 < rem) ? vp[4 * b + t] : make_uint4(0, 0, 0, 0);
     };
     uint4 E[5];
-    if (HGX_SHA_PREFETCH) load_block(0, E);
+    load_block(0, E);
     for (int64_t b = 0; b < nb; b++) {
-        if (!HGX_SHA_PREFETCH) load_block(b, E);
         const int64_t rem = len - 64 * b;   // message bytes from this block's first byte on
         uint32_t D[20];
 #pragma unroll
         for (int t = 0; t < 5; t++) { D[4 * t] = E[t].x; D[4 * t + 1] = E[t].y; D[4 * t + 2] = E[t].z; D[4 * t + 3] = E[t].w; }
-        if (HGX_SHA_PREFETCH && b + 1 < nb) load_block(b + 1, E);   // next block in flight during this compression
+        if (b + 1 < nb) load_block(b + 1, E);   // next block in flight during this compression
         uint32_t d[17];
 #pragma unroll
         for (int j = 0; j < 17; j++) d[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
@@ -139,85 +131,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGX_SHA_WAV
 }
 
 
-// Two messages per lane (2 i, 2 i + 1): the two round chains are independent, so their
-// instructions interleave and hide each other's dependency latency.
-struct ShaMsg {
-    const uint4* vp;
-    int64_t len, nb;
-    int sh16, q, sh;
-};
-
-__device__ __forceinline__ ShaMsg sha_msg(const uint8_t* data, const int64_t* offsets, int64_t i, int64_t count) {
-    ShaMsg m;
-    const int64_t off = i < count ? offsets[i] : 0;
-    m.len = i < count ? offsets[i + 1] - off : -72;   // nb = 0: no block, no load
-    m.nb = (m.len + 72) >> 6;
-    const uintptr_t a0 = (uintptr_t)(data + off);
-    m.sh16 = (int)(a0 & 15); m.q = m.sh16 >> 2; m.sh = m.sh16 & 3;
-    m.vp = (const uint4*)(data + (off - m.sh16));
-    return m;
-}
-
-__device__ __forceinline__ void sha_block_words(const ShaMsg& m, int64_t b, uint32_t w[16]) {
-    const int64_t rem = m.len - 64 * b;
-    uint32_t D[20];
-#pragma unroll
-    for (int t = 0; t < 5; t++) {
-        const uint4 e = (16 * t - m.sh16 < rem) ? m.vp[4 * b + t] : make_uint4(0, 0, 0, 0);
-        D[4 * t] = e.x; D[4 * t + 1] = e.y; D[4 * t + 2] = e.z; D[4 * t + 3] = e.w;
-    }
-    const int q = m.q;
-    const int r = (int)(rem < 64 ? (rem < -64 ? -64 : rem) : 64);   // <= 0: block after the 0x80 byte
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const uint32_t lo = q == 0 ? D[k] : q == 1 ? D[k + 1] : q == 2 ? D[k + 2] : D[k + 3];
-        const uint32_t hi = q == 0 ? D[k + 1] : q == 1 ? D[k + 2] : q == 2 ? D[k + 3] : D[k + 4];
-        const uint32_t x = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, m.sh));
-        const int v = r - 4 * k;
-        uint32_t y;
-        if (v >= 4) y = x;
-        else if (v > 0) y = (x & (0xFFFFFFFFu << (32 - 8 * v))) | (0x80u << (24 - 8 * v));
-        else y = (v == 0) ? 0x80000000u : 0u;
-        w[k] = y;
-    }
-    if (b == m.nb - 1) {
-        const uint64_t bits = (uint64_t)m.len * 8;
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-    }
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGX_SHA_WAVES))) void k_sha256_batch2(
-    const uint8_t* __restrict__ data, const int64_t* __restrict__ offsets, int64_t count, uint8_t* __restrict__ out) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (2 * p >= count) return;
-    const ShaMsg m0 = sha_msg(data, offsets, 2 * p, count), m1 = sha_msg(data, offsets, 2 * p + 1, count);
-    uint32_t s0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-    uint32_t s1[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) s1[k] = s0[k];
-    const int64_t nbm = m0.nb > m1.nb ? m0.nb : m1.nb;
-    for (int64_t b = 0; b < nbm; b++) {
-        uint32_t w0[16], w1[16], n0[8], n1[8];
-        sha_block_words(m0, b, w0);
-        sha_block_words(m1, b, w1);
-#pragma unroll
-        for (int k = 0; k < 8; k++) { n0[k] = s0[k]; n1[k] = s1[k]; }
-        sha256_compress(n0, w0);
-        sha256_compress(n1, w1);
-        const bool a0 = b < m0.nb, a1 = b < m1.nb;
-#pragma unroll
-        for (int k = 0; k < 8; k++) { s0[k] = a0 ? n0[k] : s0[k]; s1[k] = a1 ? n1[k] : s1[k]; }
-    }
-    uint32_t* o = (uint32_t*)(out + 64 * p);
-#pragma unroll
-    for (int k = 0; k < 8; k++) o[k] = __builtin_bswap32(s0[k]);
-    if (2 * p + 1 < count) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) o[8 + k] = __builtin_bswap32(s1[k]);
-    }
-}
-
 __device__ __host__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -244,13 +157,8 @@ void set_err(hgx_error* err, int32_t code, const char* msg) {
 hipError_t launch_sha256(const uint8_t* d_data, const int64_t* d_offsets, int64_t count, uint8_t* d_out,
                          hipStream_t s) {
     if (count <= 0) return hipSuccess;
-#if HGX_SHA_MSGS == 2
-    const int64_t blocks = ((count + 1) / 2 + 255) / 256;
-    hipLaunchKernelGGL(hgx::k_sha256_batch2, dim3((unsigned)blocks), dim3(256), 0, s, d_data, d_offsets, count, d_out);
-#else
     const int64_t blocks = (count + 255) / 256;
     hipLaunchKernelGGL(hgx::k_sha256_batch, dim3((unsigned)blocks), dim3(256), 0, s, d_data, d_offsets, count, d_out);
-#endif
     return hipGetLastError();
 }
 

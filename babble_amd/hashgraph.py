@@ -66,6 +66,22 @@ class Hashgraph:
         _lib.check(rc, err)
         return n_ins.value
 
+    def insert_device(self, dt: "DeviceTrace", lo: int = 0, hi: Optional[int] = None) -> int:
+        """Bulk InsertEvent of a trace already resident in HBM (hgx_insert_events_device)."""
+        hi = dt.E if hi is None else hi
+        ev = dt.events(lo, hi)
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_events_device(self.ctx, C.byref(ev), hi - lo, C.byref(n_ins), C.byref(err))
+        _lib.check(rc, err)
+        return n_ins.value
+
+    def clear(self):
+        """Forget every event: a fresh NewHashgraph (device allocations kept)."""
+        rc = self.L.hgx_clear(self.ctx)
+        if rc:
+            raise HgxError(rc, "hgx_clear failed")
+
     def insert_trace(self, t, lo: int = 0, hi: Optional[int] = None) -> int:
         hi = t.E if hi is None else hi
         sl = slice(lo, hi)
@@ -155,6 +171,76 @@ class Hashgraph:
                 raise HgxError(rc, "hgx_consensus_events failed")
         return out[:k]
 
+    def GetBlock(self, rr: int, graph: int = 0) -> dict:
+        """Store.GetBlock(rr): the block with that RoundReceived (HgxError "<rr>, Not Found")."""
+        b, err = C.c_int64(), hgx_error()
+        _lib.check(self.L.hgx_get_block(self.ctx, graph, rr, C.byref(b), C.byref(err)), err)
+        return self.Blocks(graph)[b.value]
+
+    def consensus_received(self, graph: int = 0, first: int = 0, count: Optional[int] = None):
+        """(gids, round received, consensus timestamps) along the graph's consensus order."""
+        k = int(self.L.hgx_consensus_events_count(self.ctx, graph))
+        count = k - first if count is None else count
+        g = np.zeros(max(count, 1), np.int64)
+        rr = np.zeros(max(count, 1), np.int32)
+        ts = np.zeros(max(count, 1), np.int64)
+        if count:
+            rc = self.L.hgx_consensus_received(self.ctx, graph, first, count, ptr(g), ptr(rr), ptr(ts))
+            if rc:
+                raise HgxError(rc, "hgx_consensus_received failed")
+        return g[:count], rr[:count], ts[:count]
+
+    # ------------------------------------------------------------------ Store: events by participant
+    def LastFrom(self, participant: int):
+        """(gid of the last event or -1, isRoot) (inmem_store.go:85-102)."""
+        gid, root, err = C.c_int64(), C.c_int32(), hgx_error()
+        _lib.check(self.L.hgx_last_from(self.ctx, participant, C.byref(gid), C.byref(root), C.byref(err)), err)
+        return gid.value, bool(root.value)
+
+    def ParticipantEvents(self, participant: int, skip: int) -> List[int]:
+        cnt, err = C.c_int64(), hgx_error()
+        _lib.check(self.L.hgx_participant_events(self.ctx, participant, skip, None, 0, C.byref(cnt), C.byref(err)),
+                   err)
+        out = np.zeros(max(cnt.value, 1), np.int64)
+        _lib.check(self.L.hgx_participant_events(self.ctx, participant, skip, ptr(out), cnt.value, C.byref(cnt),
+                                                 C.byref(err)), err)
+        return [int(v) for v in out[:cnt.value]]
+
+    def ParticipantEvent(self, participant: int, index: int) -> int:
+        gid, err = C.c_int64(), hgx_error()
+        _lib.check(self.L.hgx_participant_event(self.ctx, participant, index, C.byref(gid), C.byref(err)), err)
+        return gid.value
+
+    def GetRoot(self, participant: int) -> dict:
+        x, y, idx, rnd, err = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32(), hgx_error()
+        _lib.check(self.L.hgx_get_root(self.ctx, participant, C.byref(x), C.byref(y), C.byref(idx), C.byref(rnd),
+                                       C.byref(err)), err)
+        return dict(X=x.value, Y=y.value, Index=idx.value, Round=rnd.value)
+
+    def GetEvent(self, gid: int) -> dict:
+        cr, ix, sp, op, ts, nt, nil, err = (C.c_int32(), C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64(),
+                                            C.c_int32(), C.c_int32(), hgx_error())
+        _lib.check(self.L.hgx_get_event(self.ctx, gid, C.byref(cr), C.byref(ix), C.byref(sp), C.byref(op),
+                                        C.byref(ts), C.byref(nt), C.byref(nil), C.byref(err)), err)
+        return dict(creator=cr.value, index=ix.value, self_parent=sp.value, other_parent=op.value,
+                    timestamp=ts.value, ntx=nt.value, tx_nil=bool(nil.value))
+
+    def wire_info(self, first: int = 0, count: Optional[int] = None):
+        """SetWireInfo of events [first, first+count): (self-parent index, other-parent creator, other-parent index)."""
+        count = self.num_events() - first if count is None else count
+        a, b, c = (np.zeros(max(count, 1), np.int32) for _ in range(3))
+        if count:
+            rc = self.L.hgx_wire_info(self.ctx, first, count, ptr(a), ptr(b), ptr(c))
+            if rc:
+                raise HgxError(rc, "hgx_wire_info failed")
+        return a[:count], b[:count], c[:count]
+
+    def ReadWireInfo(self, creator: int, sp_index: int, op_creator: int, op_index: int):
+        sp, op, err = C.c_int64(), C.c_int64(), hgx_error()
+        _lib.check(self.L.hgx_read_wire_info(self.ctx, creator, sp_index, op_creator, op_index, C.byref(sp),
+                                             C.byref(op), C.byref(err)), err)
+        return sp.value, op.value
+
     def Blocks(self, graph: int = 0) -> List[dict]:
         res = []
         for b in range(int(self.L.hgx_num_blocks(self.ctx, graph))):
@@ -237,6 +323,17 @@ class Hashgraph:
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]))
 
+    def set_fame_tally(self, mode):
+        """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
+        m = {"popc": 0, "vote": 1, "mfma": 2}[mode] if isinstance(mode, str) else int(mode)
+        if self.L.hgx_set_fame_tally(self.ctx, m) != 0:
+            raise ValueError(f"invalid fame tally {mode}")
+
+    def reserve_rounds(self, rounds: int):
+        """Size the per-round tables (before the first DivideRounds; small values exercise growth)."""
+        if self.L.hgx_reserve_rounds(self.ctx, int(rounds)) != 0:
+            raise ValueError("hgx_reserve_rounds failed")
+
     def set_coord_storage(self, mode):
         """0 = auto (uint16 coordinates when every Index fits), 1 = always int32."""
         if self.L.hgx_set_coord_storage(self.ctx, int(mode)) != 0:
@@ -267,6 +364,34 @@ class Hashgraph:
 
     def reset_stats(self):
         self.L.hgx_reset_stats(self.ctx)
+
+
+class DeviceTrace:
+    """A trace's hgx_events columns resident in HBM (torch tensors on the context's device:
+    torch is only the allocator here). Feeds Hashgraph.insert_device."""
+
+    def __init__(self, t, device: int = 0):
+        import torch
+        dev = torch.device("cuda", device)
+
+        def up(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
+
+        self.E = int(t.creator.shape[0])
+        self.cols = dict(creator=up(t.creator, np.int32), index=up(t.index, np.int64), sp=up(t.sp, np.int64),
+                         op=up(t.op, np.int64), ts=up(t.ts, np.int64), hash=up(t.hash, np.uint8),
+                         s=up(t.s, np.uint8), ntx=up(t.ntx, np.int32), nil=up(t.txnil, np.int32))
+        torch.cuda.synchronize(dev)
+
+    def events(self, lo: int, hi: int) -> hgx_events:
+        c = self.cols
+
+        def p(name, per=1):
+            t = c[name]
+            return C.c_void_p(t.data_ptr() + lo * per * t.element_size())
+
+        return hgx_events(p("creator"), p("index"), p("sp"), p("op"), p("ts"), p("hash", 32), p("s", 32), p("ntx"),
+                          p("nil"))
 
 
 def block_hash(rr: int, txs: List[bytes], tx_nil: bool) -> bytes:

@@ -1,18 +1,23 @@
 #!/usr/bin/env python3
 """bench.py -- consensus-ordered events/sec of the MI355X Hashgraph engine.
 
-Workload (BASELINE.json metric "consensus-ordered events/sec at N=256 peers"):
-one synthetic random-gossip hashgraph per GPU (configs[2]: 256 peers, 10M events,
-fits one MI355X), seeded per rank (weak scaling: independent replicas, no
-data-path collective -- DESIGN.md §6). A step = one full pass of the hot path over
-the HBM-resident trace: DivideRounds (coordinates + rounds), DecideFame,
-FindOrder (round-received, median timestamps, total order, blocks), ending with
-the order in host memory.
+Workload (BASELINE.json metric "consensus-ordered events/sec at N=256 peers"): one synthetic
+random-gossip hashgraph per GPU (configs[2]: 256 peers, 10M events, fits one MI355X), seeded
+per rank (weak scaling: independent 256-peer simulations, no data-path collective --
+DESIGN.md §6). The trace is resident in HBM before the clock starts. A step is one whole
+pass of the hot path, from the first event append to the order in host memory:
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
+    hgx_clear -> hgx_insert_events_device (InsertEvent for every event: parent/index
+    validation + append, on the GPU) -> DivideRounds -> DecideFame -> FindOrder
+
+After the timed steps (outside the clock) the run is checked: the GPU against the CPU oracle
+on a prefix of the same trace (every output, bit-exact), and the full-size result against
+the order properties the reference guarantees (a permutation of the received events sorted
+by (round received, consensus timestamp, S), rounds monotone along every chain, blocks
+consistent). A failed check exits non-zero without a result line.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c2|c4|c5]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
-
-Prints one JSON line (rank 0) with roofline and cpu_baseline objects.
 """
 from __future__ import annotations
 
@@ -39,6 +44,10 @@ CONFIGS = {
     "c5": (1024, 1 << 20, 1, 300, 0.3, 4, "1024 peers (300 silent, 30% stale other-parents), 1,048,576 events"),
 }
 
+# oracle sample (events of graph 0's trace) for the prefix parity check and the CPU baseline:
+# about 10-30 s of single-threaded oracle work
+SAMPLE = {4: 1024, 16: 16384, 64: 100_000, 256: 100_000, 1024: 12_000}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -54,29 +63,135 @@ def make_trace(cfg, rank):
                                 for s in seeds]), G
 
 
-def cpu_baseline(cfg, budget_s=20.0):
-    """The oracle (single-threaded C restatement of the reference loops) on a bounded
-    prefix of the same workload: consensus-ordered events / wall seconds."""
+def kernel_bytes(name, n, E, m, compact):
+    """SURVEY §8(d) algorithmic bytes of one pass, per kernel: E events,
+    m events received by the pass, coordinates of `cb` bytes (2 compact, 4 int32)."""
+    cb = 2 if compact else 4
+    return {
+        "la_sweep": (3 * cb * n + 16) * E,      # la_build: read 2 parent rows, write the row (12n+16 int32)
+        "fd_build": 2 * cb * n * E,             # read LA once, write FD (8n int32)
+        "round_search": (4 * n + 16) * E,       # round_assign: 4n+16 per event (witness rows amortised)
+        "round_received": 16 * E,
+        "cts_median": (cb * n + 8 * n + 12) * m,  # FD row + <= n timestamp gathers + outputs
+        "order_sort": 2 * 44 * m,
+        "layout": 64 * E,
+    }.get(name)
+
+
+def cpu_baseline(t, n, budget_note):
+    """The oracle (single-threaded C restatement of the reference loops, oracle/hg_oracle.c)
+    on a bounded prefix of the same workload, timed on this host: InsertEvent (one C batch
+    call) + DivideRounds + DecideFame + FindOrder. Returns the baseline and the oracle."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import hgref
-    from babble_amd import trace
-    n, E, G, silent, stale, depth, _ = CONFIGS[cfg]
-    sample = min(E, {4: 1024, 16: 16384, 64: 60000, 256: 40000, 1024: 12000}.get(n, 20000))
-    t = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
     o = hgref.Oracle(n)
     t0 = time.perf_counter()
     o.insert_trace(t)
     o.divide_rounds()
-    o.decide_fame()
-    o.find_order()
+    rc, msg = o.decide_fame()
+    if not rc:
+        rc, msg = o.find_order()
     dt = time.perf_counter() - t0
+    if rc:
+        raise RuntimeError(f"oracle consensus failed: {msg}")
     ordered = len(o.consensus_events())
-    note = "" if ordered else " (no round is decided within a sample the oracle finishes in seconds: n = 1024 " \
-        "rounds take ~18k events, so no rate is reported)"
-    return dict(value=(ordered / dt) if ordered else None, unit="consensus-ordered events/s", cores=1, kind="port",
-                sample=f"first {sample} events of the {CONFIGS[cfg][6]} trace (seed 1), oracle "
-                       f"InsertEvent+DivideRounds+DecideFame+FindOrder single-threaded, {ordered} events "
-                       f"ordered in {dt:.2f}s on {platform.processor() or platform.machine()}{note}")
+    note = "" if ordered else " (no round is decided within the sample: no rate is reported)"
+    base = dict(value=(ordered / dt) if ordered else None, unit="consensus-ordered events/s", cores=1, kind="port",
+                sample=f"first {t.E} events of the {budget_note} trace (seed 1), oracle InsertEvent+DivideRounds+"
+                       f"DecideFame+FindOrder single-threaded, {ordered} events ordered in {dt:.2f}s on "
+                       f"{platform.processor() or platform.machine()}{note}")
+    return base, o
+
+
+def prefix_parity(t, o, device):
+    """GPU vs oracle on the same prefix: every output bit-exact (fails loudly)."""
+    from babble_amd.hashgraph import Hashgraph
+    h = Hashgraph(t.n, capacity=t.E, device=device)
+    h.insert_trace(t)
+    h.RunConsensus()
+    a, b = h.results(), o.results()
+    for k in ("round", "witness", "famous", "rr", "cts"):
+        if not np.array_equal(np.asarray(a[k]), np.asarray(b[k])):
+            bad = np.nonzero(np.asarray(a[k]) != np.asarray(b[k]))[0][:5]
+            raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: {k} differs at gids {bad.tolist()}")
+    if list(a["order"]) != list(b["order"]):
+        raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: consensus order")
+    for k in ("last_round", "undecided", "lcr", "lcre", "consensus_tx", "pending_loaded"):
+        if a[k] != b[k]:
+            raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: {k} {a[k]} != {b[k]}")
+    if [(x["rr"], x["ntx"], x["tx_nil"], x["committed"]) for x in a["blocks"]] != [tuple(x[:4]) for x in b["blocks"]]:
+        raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: blocks")
+    h.close()
+    return {"events": int(t.E), "ordered": int(len(b["order"])), "rounds": int(b["last_round"]) + 1,
+            "outputs": "round, witness, fame, round received, consensus timestamp, order, UndecidedRounds, "
+                       "LastConsensusRound, LastCommitedRoundEvents, counters, blocks", "result": "bit-exact"}
+
+
+def full_size_checks(h, tr, G):
+    """Order properties of the full-size run (hashgraph.go:753-858, consensus_sorter.go)."""
+    E, n = tr.E, tr.n
+    rnd, wit, _ = h.rounds()
+    rr, cts = h.received()
+    creator = tr.creator.astype(np.int64)
+    fails = []
+
+    def check(ok, what):
+        if not ok:
+            fails.append(what)
+
+    # per chain (creator), events in Index order == gid order of that creator
+    order_c = np.lexsort((np.arange(E), creator))
+    c_sorted = creator[order_c]
+    same = c_sorted[1:] == c_sorted[:-1]
+    r_c, rr_c = rnd[order_c], rr[order_c]
+    check(np.all(r_c[1:][same] >= r_c[:-1][same]), "round non-decreasing along every chain")
+    rcv = rr_c >= 0
+    check(np.all(~(rcv[1:] & ~rcv[:-1] & same)), "received events of a chain form a prefix")
+    check(np.all(rr_c[1:][same & rcv[1:]] >= rr_c[:-1][same & rcv[1:]]), "round received non-decreasing along chains")
+    check(np.all(rr[rr >= 0] > rnd[rr >= 0]), "round received > round")
+    first = np.ones(E, bool)
+    first[1:] = ~same
+    check(np.all(wit[order_c][first] == 1), "first event of every chain is a witness")
+    sp = tr.sp
+    has_sp = sp >= 0
+    check(np.all(wit[has_sp] == (rnd[has_sp] > rnd[sp[has_sp]])), "witness iff round > round(self-parent)")
+    total = 0
+    for g in range(G):
+        order = h.ConsensusEvents(g)
+        total += len(order)
+        in_g = (creator // n) == g
+        recv_g = np.nonzero(in_g & (rr >= 0))[0]
+        check(len(order) == len(recv_g) and np.array_equal(np.sort(order), recv_g),
+              f"graph {g}: order is a permutation of the received events")
+        if len(order) < 2:
+            continue
+        o_rr, o_cts = rr[order], cts[order]
+        check(np.all(o_rr[1:] >= o_rr[:-1]), f"graph {g}: round received non-decreasing along the order")
+        eq_rr = o_rr[1:] == o_rr[:-1]
+        check(np.all(o_cts[1:][eq_rr] >= o_cts[:-1][eq_rr]), f"graph {g}: consensus timestamp non-decreasing "
+                                                            "within a round received")
+        tie = eq_rr & (o_cts[1:] == o_cts[:-1])
+        if tie.any():
+            s = tr.s[order]
+            a, b = s[:-1][tie], s[1:][tie]
+            diff = a != b
+            idx = np.argmax(diff, axis=1)
+            rows = np.arange(len(idx))
+            check(np.all(diff.any(axis=1)) and np.all(a[rows, idx] < b[rows, idx]),
+                  f"graph {g}: S strictly increasing within equal (round received, timestamp)")
+        blocks = h.Blocks(g)
+        check(sum(b["n_events"] for b in blocks) == len(order), f"graph {g}: blocks cover the order")
+        check(all(b1["rr"] < b2["rr"] for b1, b2 in zip(blocks, blocks[1:])), f"graph {g}: one block per rr")
+        check(sum(b["ntx"] for b in blocks) == h.ConsensusTransactions(g), f"graph {g}: block transactions")
+        check(all(int(rr[order[b["first"]]]) == b["rr"] for b in blocks), f"graph {g}: block rr")
+    if fails:
+        raise SystemExit("FULL-SIZE CHECK FAILURE: " + "; ".join(fails))
+    return {"events": int(E), "ordered": int(total),
+            "properties": ["order is a permutation of the received events", "rr non-decreasing along the order",
+                           "cts non-decreasing within rr", "S strictly increasing within (rr, cts) ties",
+                           "round non-decreasing along every chain", "received events form a chain prefix",
+                           "rr non-decreasing along chains", "rr > round", "witness iff round > round(sp)",
+                           "blocks: one per rr, cover the order, transaction totals"], "result": "pass"}
 
 
 class Reducer:
@@ -131,7 +246,6 @@ def ingest_leg(count, steps, warmup, device):
     from babble_amd.hashgraph import sha256_bench, sha256_bench_messages
     lo, hi, seed = 400, 560, 5
     r = sha256_bench(count, lo, hi, seed, warmup=max(1, warmup), iters=steps, n_sample=64, device=device)
-    # sanity sample against the host digest (tests/test_gpu_sha256.py covers the kernel in full)
     msgs = sha256_bench_messages(64, lo, hi, seed)
     assert all(hashlib.sha256(m).digest() == bytes(d) for m, d in zip(msgs, r["sample"])), "SHA-256 mismatch"
     ms = r["ms_per_launch"]
@@ -149,77 +263,96 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (and the prefix parity check)")
     ap.add_argument("--no-ingest", action="store_true", help="skip the batched event-id SHA-256 side leg")
+    ap.add_argument("--no-check", action="store_true", help="skip the full-size property checks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     red = Reducer(world, local_rank)
-    barrier, max_over_ranks, sum_over_ranks = red.barrier, red.max, red.sum
-    dist = red.dist
 
-    from babble_amd.hashgraph import Hashgraph
+    from babble_amd.hashgraph import DeviceTrace, Hashgraph
     n, E, G, *_ = CONFIGS[args.config]
     t0 = time.time()
     tr, G = make_trace(args.config, rank)
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
-    h = Hashgraph(n, capacity=tr.E, device=local_rank if dist is None else local_rank, n_graphs=G)
-    t0 = time.time()
-    h.insert_trace(tr)
-    log(f"[rank {rank}] inserted (host validation + H2D) in {time.time() - t0:.1f}s")
+    h = Hashgraph(n, capacity=tr.E, device=local_rank, n_graphs=G)
+    dtr = DeviceTrace(tr, device=local_rank)   # resident in HBM before the clock starts
 
     def step():
-        h.reset_consensus()
+        h.clear()
+        h.insert_device(dtr)
         h.DivideRounds()
         h.DecideFame()
         h.FindOrder()
         return sum(int(h.L.hgx_consensus_events_count(h.ctx, g)) for g in range(G))
 
-    # warmup: also profiles every kernel to pick the dominant one
+    # warmup: every kernel timed with HIP events, to rank the kernels
     h.set_kernel_timing(True)
     h.reset_stats()
-    ordered = 0
     for w in range(max(1, args.warmup)):
         tw = time.time()
         ordered = step()
         log(f"[rank {rank}] warmup {w}: {ordered} ordered in {time.time() - tw:.2f}s  {h.phase_times()}")
-    ks = h.kernel_stats()
-    dom = max(ks, key=lambda k: ks[k]["ms"])
-    log(f"[rank {rank}] kernel profile (warmup): " +
-        ", ".join(f"{k}={v['ms']:.1f}ms/{v['launches']}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1]['ms'])))
-    # roofline is reported for the dominant HBM-streaming kernel
-    hbm_kernels = ("la_sweep", "fd_build", "cts_median", "round_received", "order_sort", "layout")
-    roof_k = max(hbm_kernels, key=lambda k: ks.get(k, {"ms": 0})["ms"])
+    ks_w = h.kernel_stats()
+    nw = max(1, args.warmup)
+    dom = max(ks_w, key=lambda k: ks_w[k]["ms"])
+    log(f"[rank {rank}] kernel profile (warmup, ms per pass): " +
+        ", ".join(f"{k}={v['ms'] / nw:.2f}/{v['launches'] // nw}" for k, v in
+                  sorted(ks_w.items(), key=lambda kv: -kv[1]['ms'])))
 
-    # timed region: only the roofline kernel is instrumented (HIP events on the context stream)
-    h.set_kernel_timing(roof_k)
+    # timed region: the dominant kernel alone is instrumented (HIP events on the context stream)
+    h.set_kernel_timing(dom)
     h.reset_stats()
-    barrier()
+    red.barrier()
     t_start = time.perf_counter()   # every hgx call returns with its work complete (order in host memory)
     total = 0
     for _ in range(args.steps):
         total += step()
     t_el = time.perf_counter() - t_start
-    barrier()
-    t_max = max_over_ranks(t_el)
-    total_all = sum_over_ranks(total)
+    red.barrier()
+    t_max = red.max(t_el)
+    total_all = red.sum(total)
     ks = h.kernel_stats()
     phases = h.phase_times()
+    h.set_kernel_timing(False)
+
+    # PCIe-inclusive variant: the same step with the trace in host memory
+    tp = time.perf_counter()
+    h.clear()
+    h.insert_trace(tr)
+    h.DivideRounds()
+    h.DecideFame()
+    h.FindOrder()
+    t_pcie = time.perf_counter() - tp
+
+    checks = {"full_size": "skipped"}
+    if not args.no_check:
+        tc = time.time()
+        checks["full_size"] = full_size_checks(h, tr, G)
+        log(f"[rank {rank}] full-size checks passed in {time.time() - tc:.1f}s")
 
     result = None
     if rank == 0:
-        r = ks.get(roof_k, {"ms": 0, "launches": 0, "bytes": 0})
-        avg_ms = r["ms"] / max(1, r["launches"])
-        per_launch_bytes = r["bytes"] / max(1, r["launches"])
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        m_pass = total // max(1, args.steps)
+        per_pass = {}
+        for k, v in ks_w.items():
+            ms = v["ms"] / nw
+            b = kernel_bytes(k, n, tr.E, m_pass, phases["compact"])
+            per_pass[k] = {"ms": round(ms, 4), "launches": v["launches"] // nw,
+                           "algorithmic_bytes": b, "GB_per_s": (b / (ms * 1e-3) / 1e9) if (b and ms > 0) else None}
+        r = ks.get(dom, {"ms": 0, "launches": 0})
+        dom_ms = r["ms"] / max(1, args.steps)
+        dom_bytes = kernel_bytes(dom, n, tr.E, m_pass, phases["compact"])
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and dom_bytes else 0.0
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
             try:
-                t = json.load(open(tf)).get(roof_k)
-                traffic = t["bytes_per_launch"] if isinstance(t, dict) else t
+                tj = json.load(open(tf)).get(dom)
+                traffic = tj.get("bytes_per_pass") if isinstance(tj, dict) else None
             except Exception:
                 traffic = None
         result = {
@@ -234,16 +367,26 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded random-gossip traces, synthetic event ids/signatures)",
+            "data": "synthetic (seeded random-gossip traces, synthetic event ids/signatures), resident in HBM",
             "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
                        "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
-                       "ordered_events_per_step_per_gpu": int(total // max(1, args.steps)),
+                       "ordered_events_per_step_per_gpu": int(m_pass),
+                       "step": "clear + InsertEvent (device validation) + DivideRounds + DecideFame + FindOrder",
                        "parallelism": f"replicas x{world} (seed-sharded)",
                        "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
                        "dominant_kernel": dom},
-            "roofline": {"kernel": roof_k, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
+                         "ms_per_pass": dom_ms, "launches_per_pass": r["launches"] // max(1, args.steps),
+                         "algorithmic_bytes_per_pass": dom_bytes,
+                         "note": "per pass: SURVEY 8(d) bytes of the kernel's role over all its launches / "
+                                 "its summed device time; traffic = PMC bytes per pass (profiles/)"},
+            "kernels_per_pass": per_pass,
+            "host_insert_pcie": {"value": total // max(1, args.steps) / t_pcie, "unit": "consensus-ordered events/s",
+                                 "ms_per_step": t_pcie * 1e3,
+                                 "note": "the same step with the trace in host memory (H2D of every event "
+                                         "column inside the timed step); not the headline"},
+            "checks": checks,
         }
         if not args.no_ingest:
             try:
@@ -251,13 +394,17 @@ def main():
             except Exception as e:  # reported, never fatal
                 result["ingest_sha256"] = {"error": str(e)}
         if world == 1 and not args.no_cpu_baseline:
-            try:
-                result["cpu_baseline"] = cpu_baseline(args.config)
-            except Exception as e:  # reported, never fatal
-                result["cpu_baseline"] = {"error": str(e)}
+            from babble_amd import trace
+            _, _, _, silent, stale, depth, desc = CONFIGS[args.config]
+            sample = min(E, SAMPLE.get(n, 20000))
+            ts = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
+            base, o = cpu_baseline(ts, n, desc)
+            result["cpu_baseline"] = base
+            checks["prefix_parity"] = prefix_parity(ts, o, local_rank)
+            log(f"[rank {rank}] prefix parity ({sample} events) bit-exact")
         print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if red.dist is not None:
+        red.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HGX_ABI_VERSION 1
+#define HGX_ABI_VERSION 2
 
 /* Error codes. 1..5 mirror common.StoreErrType + 1 (common/errors.go:7-13). */
 enum {
@@ -87,10 +87,19 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
 void hgx_destroy(hgx_ctx* ctx);
 
 /* ---- the four drop-in calls ------------------------------------------------ */
-/* InsertEvent(e, true) for each event in order; stops at the first failure
- * (like Core.Sync, node/core.go:199-211). *n_inserted = events accepted. */
+/* InsertEvent(e, true) for each event in order (hashgraph.go:356-401); stops at the first
+ * failure like Core.Sync (node/core.go:199-211): *n_inserted = events accepted, err = the
+ * Go error of the first rejected event. The batch is copied to HBM and validated there
+ * (CheckSelfParent :404-420, CheckOtherParent :423-445, RollingIndex.Add
+ * common/rolling_index.go:54-68) by data-parallel kernels; a whole Core.Sync batch is one call.
+ * Event.Verify (the signature) stays with the caller. */
 int32_t hgx_insert_events(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
                           hgx_error* err);
+/* The same with every hgx_events column a DEVICE pointer on the context's device (events
+ * decoded / hashed on the GPU, or a trace resident in HBM). hash and sig_s must be
+ * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */
+int32_t hgx_insert_events_device(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
+                                 hgx_error* err);
 int32_t hgx_divide_rounds(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_decide_fame(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_find_order(hgx_ctx* ctx, hgx_error* err);
@@ -100,6 +109,9 @@ int32_t hgx_run_consensus(hgx_ctx* ctx, hgx_error* err);
  * the state of a fresh NewHashgraph after InsertEvent of the same events
  * (Bootstrap replay, hashgraph.go:1008-1022). Used to repeat timed passes. */
 int32_t hgx_reset_consensus(hgx_ctx* ctx);
+/* Forget every event as well: the state of a fresh NewHashgraph (hashgraph.go:39-66) with
+ * the device allocations kept. */
+int32_t hgx_clear(hgx_ctx* ctx);
 
 /* ---- Hashgraph state (hashgraph.go:15-37) --------------------------------- */
 int64_t hgx_num_events(hgx_ctx* ctx);
@@ -125,6 +137,39 @@ int32_t hgx_consensus_events(hgx_ctx* ctx, int32_t graph, int64_t first, int64_t
 int64_t hgx_num_blocks(hgx_ctx* ctx, int32_t graph);
 int32_t hgx_block_info(hgx_ctx* ctx, int32_t graph, int64_t b, int32_t* round_received, int64_t* first,
                        int32_t* n_events, int64_t* n_tx, int32_t* tx_nil, int32_t* committed);
+/* Store.GetBlock(rr) (inmem_store.go:163-169): index b of the block with RoundReceived rr,
+ * else HGX_ERR_KEY_NOT_FOUND "<rr>, Not Found" */
+int32_t hgx_get_block(hgx_ctx* ctx, int32_t graph, int32_t round_received, int64_t* b, hgx_error* err);
+/* positions [first, first+count) of a graph's consensus order: gid, RoundReceived and
+ * consensusTimestamp (ns) of each, in one call (any output may be NULL) */
+int32_t hgx_consensus_received(hgx_ctx* ctx, int32_t graph, int64_t first, int64_t count, int64_t* gids,
+                               int32_t* round_received, int64_t* consensus_ts);
+
+/* ---- Store: events by participant (store.go:3-25, inmem_store.go:48-161) ---
+ * Participant ids are the context's creator ids (global ids in a batched context). The
+ * RollingIndex never evicts (cacheSize >= events). Errors carry Go's strings. */
+/* LastFrom: gid of the participant's last event; none: gid -1 and is_root 1 (Root.X = "") */
+int32_t hgx_last_from(hgx_ctx* ctx, int32_t participant, int64_t* gid, int32_t* is_root, hgx_error* err);
+/* ParticipantEvents(p, skip) (caches.go:54-72): the events with Index > skip, in Index
+ * order; *count = how many (gids gets the first min(count, cap)) */
+int32_t hgx_participant_events(hgx_ctx* ctx, int32_t participant, int64_t skip, int64_t* gids, int64_t cap,
+                               int64_t* count, hgx_error* err);
+/* ParticipantEvent(p, index) (caches.go:74-80): "<index>, Too Late" / "<index>, Not Found" */
+int32_t hgx_participant_event(hgx_ctx* ctx, int32_t participant, int64_t index, int64_t* gid, hgx_error* err);
+/* GetRoot (inmem_store.go:155-161): the genesis Root, X = Y = "" (-1), Index = Round = -1 */
+int32_t hgx_get_root(hgx_ctx* ctx, int32_t participant, int64_t* x, int64_t* y, int32_t* index, int32_t* round,
+                     hgx_error* err);
+/* GetEvent (inmem_store.go:48-55): the DAG fields of an inserted event (bodies stay with the caller) */
+int32_t hgx_get_event(hgx_ctx* ctx, int64_t gid, int32_t* creator, int64_t* index, int64_t* self_parent,
+                      int64_t* other_parent, int64_t* timestamp_ns, int32_t* ntx, int32_t* tx_nil, hgx_error* err);
+/* SetWireInfo (hashgraph.go:532-567) of events [first, first+count): self-parent Index
+ * (Root.Index -1 for a first event), other-parent creator id and Index (-1 for "") */
+int32_t hgx_wire_info(hgx_ctx* ctx, int64_t first, int64_t count, int32_t* self_parent_index,
+                      int32_t* other_parent_creator, int32_t* other_parent_index);
+/* ReadWireInfo (hashgraph.go:569-614): parents of a wire event as gids (-1 for an index < 0),
+ * through ParticipantEvent (its errors) */
+int32_t hgx_read_wire_info(hgx_ctx* ctx, int32_t creator, int64_t self_parent_index, int32_t other_parent_creator,
+                           int64_t other_parent_index, int64_t* self_parent, int64_t* other_parent, hgx_error* err);
 
 /* ---- per-event results (bulk) --------------------------------------------- */
 /* round (Round), witness (Witness), famous (RoundEvent.Famous: 0 Undefined,1 True,2 False) */
@@ -160,7 +205,10 @@ int32_t hgx_block_hash(int64_t round_received, int32_t ntx, const uint8_t* const
 int32_t hgx_sha256_batch(int32_t device, const uint8_t* data, const int64_t* offsets, int64_t count,
                          uint8_t* out32, hgx_error* err);
 /* The same on device-resident buffers, enqueued on `stream` (a hipStream_t; NULL = null
- * stream) without synchronising. d_out32 must be 4-byte aligned. */
+ * stream) without synchronising. d_out32 must be 4-byte aligned. Message bytes are read
+ * with 16-byte loads from the 16-byte-aligned span of each message: up to 15 bytes before
+ * d_data + offsets[i] and past d_data + offsets[i+1] may be read (harmless inside one
+ * allocation; the caller keeps that span mapped). */
 int32_t hgx_sha256_batch_device(const uint8_t* d_data, const int64_t* d_offsets, int64_t count,
                                 uint8_t* d_out32, void* stream);
 /* Measurement: `count` synthetic messages resident in HBM (message i has length
@@ -186,6 +234,12 @@ int32_t hgx_set_kernel_timing(hgx_ctx* ctx, int32_t mask);
 /* coordinate storage of later DivideRounds calls: 0 = auto (uint16 when every Index
  * <= 65533 and n is even, else int32), 1 = always int32. Same results either way. */
 int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
+/* DecideFame vote tally: 0 = witness-tiled popcount (default), 1 = per-round popcount
+ * kernel, 2 = witness-tiled int8 MFMA. Same results; for measurement. */
+int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
+/* Size the per-round device tables for `rounds` rounds (they grow on demand during
+ * DivideRounds); before the first DivideRounds only. A small value exercises the growth path. */
+int32_t hgx_reserve_rounds(hgx_ctx* ctx, int32_t rounds);
 
 /* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
 /* Seeded random gossip modelled on node/core_test.go:514-537: every active peer

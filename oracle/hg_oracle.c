@@ -658,3 +658,27 @@ int64_t hgo_block_tx(hgo* h, int64_t b, int32_t t, uint8_t* out, int64_t cap) {
     if (out) memcpy(out, h->txblob + h->tx_off.a[ti], (size_t)(l < cap ? l : cap));
     return l;
 }
+
+/* Core.Sync-style batch (node/core.go:199-211): hgo_insert for events 0..m-1 in order,
+ * stopping at the first rejected event. Payloads of event k are the next ntx[k] entries of
+ * tx_len, their bytes consecutive in tx_blob. Returns the number of events inserted; the
+ * error of the rejected event (if any) is in err / *rc. */
+int64_t hgo_insert_batch(hgo* h, int64_t m, const int32_t* creator, const int64_t* index, const int64_t* sp,
+                         const int64_t* op, const int64_t* ts, const uint8_t* hash, const uint8_t* S,
+                         const int32_t* ntx, const int32_t* tx_nil, const uint8_t* tx_blob, const int32_t* tx_len,
+                         int* rc, char* err, int errlen) {
+    int64_t tpos = 0, bpos = 0;
+    *rc = 0;
+    for (int64_t k = 0; k < m; k++) {
+        const int r = hgo_insert(h, creator[k], index[k], sp[k], op[k], ts[k], hash + 32 * k, S + 32 * k, ntx[k],
+                                 tx_nil[k], tx_blob ? tx_blob + bpos : NULL, tx_len ? tx_len + tpos : NULL, err,
+                                 errlen);
+        if (r) {
+            *rc = r;
+            return k;
+        }
+        for (int t = 0; t < ntx[k]; t++) bpos += tx_len[tpos + t];
+        tpos += ntx[k];
+    }
+    return m;
+}

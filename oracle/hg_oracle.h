@@ -36,6 +36,13 @@ int hgo_insert(hgo* h, int creator, int64_t index, int64_t self_parent, int64_t 
                int64_t ts_ns, const uint8_t* hash32, const uint8_t* s32, int ntx, int tx_nil,
                const uint8_t* tx_data, const int32_t* tx_len, char* err, int errlen);
 
+/* hgo_insert over a batch (structure of arrays), stopping at the first failure; payloads
+ * of event k: the next ntx[k] lengths of tx_len, bytes consecutive in tx_blob */
+int64_t hgo_insert_batch(hgo* h, int64_t m, const int32_t* creator, const int64_t* index, const int64_t* sp,
+                         const int64_t* op, const int64_t* ts, const uint8_t* hash, const uint8_t* S,
+                         const int32_t* ntx, const int32_t* tx_nil, const uint8_t* tx_blob, const int32_t* tx_len,
+                         int* rc, char* err, int errlen);
+
 int hgo_divide_rounds(hgo* h);                       /* hashgraph.go:616-646 */
 int hgo_decide_fame(hgo* h, char* err, int errlen);  /* hashgraph.go:649-730 */
 int hgo_decide_round_received(hgo* h, char* err, int errlen); /* :753-799 */

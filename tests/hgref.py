@@ -41,6 +41,8 @@ def oracle_lib():
     L.hgo_free.argtypes = [p]
     L.hgo_insert.restype = i32
     L.hgo_insert.argtypes = [p, i32, i64, i64, i64, i64, p, p, i32, i32, p, p, C.c_char_p, i32]
+    L.hgo_insert_batch.restype = i64
+    L.hgo_insert_batch.argtypes = [p, i64] + [p] * 11 + [C.POINTER(C.c_int), C.c_char_p, i32]
     for nm in ("hgo_divide_rounds",):
         getattr(L, nm).argtypes = [p]
         getattr(L, nm).restype = i32
@@ -282,12 +284,34 @@ class Oracle:
 
     def insert_trace(self, t: Trace, lo: int = 0, hi: Optional[int] = None):
         hi = t.E if hi is None else hi
+        if hasattr(t, "tx_seq"):   # generated gossip trace: one C call for the batch
+            return self.insert_gossip(t, lo, hi)
         for i in range(lo, hi):
             txs = t.txs(i) if callable(getattr(t, "txs", None)) else (None if t.txnil[i] else t.txs[i])
             rc, msg = self.insert(t.creator[i], t.index[i], t.sp[i], t.op[i], t.ts[i], t.hash[i].tobytes(),
                                   t.s[i].tobytes(), txs)
             if rc:
                 raise RuntimeError(f"oracle insert {i}: {msg}")
+
+    def insert_gossip(self, t, lo: int, hi: int):
+        """Batch insert of a generated trace (payloads rebuilt from tx_seq) via hgo_insert_batch."""
+        sl = slice(lo, hi)
+        cols = [np.ascontiguousarray(t.creator[sl], np.int32), np.ascontiguousarray(t.index[sl], np.int64),
+                np.ascontiguousarray(t.sp[sl], np.int64), np.ascontiguousarray(t.op[sl], np.int64),
+                np.ascontiguousarray(t.ts[sl], np.int64), np.ascontiguousarray(t.hash[sl], np.uint8),
+                np.ascontiguousarray(t.s[sl], np.uint8), np.ascontiguousarray(t.ntx[sl], np.int32),
+                np.ascontiguousarray(t.txnil[sl], np.int32)]
+        has = np.nonzero(cols[7] > 0)[0]
+        assert int(cols[7].max(initial=0)) <= 1, "generated traces carry at most one payload per event"
+        pls = [gossip_payload(int(cols[0][k]), int(t.tx_seq[lo + k])) for k in has]
+        blob = b"".join(pls)
+        lens = np.array([len(x) for x in pls] or [0], np.int32)
+        bb = C.create_string_buffer(blob, max(len(blob), 1))
+        err = C.create_string_buffer(256)
+        rc = C.c_int(0)
+        m = self.L.hgo_insert_batch(self.h, hi - lo, *[_ptr(c) for c in cols], bb, _ptr(lens), C.byref(rc), err, 256)
+        if rc.value:
+            raise RuntimeError(f"oracle insert {lo + m}: {err.value.decode(errors='replace')}")
 
     def divide_rounds(self):
         return self.L.hgo_divide_rounds(self.h)
@@ -391,6 +415,11 @@ class Oracle:
                     consensus_tx=int(L.hgo_consensus_transactions(h)),
                     pending_loaded=int(L.hgo_pending_loaded_events(h)),
                     blocks=[(b["rr"], b["ntx"], b["tx_nil"], b["committed"], b["hash"]) for b in self.blocks()])
+
+
+def gossip_payload(creator: int, seq: int) -> bytes:
+    """hgx_trace_tx_payload's bytes (include/hgx.h): "p%03d tx %08d"""
+    return b"p%03d tx %08d" % (creator, seq)
 
 
 def oracle_run(t: Trace, chunk: Optional[int] = None) -> Oracle:

@@ -17,10 +17,12 @@ def _hg(n, cap=1 << 14, graphs=1):
     return Hashgraph(n, capacity=cap, n_graphs=graphs)
 
 
-def run_gpu(t, chunk=None, cap=None, coord32=False):
+def run_gpu(t, chunk=None, cap=None, coord32=False, fame=None):
     h = _hg(t.n, cap or max(64, t.E))
     if coord32:
         h.set_coord_storage(1)
+    if fame:
+        h.set_fame_tally(fame)
     if chunk is None:
         h.insert_trace(t)
         h.RunConsensus()
@@ -257,33 +259,31 @@ FAME_CASES = [(4, 1024, 2, 0, 0.0), (7, 1500, 5, 2, 0.4), (16, 4000, 7, 5, 0.5),
 
 @pytest.mark.parametrize("mode", ["vote", "popc", "mfma"])
 @pytest.mark.parametrize("n,E,seed,silent,stale", FAME_CASES)
-def test_fame_kernels_agree_with_oracle(monkeypatch, mode, n, E, seed, silent, stale):
+def test_fame_kernels_agree_with_oracle(mode, n, E, seed, silent, stale):
     """Every DecideFame kernel (per-round popcount k_fame_vote, witness-tiled k_fame_tile with
-    the popcount or the int8 MFMA tally; HGX_FAME forces one) gives the oracle's fame, at every
-    n (small n reaches the coin rounds, (j-i) % n == 0)."""
-    monkeypatch.setenv("HGX_FAME", mode)
+    the popcount or the int8 MFMA tally; hgx_set_fame_tally picks one) gives the oracle's fame,
+    at every n (small n reaches the coin rounds, (j-i) % n == 0)."""
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
-    compare(run_gpu(t), hgref.oracle_run(t), t, hashes=False)
+    compare(run_gpu(t, fame=mode), hgref.oracle_run(t), t, hashes=False)
 
 
 @pytest.mark.parametrize("mode", ["vote", "popc", "mfma"])
 @pytest.mark.parametrize("name", ["funky_hashgraph", "consensus_hashgraph"])
-def test_fame_kernels_on_fixtures(monkeypatch, mode, name):
+def test_fame_kernels_on_fixtures(mode, name):
     """The reference fixtures (funky_hashgraph has a coin round, hashgraph_test.go:1407-1462)
     through each fame kernel."""
-    monkeypatch.setenv("HGX_FAME", mode)
     t = hgref.fixture_trace(name)
-    compare(run_gpu(t), hgref.oracle_run(t), t)
+    compare(run_gpu(t, fame=mode), hgref.oracle_run(t), t)
 
 
 @pytest.mark.parametrize("mode", ["popc", "mfma"])
-def test_fame_tile_batched_graphs(monkeypatch, mode):
+def test_fame_tile_batched_graphs(mode):
     """k_fame_tile's (graph, round, witness tile) block mapping over a batched context."""
-    monkeypatch.setenv("HGX_FAME", mode)
     G, n, Es = 3, 128, 12000
     traces = [gtrace.gossip(n, Es, 300 + g, n_silent=10 * g, stale_prob=0.15 * g, stale_depth=3) for g in range(G)]
     cat = gtrace.concat_graphs(traces)
     h = _hg(n, cap=cat.E, graphs=G)
+    h.set_fame_tally(mode)
     h.insert_trace(cat)
     h.RunConsensus()
     off = 0
