@@ -966,6 +966,39 @@ int32_t hgx_set_fame_tally(hgx_ctx* c, int32_t mode) {
     return HGX_OK;
 }
 
+// ---- device buffers for callers without their own allocator (bench, tests) ---------
+int32_t hgx_device_alloc(int32_t device, int64_t bytes, void** ptr) {
+    if (!ptr || bytes < 0) return HGX_ERR_INVALID;
+    *ptr = nullptr;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) return HGX_ERR_DEVICE;
+    const hipError_t e = hipMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1));
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    return e == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+int32_t hgx_device_free(int32_t device, void* ptr) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) return HGX_ERR_DEVICE;
+    const hipError_t e = ptr ? hipFree(ptr) : hipSuccess;
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    return e == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t bytes, int32_t to_device) {
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return HGX_ERR_INVALID;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) return HGX_ERR_DEVICE;
+    const hipError_t e = bytes ? hipMemcpy(dst, src, (size_t)bytes, to_device ? hipMemcpyHostToDevice
+                                                                               : hipMemcpyDeviceToHost)
+                               : hipSuccess;
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    return e == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
 int32_t hgx_reserve_rounds(hgx_ctx* c, int32_t rounds) {
     if (!c || rounds < 1 || c->divided) return HGX_ERR_INVALID;   // before the first DivideRounds only
     DeviceGuard dg(c);

@@ -367,31 +367,45 @@ class Hashgraph:
 
 
 class DeviceTrace:
-    """A trace's hgx_events columns resident in HBM (torch tensors on the context's device:
-    torch is only the allocator here). Feeds Hashgraph.insert_device."""
+    """A trace's hgx_events columns resident in HBM (buffers from hgx_device_alloc on the
+    context's device). Feeds Hashgraph.insert_device."""
 
     def __init__(self, t, device: int = 0):
-        import torch
-        dev = torch.device("cuda", device)
-
-        def up(a, dt):
-            return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
-
+        self.L = _lib.lib()
+        self.device = device
         self.E = int(t.creator.shape[0])
-        self.cols = dict(creator=up(t.creator, np.int32), index=up(t.index, np.int64), sp=up(t.sp, np.int64),
-                         op=up(t.op, np.int64), ts=up(t.ts, np.int64), hash=up(t.hash, np.uint8),
-                         s=up(t.s, np.uint8), ntx=up(t.ntx, np.int32), nil=up(t.txnil, np.int32))
-        torch.cuda.synchronize(dev)
+        self.bufs = {}
+        for name, src, dt in (("creator", t.creator, np.int32), ("index", t.index, np.int64),
+                              ("sp", t.sp, np.int64), ("op", t.op, np.int64), ("ts", t.ts, np.int64),
+                              ("hash", t.hash, np.uint8), ("s", t.s, np.uint8), ("ntx", t.ntx, np.int32),
+                              ("nil", t.txnil, np.int32)):
+            a = np.ascontiguousarray(src, dtype=dt)
+            p = C.c_void_p()
+            if self.L.hgx_device_alloc(device, a.nbytes, C.byref(p)) != 0:
+                self.close()
+                raise HgxError(200, "hgx_device_alloc failed")
+            self.bufs[name] = (p, a.itemsize * (32 if name in ("hash", "s") else 1))
+            if a.nbytes and self.L.hgx_device_copy(device, p, ptr(a), a.nbytes, 1) != 0:
+                self.close()
+                raise HgxError(200, "hgx_device_copy failed")
+
+    def close(self):
+        for p, _ in getattr(self, "bufs", {}).values():
+            self.L.hgx_device_free(self.device, p)
+        self.bufs = {}
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def events(self, lo: int, hi: int) -> hgx_events:
-        c = self.cols
+        def p(name):
+            base, per = self.bufs[name]
+            return C.c_void_p((base.value or 0) + lo * per)
 
-        def p(name, per=1):
-            t = c[name]
-            return C.c_void_p(t.data_ptr() + lo * per * t.element_size())
-
-        return hgx_events(p("creator"), p("index"), p("sp"), p("op"), p("ts"), p("hash", 32), p("s", 32), p("ntx"),
-                          p("nil"))
+        return hgx_events(p("creator"), p("index"), p("sp"), p("op"), p("ts"), p("hash"), p("s"), p("ntx"), p("nil"))
 
 
 def block_hash(rr: int, txs: List[bytes], tx_nil: bool) -> bytes:

@@ -241,6 +241,12 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
  * DivideRounds); before the first DivideRounds only. A small value exercises the growth path. */
 int32_t hgx_reserve_rounds(hgx_ctx* ctx, int32_t rounds);
 
+/* ---- device buffers (for callers without a device allocator: bench, tests) ---- */
+int32_t hgx_device_alloc(int32_t device, int64_t bytes, void** ptr);
+int32_t hgx_device_free(int32_t device, void* ptr);
+/* synchronous copy; to_device 1: host src -> device dst, 0: device src -> host dst */
+int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t bytes, int32_t to_device);
+
 /* ---- synthetic gossip traces (BASELINE.md / SURVEY 8d generator) ---------- */
 /* Seeded random gossip modelled on node/core_test.go:514-537: every active peer
  * emits a genesis event, then each step a uniformly chosen `to` emits
