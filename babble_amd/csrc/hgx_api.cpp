@@ -999,6 +999,12 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
     return e == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
 }
 
+int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
+    c->eng.round_kernel = mode;
+    return HGX_OK;
+}
+
 int32_t hgx_reserve_rounds(hgx_ctx* c, int32_t rounds) {
     if (!c || rounds < 1 || c->divided) return HGX_ERR_INVALID;   // before the first DivideRounds only
     DeviceGuard dg(c);

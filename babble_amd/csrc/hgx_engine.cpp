@@ -153,6 +153,7 @@ hipError_t Engine::ensure_round_cap(int32_t need) {
     drop_step_graph();
     HGX_TRY(wcoin.grow_copy((size_t)nc * Cz, (size_t)old * Cz, stream));
     HGX_TRY(active.grow_copy((size_t)nc + 1, (size_t)old + 1, stream));
+    HGX_TRY(ovf.grow_copy((size_t)nc + 2, (size_t)old + 2, stream));
     HGX_TRY(Tthr.grow_copy((size_t)nc * Cz, 0, stream));
     HGX_TRY(fw.grow_copy((size_t)nc * Cz, 0, stream));
     HGX_TRY(elig.grow_copy((size_t)nc * G, 0, stream));
@@ -166,7 +167,10 @@ hipError_t Engine::ensure_round_cap(int32_t need) {
     HGX_TRY(blk_loaded.grow_copy((size_t)nc * G, 0, stream));
     HGX_TRY(blk_ntx.grow_copy((size_t)nc * G, 0, stream));
     HGX_TRY(blk_nil.grow_copy((size_t)nc * G, 0, stream));
-    if (old < nc) HGX_TRY(hipMemsetAsync(active.p + old + 1, 0, (size_t)(nc - old) * sizeof(int32_t), stream));
+    if (old < nc) {
+        HGX_TRY(hipMemsetAsync(active.p + old + 1, 0, (size_t)(nc - old) * sizeof(int32_t), stream));
+        HGX_TRY(hipMemsetAsync(ovf.p + old + 2, 0, (size_t)(nc - old) * sizeof(int32_t), stream));
+    }
     r_cap = nc;
     return hipSuccess;
 }
@@ -345,6 +349,7 @@ hipError_t Engine::reserve_rounds(int32_t rounds) {
     Bm.release(); WLA.release(); WFD.release(); wflag.release(); wstat.release(); wcoin.release();
     active.release(); Tthr.release(); fw.release(); elig.release(); ur_empty.release(); Smat.release();
     Vbuf.release(); fame.release(); blk_cnt.release(); blk_loaded.release(); blk_ntx.release(); blk_nil.release();
+    ovf.release();
     WLAT.release();
     r_cap = 0;
     R = 0;
@@ -421,8 +426,26 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipMemsetAsync(lr.p, 0xFF, (size_t)G * 4, stream));
     HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
     HGX_TRY(hipMemsetAsync(active.p, 0, (size_t)(r_cap + 1) * 4, stream));
+    HGX_TRY(hipMemsetAsync(ovf.p, 0, (size_t)(r_cap + 2) * 4, stream));
+    {
+        const size_t need = (size_t)2 * C * round_k_ndw(n);
+        if (FD8.n < need) {
+            HGX_TRY(FD8.alloc(need));
+            drop_step_graph();
+        }
+    }
+    auto round_args = [&]() {
+        RoundArgs A{};
+        A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld;
+        A.c_len = c_len.p; A.c_off = c_off.p; A.c_base = c_base.p; A.LA = LA.p; A.FDT = FDT.p; A.compact = compact;
+        A.p_gid = p_gid.p; A.g_coin = g_coin.p; A.FD8 = FD8.p; A.ovf = ovf.p;
+        A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
+        A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
+        return A;
+    };
     kbeg(K_ROUND_GATHER);
     launch_round_gather(stream, a, 0, C, n, fd_ld);   // W'_0 = first event of every chain
+    launch_round_k_gather(stream, round_args());       // ... rebased for the per-candidate step
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int launched = 0, checked = 0;
     {   // n <= 1024 (hgx_create's limit)
@@ -436,15 +459,13 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 HGX_TRY(ensure_round_cap(need));
                 a = arrays();
             }
-            if (!step_exec) {
-                RoundArgs& A = step_args;
-                A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld;
-                A.c_len = c_len.p; A.c_off = c_off.p; A.LA = LA.p; A.FDT = FDT.p; A.compact = compact; A.p_gid = p_gid.p;
-                A.g_coin = g_coin.p;
-                A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
-                A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
+            if (!step_exec || step_kernel_captured != round_kernel || step_compact != compact) {
+                drop_step_graph();
+                step_args = round_args();
+                step_kernel_captured = round_kernel;
+                step_compact = compact;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                for (int k = 0; k < kStepBatch; k++) (void)launch_round_step(stream, A, k);
+                for (int k = 0; k < kStepBatch; k++) (void)launch_round_step(stream, step_args, k, round_kernel);
                 HGX_TRY(hipStreamEndCapture(stream, &step_graph));
                 HGX_TRY(hipGraphInstantiate(&step_exec, step_graph, nullptr, nullptr, 0));
                 // the step nodes in launch order (a linear chain)

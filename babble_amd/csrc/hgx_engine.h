@@ -111,6 +111,7 @@ class Engine {
     KernelStat kstat[K_NUM];
     uint32_t time_mask = 0;   // kernels (bit = KernelId) timed with HIP events
     int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
+    int round_kernel = 0;     // 0 per-candidate step (hgx_round_k.hip), 1 block-search step (hgx_set_round_kernel)
     int dev = 0;
 
    private:
@@ -155,10 +156,13 @@ class Engine {
     std::vector<hipGraphNode_t> step_nodes;      // the kStepBatch step nodes, in order
     std::vector<hipKernelNodeParams> step_params;
     RoundArgs step_args{};
+    int step_kernel_captured = -1, step_compact = -1;   // what the captured step graph was built for
     int32_t step_round[64] = {};
     void drop_step_graph();
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
+    DBuf<uint32_t> FD8;   // [2][C][ndw] rebased candidate rows (k_round_k)
+    DBuf<int32_t> ovf;    // [r_cap + 2]
     DBuf<int8_t> fame;
     // order
     DBuf<int32_t> recv_list, counters, order_gid, blk_cnt, blk_loaded;

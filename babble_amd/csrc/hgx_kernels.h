@@ -81,7 +81,9 @@ enum InsertCode {
 struct RoundArgs {
     int n, C, sm, nw;
     int64_t Pcap;
-    const int32_t *c_len, *c_off, *p_gid;
+    const int32_t *c_len, *c_off, *c_base, *p_gid;
+    uint32_t* FD8;    // [2][C][ndw] candidate firstDescendants rebased to 8 bits (k_round_k, by round parity)
+    int32_t* ovf;     // [rounds + 2] round r's candidate rows do not fit 8 bits: exact compares
     const void *LA, *FDT;   // int32_t or uint16_t (compact)
     int compact;
     const uint8_t* g_coin;
@@ -100,8 +102,12 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
 void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
-// one round step (hgx_rounds.hip) of round r
-hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r);
+// one round step of round r: the per-candidate kernel (hgx_round_k.hip, n <= 256) unless
+// `block_search` or n > 256 (hgx_rounds.hip)
+hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r, int block_search);
+hipError_t launch_round_k(hipStream_t s, const RoundArgs& A, int r);
+void launch_round_k_gather(hipStream_t s, const RoundArgs& A);   // round 0's rebased rows + ovf[0]
+int round_k_ndw(int n);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();   // -DHGX_STEP_PROF builds only

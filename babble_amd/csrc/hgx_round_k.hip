@@ -1,0 +1,427 @@
+// Round step with one lane per candidate (RoundInc, hashgraph.go:285-305; StronglySee
+// hashgraph.go:170-198). DESIGN.md §3.3.
+//
+// Step s finds, for chain c, the boundary Bm[s+1][c] = first offset k >= Bm[s][c] whose
+// event strongly sees >= SM candidates w of W'_s (the first event of each chain with round
+// >= s; its own candidate does not count at the probe that is itself). Strongly seeing w is
+// monotone along the chain (lastAncestors only grow), so every candidate has a first
+// strongly-seeing probe K(w) in a window of P probe rows, and the boundary is the SM-th
+// smallest K(w): each lane binary-searches its own candidate's K(w), an LDS histogram of
+// the K(w) gives the boundary. No barrier per search level, and the per-(probe, candidate)
+// count never leaves the lane.
+//
+// The count #{i : LA[x][i] >= FD[w][i]} runs on 8-bit SWAR: every coordinate is rebased
+// per round to base_i = Index of the candidate of round s-1 on chain i (c_base + Bm[s-1][i]).
+// A candidate of round s has FD[w][i] >= base_i (its descendants have round >= s, so they sit
+// at or after Bm[s][i] >= Bm[s-1][i]), so FD' = FD - base + 1 is in [1, 126] when the
+// candidate's first descendants are within 125 events of base (127 = none), and the probe
+// values are LA' = clamp(LA - base + 1, 0, 126) with the byte's top bit set: per byte,
+// (0x80 | LA') - FD' never borrows and its bit 7 is [LA' >= FD'] = [LA >= FD]. One v_sub,
+// one v_and, one v_bcnt per 4 coordinates. The producer of a candidate row (the step that
+// found it) writes it rebased and flags the round if a value does not fit; a flagged round
+// runs the exact int32 compare instead (same search, slower).
+//
+// The step also writes what the next step needs: the new candidate's rows (WLA, raw WFD,
+// rebased FD8) and its strongly-seen bitmask, DecideFame's S row (hashgraph.go:688-705).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hgx_device.h"
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+constexpr int kWinP = 31;   // probes per window: K in [0, 31], 5 binary-search levels
+
+// window row stride in dwords: even (8-byte reads) and == 2 mod 4, so that 32 lanes reading
+// 32 different rows at the same column hit 32 distinct bank pairs (MI355X_MICROARCH.md, LDS)
+__host__ __device__ constexpr int win_stride(int ndw) { return (ndw % 4 == 0) ? ndw + 2 : ndw + 4; }
+
+struct RoundKLds {
+    int win, raw, fdc, base, bm1, hist, total;
+};
+
+// one chain group's LDS: rebased byte window | raw LA rows | FD columns (stg) | bases | histogram
+__host__ __device__ inline RoundKLds round_k_lds(int n, int ndw, int csz, bool stg) {
+    RoundKLds L{};
+    int o = 0;
+    L.win = o;
+    o += kWinP * win_stride(ndw) * 4;
+    L.raw = o;
+    if (stg) o += ((kWinP * n * csz + 15) / 16) * 16;
+    L.fdc = o;
+    if (stg) o += (csz == 2) ? n * (kWinP / 2 + 1) * 4 : n * kWinP * 4;
+    L.base = o;
+    o += n * 4;
+    L.bm1 = o;
+    o += n * 4;
+    L.hist = o;
+    o += 32 * 4;
+    L.total = (o + 15) & ~15;
+    return L;
+}
+
+template <typename CT, int NDW, int GW, bool STG>
+__global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
+    constexpr int P = kWinP;
+    constexpr int GL = 64 * GW;          // lanes of one chain group (one candidate each)
+    constexpr int GPB = 4 / GW;          // chain groups per 256-thread block
+    constexpr int WS = win_stride(NDW);
+    constexpr int FDW = P / 2 + 1;       // dwords per compact FD column (32 positions from an even start)
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ int s_B[GPB], s_tot[GPB];
+
+    const int n = A.n, C = A.C, sm = A.sm;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = wave / GW, wg = wave % GW, gt = wg * 64 + lane;
+    const int gc = blockIdx.x * GPB + grp;
+    if (gc >= C) return;   // group-uniform; block barriers are only used when GPB == 1
+    const RoundKLds L = round_k_lds(n, NDW, (int)sizeof(CT), STG);
+    uint8_t* gl = lds + (size_t)grp * L.total;
+    uint32_t* win = (uint32_t*)(gl + L.win);
+    CT* raw = (CT*)(gl + L.raw);
+    CT* fdc = (CT*)(gl + L.fdc);
+    int32_t* base = (int32_t*)(gl + L.base);
+    int32_t* bm1 = (int32_t*)(gl + L.bm1);
+    int32_t* hist = (int32_t*)(gl + L.hist);
+    auto gsync = [&]() {
+        if (GW == 1) wave_lds_fence();
+        else __syncthreads();
+    };
+
+    const int g = gc / n, cl = gc % n;
+    const int len = A.c_len[gc], off = A.c_off[gc];
+    const int b = A.Bm[(size_t)s * C + gc];
+    if (b >= len) {
+        if (gt == 0) {
+            A.wstat[(size_t)s * C + gc] = 0;
+            A.wflag[(size_t)(s + 1) * C + gc] = 0;
+            A.Bm[(size_t)(s + 1) * C + gc] = len;
+        }
+        return;
+    }
+    const int par = s & 1;
+    const bool exact = A.ovf[s] != 0;   // a candidate row of this round did not fit 8 bits
+    const size_t wrow = (size_t)s * C + (size_t)g * n;
+    for (int i = gt; i < n; i += GL) {
+        const int cb = A.c_base[g * n + i];
+        base[i] = cb + (s > 0 ? A.Bm[wrow - C + i] : 0);   // base(s): Index of round s-1's candidate
+        bm1[i] = cb + A.Bm[wrow + i];                      // base(s+1)
+    }
+    if (gt < 32) hist[gt] = 0;
+
+    // the window: raw LA rows [kbase, kbase+np) (contiguous) and, when staged, the window's
+    // FD columns (the new candidate's FD row comes from there), by LDS-DMA
+    int fsh = 0;
+    auto stage = [&](int kbase, int np) {
+        if constexpr (STG) {
+            const int nel = (int)((size_t)np * n * sizeof(CT) / 4);
+            const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
+            uint32_t* raw_w = (uint32_t*)raw;
+            if (((n * (int)sizeof(CT)) & 15) == 0) {
+                for (int c0 = wg * 256; c0 < nel; c0 += GW * 256) {
+                    const int t = c0 + lane * 4;
+                    if (t < nel)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 16, 0, 0);
+                }
+            } else {
+                for (int c0 = wg * 64; c0 < nel; c0 += GW * 64) {
+                    const int t = c0 + lane;
+                    if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 4, 0, 0);
+                }
+            }
+            if constexpr (sizeof(CT) == 4) {
+                // column i: positions [kbase, kbase+np), one lane per (column, position)
+                constexpr int CPI = 64 / 32;   // columns per wave instruction (32 lanes each)
+                const int pcol = lane % 32, icol = lane / 32;
+                const CT* __restrict__ fsrc = (const CT*)A.FDT + off + kbase + pcol;
+                for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
+                    const int i = i0 + icol;
+                    if (i < n && pcol < np)
+                        __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * A.Pcap),
+                                                         (lds_ptr_t)(fdc + (size_t)i0 * P), 4, 0, 0);
+                }
+            } else {
+                // column i: FDW dwords covering positions [p0, p0 + 2*FDW), p0 = even start
+                constexpr int CPI = 64 / FDW;
+                const int64_t p0 = (off + kbase) & ~1;
+                fsh = (off + kbase) & 1;
+                const int pcol = lane % FDW, icol = lane / FDW;
+                const uint32_t* __restrict__ fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
+                uint32_t* fd_w = (uint32_t*)fdc;
+                for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
+                    const int i = i0 + icol;
+                    if (i < n && icol < CPI)
+                        __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * (A.Pcap / 2)),
+                                                         (lds_ptr_t)(fd_w + (size_t)i0 * FDW), 4, 0, 0);
+                }
+            }
+        }
+    };
+    auto la_at = [&](int kbase, int p, int i) -> int32_t {   // decoded lastAncestors of window row p
+        if constexpr (STG) return Coord<CT>::la(raw[p * n + i]);
+        else return Coord<CT>::la(((const CT*)A.LA)[(size_t)(off + kbase + p) * n + i]);
+    };
+    // rebased byte window: (0x80 | LA') per coordinate, padding coordinates LA' = 0
+    auto convert = [&](int kbase, int np) {
+        for (int t = gt; t < np * NDW; t += GL) {
+            const int p = t / NDW, d = t % NDW;
+            uint32_t w = 0x80808080u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = 4 * d + q;
+                if (i < n) {
+                    const int32_t x = la_at(kbase, p, i) - base[i] + 1;
+                    w |= (uint32_t)min(max(x, 0), 126) << (8 * q);
+                }
+            }
+            win[p * WS + d] = w;
+        }
+    };
+
+    constexpr int CH = 1;   // candidates per lane (n <= GL); see k_round_k_chunked for n > 256
+    uint32_t fd[NDW];
+    const int j = gt;
+    bool cand = false;
+    {   // this lane's candidate row: rebased FD bytes (written by the step that found it)
+        cand = j < n && A.wflag[wrow + j] == 1;
+        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + (j < n ? j : 0)) * NDW;
+        if constexpr (NDW % 4 == 0) {
+#pragma unroll
+            for (int d = 0; d < NDW; d += 4) {
+                const uint4 v = *(const uint4*)(row + d);
+                fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < NDW; d += 2) {
+                const uint2 v = *(const uint2*)(row + d);
+                fd[d] = v.x; fd[d + 1] = v.y;
+            }
+        }
+    }
+    int kbase = b, np = min(P, len - b), kstar = len, carried = 0, B = -1, K = P;
+    bool done = false;   // seen in an earlier window: seen at every later probe
+    for (;;) {
+        stage(kbase, np);
+        __builtin_amdgcn_s_waitcnt(0);
+        gsync();
+        convert(kbase, np);
+        gsync();
+        // first probe of the window that strongly sees this lane's candidate (np: none);
+        // probes past the window's end count as seeing (keeps the predicate monotone)
+        int lo = 0, hi = P;
+        if (!exact) {
+            uint32_t f[NDW];
+#pragma unroll
+            for (int d = 0; d < NDW; d++) f[d] = cand ? fd[d] : 0x7F7F7F7Fu;
+#pragma unroll
+            for (int it = 0; it < 5; it++) {
+                const int mid = (lo + hi) >> 1;
+                const uint32_t* row = win + mid * WS;
+                uint32_t cnt = 0;
+#pragma unroll
+                for (int d = 0; d < NDW; d += 2) {
+                    const uint2 v = *(const uint2*)(row + d);
+                    cnt += __builtin_popcount((v.x - f[d]) & 0x80808080u);
+                    cnt += __builtin_popcount((v.y - f[d + 1]) & 0x80808080u);
+                }
+                const bool seen = done || mid >= np || ((int)cnt >= sm && !(j == cl && kbase + mid == b));
+                if (seen) hi = mid; else lo = mid + 1;
+            }
+        } else {
+            // exact int32 compares against the raw candidate row (rounds flagged by the producer)
+            const int jj = j < n ? j : 0;
+            for (int it = 0; it < 5; it++) {
+                const int mid = (lo + hi) >> 1;
+                int cnt = 0;
+                if (cand && !done && mid < np) {
+                    for (int i = 0; i < n; i++) {
+                        const int32_t fdv = (sizeof(CT) == 2)
+                                                ? Coord<uint16_t>::fd(((const uint16_t*)A.WFD)[(wrow + jj) * n + i])
+                                                : A.WFD[(wrow + jj) * n + i];
+                        const int32_t lav = min(la_at(kbase, mid, i), kMaxI32 - 1);
+                        cnt += lav >= fdv ? 1 : 0;
+                    }
+                }
+                const bool seen = done || mid >= np || (cand && cnt >= sm && !(j == cl && kbase + mid == b));
+                if (seen) hi = mid; else lo = mid + 1;
+            }
+        }
+        K = lo;
+        if (K < np && cand) atomicAdd(&hist[K], 1);
+        gsync();
+        if (wg == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
+            const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
+            const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
+            const uint64_t m = __ballot(lane < np && (int)inc >= sm);
+            const int tot = __builtin_amdgcn_readlane((int)inc, 63);
+            if (lane == 0) {
+                s_B[grp] = m ? (int)__builtin_ctzll(m) : -1;
+                s_tot[grp] = tot;
+            }
+        }
+        gsync();
+        B = s_B[grp];
+        if (B >= 0) {
+            kstar = kbase + B;
+            break;
+        }
+        carried = s_tot[grp];
+        done = done || (cand && K < np);
+        if (gt < 32) hist[gt] = 0;
+        kbase += np;
+        if (kbase >= len) {
+            kstar = len;
+            break;
+        }
+        np = min(P, len - kbase);
+        gsync();
+    }
+    (void)CH;
+
+    // outputs of round s for this chain
+    for (int k = b + gt; k < kstar; k += GL) A.p_round[off + k] = s;
+    if (gt == 0) {
+        A.wstat[(size_t)s * C + gc] = (kstar > b) ? 2 : 1;
+        if (kstar < len) A.active[s] = 1;   // same value from every writer: a plain store
+        A.Bm[(size_t)(s + 1) * C + gc] = kstar;
+    }
+    if (kstar < len) {
+        const int pk = kstar - kbase;   // inside the staged window
+        // S row of the boundary event: the candidates it strongly sees (bit j of word j/64)
+        const uint64_t bits = __ballot(cand && K <= B);
+        const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
+        if (lane == 0 && wg < A.nw) A.Smat[srow + wg] = bits;
+        // the new candidate's rows for round s+1
+        const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
+        auto fd_raw = [&](int i) -> CT {
+            if constexpr (STG) {
+                if constexpr (sizeof(CT) == 2) return fdc[i * 2 * FDW + fsh + pk];
+                else return fdc[i * P + pk];
+            } else {
+                return ((const CT*)A.FDT)[(size_t)i * A.Pcap + off + kstar];
+            }
+        };
+        for (int i = gt; i < n; i += GL) {
+            A.WLA[nrow + i] = la_at(kbase, pk, i);
+            const CT f = fd_raw(i);
+            if constexpr (sizeof(CT) == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
+            else A.WFD[nrow + i] = f;
+        }
+        // rebased FD row (base(s+1) = Index of this round's candidates) for the next step
+        uint32_t* nfd = A.FD8 + ((size_t)(par ^ 1) * C + gc) * NDW;
+        bool of = false;
+        for (int d = gt; d < NDW; d += GL) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int i = 4 * d + q;
+                uint32_t v = 127u;
+                if (i < n) {
+                    const int32_t f = Coord<CT>::fd(fd_raw(i));
+                    if (f != kMaxI32) {
+                        const int32_t x = f - bm1[i] + 1;
+                        if (x > 126) of = true;
+                        else v = (uint32_t)x;
+                    }
+                }
+                w |= v << (8 * q);
+            }
+            nfd[d] = w;
+        }
+        if (of) A.ovf[s + 1] = 1;   // same value from every writer
+        if (gt == 0) A.wflag[(size_t)(s + 1) * C + gc] = 1;
+    } else if (gt == 0) {
+        A.wflag[(size_t)(s + 1) * C + gc] = 0;
+    }
+}
+
+// round 0's candidate rows (the first event of every chain), rebased to base(0) = c_base
+template <typename CT>
+__global__ void k_round_k_gather(RoundArgs A, int ndw) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)A.C * ndw) return;
+    const int gc = (int)(t / ndw), d = (int)(t % ndw);
+    const int n = A.n, g = gc / n;
+    uint32_t w = 0;
+    bool of = false;
+    const bool have = A.c_len[gc] > 0;
+    for (int q = 0; q < 4; q++) {
+        const int i = 4 * d + q;
+        uint32_t v = 127u;
+        if (have && i < n) {
+            const int32_t f = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + A.c_off[gc]]);
+            if (f != kMaxI32) {
+                const int32_t x = f - A.c_base[g * n + i] + 1;
+                if (x > 126) of = true;
+                else v = (uint32_t)x;
+            }
+        }
+        w |= v << (8 * q);
+    }
+    A.FD8[(size_t)gc * ndw + d] = w;
+    if (of) A.ovf[0] = 1;
+}
+
+int round_k_ndw(int n) {
+    int d = (n + 3) / 4;
+    int p = 2;
+    while (p < d) p *= 2;
+    return p;
+}
+
+template <typename CT, int NDW, int GW, bool STG>
+static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
+    const void* f = (const void*)k_round_k<CT, NDW, GW, STG>;
+    const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), STG);
+    constexpr int GPB = 4 / GW;
+    const size_t lds = (size_t)L.total * GPB;
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
+    hipLaunchKernelGGL((k_round_k<CT, NDW, GW, STG>), dim3(grid), dim3(256), lds, st, A, s);
+    return hipGetLastError();
+}
+
+template <typename CT, int NDW, int GW>
+static hipError_t round_k_launch(hipStream_t st, const RoundArgs& A, int s) {
+    const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), true);
+    if ((size_t)L.total * (4 / GW) <= 150 * 1024) return round_k_launch_v<CT, NDW, GW, true>(st, A, s);
+    return round_k_launch_v<CT, NDW, GW, false>(st, A, s);
+}
+
+template <typename CT>
+static hipError_t launch_round_k_t(hipStream_t st, const RoundArgs& A, int s) {
+    switch (round_k_ndw(A.n)) {
+        case 2: return round_k_launch<CT, 2, 1>(st, A, s);
+        case 4: return round_k_launch<CT, 4, 1>(st, A, s);
+        case 8: return round_k_launch<CT, 8, 1>(st, A, s);
+        case 16: return round_k_launch<CT, 16, 1>(st, A, s);
+        case 32: return round_k_launch<CT, 32, 4>(st, A, s);
+        case 64: return round_k_launch<CT, 64, 4>(st, A, s);
+        default: return hipErrorInvalidValue;   // n > 256: k_round_step_big
+    }
+}
+
+hipError_t launch_round_k(hipStream_t st, const RoundArgs& A, int s) {
+    return A.compact ? launch_round_k_t<uint16_t>(st, A, s) : launch_round_k_t<int32_t>(st, A, s);
+}
+
+void launch_round_k_gather(hipStream_t st, const RoundArgs& A) {
+    const int ndw = round_k_ndw(A.n);
+    const int64_t work = (int64_t)A.C * ndw;
+    if (work <= 0) return;
+    if (A.compact)
+        hipLaunchKernelGGL(k_round_k_gather<uint16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw);
+    else
+        hipLaunchKernelGGL(k_round_k_gather<int32_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw);
+}
+
+}  // namespace hgx

@@ -329,6 +329,12 @@ class Hashgraph:
         if self.L.hgx_set_fame_tally(self.ctx, m) != 0:
             raise ValueError(f"invalid fame tally {mode}")
 
+    def set_round_kernel(self, mode):
+        """DivideRounds step (n <= 256): "candidate" (default) or "block" (block binary search)."""
+        m = {"candidate": 0, "block": 1}[mode] if isinstance(mode, str) else int(mode)
+        if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
+            raise ValueError(f"invalid round kernel {mode}")
+
     def reserve_rounds(self, rounds: int):
         """Size the per-round tables (before the first DivideRounds; small values exercise growth)."""
         if self.L.hgx_reserve_rounds(self.ctx, int(rounds)) != 0:

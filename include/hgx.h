@@ -237,6 +237,9 @@ int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
 /* DecideFame vote tally: 0 = witness-tiled popcount (default), 1 = per-round popcount
  * kernel, 2 = witness-tiled int8 MFMA. Same results; for measurement. */
 int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
+/* DivideRounds round step for n <= 256: 0 = one lane per candidate, 8-bit rebased compares
+ * (default, hgx_round_k.hip), 1 = block binary search (hgx_rounds.hip). Same results. */
+int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
 /* Size the per-round device tables for `rounds` rounds (they grow on demand during
  * DivideRounds); before the first DivideRounds only. A small value exercises the growth path. */
 int32_t hgx_reserve_rounds(hgx_ctx* ctx, int32_t rounds);

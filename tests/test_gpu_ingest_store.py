@@ -187,7 +187,7 @@ def test_round_table_growth_keeps_rows(n, E, seed):
     h.insert_trace(t)
     h.RunConsensus()
     a, b = h.results(), hgref.oracle_run(t).results()
-    assert b["last_round"] > 40
+    assert b["last_round"] > 20
     for k in ("round", "witness", "famous", "rr", "cts"):
         assert np.array_equal(a[k], b[k]), k
     assert list(a["order"]) == list(b["order"])

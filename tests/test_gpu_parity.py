@@ -17,10 +17,12 @@ def _hg(n, cap=1 << 14, graphs=1):
     return Hashgraph(n, capacity=cap, n_graphs=graphs)
 
 
-def run_gpu(t, chunk=None, cap=None, coord32=False, fame=None):
+def run_gpu(t, chunk=None, cap=None, coord32=False, fame=None, round_kernel=None):
     h = _hg(t.n, cap or max(64, t.E))
     if coord32:
         h.set_coord_storage(1)
+    if round_kernel:
+        h.set_round_kernel(round_kernel)
     if fame:
         h.set_fame_tally(fame)
     if chunk is None:
@@ -114,6 +116,14 @@ GOSSIP = [
 def test_gossip_batch(n, E, seed, silent, stale):
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
     compare(run_gpu(t), hgref.oracle_run(t), t, hashes=(E <= 6000))
+
+
+@pytest.mark.parametrize("n,E,seed,silent,stale", [(4, 1024, 1, 0, 0.0), (7, 1500, 5, 2, 0.4), (64, 12000, 10, 21, 0.2),
+                                                   (128, 20000, 12, 0, 0.0), (256, 30000, 16, 0, 0.0)])
+def test_gossip_block_search_round_kernel(n, E, seed, silent, stale):
+    """The block binary-search round step (hgx_set_round_kernel(ctx, 1)) against the oracle."""
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
+    compare(run_gpu(t, round_kernel="block"), hgref.oracle_run(t), t, hashes=False)
 
 
 def _expect_compact(t):
