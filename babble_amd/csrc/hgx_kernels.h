@@ -110,7 +110,8 @@ void launch_round_k_gather(hipStream_t s, const RoundArgs& A);   // round 0's re
 int round_k_ndw(int n);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
-void step_prof_dump();   // -DHGX_STEP_PROF builds only
+void step_prof_dump();     // -DHGX_STEP_PROF builds only
+void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
 void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G, int tally);
 void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);

@@ -26,11 +26,46 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
 
 namespace hgx {
+
+// Optional phase clocks (-DHGX_STEP_PROF, build variant "prof"): thread 0 of each block adds
+// s_memtime deltas per phase to hgx_rk_prof[] once, at the end of the step.
+#ifdef HGX_STEP_PROF
+__device__ unsigned long long hgx_rk_prof[8];
+#define RK_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define RK_PROF(i)                                                \
+    do {                                                          \
+        if (threadIdx.x == 0) {                                   \
+            const long long _t = clock64();                       \
+            _pa[i] += (unsigned long long)(_t - _pt);             \
+            _pt = _t;                                             \
+        }                                                         \
+    } while (0)
+#define RK_PROF_END()                                                              \
+    do {                                                                           \
+        if (threadIdx.x == 0) {                                                    \
+            _pa[7] += 1;                                                           \
+            for (int _i = 0; _i < 8; _i++)                                         \
+                if (_pa[_i]) atomicAdd(&hgx_rk_prof[_i], _pa[_i]);                 \
+        }                                                                          \
+    } while (0)
+void round_k_prof_dump() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rk_prof), sizeof(h)) != hipSuccess) return;
+    fprintf(stderr, "[hgx] k_round_k phases (clk sums): head %llu window %llu convert %llu search %llu boundary %llu "
+            "outputs %llu | block-steps %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[7]);
+}
+#else
+#define RK_PROF_BEGIN() (void)0
+#define RK_PROF(i) (void)0
+#define RK_PROF_END() (void)0
+void round_k_prof_dump() {}
+#endif
 
 constexpr int kWinP = 31;   // probes per window: K in [0, 31], 5 binary-search levels
 
@@ -51,7 +86,10 @@ __host__ __device__ inline RoundKLds round_k_lds(int n, int ndw, int csz, bool s
     L.raw = o;
     if (stg) o += ((kWinP * n * csz + 15) / 16) * 16;
     L.fdc = o;
-    if (stg) o += (csz == 2) ? n * (kWinP / 2 + 1) * 4 : n * kWinP * 4;
+    if (stg) {   // FD columns in groups of one LDS-DMA instruction (64 dwords) + 1 pad dword
+        const int cpi = (csz == 2) ? 4 : 2;
+        o += ((n + cpi - 1) / cpi) * 65 * 4;
+    }
     L.base = o;
     o += n * 4;
     L.bm1 = o;
@@ -69,6 +107,8 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     constexpr int GPB = 4 / GW;          // chain groups per 256-thread block
     constexpr int WS = win_stride(NDW);
     constexpr int FDW = P / 2 + 1;       // dwords per compact FD column (32 positions from an even start)
+    constexpr int CW = (sizeof(CT) == 2) ? FDW : 32;   // dwords per staged FD column
+    constexpr int CPI = 64 / CW;                        // FD columns per LDS-DMA wave instruction
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ int s_B[GPB], s_tot[GPB];
@@ -78,6 +118,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     const int grp = wave / GW, wg = wave % GW, gt = wg * 64 + lane;
     const int gc = blockIdx.x * GPB + grp;
     if (gc >= C) return;   // group-uniform; block barriers are only used when GPB == 1
+    RK_PROF_BEGIN();
     const RoundKLds L = round_k_lds(n, NDW, (int)sizeof(CT), STG);
     uint8_t* gl = lds + (size_t)grp * L.total;
     uint32_t* win = (uint32_t*)(gl + L.win);
@@ -92,8 +133,44 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     };
 
     const int g = gc / n, cl = gc % n;
-    const int len = A.c_len[gc], off = A.c_off[gc];
+    const int par = s & 1;
+    const size_t wrow = (size_t)s * C + (size_t)g * n;
+    // every load that does not depend on this chain's boundary is issued first, so their
+    // latencies overlap the boundary load: the boundary, this lane's candidate row (rebased
+    // FD bytes, written by the step that found it), the candidate flags and the bases
     const int b = A.Bm[(size_t)s * C + gc];
+    const int len = A.c_len[gc], off = A.c_off[gc];
+    const int j = gt;
+    const int jj = j < n ? j : 0;
+    uint32_t fd[NDW];
+    {
+        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + jj) * NDW;
+        if constexpr (NDW % 4 == 0) {
+#pragma unroll
+            for (int d = 0; d < NDW; d += 4) {
+                const uint4 v = *(const uint4*)(row + d);
+                fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < NDW; d += 2) {
+                const uint2 v = *(const uint2*)(row + d);
+                fd[d] = v.x; fd[d + 1] = v.y;
+            }
+        }
+    }
+    const uint8_t wfl = A.wflag[wrow + jj];
+    const int ovf_s = A.ovf[s];
+    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256 here)
+    int cbv[BPT], bmp[BPT], bmc[BPT];
+#pragma unroll
+    for (int u = 0; u < BPT; u++) {
+        const int i = gt + u * GL;
+        const int ii = i < n ? i : 0;
+        cbv[u] = A.c_base[g * n + ii];
+        bmp[u] = s > 0 ? A.Bm[wrow - C + ii] : 0;
+        bmc[u] = A.Bm[wrow + ii];
+    }
     if (b >= len) {
         if (gt == 0) {
             A.wstat[(size_t)s * C + gc] = 0;
@@ -102,13 +179,15 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         }
         return;
     }
-    const int par = s & 1;
-    const bool exact = A.ovf[s] != 0;   // a candidate row of this round did not fit 8 bits
-    const size_t wrow = (size_t)s * C + (size_t)g * n;
-    for (int i = gt; i < n; i += GL) {
-        const int cb = A.c_base[g * n + i];
-        base[i] = cb + (s > 0 ? A.Bm[wrow - C + i] : 0);   // base(s): Index of round s-1's candidate
-        bm1[i] = cb + A.Bm[wrow + i];                      // base(s+1)
+    const bool exact = ovf_s != 0;   // a candidate row of this round did not fit 8 bits
+    const bool cand = j < n && wfl == 1;
+#pragma unroll
+    for (int u = 0; u < BPT; u++) {
+        const int i = gt + u * GL;
+        if (i < n) {
+            base[i] = cbv[u] + bmp[u];   // base(s): Index of round s-1's candidate on chain i
+            bm1[i] = cbv[u] + bmc[u];    // base(s+1)
+        }
     }
     if (gt < 32) hist[gt] = 0;
 
@@ -132,31 +211,30 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
                     if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 4, 0, 0);
                 }
             }
+            // FD columns: one wave instruction stages CPI columns of CW dwords each (positions
+            // [kbase, kbase+np) for int32; the 2*FDW positions from the even start below kbase for
+            // uint16) into a 64-dword group; groups are 65 dwords apart (bank spread)
+            uint32_t* fd_w = (uint32_t*)fdc;
+            const int pcol = lane % CW, icol = lane / CW;
+            const uint32_t* __restrict__ fsrc;
+            size_t cstride;
+            bool pok;
             if constexpr (sizeof(CT) == 4) {
-                // column i: positions [kbase, kbase+np), one lane per (column, position)
-                constexpr int CPI = 64 / 32;   // columns per wave instruction (32 lanes each)
-                const int pcol = lane % 32, icol = lane / 32;
-                const CT* __restrict__ fsrc = (const CT*)A.FDT + off + kbase + pcol;
-                for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
-                    const int i = i0 + icol;
-                    if (i < n && pcol < np)
-                        __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * A.Pcap),
-                                                         (lds_ptr_t)(fdc + (size_t)i0 * P), 4, 0, 0);
-                }
+                fsrc = (const uint32_t*)A.FDT + off + kbase + pcol;
+                cstride = (size_t)A.Pcap;
+                pok = pcol < np;
             } else {
-                // column i: FDW dwords covering positions [p0, p0 + 2*FDW), p0 = even start
-                constexpr int CPI = 64 / FDW;
                 const int64_t p0 = (off + kbase) & ~1;
                 fsh = (off + kbase) & 1;
-                const int pcol = lane % FDW, icol = lane / FDW;
-                const uint32_t* __restrict__ fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
-                uint32_t* fd_w = (uint32_t*)fdc;
-                for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
-                    const int i = i0 + icol;
-                    if (i < n && icol < CPI)
-                        __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * (A.Pcap / 2)),
-                                                         (lds_ptr_t)(fd_w + (size_t)i0 * FDW), 4, 0, 0);
-                }
+                fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
+                cstride = (size_t)(A.Pcap / 2);
+                pok = true;
+            }
+            for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
+                const int i = i0 + icol;
+                if (i < n && pok)
+                    __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride),
+                                                     (lds_ptr_t)(fd_w + (size_t)(i0 / CPI) * 65), 4, 0, 0);
             }
         }
     };
@@ -164,52 +242,61 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         if constexpr (STG) return Coord<CT>::la(raw[p * n + i]);
         else return Coord<CT>::la(((const CT*)A.LA)[(size_t)(off + kbase + p) * n + i]);
     };
-    // rebased byte window: (0x80 | LA') per coordinate, padding coordinates LA' = 0
+    // rebased byte window: (0x80 | LA') per coordinate, padding coordinates LA' = 0. A thread
+    // keeps one dword column d (4 coordinates, their bases in registers) over rows p.
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     auto convert = [&](int kbase, int np) {
-        for (int t = gt; t < np * NDW; t += GL) {
-            const int p = t / NDW, d = t % NDW;
-            uint32_t w = 0x80808080u;
+        constexpr int RS = (GL >= NDW) ? GL / NDW : 1;   // rows per pass
+        for (int d = gt % NDW; d < NDW; d += GL) {
+            const int i0 = 4 * d;
+            if constexpr (STG && sizeof(CT) == 2) {
+                // packed: LA' = min(sat(raw - base), 126) on coordinate pairs (raw = LA + 1)
+                u16x2 b01 = {0, 0}, b23 = {0, 0};
+                if (i0 < n) b01 = u16x2{(unsigned short)base[i0], (unsigned short)base[i0 + 1]};
+                if (i0 + 2 < n) b23 = u16x2{(unsigned short)base[i0 + 2], (unsigned short)base[i0 + 3]};
+                const u16x2 cap = {126, 126};
+                for (int p = gt / NDW; p < np; p += RS) {
+                    const uint32_t* rp = (const uint32_t*)(raw + p * n + i0);
+                    const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
+                    const u16x2 y01 = __builtin_elementwise_min(
+                        __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
+                    const u16x2 y23 = __builtin_elementwise_min(
+                        __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
+                    const uint32_t w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23),
+                                                             __builtin_bit_cast(uint32_t, y01), 0x06040200u);
+                    win[p * WS + d] = w | 0x80808080u;
+                }
+            } else {
+                int32_t bq[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int i = 4 * d + q;
-                if (i < n) {
-                    const int32_t x = la_at(kbase, p, i) - base[i] + 1;
-                    w |= (uint32_t)min(max(x, 0), 126) << (8 * q);
+                for (int q = 0; q < 4; q++) bq[q] = (i0 + q < n) ? base[i0 + q] : 0;
+                for (int p = gt / NDW; p < np; p += RS) {
+                    uint32_t w = 0x80808080u;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int i = i0 + q;
+                        if (i < n) {
+                            const int32_t x = la_at(kbase, p, i) - bq[q] + 1;
+                            w |= (uint32_t)min(max(x, 0), 126) << (8 * q);
+                        }
+                    }
+                    win[p * WS + d] = w;
                 }
             }
-            win[p * WS + d] = w;
         }
     };
 
-    constexpr int CH = 1;   // candidates per lane (n <= GL); see k_round_k_chunked for n > 256
-    uint32_t fd[NDW];
-    const int j = gt;
-    bool cand = false;
-    {   // this lane's candidate row: rebased FD bytes (written by the step that found it)
-        cand = j < n && A.wflag[wrow + j] == 1;
-        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + (j < n ? j : 0)) * NDW;
-        if constexpr (NDW % 4 == 0) {
-#pragma unroll
-            for (int d = 0; d < NDW; d += 4) {
-                const uint4 v = *(const uint4*)(row + d);
-                fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < NDW; d += 2) {
-                const uint2 v = *(const uint2*)(row + d);
-                fd[d] = v.x; fd[d + 1] = v.y;
-            }
-        }
-    }
     int kbase = b, np = min(P, len - b), kstar = len, carried = 0, B = -1, K = P;
     bool done = false;   // seen in an earlier window: seen at every later probe
+    RK_PROF(0);
     for (;;) {
         stage(kbase, np);
         __builtin_amdgcn_s_waitcnt(0);
         gsync();
+        RK_PROF(1);
         convert(kbase, np);
         gsync();
+        RK_PROF(2);
         // first probe of the window that strongly sees this lane's candidate (np: none);
         // probes past the window's end count as seeing (keeps the predicate monotone)
         int lo = 0, hi = P;
@@ -233,7 +320,6 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
             }
         } else {
             // exact int32 compares against the raw candidate row (rounds flagged by the producer)
-            const int jj = j < n ? j : 0;
             for (int it = 0; it < 5; it++) {
                 const int mid = (lo + hi) >> 1;
                 int cnt = 0;
@@ -251,6 +337,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
             }
         }
         K = lo;
+        RK_PROF(3);
         if (K < np && cand) atomicAdd(&hist[K], 1);
         gsync();
         if (wg == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
@@ -265,6 +352,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         }
         gsync();
         B = s_B[grp];
+        RK_PROF(4);
         if (B >= 0) {
             kstar = kbase + B;
             break;
@@ -280,7 +368,6 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         np = min(P, len - kbase);
         gsync();
     }
-    (void)CH;
 
     // outputs of round s for this chain
     for (int k = b + gt; k < kstar; k += GL) A.p_round[off + k] = s;
@@ -299,8 +386,9 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
         auto fd_raw = [&](int i) -> CT {
             if constexpr (STG) {
-                if constexpr (sizeof(CT) == 2) return fdc[i * 2 * FDW + fsh + pk];
-                else return fdc[i * P + pk];
+                const int col = (i / CPI) * 65 + (i % CPI) * CW;   // dword offset of column i
+                if constexpr (sizeof(CT) == 2) return fdc[2 * col + fsh + pk];
+                else return fdc[col + pk];
             } else {
                 return ((const CT*)A.FDT)[(size_t)i * A.Pcap + off + kstar];
             }
@@ -337,6 +425,8 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     } else if (gt == 0) {
         A.wflag[(size_t)(s + 1) * C + gc] = 0;
     }
+    RK_PROF(5);
+    RK_PROF_END();
 }
 
 // round 0's candidate rows (the first event of every chain), rebased to base(0) = c_base

@@ -783,6 +783,7 @@ void step_prof_dump() {
     fprintf(stderr, "[hgx] round phases (clk sums; 0 = block-rounds, 6 = wave-0 tallies*1000 + levels):");
     for (int i = 0; i < 8; i++) fprintf(stderr, " %d:%llu", i, h[i]);
     fprintf(stderr, "\n");
+    round_k_prof_dump();
 }
 #else
 void step_prof_dump() {}

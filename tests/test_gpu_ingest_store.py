@@ -194,17 +194,20 @@ def test_round_table_growth_keeps_rows(n, E, seed):
 
 
 def test_round_table_growth_uneven_batched_graphs():
-    """A batched context whose events are all in graph 0 (the initial round-table guess
-    assumes an even spread over graphs)."""
+    """A batched context whose events are nearly all in graph 0 (the initial round-table
+    guess assumes an even spread over graphs)."""
     n, G = 16, 8
-    t = gtrace.gossip(n, 16000, 81)
-    h = _hg(n, cap=t.E, graphs=G)
-    h.insert_trace(t)
+    traces = [gtrace.gossip(n, 16000, 81)] + [gtrace.gossip(n, 64, 82 + g) for g in range(1, G)]
+    h = _hg(n, cap=sum(t.E for t in traces), graphs=G)
+    h.insert_trace(gtrace.concat_graphs(traces))
     h.RunConsensus()
-    o = hgref.oracle_run(t).results()
-    assert list(h.ConsensusEvents(0)) == list(o["order"])
-    assert h.UndecidedRounds(0) == o["undecided"] and h.LastConsensusRound(0) == o["lcr"]
-    assert all(h.LastRound(g) == -1 for g in range(1, G))
+    off = 0
+    for g, t in enumerate(traces):
+        o = hgref.oracle_run(t).results()
+        assert list(h.ConsensusEvents(g) - off) == list(o["order"]), g
+        assert h.UndecidedRounds(g) == o["undecided"] and h.LastConsensusRound(g) == o["lcr"], g
+        assert h.LastRound(g) == o["last_round"], g
+        off += t.E
 
 
 def test_primitives_across_batched_graphs():
