@@ -100,22 +100,30 @@ __host__ __device__ inline RoundKLds round_k_lds(int n, int ndw, int csz, bool s
     return L;
 }
 
-template <typename CT, int NDW, int GW, bool STG>
-__global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
+// CG waves of 64 candidates each; every candidate's row is split over H waves (coordinate
+// dwords [h*NDW/H, (h+1)*NDW/H)), whose partial counts meet in LDS once per search level, so
+// that two waves share each SIMD; GPB chain groups per block when a group is one wave.
+template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
+__global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int s) {
     constexpr int P = kWinP;
-    constexpr int GL = 64 * GW;          // lanes of one chain group (one candidate each)
-    constexpr int GPB = 4 / GW;          // chain groups per 256-thread block
+    constexpr int GW = CG * H;           // waves of one chain group
+    constexpr int GL = 64 * GW;          // threads of one chain group
+    constexpr int HD = NDW / H;          // candidate-row dwords per wave
     constexpr int WS = win_stride(NDW);
     constexpr int FDW = P / 2 + 1;       // dwords per compact FD column (32 positions from an even start)
     constexpr int CW = (sizeof(CT) == 2) ? FDW : 32;   // dwords per staged FD column
     constexpr int CPI = 64 / CW;                        // FD columns per LDS-DMA wave instruction
+    static_assert(GPB == 1 || GW == 1, "several chain groups per block only with one-wave groups");
+    static_assert(NDW % (2 * H) == 0, "row split");
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ int s_B[GPB], s_tot[GPB];
+    __shared__ int pc[(H > 1) ? 2 * H * 64 * CG : 1];   // partial counts by level parity
 
     const int n = A.n, C = A.C, sm = A.sm;
     const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp = wave / GW, wg = wave % GW, gt = wg * 64 + lane;
+    const int grp = wave / GW, wh = wave % GW, h = wh / CG, cw = wh % CG;
+    const int gt = wh * 64 + lane;       // thread within the chain group
     const int gc = blockIdx.x * GPB + grp;
     if (gc >= C) return;   // group-uniform; block barriers are only used when GPB == 1
     RK_PROF_BEGIN();
@@ -128,7 +136,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     int32_t* bm1 = (int32_t*)(gl + L.bm1);
     int32_t* hist = (int32_t*)(gl + L.hist);
     auto gsync = [&]() {
-        if (GW == 1) wave_lds_fence();
+        if constexpr (GW == 1) wave_lds_fence();
         else __syncthreads();
     };
 
@@ -136,24 +144,24 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     const int par = s & 1;
     const size_t wrow = (size_t)s * C + (size_t)g * n;
     // every load that does not depend on this chain's boundary is issued first, so their
-    // latencies overlap the boundary load: the boundary, this lane's candidate row (rebased
-    // FD bytes, written by the step that found it), the candidate flags and the bases
+    // latencies overlap the boundary load: the boundary, this lane's part of its candidate's
+    // rebased row (written by the step that found the candidate), the flags and the bases
     const int b = A.Bm[(size_t)s * C + gc];
     const int len = A.c_len[gc], off = A.c_off[gc];
-    const int j = gt;
+    const int j = cw * 64 + lane;        // this lane's candidate
     const int jj = j < n ? j : 0;
-    uint32_t fd[NDW];
+    uint32_t fd[HD];
     {
-        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + jj) * NDW;
-        if constexpr (NDW % 4 == 0) {
+        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + jj) * NDW + h * HD;
+        if constexpr (HD % 4 == 0) {
 #pragma unroll
-            for (int d = 0; d < NDW; d += 4) {
+            for (int d = 0; d < HD; d += 4) {
                 const uint4 v = *(const uint4*)(row + d);
                 fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
             }
         } else {
 #pragma unroll
-            for (int d = 0; d < NDW; d += 2) {
+            for (int d = 0; d < HD; d += 2) {
                 const uint2 v = *(const uint2*)(row + d);
                 fd[d] = v.x; fd[d + 1] = v.y;
             }
@@ -161,7 +169,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     }
     const uint8_t wfl = A.wflag[wrow + jj];
     const int ovf_s = A.ovf[s];
-    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256 here)
+    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256)
     int cbv[BPT], bmp[BPT], bmc[BPT];
 #pragma unroll
     for (int u = 0; u < BPT; u++) {
@@ -200,13 +208,13 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
             const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
             uint32_t* raw_w = (uint32_t*)raw;
             if (((n * (int)sizeof(CT)) & 15) == 0) {
-                for (int c0 = wg * 256; c0 < nel; c0 += GW * 256) {
+                for (int c0 = wh * 256; c0 < nel; c0 += GW * 256) {
                     const int t = c0 + lane * 4;
                     if (t < nel)
                         __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 16, 0, 0);
                 }
             } else {
-                for (int c0 = wg * 64; c0 < nel; c0 += GW * 64) {
+                for (int c0 = wh * 64; c0 < nel; c0 += GW * 64) {
                     const int t = c0 + lane;
                     if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 4, 0, 0);
                 }
@@ -230,7 +238,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
                 cstride = (size_t)(A.Pcap / 2);
                 pok = true;
             }
-            for (int i0 = wg * CPI; i0 < n; i0 += GW * CPI) {
+            for (int i0 = wh * CPI; i0 < n; i0 += GW * CPI) {
                 const int i = i0 + icol;
                 if (i < n && pok)
                     __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride),
@@ -247,6 +255,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     auto convert = [&](int kbase, int np) {
         constexpr int RS = (GL >= NDW) ? GL / NDW : 1;   // rows per pass
+        constexpr int NP = (P + RS - 1) / RS;              // passes (fixed trip count)
         for (int d = gt % NDW; d < NDW; d += GL) {
             const int i0 = 4 * d;
             if constexpr (STG && sizeof(CT) == 2) {
@@ -255,16 +264,20 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
                 if (i0 < n) b01 = u16x2{(unsigned short)base[i0], (unsigned short)base[i0 + 1]};
                 if (i0 + 2 < n) b23 = u16x2{(unsigned short)base[i0 + 2], (unsigned short)base[i0 + 3]};
                 const u16x2 cap = {126, 126};
-                for (int p = gt / NDW; p < np; p += RS) {
-                    const uint32_t* rp = (const uint32_t*)(raw + p * n + i0);
-                    const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
-                    const u16x2 y01 = __builtin_elementwise_min(
-                        __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
-                    const u16x2 y23 = __builtin_elementwise_min(
-                        __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
-                    const uint32_t w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23),
-                                                             __builtin_bit_cast(uint32_t, y01), 0x06040200u);
-                    win[p * WS + d] = w | 0x80808080u;
+#pragma unroll
+                for (int u = 0; u < NP; u++) {
+                    const int p = gt / NDW + u * RS;
+                    if (p < np) {
+                        const uint32_t* rp = (const uint32_t*)(raw + p * n + i0);
+                        const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
+                        const u16x2 y01 = __builtin_elementwise_min(
+                            __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
+                        const u16x2 y23 = __builtin_elementwise_min(
+                            __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
+                        const uint32_t w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23),
+                                                                 __builtin_bit_cast(uint32_t, y01), 0x06040200u);
+                        win[p * WS + d] = w | 0x80808080u;
+                    }
                 }
             } else {
                 int32_t bq[4];
@@ -285,6 +298,20 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
             }
         }
     };
+    // total count over the H waves of this candidate (partial counts meet in LDS)
+    auto combine = [&](uint32_t part, int it) -> uint32_t {
+        if constexpr (H == 1) {
+            return part;
+        } else {
+            int* pcb = pc + (it & 1) * (H * 64 * CG);
+            pcb[h * 64 * CG + j] = (int)part;
+            gsync();
+            uint32_t t = 0;
+#pragma unroll
+            for (int q = 0; q < H; q++) t += (uint32_t)pcb[q * 64 * CG + j];
+            return t;
+        }
+    };
 
     int kbase = b, np = min(P, len - b), kstar = len, carried = 0, B = -1, K = P;
     bool done = false;   // seen in an earlier window: seen at every later probe
@@ -301,46 +328,49 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         // probes past the window's end count as seeing (keeps the predicate monotone)
         int lo = 0, hi = P;
         if (!exact) {
-            uint32_t f[NDW];
+            uint32_t f[HD];
 #pragma unroll
-            for (int d = 0; d < NDW; d++) f[d] = cand ? fd[d] : 0x7F7F7F7Fu;
+            for (int d = 0; d < HD; d++) f[d] = cand ? fd[d] : 0x7F7F7F7Fu;
 #pragma unroll
             for (int it = 0; it < 5; it++) {
                 const int mid = (lo + hi) >> 1;
-                const uint32_t* row = win + mid * WS;
+                const uint32_t* row = win + mid * WS + h * HD;
                 uint32_t cnt = 0;
 #pragma unroll
-                for (int d = 0; d < NDW; d += 2) {
+                for (int d = 0; d < HD; d += 2) {
                     const uint2 v = *(const uint2*)(row + d);
                     cnt += __builtin_popcount((v.x - f[d]) & 0x80808080u);
                     cnt += __builtin_popcount((v.y - f[d + 1]) & 0x80808080u);
                 }
+                cnt = combine(cnt, it);
                 const bool seen = done || mid >= np || ((int)cnt >= sm && !(j == cl && kbase + mid == b));
                 if (seen) hi = mid; else lo = mid + 1;
             }
         } else {
             // exact int32 compares against the raw candidate row (rounds flagged by the producer)
+            const int i_lo = h * HD * 4, i_hi = min(n, (h + 1) * HD * 4);
             for (int it = 0; it < 5; it++) {
                 const int mid = (lo + hi) >> 1;
-                int cnt = 0;
+                uint32_t cnt = 0;
                 if (cand && !done && mid < np) {
-                    for (int i = 0; i < n; i++) {
+                    for (int i = i_lo; i < i_hi; i++) {
                         const int32_t fdv = (sizeof(CT) == 2)
                                                 ? Coord<uint16_t>::fd(((const uint16_t*)A.WFD)[(wrow + jj) * n + i])
                                                 : A.WFD[(wrow + jj) * n + i];
                         const int32_t lav = min(la_at(kbase, mid, i), kMaxI32 - 1);
-                        cnt += lav >= fdv ? 1 : 0;
+                        cnt += lav >= fdv ? 1u : 0u;
                     }
                 }
-                const bool seen = done || mid >= np || (cand && cnt >= sm && !(j == cl && kbase + mid == b));
+                cnt = combine(cnt, it);
+                const bool seen = done || mid >= np || (cand && (int)cnt >= sm && !(j == cl && kbase + mid == b));
                 if (seen) hi = mid; else lo = mid + 1;
             }
         }
         K = lo;
         RK_PROF(3);
-        if (K < np && cand) atomicAdd(&hist[K], 1);
+        if (h == 0 && K < np && cand && !done) atomicAdd(&hist[K], 1);   // earlier windows are in `carried`
         gsync();
-        if (wg == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
+        if (wh == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
             const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
             const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
             const uint64_t m = __ballot(lane < np && (int)inc >= sm);
@@ -381,7 +411,7 @@ __global__ void __launch_bounds__(256) k_round_k(RoundArgs A, int s) {
         // S row of the boundary event: the candidates it strongly sees (bit j of word j/64)
         const uint64_t bits = __ballot(cand && K <= B);
         const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
-        if (lane == 0 && wg < A.nw) A.Smat[srow + wg] = bits;
+        if (h == 0 && lane == 0 && cw < A.nw) A.Smat[srow + cw] = bits;
         // the new candidate's rows for round s+1
         const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
         auto fd_raw = [&](int i) -> CT {
@@ -463,39 +493,41 @@ int round_k_ndw(int n) {
     return p;
 }
 
-template <typename CT, int NDW, int GW, bool STG>
+template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
 static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
-    const void* f = (const void*)k_round_k<CT, NDW, GW, STG>;
+    const void* f = (const void*)k_round_k<CT, NDW, CG, H, GPB, STG>;
     const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), STG);
-    constexpr int GPB = 4 / GW;
     const size_t lds = (size_t)L.total * GPB;
     static bool attr = false;
     if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
         if (e != hipSuccess) return e;
         attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
-    hipLaunchKernelGGL((k_round_k<CT, NDW, GW, STG>), dim3(grid), dim3(256), lds, st, A, s);
+    hipLaunchKernelGGL((k_round_k<CT, NDW, CG, H, GPB, STG>), dim3(grid), dim3(64 * CG * H * GPB), lds, st, A, s);
     return hipGetLastError();
 }
 
-template <typename CT, int NDW, int GW>
+template <typename CT, int NDW, int CG, int H, int GPB>
 static hipError_t round_k_launch(hipStream_t st, const RoundArgs& A, int s) {
     const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), true);
-    if ((size_t)L.total * (4 / GW) <= 150 * 1024) return round_k_launch_v<CT, NDW, GW, true>(st, A, s);
-    return round_k_launch_v<CT, NDW, GW, false>(st, A, s);
+    if ((size_t)L.total * GPB <= 140 * 1024) return round_k_launch_v<CT, NDW, CG, H, GPB, true>(st, A, s);
+    return round_k_launch_v<CT, NDW, CG, H, GPB, false>(st, A, s);
 }
 
+// one wave per chain, four chains per block, when chains are many (batched simulations);
+// otherwise one chain per block with its rows split over 8 waves (two per SIMD)
 template <typename CT>
 static hipError_t launch_round_k_t(hipStream_t st, const RoundArgs& A, int s) {
+    const bool many = A.C >= 1024;
     switch (round_k_ndw(A.n)) {
-        case 2: return round_k_launch<CT, 2, 1>(st, A, s);
-        case 4: return round_k_launch<CT, 4, 1>(st, A, s);
-        case 8: return round_k_launch<CT, 8, 1>(st, A, s);
-        case 16: return round_k_launch<CT, 16, 1>(st, A, s);
-        case 32: return round_k_launch<CT, 32, 4>(st, A, s);
-        case 64: return round_k_launch<CT, 64, 4>(st, A, s);
+        case 2: return many ? round_k_launch<CT, 2, 1, 1, 4>(st, A, s) : round_k_launch<CT, 2, 1, 1, 1>(st, A, s);
+        case 4: return many ? round_k_launch<CT, 4, 1, 1, 4>(st, A, s) : round_k_launch<CT, 4, 1, 2, 1>(st, A, s);
+        case 8: return many ? round_k_launch<CT, 8, 1, 1, 4>(st, A, s) : round_k_launch<CT, 8, 1, 4, 1>(st, A, s);
+        case 16: return many ? round_k_launch<CT, 16, 1, 1, 4>(st, A, s) : round_k_launch<CT, 16, 1, 8, 1>(st, A, s);
+        case 32: return round_k_launch<CT, 32, 2, 4, 1>(st, A, s);
+        case 64: return round_k_launch<CT, 64, 4, 2, 1>(st, A, s);
         default: return hipErrorInvalidValue;   // n > 256: k_round_step_big
     }
 }
