@@ -494,7 +494,8 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     RK_PROF_END();
 }
 
-// round 0's candidate rows (the first event of every chain), rebased to base(0) = c_base
+// round 0's candidate rows (the first event of every chain), rebased to base(0) = c_base,
+// from the row-major WFD rows k_round_gather has just written (raw uint16 or int32 FD)
 template <typename CT>
 __global__ void k_round_k_gather(RoundArgs A, int ndw) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -504,11 +505,12 @@ __global__ void k_round_k_gather(RoundArgs A, int ndw) {
     uint32_t w = 0;
     bool of = false;
     const bool have = A.c_len[gc] > 0;
+    const CT* __restrict__ row = (const CT*)A.WFD + (size_t)gc * n;   // round 0's rows
     for (int q = 0; q < 4; q++) {
         const int i = 4 * d + q;
         uint32_t v = 127u;
         if (have && i < n) {
-            const int32_t f = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + A.c_off[gc]]);
+            const int32_t f = Coord<CT>::fd(row[i]);
             if (f != kMaxI32) {
                 const int32_t x = f - A.c_base[g * n + i] + 1;
                 if (x > 126) of = true;
