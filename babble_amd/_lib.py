@@ -113,6 +113,7 @@ def lib():
     _sig(L, "hgx_set_coord_storage", i32, [p, i32])
     _sig(L, "hgx_set_fame_tally", i32, [p, i32])
     _sig(L, "hgx_set_round_kernel", i32, [p, i32])
+    _sig(L, "hgx_set_incremental", i32, [p, i32])
     _sig(L, "hgx_reserve_rounds", i32, [p, i32])
     _sig(L, "hgx_device_alloc", i32, [i32, i64, C.POINTER(C.c_void_p)])
     _sig(L, "hgx_device_free", i32, [i32, p])

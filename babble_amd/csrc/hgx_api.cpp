@@ -377,8 +377,9 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
         s.queued_upto = std::max(s.queued_upto, LR);
         s.last_round = LR;
         s.fame.resize((size_t)(LR + 1) * n, 0);
-        s.round_events.assign(LR + 1, 0);
-        for (int32_t r = 0; r <= LR; r++) {
+        // rounds below r_lo kept their boundaries (incremental DivideRounds)
+        s.round_events.resize(LR + 1, 0);
+        for (int32_t r = std::min(c->rh.r_lo, LR + 1); r <= LR; r++) {
             int64_t cnt = 0;
             for (int cl = 0; cl < n; cl++) {
                 const int gc = g * n + cl;
@@ -409,7 +410,12 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
     DeviceGuard dg(c);
     std::vector<int8_t> dev;
     if (c->divided) {
-        hipError_t e = c->eng.decide_fame(dev);
+        // decided fame is never revisited: only rounds from the first undecided one
+        int32_t f0 = c->rh.R;
+        for (int g = 0; g < c->G; g++)
+            for (int32_t r : c->gs[g].undecided)
+                if (r >= 0 && r <= c->gs[g].last_round) f0 = std::min(f0, r);
+        hipError_t e = c->eng.decide_fame(f0, dev);
         if (e != hipSuccess) return dev_err(err, e, "hgx_decide_fame");
     }
     int32_t rc = HGX_OK;
@@ -459,12 +465,15 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
     DeviceGuard dg(c);
     const int n = c->n, C = c->C, G = c->G;
     const int32_t R = c->rh.R;
+    // rounds below r0 cannot be the roundReceived of an event not received yet
+    int max_unrecv = 0;
+    const int32_t r0 = c->eng.recv_round_lo(c->rh, max_unrecv);
     std::vector<uint8_t> elig((size_t)G * std::max(R, 1), 0), fw((size_t)std::max(R, 1) * C, 0), ure(G, 0);
     for (int g = 0; g < G; g++) {
         const GraphState& s = c->gs[g];
         ure[g] = s.undecided.empty() ? 1 : 0;
         const int32_t U0 = s.undecided.empty() ? -1 : s.undecided[0];
-        for (int32_t i = 0; i <= s.last_round; i++) {
+        for (int32_t i = std::max(r0, 0); i <= s.last_round; i++) {
             // one pass over the round's chains: famous witnesses, and WitnessesDecided
             // (roundInfo.go:64-71) for the DecideRoundReceived skip rule (hashgraph.go:763)
             bool decided = true;
@@ -480,7 +489,7 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
         }
     }
     hgx::OrderHost oh;
-    hipError_t e = c->eng.find_order(elig, fw, ure, oh);
+    hipError_t e = c->eng.find_order(elig, fw, ure, r0, max_unrecv, oh);
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     if (oh.panic) {
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
@@ -922,9 +931,10 @@ int32_t hgx_witness(hgx_ctx* c, int64_t x) {
 // ---- instrumentation / knobs ----------------------------------------------------------
 int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
     if (!c || !out) return 0;
-    const int32_t m = std::min<int32_t>(cap, 7);
-    double v[7] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
-                   (double)c->eng.la_sweeps, (double)c->eng.R, (double)c->eng.compact};
+    const int32_t m = std::min<int32_t>(cap, 10);
+    double v[10] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
+                    (double)c->eng.la_sweeps, (double)c->eng.R, (double)c->eng.compact,
+                    (double)c->eng.la_rows, c->eng.last_rebuild ? 1.0 : 0.0, (double)c->rh.r_lo};
     for (int32_t i = 0; i < m; i++) out[i] = v[i];
     return m;
 }
@@ -1002,6 +1012,12 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
     c->eng.round_kernel = mode;
+    return HGX_OK;
+}
+
+int32_t hgx_set_incremental(hgx_ctx* c, int32_t on) {
+    if (!c || on < 0 || on > 1) return HGX_ERR_INVALID;
+    c->eng.incremental = on != 0;
     return HGX_OK;
 }
 

@@ -101,6 +101,9 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     nw = (n + 63) / 64;
     cap = std::max<int64_t>(cap_events, 1);
     const size_t P = (size_t)cap;
+    // positions: the events plus slack for chains to grow in place between DivideRounds
+    Ppos = cap + std::max<int64_t>(cap / 4, (int64_t)256 * C);
+    const size_t PP = (size_t)Ppos;
     HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_sp.alloc(P)); HGX_TRY(g_op.alloc(P));
     HGX_TRY(g_ntx.alloc(P)); HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P));
     HGX_TRY(g_cts.alloc(P)); HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
@@ -116,13 +119,13 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (size_t)C * 4, stream));
     HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
     HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
-    HGX_TRY(p_gid.alloc(P)); HGX_TRY(p_chain.alloc(P)); HGX_TRY(p_op.alloc(P)); HGX_TRY(p_opu.alloc(P)); HGX_TRY(p_round.alloc(P));
-    HGX_TRY(p_rr.alloc(P)); HGX_TRY(p_ts.alloc(P)); HGX_TRY(p_cts.alloc(P));
-    fd_ld = (cap + 1) & ~(int64_t)1;
-    HGX_TRY(LA.alloc(P * n));
+    HGX_TRY(c_old.alloc(C)); HGX_TRY(fu.alloc(C)); HGX_TRY(rcnt.alloc(C));
+    HGX_TRY(p_gid.alloc(PP)); HGX_TRY(p_chain.alloc(PP)); HGX_TRY(p_op.alloc(PP)); HGX_TRY(p_opu.alloc(PP));
+    HGX_TRY(p_round.alloc(PP)); HGX_TRY(p_rr.alloc(PP)); HGX_TRY(p_ts.alloc(PP)); HGX_TRY(p_cts.alloc(PP));
+    fd_ld = (Ppos + 1) & ~(int64_t)1;
+    HGX_TRY(LA.alloc(PP * n));
     HGX_TRY(FDT.alloc((size_t)fd_ld * n + 128));   // slack: compact window staging reads past a column
     HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8)); HGX_TRY(order_gid.alloc(P));
-    HGX_TRY(p_new.alloc(P));
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
@@ -188,7 +191,7 @@ DevArrays Engine::arrays() {
     a.active = active.p; a.lr = lr.p;
     a.Smat = Smat.p; a.Vbuf = Vbuf.p; a.fame = fame.p;
     a.elig = elig.p; a.fw = fw.p; a.ur_empty = ur_empty.p; a.T = Tthr.p;
-    a.recv_list = recv_list.p; a.counters = counters.p; a.p_new = p_new.p; a.scan_part = scan_part.p;
+    a.recv_list = recv_list.p; a.counters = counters.p; a.fu = fu.p; a.rcnt = rcnt.p; a.scan_part = scan_part.p;
     a.key_a = key_a.p; a.key_b = key_b.p; a.val_a = val_a.p; a.val_b = val_b.p; a.hist = hist.p;
     a.minmax = minmax.p; a.order_gid = order_gid.p;
     a.blk_cnt = blk_cnt.p; a.blk_loaded = blk_loaded.p; a.blk_ntx = blk_ntx.p; a.blk_nil = blk_nil.p;
@@ -316,6 +319,7 @@ hipError_t Engine::clear() {
     E = 0;
     E_div = 0;
     R = 0;
+    laid_out = false;
     return hipStreamSynchronize(stream);
 }
 
@@ -359,48 +363,99 @@ hipError_t Engine::reserve_rounds(int32_t rounds) {
 }
 
 // ---- DivideRounds ---------------------------------------------------------------
+// Chains are laid out with slack (positions [c_off[c], c_off[c] + slot)), so that a call
+// after more InsertEvents only appends rows: the events of earlier calls keep their
+// positions, lastAncestors rows and rounds, and the call works on the new events (DESIGN.md
+// §3.7). The layout is rebuilt (and everything recomputed) when a chain outgrows its slot,
+// the coordinate storage changes, or after reset_received / reserve_rounds / clear.
 hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_len,
                                  const std::vector<int32_t>& chain_base, RoundsHost& out) {
-    E = En;
-    E_div = En;
-    h_off.assign(C + 1, 0);
-    max_len = 0;
+    int32_t max_index = -1;
+    int new_max_len = 0;
     for (int c = 0; c < C; c++) {
-        h_off[c + 1] = h_off[c] + chain_len[c];
-        max_len = std::max(max_len, chain_len[c]);
+        if (chain_len[c] > 0) max_index = std::max(max_index, chain_base[c] + chain_len[c] - 1);
+        new_max_len = std::max(new_max_len, chain_len[c]);
     }
-    HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(c_len.p, chain_len.data(), C * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
     // compact (uint16) coordinates when every Index fits below the sentinels
     // (Coord<uint16_t>, hgx_device.h) and rows are whole dwords
-    int32_t max_index = -1;
-    for (int c = 0; c < C; c++)
-        if (chain_len[c] > 0) max_index = std::max(max_index, chain_base[c] + chain_len[c] - 1);
-    compact = (!force_coord32 && (n % 2) == 0 && max_index <= 65533) ? 1 : 0;
+    const int new_compact = (!force_coord32 && (n % 2) == 0 && max_index <= 65533) ? 1 : 0;
+    bool rebuild = !laid_out || E_div == 0 || new_compact != compact || !incremental;
+    if (!rebuild)
+        for (int c = 0; c < C; c++)
+            if (chain_len[c] > h_off[c + 1] - h_off[c]) { rebuild = true; break; }
+    const int64_t E0 = rebuild ? 0 : E_div;
+    E = En;
+    compact = new_compact;
+    max_len = new_max_len;
     const size_t csz = compact ? 2 : 4;
+    if (rebuild) {
+        // slack shared evenly by the chains
+        const int64_t slack = (Ppos - En) / C;
+        h_off.assign(C + 1, 0);
+        for (int c = 0; c < C; c++) h_off[c + 1] = h_off[c] + chain_len[c] + (int32_t)slack;
+        HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
+        h_len_div.assign(C, 0);
+        last_rebuild = true;
+    } else {
+        last_rebuild = false;
+    }
+    HGX_TRY(hipMemcpyAsync(c_len.p, chain_len.data(), C * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(c_old.p, h_len_div.data(), C * 4, hipMemcpyHostToDevice, stream));
+    // first round whose step can change: the lowest round of the last old event of a chain
+    // that got new events (every boundary below it is among old events)
+    int32_t r_lo = 0;
+    if (!rebuild) {
+        r_lo = 0x7FFFFFFF;
+        const int32_t Rp = out.R;
+        for (int c = 0; c < C && r_lo > 0; c++) {
+            if (chain_len[c] <= h_len_div[c]) continue;
+            const int32_t last = h_len_div[c] - 1;
+            if (last < 0 || Rp == 0) { r_lo = 0; break; }
+            int32_t lo = 0, hi = Rp;   // largest r in [0, Rp] with bm[r][c] <= last
+            while (lo < hi) {
+                const int32_t mid = (lo + hi + 1) / 2;
+                if (out.bm[(size_t)mid * C + c] <= last) lo = mid; else hi = mid - 1;
+            }
+            r_lo = std::min(r_lo, lo);
+        }
+        if (r_lo == 0x7FFFFFFF) r_lo = 0;
+    }
+    int max_new = 0;
+    for (int c = 0; c < C; c++) max_new = std::max(max_new, chain_len[c] - h_len_div[c]);
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
     const int seg = kLaSeg;
     kbeg(K_LAYOUT);
-    launch_layout(stream, E, a, C, seg);
-    kend(K_LAYOUT, (double)E * 64);
-    // lastAncestors: fixed point from all -1, dirty-tracked sweeps (k_la_sweep)
-    HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)E * n * csz, stream));
+    launch_layout(stream, E0, En, a, C, seg);
+    kend(K_LAYOUT, (double)(En - E0) * 64);
+    // lastAncestors: fixed point from all -1 (new rows), dirty-tracked sweeps (k_la_sweep)
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
-    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.alloc(2 * nunits));
-    if (la_usum.n < nunits) HGX_TRY(la_usum.alloc(nunits));
+    int64_t u0 = 0;
+    if (rebuild) {
+        HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
+    } else {
+        launch_init_new(stream, a, E0, En - E0, n, fd_ld);
+        int32_t smin = 0x7FFFFFFF;
+        for (int c = 0; c < C; c++)
+            if (chain_len[c] > h_len_div[c]) smin = std::min(smin, h_len_div[c] / seg);
+        u0 = (int64_t)smin * C;
+    }
+    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.grow_copy(2 * nunits, 0, stream));
+    if (la_usum.n < nunits) HGX_TRY(la_usum.grow_copy(nunits, la_usum.n, stream));
+    HGX_TRY(hipMemsetAsync(la_chg.p, 0, 2 * nunits, stream));   // no stale flags of an earlier call
+    const int32_t* cold = rebuild ? nullptr : c_old.p;
     la_sweeps = 0;
     la_rows = 0;
     for (;;) {
         uint8_t* chg_prev = la_chg.p + (size_t)(la_sweeps & 1) * nunits;
         uint8_t* chg_cur = la_chg.p + (size_t)((la_sweeps + 1) & 1) * nunits;
-        HGX_TRY(hipMemsetAsync(chg_cur, 0, nunits, stream));
+        HGX_TRY(hipMemsetAsync(chg_cur + u0, 0, nunits - (size_t)u0, stream));
         HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 8, stream));
         HGX_TRY(hipMemsetAsync(counters.p + 4, 0, 4, stream));
         kbeg(K_LA_SWEEP);
         launch_la_sweep(stream, a, C, n, max_len, seg, la_sweeps == 0 ? 1 : 0, chg_prev, chg_cur, la_usum.p,
-                        counters.p + 2);
+                        counters.p + 2, cold, u0);
         kend(K_LA_SWEEP, 0);
         HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 12, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
@@ -413,20 +468,31 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         if (la_sweeps > 100000) return hipErrorUnknown;
     }
     kbeg(K_FD_BUILD);
-    launch_fd_build(stream, a, C, n, max_len, fd_ld);
-    kend(K_FD_BUILD, (double)E * 2.0 * csz * n);
+    launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
+    kend(K_FD_BUILD, (double)(En - E0) * 2.0 * csz * n);
+    if (rebuild) {   // events received before the rebuild (a prefix of every chain)
+        HGX_TRY(hipMemsetAsync(fu.p, 0, (size_t)C * 4, stream));
+        launch_fu_count(stream, a, En);
+        h_fu.assign(C, 0);
+        HGX_TRY(hipMemcpyAsync(h_fu.data(), fu.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    }
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     float ms = 0;
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[0] = ms;
+    h_len_div = chain_len;
+    E_div = En;
+    laid_out = true;
 
-    // rounds, step by step
+    // rounds, step by step from r_lo
     HGX_TRY(hipEventRecord(ph0, stream));
+    HGX_TRY(ensure_round_cap(r_lo + 2 * kStepBatch + 2));
+    a = arrays();
     HGX_TRY(hipMemsetAsync(lr.p, 0xFF, (size_t)G * 4, stream));
-    HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(active.p, 0, (size_t)(r_cap + 1) * 4, stream));
-    HGX_TRY(hipMemsetAsync(ovf.p, 0, (size_t)(r_cap + 2) * 4, stream));
+    if (r_lo == 0) HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
+    HGX_TRY(hipMemsetAsync(active.p + r_lo, 0, (size_t)(r_cap + 1 - r_lo) * 4, stream));
+    HGX_TRY(hipMemsetAsync(ovf.p + r_lo, 0, (size_t)(r_cap + 2 - r_lo) * 4, stream));
     {
         const size_t need = (size_t)2 * C * round_k_ndw(n);
         if (FD8.n < need) {
@@ -444,8 +510,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         return A;
     };
     kbeg(K_ROUND_GATHER);
-    launch_round_gather(stream, a, 0, C, n, fd_ld);   // W'_0 = first event of every chain
-    launch_round_k_gather(stream, round_args());       // ... rebased for the per-candidate step
+    launch_round_gather(stream, a, r_lo, C, n, fd_ld);   // W'_{r_lo}: round 0 = first event of every chain
+    launch_round_k_gather(stream, round_args(), r_lo);   // ... rebased for the per-candidate step
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int launched = 0, checked = 0;
     {   // n <= 1024 (hgx_create's limit)
@@ -454,7 +520,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // knows its round without a dependent device load. Batch i+1 is queued before
         // the host looks at batch i's "any candidate left" flag (pipelined check).
         auto launch_batch = [&]() -> hipError_t {
-            const int need = (launched + 2) * kStepBatch + 2;
+            const int need = r_lo + (launched + 2) * kStepBatch + 2;
             if (need > r_cap) {
                 HGX_TRY(ensure_round_cap(need));
                 a = arrays();
@@ -496,7 +562,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 if ((int)step_nodes.size() != kStepBatch) return hipErrorUnknown;
             }
             for (int k = 0; k < kStepBatch; k++) {
-                step_round[k] = launched * kStepBatch + k;
+                step_round[k] = r_lo + launched * kStepBatch + k;
                 void* args[2] = {(void*)&step_args, (void*)&step_round[k]};
                 hipKernelNodeParams kp = step_params[k];
                 kp.kernelParams = args;
@@ -507,7 +573,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(hipGraphLaunch(step_exec, stream));
             kend(K_ROUND_SEARCH, 0);
             const int slot = launched & 1;
-            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + ((launched + 1) * kStepBatch - 1), 4,
+            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + (r_lo + (launched + 1) * kStepBatch - 1), 4,
                                    hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipEventRecord(flag_ev[slot], stream));
             launched++;
@@ -523,7 +589,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_batch());
         }
     }
-    launch_last_round(stream, launched * kStepBatch, G, C, n, wstat.p, lr.p);
+    launch_last_round(stream, r_lo + launched * kStepBatch, G, C, n, wstat.p, lr.p);
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
@@ -531,11 +597,16 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     for (int g = 0; g < G; g++) mx = std::max(mx, out.last_round[g]);
     R = mx + 1;
     out.R = R;
-    launch_wcoin(stream, a, R, C);
+    out.r_lo = std::min(r_lo, R);
+    launch_wcoin(stream, a, out.r_lo, R, C);
+    // the host copies keep the rows below r_lo
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
-    HGX_TRY(hipMemcpyAsync(out.bm.data(), Bm.p, out.bm.size() * 4, hipMemcpyDeviceToHost, stream));
-    if (R) HGX_TRY(hipMemcpyAsync(out.wflag.data(), wstat.p, out.wflag.size(), hipMemcpyDeviceToHost, stream));
+    const size_t b0 = (size_t)out.r_lo * C;
+    HGX_TRY(hipMemcpyAsync(out.bm.data() + b0, Bm.p + b0, out.bm.size() * 4 - b0 * 4, hipMemcpyDeviceToHost, stream));
+    if (R > out.r_lo)
+        HGX_TRY(hipMemcpyAsync(out.wflag.data() + b0, wstat.p + b0, out.wflag.size() - b0, hipMemcpyDeviceToHost,
+                               stream));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
@@ -544,16 +615,39 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     return collect_kernel_times();
 }
 
+// 1 + the lowest round of an event not yet received (rounds below it cannot be a
+// roundReceived any more), R when every event is received; max_unrecv = most unreceived
+// events of one chain
+int32_t Engine::recv_round_lo(const RoundsHost& rh, int& max_unrecv) const {
+    int32_t lo = R;
+    max_unrecv = 0;
+    if (E_div == 0 || rh.R == 0) return lo;
+    for (int c = 0; c < C; c++) {
+        const int32_t k = h_fu[c], len = h_len_div[c];
+        if (k >= len) continue;
+        max_unrecv = std::max(max_unrecv, len - k);
+        int32_t a = 0, b = rh.R;   // round of offset k: largest r with bm[r][c] <= k
+        while (a < b) {
+            const int32_t mid = (a + b + 1) / 2;
+            if (rh.bm[(size_t)mid * C + c] <= k) a = mid; else b = mid - 1;
+        }
+        lo = std::min(lo, a + 1);
+    }
+    return lo;
+}
+
 // ---- DecideFame -----------------------------------------------------------------
-hipError_t Engine::decide_fame(std::vector<int8_t>& fame_out) {
+hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
     fame_out.assign((size_t)R * C, 0);
-    if (R == 0) return hipSuccess;
+    r0 = std::max(r0, 0);
+    if (R <= r0) return hipSuccess;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
     kbeg(K_FAME);
-    launch_fame(stream, a, R, C, n, nw, sm, G, fame_tally);
+    launch_fame(stream, a, r0, R, C, n, nw, sm, G, fame_tally);
     kend(K_FAME, 0);
-    HGX_TRY(hipMemcpyAsync(fame_out.data(), fame.p, fame_out.size(), hipMemcpyDeviceToHost, stream));
+    const size_t o = (size_t)r0 * C;
+    HGX_TRY(hipMemcpyAsync(fame_out.data() + o, fame.p + o, fame_out.size() - o, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     float ms = 0;
@@ -564,39 +658,48 @@ hipError_t Engine::decide_fame(std::vector<int8_t>& fame_out) {
 
 // ---- FindOrder ------------------------------------------------------------------
 hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
-                              const std::vector<uint8_t>& ure, OrderHost& out) {
+                              const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
     out = OrderHost();
     out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
     out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
     out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
     out.blk_nil.assign((size_t)G * std::max(R, 1), 0);
-    if (R == 0 || E_div == 0) return hipSuccess;
+    if (R == 0 || E_div == 0 || max_unrecv == 0 || r0 >= R) return hipSuccess;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
+    const size_t o = (size_t)r0 * C;
     HGX_TRY(hipMemcpyAsync(elig.p, el.data(), (size_t)G * R, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(fw.p, famous.data(), (size_t)R * C, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(fw.p + o, famous.data() + o, (size_t)R * C - o, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(ur_empty.p, ure.data(), (size_t)G, hipMemcpyHostToDevice, stream));
     if (WLAT.n < (size_t)R * C * n) {
         HGX_TRY(WLAT.alloc((size_t)R * C * n + (size_t)C * n));
         a = arrays();
     }
     kbeg(K_THRESHOLD);
-    launch_wla_transpose(stream, a, R, G, C, n);
-    launch_threshold(stream, a, R, C, n);
+    launch_wla_transpose(stream, a, r0, R, G, C, n);
+    launch_threshold(stream, a, r0, R, C, n);
     kend(K_THRESHOLD, 0);
     HGX_TRY(hipMemsetAsync(counters.p, 0, 8, stream));
-    HGX_TRY(hipMemsetAsync(p_new.p, 0, (size_t)E_div, stream));
+    HGX_TRY(hipMemsetAsync(rcnt.p, 0, (size_t)C * 4, stream));
     kbeg(K_ROUND_RECEIVED);
-    launch_round_received(stream, a, E_div, R, C, n);
-    kend(K_ROUND_RECEIVED, (double)E_div * 16);
+    launch_round_received(stream, a, R, C, n, max_unrecv);
+    kend(K_ROUND_RECEIVED, 0);
     HGX_TRY(hipMemcpyAsync(h_small, counters.p, 8, hipMemcpyDeviceToHost, stream));
+    std::vector<int32_t> cnt(C);
+    HGX_TRY(hipMemcpyAsync(cnt.data(), rcnt.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
     const int32_t m = h_small[0];
     out.panic = h_small[1] != 0;
     out.m = m;
+    int max_cnt = 0, unrecv = 0;
+    for (int c = 0; c < C; c++) {
+        max_cnt = std::max(max_cnt, cnt[c]);
+        unrecv += h_len_div[c] - h_fu[c];
+    }
+    kadd_bytes(K_ROUND_RECEIVED, (double)unrecv * 16);
     if (out.panic || m == 0) return collect_kernel_times();
     kbeg(K_CTS);
-    launch_cts(stream, a, E_div, C, n, fd_ld, max_len);
+    launch_cts(stream, a, C, n, fd_ld, max_cnt);
     kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
     // sort keys: cts range, then (graph, rr)
     const unsigned long long init[2] = {~0ull, 0ull};
@@ -620,6 +723,8 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
     HGX_TRY(hipMemsetAsync(blk_nil.p, 0, (size_t)G * R, stream));
     launch_finish_order(stream, a, m, vals, R, n);
+    launch_fu_advance(stream, a, C);
+    for (int c = 0; c < C; c++) h_fu[c] += cnt[c];
     HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
@@ -644,6 +749,7 @@ hipError_t Engine::reset_received() {
     }
     E_div = 0;
     R = 0;
+    laid_out = false;
     return hipStreamSynchronize(stream);
 }
 

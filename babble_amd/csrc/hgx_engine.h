@@ -39,6 +39,7 @@ struct DBuf {
 // What the host bookkeeping needs after DivideRounds
 struct RoundsHost {
     int32_t R = 0;                    // rounds materialised: max over graphs of LastRound + 1
+    int32_t r_lo = 0;                 // rows below r_lo are unchanged by the last DivideRounds
     std::vector<int32_t> last_round;  // [G], -1 = no events
     std::vector<int32_t> bm;          // [(R+1) x C] first chain offset with round >= r
     std::vector<uint8_t> wflag;       // [R x C] 0 none, 1 candidate with higher round, 2 witness
@@ -84,9 +85,12 @@ class Engine {
     hipError_t get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil);
     hipError_t divide_rounds(int64_t E, const std::vector<int32_t>& chain_len,
                              const std::vector<int32_t>& chain_base, RoundsHost& out);
-    hipError_t decide_fame(std::vector<int8_t>& fame_out);
+    // fame of the witnesses of rounds >= r0 (the first undecided round); rows below stay 0
+    hipError_t decide_fame(int32_t r0, std::vector<int8_t>& fame_out);
+    // round received etc. for the events not yet received; r0 / max_unrecv from recv_round_lo
     hipError_t find_order(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
-                          const std::vector<uint8_t>& ur_empty, OrderHost& out);
+                          const std::vector<uint8_t>& ur_empty, int32_t r0, int max_unrecv, OrderHost& out);
+    int32_t recv_round_lo(const RoundsHost& rh, int& max_unrecv) const;
     // D2H of order[first, first+count) of the last find_order (async; then sync())
     hipError_t copy_order(int32_t* dst, int64_t first, int64_t count);
     hipError_t sync() { return hipStreamSynchronize(stream); }
@@ -100,6 +104,9 @@ class Engine {
 
     int n = 0, G = 0, C = 0, sm = 0, nw = 1;
     int64_t cap = 0, E = 0, E_div = 0;   // E_div: events laid out by the last divide_rounds
+    int64_t Ppos = 0;                    // chain-major positions (events + per-chain slack)
+    bool incremental = true;             // hgx_set_incremental(0): every DivideRounds rebuilds
+    bool last_rebuild = false;           // the last divide_rounds rebuilt the layout
     int32_t R = 0;
     int la_sweeps = 0;
     int compact = 0;             // coordinates of the last DivideRounds stored as uint16
@@ -124,7 +131,10 @@ class Engine {
     DevArrays arrays();
 
     int max_len = 0;
-    std::vector<int32_t> h_off;
+    bool laid_out = false;
+    std::vector<int32_t> h_off;        // [C+1] chain slots (positions), fixed until a rebuild
+    std::vector<int32_t> h_len_div;    // [C] chain lengths at the last divide_rounds
+    std::vector<int32_t> h_fu;         // [C] events of each chain received so far (a prefix)
     // gid order
     DBuf<int32_t> g_creator, g_index, g_sp, g_op, g_ntx, g_rr, g_pos;
     DBuf<int64_t> g_ts, g_cts;
@@ -138,7 +148,7 @@ class Engine {
     DBuf<int64_t> st_index, st_sp, st_op, st_ts;
     DBuf<uint8_t> st_hash, st_S;
     // chains
-    DBuf<int32_t> c_off, c_len, c_base;
+    DBuf<int32_t> c_off, c_len, c_base, c_old, fu, rcnt;
     // positions
     DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_round, p_rr;
     DBuf<uint8_t> la_chg;   // [2 x units] ping-pong dirty flags of the lastAncestors sweeps
@@ -166,7 +176,7 @@ class Engine {
     DBuf<int8_t> fame;
     // order
     DBuf<int32_t> recv_list, counters, order_gid, blk_cnt, blk_loaded;
-    DBuf<uint8_t> p_new, blk_nil;
+    DBuf<uint8_t> blk_nil;
     DBuf<uint32_t> scan_part;
     DBuf<uint64_t> key_a, key_b;
     DBuf<uint32_t> val_a, val_b, hist;

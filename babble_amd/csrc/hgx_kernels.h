@@ -37,7 +37,7 @@ struct DevArrays {
     uint8_t *elig, *fw, *ur_empty;
     int32_t* T;
     int32_t* recv_list;
-    uint8_t* p_new;       // [P] received by the current FindOrder
+    int32_t *fu, *rcnt;   // [C] per chain: events received by earlier calls (a prefix) / by this call
     uint32_t* scan_part;  // scan partials
     int32_t* counters;   // [0] received count, [1] panic flag, [2] LA changed
     // order
@@ -94,31 +94,44 @@ struct RoundArgs {
 
 int fd_tile_rows(int n, int compact);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
-void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg);
-// one Gauss-Seidel sweep over the dirty units (all when `first`); out[0] += rows
-// recomputed, out[1] += units whose values changed (marked in chg_cur; usum = per-unit sums)
+// (gids [E0, E))
+void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int seg);
+// one Gauss-Seidel sweep over the dirty units (all when `first`) from unit u0; out[0] +=
+// rows recomputed, out[1] += units whose values changed (marked in chg_cur; usum = per-unit
+// sums). c_old (incremental, else null): rows below c_old[c] are final and skipped.
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out);
-void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P);
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out, const int32_t* c_old,
+                     int64_t u0);
+// c_old (incremental, else null): only tiles from each chain's first new row; max_new = the
+// most new rows of one chain
+void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
+                     int max_new);
+// LA rows and FD entries of the new events gids [E0, E0 + m) set to none
+void launch_init_new(hipStream_t s, const DevArrays& a, int64_t E0, int64_t m, int n, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
-void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C);
+void launch_wcoin(hipStream_t s, const DevArrays& a, int r0, int R, int C);
 // one round step of round r: the per-candidate kernel (hgx_round_k.hip, n <= 256) unless
 // `block_search` or n > 256 (hgx_rounds.hip)
 hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r, int block_search);
 hipError_t launch_round_k(hipStream_t s, const RoundArgs& A, int r);
-void launch_round_k_gather(hipStream_t s, const RoundArgs& A);   // round 0's rebased rows + ovf[0]
+void launch_round_k_gather(hipStream_t s, const RoundArgs& A, int r);   // round r's rebased rows + ovf[r]
 int round_k_ndw(int n);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();     // -DHGX_STEP_PROF builds only
 void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
-void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G, int tally);
-void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n);
-void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n);
-void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n);
-// time-major tiles of 32 positions per chain (max_len = longest chain)
-void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len);
+// rounds [r0, R) (r0 = the first undecided round)
+void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n, int nw, int sm, int G, int tally);
+// rounds [r0, R) (r0 = 1 + the lowest round of an event not yet received)
+void launch_wla_transpose(hipStream_t s, const DevArrays& a, int r0, int R, int G, int C, int n);
+void launch_threshold(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n);
+// chains' unreceived events [fu, len) (max_unrecv = the most of one chain); rcnt += received
+void launch_round_received(hipStream_t s, const DevArrays& a, int R, int C, int n, int max_unrecv);
+void launch_fu_advance(hipStream_t s, const DevArrays& a, int C);           // fu += rcnt
+void launch_fu_count(hipStream_t s, const DevArrays& a, int64_t E);         // fu += received events (fu preset 0)
+// the newly received events [fu, fu + rcnt) of every chain (max_cnt = the largest rcnt)
+void launch_cts(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt);
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);

@@ -55,7 +55,7 @@ __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __
     p_cts[p] = g_cts[gid];
 }
 
-__global__ void __launch_bounds__(256) k_layout(int64_t E, const int32_t* __restrict__ g_creator,
+__global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
                                                 const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
                                                 const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
                                                 const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E, const int32_t* __rest
     __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
     __shared__ int32_t s_slot[kLayoutB];   // slot -> gid offset in the block
     __shared__ int32_t s_lo, s_hi;
-    const int64_t g0 = (int64_t)blockIdx.x * kLayoutB;
+    const int64_t g0 = E0 + (int64_t)blockIdx.x * kLayoutB;
     const int nb = (int)min<int64_t>(kLayoutB, E - g0);
     if (threadIdx.x == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
     for (int h = threadIdx.x; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
@@ -189,7 +189,8 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
                            const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
                            int nwd, int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
-                           uint8_t* __restrict__ chg_cur, int64_t* __restrict__ usum, int32_t* __restrict__ out) {
+                           uint8_t* __restrict__ chg_cur, int64_t* __restrict__ usum, int32_t* __restrict__ out,
+                           const int32_t* __restrict__ c_old, int64_t u0) {
     typedef LaWord<CT> W;
     const int lane = lane_id();
     const int gl = lane % GS;
@@ -197,7 +198,7 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
     // grid-stride over units in time-major order (one reduction + atomic per wave)
     const int64_t nunits = (int64_t)nseg * C;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x / GS;
-    for (int64_t unit = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    for (int64_t unit = u0 + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS;
          unit - (lane / GS) < nunits; unit += stride) {
         if (unit >= nunits) continue;
         const int s = (int)(unit / C), c = (int)(unit % C);
@@ -206,6 +207,8 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
         if (k0 >= len) continue;
         const int off = c_off[c];
         const int k1 = min(len, k0 + seg);
+        // incremental DivideRounds: rows of earlier calls are final (their parents are)
+        if (c_old && k1 <= c_old[c]) continue;
         if (!first) {
             // dirty iff the carry unit or an op unit of one of its rows changed last sweep
             bool d = (s > 0 && gl == 0) ? chg_prev[unit - C] != 0 : false;
@@ -297,11 +300,18 @@ __device__ __forceinline__ int wave_incl_max(int x) {
 template <typename CT>
 __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int n, int nwd,
-                           int FT, int64_t P) {
+                           int FT, int64_t P, const int32_t* __restrict__ c_old) {
     typedef Coord<CT> K;
     extern __shared__ __attribute__((aligned(16))) int32_t sm[];
-    const int c = blockIdx.x, t = blockIdx.y;
+    const int c = blockIdx.x;
     const int len = c_len[c];
+    // incremental: from the tile holding the chain's first new row (entries of earlier rows
+    // in that tile are rewritten with the same values); new positions start as none
+    int t = blockIdx.y;
+    if (c_old) {
+        if (c_old[c] >= len) return;
+        t += c_old[c] / FT;
+    }
     const int ntiles = max(1, (len + FT - 1) / FT);
     if (t >= ntiles) return;
     const int k0 = t * FT, k1 = min(len, k0 + FT), rows = k1 - k0;
@@ -448,7 +458,7 @@ __global__ void k_wcoin(int64_t RC, int C, const int32_t* __restrict__ Bm, const
 // vote tally and decisions (DecideFame, hashgraph.go:649-730). One block per
 // (graph g, round i). Votes V[x] are bit masks over the witnesses of the previous
 // round; yays = popcount(S_j[y] & V[x]). Ties vote yes; coin rounds use middleBit.
-__global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t* __restrict__ lr,
+__global__ void __launch_bounds__(256) k_fame_vote(int R, int r0, int nw, const int32_t* __restrict__ lr,
                             const uint8_t* __restrict__ wstat, const uint8_t* __restrict__ wcoin,
                             const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
                             const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
@@ -457,7 +467,8 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int nw, const int32_t*
     __shared__ int32_t dec[1024];
     __shared__ int32_t s_nx, s_und;
     __shared__ unsigned long long wm[16];   // witnesses of round j-1 (S rows may cover jumped candidates)
-    const int g = blockIdx.x / R, i = blockIdx.x % R;
+    const int RR = R - r0;
+    const int g = blockIdx.x / RR, i = r0 + blockIdx.x % RR;
     const int LR = lr[g];
     if (i > LR) return;
     const size_t gi = (size_t)g * n;
@@ -588,7 +599,7 @@ __device__ __forceinline__ void compact_witnesses(const uint8_t* __restrict__ st
 }
 
 template <bool kMfma>
-__global__ void __launch_bounds__(256) k_fame_tile(int R, int XT, const int32_t* __restrict__ lr,
+__global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const int32_t* __restrict__ lr,
                             const uint8_t* __restrict__ wstat, const uint8_t* __restrict__ wcoin,
                             const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
                             const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
@@ -599,9 +610,10 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int XT, const int32_t*
     __shared__ int32_t s_ny, s_und;
     __shared__ uint64_t wmask[2][kFameMaxW];   // witness masks of rounds j-1 / j (by parity)
     __shared__ uint64_t Vb[2][kFameTile][kFameMaxW];   // vote bit rows V[x][w] (current / next)
+    const int RR = R - r0;   // rounds [r0, R): the undecided ones and later
     const int xt = blockIdx.x % XT;
-    const int i = (blockIdx.x / XT) % R;
-    const int g = blockIdx.x / (XT * R);
+    const int i = r0 + (blockIdx.x / XT) % RR;
+    const int g = blockIdx.x / (XT * RR);
     const int LR = lr[g];
     if (i > LR) return;
     const size_t gi = (size_t)g * n;
@@ -749,10 +761,11 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int XT, const int32_t*
 // WLAT[i][g][d][c] = WLA[i][g][c][d]: per round, the lastAncestors of the candidates
 // transposed so that "which witnesses of round i see chain d up to index j" is one
 // contiguous row (k_threshold, k_cts_*). 64 x 64 tiles through LDS; eligible rounds only.
-__global__ void __launch_bounds__(256) k_wla_transpose(int R, int G, int C, int n, const uint8_t* __restrict__ elig,
+__global__ void __launch_bounds__(256) k_wla_transpose(int R, int r0, int G, int C, int n,
+                                                       const uint8_t* __restrict__ elig,
                                                        const int32_t* __restrict__ WLA, int32_t* __restrict__ WLAT) {
     __shared__ int32_t t[64][65];
-    const int ig = blockIdx.y, i = ig / G, g = ig % G;
+    const int ig = blockIdx.y, i = r0 + ig / G, g = ig % G;
     if (!elig[(size_t)g * R + i]) return;
     const int nt = (n + 63) / 64, tc = blockIdx.x % nt, td = blockIdx.x / nt;
     const size_t base = ((size_t)i * C + (size_t)g * n) * n;
@@ -771,11 +784,12 @@ __global__ void __launch_bounds__(256) k_wla_transpose(int R, int G, int C, int 
 // round i (DecideRoundReceived hashgraph.go:767-775). One wave per (i, d),
 // reading the contiguous WLAT row.
 template <int CPL>
-__global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restrict__ elig, const uint8_t* __restrict__ fw,
+__global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t* __restrict__ elig,
+                            const uint8_t* __restrict__ fw,
                             const int32_t* __restrict__ WLAT, int32_t* __restrict__ T, int C, int n) {
     const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (item >= (int64_t)R * C) return;
-    const int i = (int)(item / C), gd = (int)(item % C);
+    if (item >= (int64_t)(R - r0) * C) return;
+    const int i = r0 + (int)(item / C), gd = (int)(item % C);
     const int g = gd / n;
     if (!elig[(size_t)g * R + i]) return;
     __shared__ uint32_t whist[4][256];
@@ -802,22 +816,30 @@ __global__ void __launch_bounds__(256) k_threshold(int R, const uint8_t* __restr
 }
 
 // rr(x) = first eligible i > round(x) with Index(x) <= T[i][cr(x)]; compacts the
-// newly received positions (block-aggregated append).
-__global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const int32_t* __restrict__ p_chain,
-                                 const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
-                                 const int32_t* __restrict__ p_round, const int32_t* __restrict__ lr,
-                                 const uint8_t* __restrict__ elig, const uint8_t* __restrict__ ur_empty,
-                                 const int32_t* __restrict__ T, int32_t* __restrict__ p_rr,
-                                 uint8_t* __restrict__ p_new, int32_t* __restrict__ recv_list,
+// newly received positions (block-aggregated append). Block = (tile of 256, chain c) over
+// the chain's events not received by an earlier call, [fu[c], len[c]). The received events
+// of a chain are always a prefix of it: a famous witness that sees x sees x's self-parent,
+// so rr(self-parent) <= rr(x) under the same eligible rounds (hashgraph.go:753-799). So the
+// newly received events of chain c are [fu[c], fu[c] + rcnt[c]).
+__global__ void __launch_bounds__(256) k_round_received(int R, const int32_t* __restrict__ c_off,
+                                 const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base,
+                                 const int32_t* __restrict__ fu, const int32_t* __restrict__ p_round,
+                                 const int32_t* __restrict__ lr, const uint8_t* __restrict__ elig,
+                                 const uint8_t* __restrict__ ur_empty, const int32_t* __restrict__ T,
+                                 int32_t* __restrict__ p_rr, int32_t* __restrict__ rcnt, int32_t* __restrict__ recv_list,
                                  int32_t* __restrict__ counters, int C, int n) {
     __shared__ int32_t s_cnt, s_base;
+    const int gc = blockIdx.y;
+    const int k = fu[gc] + blockIdx.x * 256 + threadIdx.x;
+    const int len = c_len[gc];
+    if (fu[gc] + (int)blockIdx.x * 256 >= len) return;   // block-uniform
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int slot = -1;
-    if (p < Pn && p_rr[p] < 0) {
-        const int gc = p_chain[p], g = gc / n;
-        const int j = c_base[gc] + (int)(p - c_off[gc]);
+    const int64_t p = (int64_t)c_off[gc] + k;
+    if (k < len) {
+        const int g = gc / n;
+        const int j = c_base[gc] + k;
         const int r = p_round[p];
         const int LR = lr[g];
         if (r + 1 <= LR && ur_empty[g]) atomicOr(&counters[1], 1);   // Go panics on UndecidedRounds[0]
@@ -827,14 +849,44 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
         }
         if (rr >= 0) {
             p_rr[p] = rr;
-            p_new[p] = 1;
             slot = atomicAdd(&s_cnt, 1);
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&counters[0], s_cnt) : 0;
+    if (threadIdx.x == 0 && s_cnt) {
+        s_base = atomicAdd(&counters[0], s_cnt);
+        atomicAdd(&rcnt[gc], s_cnt);
+    }
     __syncthreads();
     if (slot >= 0) recv_list[s_base + slot] = (int32_t)p;
+}
+
+// fu[c] += rcnt[c] after the order of a FindOrder is written
+__global__ void k_fu_advance(int C, int32_t* __restrict__ fu, const int32_t* __restrict__ rcnt) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) fu[c] += rcnt[c];
+}
+
+// fu[c] = events of chain c already received (a prefix, see k_round_received): after a
+// rebuild of the layout, from the gid-order roundReceived
+__global__ void k_fu_count(int64_t E, const int32_t* __restrict__ g_creator, const int32_t* __restrict__ g_rr,
+                           int32_t* __restrict__ fu) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < E && g_rr[gid] >= 0) atomicAdd(&fu[g_creator[gid]], 1);
+}
+
+// new rows of an incremental DivideRounds start as none: LA rows (read before they are
+// computed by the sweeps) and FD entries (no chain has seen the new events yet)
+template <typename CT>
+__global__ void k_init_new(int64_t E0, int64_t m, const int32_t* __restrict__ g_pos, CT* __restrict__ LA,
+                           CT* __restrict__ FDT, int n, int64_t P) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * n) return;
+    const int64_t k = t / n;
+    const int i = (int)(t % n);
+    const int p = g_pos[E0 + k];
+    LA[(size_t)p * n + i] = Coord<CT>::enc_la(-1);
+    FDT[(size_t)i * P + p] = Coord<CT>::enc_fd(kMaxI32);
 }
 
 // consensus timestamp: upper median (ByTimestamp, index floor(|s|/2), event.go:227-237)
@@ -846,16 +898,18 @@ __global__ void __launch_bounds__(256) k_round_received(int64_t Pn, int R, const
 // n <= 32: one lane per event; FDT[c][p] over consecutive p is coalesced, the
 // selection is a rank count over <= 32 values in registers.
 template <int NP, typename CT>
-__global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __restrict__ p_new,
-                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+__global__ void __launch_bounds__(256) k_cts_small(const int32_t* __restrict__ fu, const int32_t* __restrict__ rcnt,
+                                                   const int32_t* __restrict__ p_rr,
                                                    const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                    const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                    const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
                                                    int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= Pn || !p_new[p]) return;
-    const int gc = p_chain[p], g = gc / n;
-    const int j = c_base[gc] + (int)(p - c_off[gc]);
+    const int gc = blockIdx.y;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rcnt[gc]) return;
+    const int g = gc / n;
+    const int64_t p = (int64_t)c_off[gc] + fu[gc] + e;
+    const int j = c_base[gc] + fu[gc] + e;
     const int i = p_rr[p];
     const size_t row = ((size_t)i * C + gc) * n;
     const size_t fb = (size_t)i * C + (size_t)g * n;
@@ -894,8 +948,8 @@ __global__ void __launch_bounds__(256) k_cts_small(int64_t Pn, const uint8_t* __
 // per event: radix select of element floor(m/2) in registers.
 constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8
 template <int NPAD, typename CT>
-__global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __restrict__ p_new,
-                                                  const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+__global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu, const int32_t* __restrict__ rcnt,
+                                                  const int32_t* __restrict__ p_rr,
                                                   const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                   const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                   const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
@@ -910,12 +964,13 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
     __shared__ int32_t e_ovf[T];
     __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
     __shared__ int32_t s_any;
-    // time-major tiles: block i = tile i / C of chain i % C, so the blocks in flight cover
-    // every chain at about the same time and their timestamp gathers (events of other
-    // chains at that time) share lines in L2
+    // time-major tiles over the newly received events [fu, fu + rcnt) of each chain: block
+    // i = tile i / C of chain i % C, so the blocks in flight cover every chain at about the
+    // same time and their timestamp gathers (events of other chains at that time) share
+    // lines in L2
     const int tc = (int)(blockIdx.x % (unsigned)C), tt = (int)(blockIdx.x / (unsigned)C);
-    const int64_t p0 = (int64_t)c_off[tc] + (int64_t)tt * T;
-    const int64_t pend = min((int64_t)c_off[tc + 1], Pn);
+    const int64_t p0 = (int64_t)c_off[tc] + fu[tc] + (int64_t)tt * T;
+    const int64_t pend = (int64_t)c_off[tc] + fu[tc] + rcnt[tc];
     if (threadIdx.x == 0) s_any = 0;
     for (int k = threadIdx.x; k < T * (NPAD / 32); k += 256) mem[k / (NPAD / 32)][k % (NPAD / 32)] = 0;
     __syncthreads();
@@ -923,9 +978,9 @@ __global__ void __launch_bounds__(256) k_cts_tile(int64_t Pn, const uint8_t* __r
         const int e = threadIdx.x;
         const int64_t p = p0 + e;
         int row = -1;
-        if (p < pend && p_new[p]) {
+        if (p < pend) {
             s_any = 1;
-            const int gc = p_chain[p], g = gc / n, i = p_rr[p];
+            const int gc = tc, g = gc / n, i = p_rr[p];
             row = i;
             e_j[e] = c_base[gc] + (int)(p - c_off[gc]);
             e_fb[e] = i * C + g * n;   // < 2^31: round tables are int32-indexed
@@ -1382,24 +1437,25 @@ __global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const i
 
 static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
 
-void launch_layout(hipStream_t s, int64_t E, const DevArrays& a, int C, int seg) {
-    if (E <= 0) return;
-    hipLaunchKernelGGL(k_layout, dim3(nblk(E, kLayoutB)), dim3(256), 0, s, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
+void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int seg) {
+    if (E <= E0) return;
+    hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
                        a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_ts,
                        a.p_rr, a.p_cts, C, seg);
 }
 
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out) {
+                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out, const int32_t* c_old,
+                     int64_t u0) {
     const int nseg = (max_len + seg - 1) / seg;
-    if (nseg == 0) return;
+    if ((int64_t)nseg * C <= u0) return;
     const int nwd = a.compact ? n / 2 : n;
 #define LA_LAUNCH_T(GS, CPL, CT)                                                                              \
     {                                                                                                         \
-        const int64_t threads = (int64_t)nseg * C * GS;                                                       \
+        const int64_t threads = ((int64_t)nseg * C - u0) * GS;                                                \
         hipLaunchKernelGGL((k_la_sweep<GS, CPL, CT>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, \
                            s, (uint32_t*)a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nwd, nseg, seg, \
-                           first, chg_prev, chg_cur, usum, out);                                              \
+                           first, chg_prev, chg_cur, usum, out, c_old, u0);                                   \
     }
 #define LA_LAUNCH(GS, CPL, NW)                                        \
     {                                                                 \
@@ -1421,18 +1477,21 @@ int fd_tile_rows(int n, int compact) {
     return ft;
 }
 
-void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P) {
+void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
+                     int max_new) {
     const int ft = fd_tile_rows(n, a.compact);
-    const int tiles = max(1, (max_len + ft - 1) / ft);
+    // incremental (c_old): tiles from the one holding each chain's first new row;
+    // max_new = the most new rows of a chain
+    const int tiles = c_old ? (max_new + ft - 1) / ft + 1 : max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
     // + 8 waves x 64 owner slots
     const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n + 8 * 64) * sizeof(int32_t);
     if (a.compact)
         hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P);
+                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
     else
         hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P);
+                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
 }
 
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
@@ -1446,21 +1505,23 @@ void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n,
                            a.WFD, a.wflag, a.wcoin, C, n, P, 0);
 }
 
-void launch_wcoin(hipStream_t s, const DevArrays& a, int R, int C) {
-    const int64_t RC = (int64_t)R * C;
+void launch_wcoin(hipStream_t s, const DevArrays& a, int r0, int R, int C) {
+    const int64_t RC = (int64_t)(R - r0) * C;
     if (RC <= 0) return;
-    hipLaunchKernelGGL(k_wcoin, dim3(nblk(RC, 256)), dim3(256), 0, s, RC, C, a.Bm, a.c_off, a.c_len, a.p_gid, a.g_coin,
-                       a.wcoin);
+    const size_t o = (size_t)r0 * C;
+    hipLaunchKernelGGL(k_wcoin, dim3(nblk(RC, 256)), dim3(256), 0, s, RC, C, a.Bm + o, a.c_off, a.c_len, a.p_gid,
+                       a.g_coin, a.wcoin + o);
 }
 
 // fame kernel choice (hgx_set_fame_tally): the witness-tiled kernel with the popcount tally
 // by default (measured faster than the int8 MFMA tally at every n); the
 // per-round popcount kernel and the MFMA tally stay selectable for measurement.
-void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw, int sm, int G, int tally) {
+void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n, int nw, int sm, int G, int tally) {
+    if (R <= r0) return;
     const int mode = tally == 1 ? 0 : tally == 2 ? 2 : 1;
     if (mode != 0 && n <= kFameMaxW * 64) {
         const int XT = (n + kFameTile - 1) / kFameTile;
-        const dim3 grid((unsigned)((int64_t)G * R * XT));
+        const dim3 grid((unsigned)((int64_t)G * (R - r0) * XT));
         if (mode == 2) {
             const int shm = kFameTile * (nw * 64 + 16);
             static bool attr = false;
@@ -1469,50 +1530,70 @@ void launch_fame(hipStream_t s, const DevArrays& a, int R, int C, int n, int nw,
                                           kFameTile * (kFameMaxW * 64 + 16));
                 attr = true;
             }
-            hipLaunchKernelGGL(k_fame_tile<true>, grid, dim3(256), shm, s, R, XT, a.lr, a.wstat, a.wcoin, a.Bm,
+            hipLaunchKernelGGL(k_fame_tile<true>, grid, dim3(256), shm, s, R, r0, XT, a.lr, a.wstat, a.wcoin, a.Bm,
                                a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
         } else {
-            hipLaunchKernelGGL(k_fame_tile<false>, grid, dim3(256), 0, s, R, XT, a.lr, a.wstat, a.wcoin, a.Bm,
+            hipLaunchKernelGGL(k_fame_tile<false>, grid, dim3(256), 0, s, R, r0, XT, a.lr, a.wstat, a.wcoin, a.Bm,
                                a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
         }
         return;
     }
-    hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * R), dim3(256), 0, s, R, nw, a.lr, a.wstat, a.wcoin, a.Bm,
+    hipLaunchKernelGGL(k_fame_vote, dim3((unsigned)G * (R - r0)), dim3(256), 0, s, R, r0, nw, a.lr, a.wstat, a.wcoin, a.Bm,
                        a.c_base, a.WLA, a.Smat, a.Vbuf, a.fame, C, n, sm);
 }
 
-void launch_wla_transpose(hipStream_t s, const DevArrays& a, int R, int G, int C, int n) {
-    if (R <= 0) return;
+void launch_wla_transpose(hipStream_t s, const DevArrays& a, int r0, int R, int G, int C, int n) {
+    if (R <= r0) return;
     const int nt = (n + 63) / 64;
-    hipLaunchKernelGGL(k_wla_transpose, dim3(nt * nt, R * G), dim3(256), 0, s, R, G, C, n, a.elig, a.WLA, a.WLAT);
+    hipLaunchKernelGGL(k_wla_transpose, dim3(nt * nt, (R - r0) * G), dim3(256), 0, s, R, r0, G, C, n, a.elig, a.WLA,
+                       a.WLAT);
 }
 
-void launch_threshold(hipStream_t s, const DevArrays& a, int R, int C, int n) {
-    if (R <= 0) return;
+void launch_threshold(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n) {
+    if (R <= r0) return;
 #define TH_LAUNCH(GS, CPL, NW)                                                                                \
     {                                                                                                         \
-        const int64_t threads = (int64_t)R * C * 64;                                                          \
-        hipLaunchKernelGGL((k_threshold<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, a.elig, a.fw,   \
+        const int64_t threads = (int64_t)(R - r0) * C * 64;                                                   \
+        hipLaunchKernelGGL((k_threshold<CPL>), dim3(nblk(threads, 256)), dim3(256), 0, s, R, r0, a.elig, a.fw, \
                            a.WLAT, a.T, C, n);                                                                \
     }
     HGX_DISPATCH_N(n, TH_LAUNCH);
 #undef TH_LAUNCH
 }
 
-void launch_round_received(hipStream_t s, const DevArrays& a, int64_t Pn, int R, int C, int n) {
-    if (Pn <= 0) return;
-    hipLaunchKernelGGL(k_round_received, dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, R, a.p_chain, a.c_off, a.c_base,
-                       a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.p_new, a.recv_list, a.counters, C, n);
+void launch_round_received(hipStream_t s, const DevArrays& a, int R, int C, int n, int max_unrecv) {
+    if (max_unrecv <= 0) return;
+    hipLaunchKernelGGL(k_round_received, dim3(nblk(max_unrecv, 256), C), dim3(256), 0, s, R, a.c_off, a.c_len,
+                       a.c_base, a.fu, a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.rcnt, a.recv_list,
+                       a.counters, C, n);
+}
+
+void launch_fu_advance(hipStream_t s, const DevArrays& a, int C) {
+    hipLaunchKernelGGL(k_fu_advance, dim3(nblk(C, 256)), dim3(256), 0, s, C, a.fu, a.rcnt);
+}
+
+void launch_fu_count(hipStream_t s, const DevArrays& a, int64_t E) {
+    if (E > 0) hipLaunchKernelGGL(k_fu_count, dim3(nblk(E, 256)), dim3(256), 0, s, E, a.g_creator, a.g_rr, a.fu);
+}
+
+void launch_init_new(hipStream_t s, const DevArrays& a, int64_t E0, int64_t m, int n, int64_t P) {
+    if (m <= 0) return;
+    if (a.compact)
+        hipLaunchKernelGGL(k_init_new<uint16_t>, dim3(nblk(m * n, 256)), dim3(256), 0, s, E0, m, a.g_pos,
+                           (uint16_t*)a.LA, (uint16_t*)a.FDT, n, P);
+    else
+        hipLaunchKernelGGL(k_init_new<int32_t>, dim3(nblk(m * n, 256)), dim3(256), 0, s, E0, m, a.g_pos,
+                           (int32_t*)a.LA, (int32_t*)a.FDT, n, P);
 }
 
 template <int NP, typename CT>
-static void cts_small_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P) {
-    hipLaunchKernelGGL((k_cts_small<NP, CT>), dim3(nblk(Pn, 256)), dim3(256), 0, s, Pn, a.p_new, a.p_chain, a.p_rr,
+static void cts_small_launch(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
+    hipLaunchKernelGGL((k_cts_small<NP, CT>), dim3(nblk(max_cnt, 256), C), dim3(256), 0, s, a.fu, a.rcnt, a.p_rr,
                        a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
 }
 
 template <int NPAD, typename CT>
-static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
+static void cts_tile_launch(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
     const size_t lds = (size_t)NPAD * (kCtsTile + 1) * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
@@ -1520,29 +1601,29 @@ static void cts_tile_launch(hipStream_t s, const DevArrays& a, int64_t Pn, int C
                                   (int)lds);
         attr = true;
     }
-    const unsigned grid = (unsigned)((int64_t)C * ((max_len + kCtsTile - 1) / kCtsTile));
+    const unsigned grid = (unsigned)((int64_t)C * ((max_cnt + kCtsTile - 1) / kCtsTile));
     if (grid == 0) return;
-    hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, Pn, a.p_new, a.p_chain, a.p_rr,
+    hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, a.fu, a.rcnt, a.p_rr,
                        a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
 }
 
 template <typename CT>
-static void launch_cts_t(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
-    if (n <= 4) cts_small_launch<4, CT>(s, a, Pn, C, n, P);
-    else if (n <= 8) cts_small_launch<8, CT>(s, a, Pn, C, n, P);
-    else if (n <= 16) cts_small_launch<16, CT>(s, a, Pn, C, n, P);
-    else if (n <= 32) cts_small_launch<32, CT>(s, a, Pn, C, n, P);
-    else if (n <= 64) cts_tile_launch<64, CT>(s, a, Pn, C, n, P, max_len);
-    else if (n <= 128) cts_tile_launch<128, CT>(s, a, Pn, C, n, P, max_len);
-    else if (n <= 256) cts_tile_launch<256, CT>(s, a, Pn, C, n, P, max_len);
-    else if (n <= 512) cts_tile_launch<512, CT>(s, a, Pn, C, n, P, max_len);
-    else cts_tile_launch<1024, CT>(s, a, Pn, C, n, P, max_len);
+static void launch_cts_t(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
+    if (n <= 4) cts_small_launch<4, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 8) cts_small_launch<8, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 16) cts_small_launch<16, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 32) cts_small_launch<32, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 64) cts_tile_launch<64, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 128) cts_tile_launch<128, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 256) cts_tile_launch<256, CT>(s, a, C, n, P, max_cnt);
+    else if (n <= 512) cts_tile_launch<512, CT>(s, a, C, n, P, max_cnt);
+    else cts_tile_launch<1024, CT>(s, a, C, n, P, max_cnt);
 }
 
-void launch_cts(hipStream_t s, const DevArrays& a, int64_t Pn, int C, int n, int64_t P, int max_len) {
-    if (Pn <= 0) return;
-    if (a.compact) launch_cts_t<uint16_t>(s, a, Pn, C, n, P, max_len);
-    else launch_cts_t<int32_t>(s, a, Pn, C, n, P, max_len);
+void launch_cts(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
+    if (max_cnt <= 0) return;
+    if (a.compact) launch_cts_t<uint16_t>(s, a, C, n, P, max_cnt);
+    else launch_cts_t<int32_t>(s, a, C, n, P, max_cnt);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

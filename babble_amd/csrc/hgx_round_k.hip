@@ -494,33 +494,35 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     RK_PROF_END();
 }
 
-// round 0's candidate rows (the first event of every chain), rebased to base(0) = c_base,
-// from the row-major WFD rows k_round_gather has just written (raw uint16 or int32 FD)
+// round r's candidate rows (round 0: the first event of every chain; r > 0: the restart
+// round of an incremental DivideRounds), rebased to base(r) = c_base + Bm[r-1], from the
+// row-major WFD rows k_round_gather has just written (raw uint16 or int32 FD)
 template <typename CT>
-__global__ void k_round_k_gather(RoundArgs A, int ndw) {
+__global__ void k_round_k_gather(RoundArgs A, int ndw, int r) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)A.C * ndw) return;
     const int gc = (int)(t / ndw), d = (int)(t % ndw);
-    const int n = A.n, g = gc / n;
+    const int n = A.n, C = A.C, g = gc / n;
     uint32_t w = 0;
     bool of = false;
-    const bool have = A.c_len[gc] > 0;
-    const CT* __restrict__ row = (const CT*)A.WFD + (size_t)gc * n;   // round 0's rows
+    const bool have = A.wflag[(size_t)r * C + gc] != 0;
+    const CT* __restrict__ row = (const CT*)A.WFD + ((size_t)r * C + gc) * n;
     for (int q = 0; q < 4; q++) {
         const int i = 4 * d + q;
         uint32_t v = 127u;
         if (have && i < n) {
             const int32_t f = Coord<CT>::fd(row[i]);
             if (f != kMaxI32) {
-                const int32_t x = f - A.c_base[g * n + i] + 1;
+                const int32_t bs = A.c_base[g * n + i] + (r > 0 ? A.Bm[(size_t)(r - 1) * C + g * n + i] : 0);
+                const int32_t x = f - bs + 1;
                 if (x > 126) of = true;
                 else v = (uint32_t)x;
             }
         }
         w |= v << (8 * q);
     }
-    A.FD8[(size_t)gc * ndw + d] = w;
-    if (of) A.ovf[0] = 1;
+    A.FD8[((size_t)(r & 1) * C + gc) * ndw + d] = w;
+    if (of) A.ovf[r] = 1;
 }
 
 int round_k_ndw(int n) {
@@ -573,14 +575,14 @@ hipError_t launch_round_k(hipStream_t st, const RoundArgs& A, int s) {
     return A.compact ? launch_round_k_t<uint16_t>(st, A, s) : launch_round_k_t<int32_t>(st, A, s);
 }
 
-void launch_round_k_gather(hipStream_t st, const RoundArgs& A) {
+void launch_round_k_gather(hipStream_t st, const RoundArgs& A, int r) {
     const int ndw = round_k_ndw(A.n);
     const int64_t work = (int64_t)A.C * ndw;
     if (work <= 0) return;
     if (A.compact)
-        hipLaunchKernelGGL(k_round_k_gather<uint16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw);
+        hipLaunchKernelGGL(k_round_k_gather<uint16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, r);
     else
-        hipLaunchKernelGGL(k_round_k_gather<int32_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw);
+        hipLaunchKernelGGL(k_round_k_gather<int32_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, r);
 }
 
 }  // namespace hgx

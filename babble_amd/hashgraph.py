@@ -318,10 +318,11 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(7, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 7)
+        out = np.zeros(10, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 10)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
-                    la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]))
+                    la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
+                    la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
@@ -334,6 +335,11 @@ class Hashgraph:
         m = {"candidate": 0, "block": 1}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
+
+    def set_incremental(self, on: bool):
+        """DivideRounds schedule: incremental (default) or full recompute on every call."""
+        if self.L.hgx_set_incremental(self.ctx, 1 if on else 0) != 0:
+            raise ValueError("invalid schedule")
 
     def reserve_rounds(self, rounds: int):
         """Size the per-round tables (before the first DivideRounds; small values exercise growth)."""

@@ -221,7 +221,9 @@ int32_t hgx_sha256_bench(int32_t device, int64_t count, int32_t min_len, int32_t
 
 /* ---- timing / instrumentation --------------------------------------------- */
 /* per-phase device times (ms) of the last calls: coords, rounds, fame, order; then
- * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16) */
+ * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16); then of the last
+ * DivideRounds: lastAncestors rows recomputed, 1 if it rebuilt the layout (0: incremental),
+ * the first round step it ran */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
  * name of the kernel, summed device ms, launches, algorithmic bytes moved */
@@ -240,6 +242,11 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds round step for n <= 256: 0 = one lane per candidate, 8-bit rebased compares
  * (default, hgx_round_k.hip), 1 = block binary search (hgx_rounds.hip). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
+/* DivideRounds schedule: 1 = incremental (default: a call after more InsertEvents extends
+ * lastAncestors/firstDescendants for the new events only and resumes the round steps at the
+ * lowest round that can change; FindOrder works on the events not yet received), 0 = every
+ * call recomputes from the whole DAG. Same results. */
+int32_t hgx_set_incremental(hgx_ctx* ctx, int32_t on);
 /* Size the per-round device tables for `rounds` rounds (they grow on demand during
  * DivideRounds); before the first DivideRounds only. A small value exercises the growth path. */
 int32_t hgx_reserve_rounds(hgx_ctx* ctx, int32_t rounds);
