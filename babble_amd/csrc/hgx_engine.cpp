@@ -68,6 +68,8 @@ Engine::~Engine() {
     if (h_small) (void)hipHostFree(h_small);
     for (auto e : flag_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto e : la_ev)
+        if (e) (void)hipEventDestroy(e);
     drop_step_graph();
     if (stream) (void)hipStreamDestroy(stream);
 }
@@ -125,12 +127,13 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     fd_ld = (Ppos + 1) & ~(int64_t)1;
     HGX_TRY(LA.alloc(PP * n));
     HGX_TRY(FDT.alloc((size_t)fd_ld * n + 128));   // slack: compact window staging reads past a column
-    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8)); HGX_TRY(order_gid.alloc(P));
+    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8 + 4 * kLaRing)); HGX_TRY(order_gid.alloc(P));
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
     HGX_TRY(minmax.alloc(2));
     HGX_TRY(lr.alloc(G));
+    for (auto& e : la_ev) HGX_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[1], hipEventDisableTiming));
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
@@ -441,31 +444,46 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             if (chain_len[c] > h_len_div[c]) smin = std::min(smin, h_len_div[c] / seg);
         u0 = (int64_t)smin * C;
     }
-    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.grow_copy(2 * nunits, 0, stream));
-    if (la_usum.n < nunits) HGX_TRY(la_usum.grow_copy(nunits, la_usum.n, stream));
+    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.grow_copy(std::max(2 * nunits, 2 * la_chg.n), 0, stream));
+    if (la_usum.n < nunits) HGX_TRY(la_usum.grow_copy(std::max(nunits, 2 * la_usum.n), la_usum.n, stream));
     HGX_TRY(hipMemsetAsync(la_chg.p, 0, 2 * nunits, stream));   // no stale flags of an earlier call
     const int32_t* cold = rebuild ? nullptr : c_old.p;
     la_sweeps = 0;
     la_rows = 0;
-    for (;;) {
-        uint8_t* chg_prev = la_chg.p + (size_t)(la_sweeps & 1) * nunits;
-        uint8_t* chg_cur = la_chg.p + (size_t)((la_sweeps + 1) & 1) * nunits;
-        HGX_TRY(hipMemsetAsync(chg_cur + u0, 0, nunits - (size_t)u0, stream));
-        HGX_TRY(hipMemsetAsync(counters.p + 2, 0, 8, stream));
-        HGX_TRY(hipMemsetAsync(counters.p + 4, 0, 4, stream));
-        kbeg(K_LA_SWEEP);
-        launch_la_sweep(stream, a, C, n, max_len, seg, la_sweeps == 0 ? 1 : 0, chg_prev, chg_cur, la_usum.p,
-                        counters.p + 2, cold, u0);
-        kend(K_LA_SWEEP, 0);
-        HGX_TRY(hipMemcpyAsync(h_small, counters.p + 2, 12, hipMemcpyDeviceToHost, stream));
-        HGX_TRY(hipStreamSynchronize(stream));
-        // algorithmic bytes of the rows this sweep recomputed (read the two
-        // parent rows, write the row, 12n + 16; the self-parent row is the register carry)
-        la_rows += h_small[0];
-        kadd_bytes(K_LA_SWEEP, (double)h_small[0] * (3.0 * csz * n + 16));
-        la_sweeps++;
-        if (h_small[1] == 0) break;
-        if (la_sweeps > 100000) return hipErrorUnknown;
+    {
+        // sweep k's counters in ring slot k % kLaRing; up to kLaAhead sweeps are queued
+        // before the host reads the oldest one's "units changed" (a sweep after the one that
+        // changed nothing finds no dirty unit and does nothing)
+        int launched_s = 0;
+        auto launch_sweep = [&]() -> hipError_t {
+            const int slot = launched_s % kLaRing;
+            uint8_t* chg_prev = la_chg.p + (size_t)(launched_s & 1) * nunits;
+            uint8_t* chg_cur = la_chg.p + (size_t)((launched_s + 1) & 1) * nunits;
+            int32_t* cnt = counters.p + 8 + 4 * slot;
+            HGX_TRY(hipMemsetAsync(chg_cur + u0, 0, nunits - (size_t)u0, stream));
+            HGX_TRY(hipMemsetAsync(cnt, 0, 16, stream));
+            kbeg(K_LA_SWEEP);
+            launch_la_sweep(stream, a, C, n, max_len, seg, launched_s == 0 ? 1 : 0, chg_prev, chg_cur, la_usum.p, cnt,
+                            cold, u0);
+            kend(K_LA_SWEEP, 0);
+            HGX_TRY(hipMemcpyAsync(h_small + 16 + 4 * slot, cnt, 8, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipEventRecord(la_ev[slot], stream));
+            launched_s++;
+            return hipSuccess;
+        };
+        for (;;) {
+            while (launched_s < la_sweeps + kLaAhead) HGX_TRY(launch_sweep());
+            const int slot = la_sweeps % kLaRing;
+            HGX_TRY(hipEventSynchronize(la_ev[slot]));
+            const int32_t rows = h_small[16 + 4 * slot], changed = h_small[16 + 4 * slot + 1];
+            // algorithmic bytes of the rows this sweep recomputed (read the two
+            // parent rows, write the row, 12n + 16; the self-parent row is the register carry)
+            la_rows += rows;
+            kadd_bytes(K_LA_SWEEP, (double)rows * (3.0 * csz * n + 16));
+            la_sweeps++;
+            if (changed == 0) break;
+            if (la_sweeps > 100000) return hipErrorUnknown;
+        }
     }
     kbeg(K_FD_BUILD);
     launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
@@ -514,33 +532,37 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     launch_round_k_gather(stream, round_args(), r_lo);   // ... rebased for the per-candidate step
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int launched = 0, checked = 0;
+    // a rebuild replays kStepBatch steps per hipGraph; a resumed call (a few rounds) kStepBatchSmall
+    StepGraph& sgr = step_g[rebuild ? 0 : 1];
+    const int nb = rebuild ? kStepBatch : kStepBatchSmall;
     {   // n <= 1024 (hgx_create's limit)
-        // kStepBatch step nodes replayed as one hipGraph; before each replay the nodes'
-        // round arguments are rewritten (hipGraphExecKernelNodeSetParams), so a step
-        // knows its round without a dependent device load. Batch i+1 is queued before
-        // the host looks at batch i's "any candidate left" flag (pipelined check).
+        // nb step nodes replayed as one hipGraph; before each replay the nodes' round
+        // arguments are rewritten (hipGraphExecKernelNodeSetParams), so a step knows its
+        // round without a dependent device load. Batch i+1 is queued before the host looks
+        // at batch i's "any candidate left" flag (pipelined check).
         auto launch_batch = [&]() -> hipError_t {
-            const int need = r_lo + (launched + 2) * kStepBatch + 2;
+            const int need = r_lo + (launched + 2) * nb + 2;
             if (need > r_cap) {
                 HGX_TRY(ensure_round_cap(need));
                 a = arrays();
             }
-            if (!step_exec || step_kernel_captured != round_kernel || step_compact != compact) {
-                drop_step_graph();
-                step_args = round_args();
-                step_kernel_captured = round_kernel;
-                step_compact = compact;
+            if (!sgr.exec || sgr.kernel != round_kernel || sgr.compact != compact || sgr.nb != nb) {
+                sgr.drop();
+                sgr.args = round_args();
+                sgr.kernel = round_kernel;
+                sgr.compact = compact;
+                sgr.nb = nb;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                for (int k = 0; k < kStepBatch; k++) (void)launch_round_step(stream, step_args, k, round_kernel);
-                HGX_TRY(hipStreamEndCapture(stream, &step_graph));
-                HGX_TRY(hipGraphInstantiate(&step_exec, step_graph, nullptr, nullptr, 0));
+                for (int k = 0; k < nb; k++) (void)launch_round_step(stream, sgr.args, k, round_kernel);
+                HGX_TRY(hipStreamEndCapture(stream, &sgr.graph));
+                HGX_TRY(hipGraphInstantiate(&sgr.exec, sgr.graph, nullptr, nullptr, 0));
                 // the step nodes in launch order (a linear chain)
                 size_t nn = 0;
-                HGX_TRY(hipGraphGetNodes(step_graph, nullptr, &nn));
+                HGX_TRY(hipGraphGetNodes(sgr.graph, nullptr, &nn));
                 std::vector<hipGraphNode_t> nodes(nn);
-                HGX_TRY(hipGraphGetNodes(step_graph, nodes.data(), &nn));
-                step_nodes.clear();
-                step_params.clear();
+                HGX_TRY(hipGraphGetNodes(sgr.graph, nodes.data(), &nn));
+                sgr.nodes.clear();
+                sgr.params.clear();
                 hipGraphNode_t cur = nullptr;
                 for (auto nd : nodes) {
                     size_t nd_deps = 0;
@@ -550,8 +572,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 while (cur) {
                     hipKernelNodeParams kp;
                     HGX_TRY(hipGraphKernelNodeGetParams(cur, &kp));
-                    step_nodes.push_back(cur);
-                    step_params.push_back(kp);
+                    sgr.nodes.push_back(cur);
+                    sgr.params.push_back(kp);
                     size_t nd_out = 0;
                     HGX_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd_out));
                     if (nd_out == 0) break;
@@ -559,21 +581,21 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                     HGX_TRY(hipGraphNodeGetDependentNodes(cur, outs.data(), &nd_out));
                     cur = outs[0];
                 }
-                if ((int)step_nodes.size() != kStepBatch) return hipErrorUnknown;
+                if ((int)sgr.nodes.size() != nb) return hipErrorUnknown;
             }
-            for (int k = 0; k < kStepBatch; k++) {
-                step_round[k] = r_lo + launched * kStepBatch + k;
-                void* args[2] = {(void*)&step_args, (void*)&step_round[k]};
-                hipKernelNodeParams kp = step_params[k];
+            for (int k = 0; k < nb; k++) {
+                sgr.round[k] = r_lo + launched * nb + k;
+                void* args[2] = {(void*)&sgr.args, (void*)&sgr.round[k]};
+                hipKernelNodeParams kp = sgr.params[k];
                 kp.kernelParams = args;
                 kp.extra = nullptr;
-                HGX_TRY(hipGraphExecKernelNodeSetParams(step_exec, step_nodes[k], &kp));
+                HGX_TRY(hipGraphExecKernelNodeSetParams(sgr.exec, sgr.nodes[k], &kp));
             }
             kbeg(K_ROUND_SEARCH);
-            HGX_TRY(hipGraphLaunch(step_exec, stream));
+            HGX_TRY(hipGraphLaunch(sgr.exec, stream));
             kend(K_ROUND_SEARCH, 0);
             const int slot = launched & 1;
-            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + (r_lo + (launched + 1) * kStepBatch - 1), 4,
+            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + (r_lo + (launched + 1) * nb - 1), 4,
                                    hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipEventRecord(flag_ev[slot], stream));
             launched++;
@@ -589,7 +611,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_batch());
         }
     }
-    launch_last_round(stream, r_lo + launched * kStepBatch, G, C, n, wstat.p, lr.p);
+    launch_last_round(stream, r_lo + launched * nb, G, C, n, wstat.p, lr.p);
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
@@ -671,8 +693,8 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemcpyAsync(elig.p, el.data(), (size_t)G * R, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(fw.p + o, famous.data() + o, (size_t)R * C - o, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(ur_empty.p, ure.data(), (size_t)G, hipMemcpyHostToDevice, stream));
-    if (WLAT.n < (size_t)R * C * n) {
-        HGX_TRY(WLAT.alloc((size_t)R * C * n + (size_t)C * n));
+    if (WLAT.n < (size_t)R * C * n) {   // grown geometrically: R grows by a round or two per call
+        HGX_TRY(WLAT.alloc(std::max((size_t)R * C * n + (size_t)C * n, 2 * WLAT.n)));
         a = arrays();
     }
     kbeg(K_THRESHOLD);
@@ -701,23 +723,30 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     kbeg(K_CTS);
     launch_cts(stream, a, C, n, fd_ld, max_cnt);
     kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
-    // sort keys: cts range, then (graph, rr)
-    const unsigned long long init[2] = {~0ull, 0ull};
-    HGX_TRY(hipMemcpyAsync(minmax.p, init, 16, hipMemcpyHostToDevice, stream));
-    launch_minmax(stream, a, m);
-    unsigned long long mm[2];
-    HGX_TRY(hipMemcpyAsync(mm, minmax.p, 16, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipStreamSynchronize(stream));
-    const int64_t cmin = (int64_t)(mm[0] ^ 0x8000000000000000ull);
-    const int64_t cmax = (int64_t)(mm[1] ^ 0x8000000000000000ull);
-    const int cts_bits = bitlen((uint64_t)(cmax - cmin));
-    const int seg_bits = bitlen((uint64_t)G * (uint64_t)R - 1);
     uint32_t* vals = nullptr;
-    uint64_t* keys = nullptr;
-    kbeg(K_SORT);
-    launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
-    kend(K_SORT, (double)m * 24.0 *
-                     (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8 : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+    if (sort_small_ok(m)) {
+        kbeg(K_SORT);
+        launch_sort_small(stream, a, m, n, &vals);
+        kend(K_SORT, (double)m * 24.0);
+    } else {
+        // sort keys: cts range, then (graph, rr)
+        const unsigned long long init[2] = {~0ull, 0ull};
+        HGX_TRY(hipMemcpyAsync(minmax.p, init, 16, hipMemcpyHostToDevice, stream));
+        launch_minmax(stream, a, m);
+        unsigned long long mm[2];
+        HGX_TRY(hipMemcpyAsync(mm, minmax.p, 16, hipMemcpyDeviceToHost, stream));
+        HGX_TRY(hipStreamSynchronize(stream));
+        const int64_t cmin = (int64_t)(mm[0] ^ 0x8000000000000000ull);
+        const int64_t cmax = (int64_t)(mm[1] ^ 0x8000000000000000ull);
+        const int cts_bits = bitlen((uint64_t)(cmax - cmin));
+        const int seg_bits = bitlen((uint64_t)G * (uint64_t)R - 1);
+        uint64_t* keys = nullptr;
+        kbeg(K_SORT);
+        launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
+        kend(K_SORT, (double)m * 24.0 *
+                         (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
+                                                    : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+    }
     HGX_TRY(hipMemsetAsync(blk_cnt.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
     HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
@@ -797,10 +826,14 @@ hipError_t Engine::get_coords(int64_t gid, int32_t* la, int32_t* fd) {
 
 
 namespace hgx {
+void StepGraph::drop() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+}
+
 void Engine::drop_step_graph() {
-    if (step_exec) (void)hipGraphExecDestroy(step_exec);
-    if (step_graph) (void)hipGraphDestroy(step_graph);
-    step_exec = nullptr;
-    step_graph = nullptr;
+    for (auto& g : step_g) g.drop();
 }
 }  // namespace hgx

@@ -13,7 +13,20 @@
 namespace hgx {
 
 
-constexpr int kStepBatch = 16;   // round steps per hipGraph replay
+constexpr int kStepBatch = 16;        // round steps per hipGraph replay (a full DivideRounds)
+constexpr int kStepBatchSmall = 4;    // ... when resuming at the lowest changed round
+
+// kStepBatch round steps captured as one hipGraph, replayed with rewritten round arguments
+struct StepGraph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<hipGraphNode_t> nodes;   // the step nodes, in order
+    std::vector<hipKernelNodeParams> params;
+    RoundArgs args{};
+    int kernel = -1, compact = -1, nb = 0;   // what the graph was captured for
+    int32_t round[64] = {};
+    void drop();
+};
 
 enum KernelId {
     K_LAYOUT = 0, K_LA_SWEEP, K_FD_BUILD, K_ROUND_GATHER, K_ROUND_SEARCH, K_FAME, K_THRESHOLD,
@@ -161,13 +174,9 @@ class Engine {
     int32_t r_cap = 0;
     DBuf<int32_t> Bm, WLA, WFD, WLAT, Tthr, active, lr;
     hipEvent_t flag_ev[2] = {nullptr, nullptr};
-    hipGraph_t step_graph = nullptr;       // kStepBatch round steps, replayed per batch
-    hipGraphExec_t step_exec = nullptr;
-    std::vector<hipGraphNode_t> step_nodes;      // the kStepBatch step nodes, in order
-    std::vector<hipKernelNodeParams> step_params;
-    RoundArgs step_args{};
-    int step_kernel_captured = -1, step_compact = -1;   // what the captured step graph was built for
-    int32_t step_round[64] = {};
+    static constexpr int kLaRing = 8, kLaAhead = 3;   // lastAncestors sweeps queued ahead of the check
+    hipEvent_t la_ev[kLaRing] = {};
+    StepGraph step_g[2];   // [0] full DivideRounds, [1] resumed (incremental) calls
     void drop_step_graph();
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;

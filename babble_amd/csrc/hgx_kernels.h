@@ -135,6 +135,9 @@ void launch_cts(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);
+// m <= 4096: one block sorts (graph, rr, cts, S) (no cts range needed)
+bool sort_small_ok(int32_t m);
+void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals);
 void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n);
 void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst);
 

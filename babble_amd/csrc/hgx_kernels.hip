@@ -1421,6 +1421,61 @@ __global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const i
 }
 
 // ---------------------------------------------------------------------------------
+// order of a small received set (m <= kSortSmallMax, the incremental schedule's usual
+// case): one block bitonic-sorts (graph, rr, cts, S) in LDS, S compared from HBM only on
+// equal (graph, rr, cts) (consensus_sorter.go:36-51). Replaces the radix passes' ~40
+// launches and the cts range read-back.
+constexpr int kSortSmallMax = 4096;
+
+__global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* __restrict__ list,
+                                                     const int64_t* __restrict__ p_cts,
+                                                     const int32_t* __restrict__ p_chain,
+                                                     const int32_t* __restrict__ p_rr, const int32_t* __restrict__ p_gid,
+                                                     const uint8_t* __restrict__ g_S, int n,
+                                                     uint32_t* __restrict__ out) {
+    __shared__ uint64_t khi[kSortSmallMax], klo[kSortSmallMax];
+    __shared__ int32_t kv[kSortSmallMax];
+    int NP = 1;
+    while (NP < m) NP <<= 1;
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) {
+        if (i < m) {
+            const int p = list[i];
+            khi[i] = ((uint64_t)(uint32_t)(p_chain[p] / n) << 32) | (uint64_t)(uint32_t)p_rr[p];
+            klo[i] = (uint64_t)p_cts[p] ^ 0x8000000000000000ull;
+            kv[i] = p;
+        } else {   // padding sorts last
+            khi[i] = ~0ull;
+            klo[i] = ~0ull;
+            kv[i] = -1;
+        }
+    }
+    __syncthreads();
+    auto less = [&](int a, int b) -> bool {   // element a before element b
+        if (khi[a] != khi[b]) return khi[a] < khi[b];
+        if (klo[a] != klo[b]) return klo[a] < klo[b];
+        if (kv[a] < 0 || kv[b] < 0) return kv[b] < 0 && kv[a] >= 0;
+        return cmp_s(g_S + (size_t)p_gid[kv[a]] * 32, g_S + (size_t)p_gid[kv[b]] * 32) < 0;
+    };
+    for (int k = 2; k <= NP; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < NP / 2; t += blockDim.x) {
+                const int i = 2 * t - (t & (j - 1));   // lower index of the pair (bit j clear)
+                const int l = i + j;
+                const bool up = (i & k) == 0;
+                if (up ? less(l, i) : less(i, l)) {
+                    const uint64_t h = khi[i], o = klo[i];
+                    const int32_t v = kv[i];
+                    khi[i] = khi[l]; klo[i] = klo[l]; kv[i] = kv[l];
+                    khi[l] = h; klo[l] = o; kv[l] = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < m; i += blockDim.x) out[i] = (uint32_t)kv[i];
+}
+
+// ---------------------------------------------------------------------------------
 // host-side launchers (template dispatch on n)
 #define HGX_DISPATCH_N(n, MACRO)                      \
     do {                                              \
@@ -1684,6 +1739,14 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
     hipLaunchKernelGGL(k_tiefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_cts, a.p_gid, a.g_S);
     *final_vals = va;
     *final_keys = ka;
+}
+
+bool sort_small_ok(int32_t m) { return m <= kSortSmallMax; }
+
+void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals) {
+    hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr, a.p_gid,
+                       a.g_S, n, a.val_a);
+    *final_vals = a.val_a;
 }
 
 void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n) {
