@@ -103,6 +103,8 @@ def lib():
     _sig(L, "hgx_block_hash", i32, [i64, i32, p, p, i32, p])
     _sig(L, "hgx_sha256_batch", i32, [i32, p, p, i64, p, p])
     _sig(L, "hgx_sha256_batch_device", i32, [p, p, i64, p, p])
+    _sig(L, "hgx_p256_verify_batch", i32, [i32, p, i32, p, p, p, p, i64, p, p])
+    _sig(L, "hgx_p256_verify_bench", i32, [i32, p, i32, p, p, p, p, i64, i32, i32, p, C.POINTER(C.c_double)])
     _sig(L, "hgx_sha256_bench", i32, [i32, i64, i32, i32, C.c_uint64, i32, i32, C.POINTER(C.c_double),
                                       C.POINTER(C.c_int64), C.POINTER(C.c_int64), i64, p])
     _sig(L, "hgx_phase_times", i32, [p, p, i32])

@@ -141,6 +141,13 @@ void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint
 void launch_finish_order(hipStream_t s, const DevArrays& a, int32_t m, const uint32_t* vals, int R, int n);
 void launch_gather_i32(hipStream_t s, int64_t E, const int32_t* src, const int32_t* g_pos, int32_t* dst);
 
+// ECDSA P-256 verify (hgx_p256.hip): per-key window tables (+ the base point as key nk),
+// then one lane per signature
+size_t p256_table_bytes(int nk);
+void launch_p256_tables(hipStream_t s, int nk, const uint8_t* keys65, uint32_t* tab, uint8_t* valid);
+void launch_p256_verify(hipStream_t s, int64_t count, int nk, const int32_t* key_idx, const uint8_t* dig,
+                        const uint8_t* r, const uint8_t* sg, const uint32_t* tab, const uint8_t* valid, uint8_t* out);
+
 // insert path (hgx_insert.hip): events k in [0, m) get gid E0 + k
 void launch_insert_claim(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, const InsertIn& in,
                          const InsertState& st);

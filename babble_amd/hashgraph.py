@@ -491,3 +491,35 @@ def sha256_bench(count: int, min_len: int, max_len: int, seed: int = 5, warmup: 
     if rc:
         raise HgxError(rc, "hgx_sha256_bench failed")
     return {"ms_per_launch": ms.value, "bytes": tot.value, "blocks": nb.value, "sample": sample}
+
+
+def _p256_cols(keys65, key_idx, digest, r, s):
+    k = np.ascontiguousarray(keys65, np.uint8).reshape(-1, 65)
+    cols = [np.ascontiguousarray(key_idx, np.int32)] + [np.ascontiguousarray(x, np.uint8).reshape(-1, 32)
+                                                         for x in (digest, r, s)]
+    m = cols[0].shape[0]
+    assert all(c.shape[0] == m for c in cols[1:])
+    return k, cols, m
+
+
+def p256_verify(keys65, key_idx, digest, r, s, device: int = 0) -> np.ndarray:
+    """Event.Verify for a batch (hgx_p256_verify_batch): 1 valid, 0 invalid, 2 key not a P-256 point."""
+    k, cols, m = _p256_cols(keys65, key_idx, digest, r, s)
+    out = np.zeros(m, np.uint8)
+    err = hgx_error()
+    rc = _lib.lib().hgx_p256_verify_batch(device, ptr(k), k.shape[0], *[ptr(c) for c in cols], m, ptr(out),
+                                          C.byref(err))
+    _lib.check(rc, err)
+    return out
+
+
+def p256_verify_bench(keys65, key_idx, digest, r, s, warmup: int = 1, iters: int = 3, device: int = 0) -> dict:
+    """Device-resident verify throughput (hgx_p256_verify_bench): ms per (tables + verify) launch."""
+    k, cols, m = _p256_cols(keys65, key_idx, digest, r, s)
+    out = np.zeros(m, np.uint8)
+    ms = C.c_double()
+    rc = _lib.lib().hgx_p256_verify_bench(device, ptr(k), k.shape[0], *[ptr(c) for c in cols], m, warmup, iters,
+                                          ptr(out), C.byref(ms))
+    if rc:
+        raise HgxError(rc, "hgx_p256_verify_bench failed")
+    return {"ms_per_launch": ms.value, "out": out}

@@ -219,6 +219,23 @@ int32_t hgx_sha256_bench(int32_t device, int64_t count, int32_t min_len, int32_t
                          int32_t warmup, int32_t iters, double* ms_per_launch, int64_t* total_bytes,
                          int64_t* n_blocks, int64_t n_sample, uint8_t* sample32);
 
+/* ---- ingest front end: batched ECDSA P-256 verify ------ */
+/* Event.Verify (hashgraph/event.go:142-152) for a whole sync batch: crypto.ToECDSAPub of
+ * Body.Creator (crypto/utils.go:22-28) and crypto.Verify (crypto/utils.go:41-43) = Go's
+ * ecdsa.Verify on P-256. keys65: n_keys public keys, 65 bytes each (0x04 || X || Y, the
+ * bytes of Body.Creator); key_idx[i]: the key of signature i; digest32: EventBody.Hash
+ * (SHA-256 of the body, hgx_sha256_batch); r32, s32: R and S big-endian, zero-padded.
+ * out[i] = 1 valid, 0 invalid, 2 the key is not a P-256 point (Go's elliptic.Unmarshal
+ * returns nil there). Pinned by libcrypto answers (oracle/p256_ref.c). */
+int32_t hgx_p256_verify_batch(int32_t device, const uint8_t* keys65, int32_t n_keys, const int32_t* key_idx,
+                              const uint8_t* digest32, const uint8_t* r32, const uint8_t* s32, int64_t count,
+                              uint8_t* out, hgx_error* err);
+/* bench.py: the same batch resident in HBM, (tables + verify) warmup + iters times, device
+ * time per launch from HIP events; out = the results of the last launch */
+int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_keys, const int32_t* key_idx,
+                              const uint8_t* digest32, const uint8_t* r32, const uint8_t* s32, int64_t count,
+                              int32_t warmup, int32_t iters, uint8_t* out, double* ms_per_launch);
+
 /* ---- timing / instrumentation --------------------------------------------- */
 /* per-phase device times (ms) of the last calls: coords, rounds, fame, order; then
  * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16); then of the last
