@@ -116,6 +116,12 @@ def lib():
     _sig(L, "hgx_set_fame_tally", i32, [p, i32])
     _sig(L, "hgx_set_round_kernel", i32, [p, i32])
     _sig(L, "hgx_set_incremental", i32, [p, i32])
+    _sig(L, "hgx_find_order_begin", i32, [p, p])
+    _sig(L, "hgx_find_order_end", i32, [p, p])
+    _sig(L, "hgx_set_shard", i32, [p, i32, i32])
+    _sig(L, "hgx_shard_values", i64, [p, i32])
+    _sig(L, "hgx_shard_export", i32, [p, p, i32])
+    _sig(L, "hgx_shard_import", i32, [p, i32, p, i32])
     _sig(L, "hgx_reserve_rounds", i32, [p, i32])
     _sig(L, "hgx_device_alloc", i32, [i32, i64, C.POINTER(C.c_void_p)])
     _sig(L, "hgx_device_free", i32, [i32, p])

@@ -108,6 +108,10 @@ struct hgx_ctx {
     bool recv_cached = false;
     std::vector<int32_t> rr_cache;
     std::vector<int64_t> cts_cache;
+    // FindOrder in progress (between hgx_find_order_begin and _end) and the row shard
+    bool fo_open = false;
+    hgx::OrderHost fo;
+    int32_t shard_rank = 0, shard_world = 1;
 };
 
 static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
@@ -459,8 +463,12 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
 }
 
 // ---- FindOrder (hashgraph.go:801-858) --------------------------------------------
-int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
+// In two halves: begin = DecideRoundReceived and the consensus timestamps of this context's
+// shard of chains (all chains unless hgx_set_shard); end = the ConsensusSorter order and the
+// blocks. A row-sharded graph exchanges the shards' timestamps in between.
+int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    c->fo_open = false;
     if (!c->divided) return ok(err);
     DeviceGuard dg(c);
     const int n = c->n, C = c->C, G = c->G;
@@ -488,13 +496,28 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
             elig[(size_t)g * R + i] = (U0 >= 0 && i < U0 && decided) ? 1 : 0;
         }
     }
-    hgx::OrderHost oh;
-    hipError_t e = c->eng.find_order(elig, fw, ure, r0, max_unrecv, oh);
+    hgx::OrderHost& oh = c->fo;
+    hipError_t e = c->eng.find_order_begin(elig, fw, ure, r0, max_unrecv, oh);
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     if (oh.panic) {
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
         return HGX_ERR_PANIC;
     }
+    c->fo_open = true;
+    return ok(err);
+}
+
+int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
+    if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
+    if (!c->fo_open) return ok(err);
+    c->fo_open = false;
+    DeviceGuard dg(c);
+    const int n = c->n, G = c->G;
+    (void)n;
+    const int32_t R = c->rh.R;
+    hgx::OrderHost& oh = c->fo;
+    hipError_t e = c->eng.find_order_end(oh);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     c->recv_cached = false;
     // the device order is graph-major: one D2H copy appends it to the arena and every
     // graph gets its segment
@@ -549,6 +572,56 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
         s.undetermined -= mg;
     }
     return ok(err);
+}
+
+int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
+    if (c && c->shard_world > 1) {
+        set_err(err, HGX_ERR_INVALID, "hgx_find_order: a sharded context exchanges timestamps between "
+                                      "hgx_find_order_begin and hgx_find_order_end");
+        return HGX_ERR_INVALID;
+    }
+    const int32_t rc = hgx_find_order_begin(c, err);
+    if (rc) return rc;
+    return hgx_find_order_end(c, err);
+}
+
+// ---- row-sharded graph --------------------------------------------------
+static void shard_range(const hgx_ctx* c, int32_t rank, int* lo, int* hi) {
+    *lo = (int)((int64_t)c->C * rank / c->shard_world);
+    *hi = (int)((int64_t)c->C * (rank + 1) / c->shard_world);
+}
+
+int32_t hgx_set_shard(hgx_ctx* c, int32_t rank, int32_t world) {
+    if (!c || world < 1 || rank < 0 || rank >= world || world > c->C) return HGX_ERR_INVALID;
+    c->shard_rank = rank;
+    c->shard_world = world;
+    shard_range(c, rank, &c->eng.shard_lo, &c->eng.shard_hi);
+    return HGX_OK;
+}
+
+int64_t hgx_shard_values(hgx_ctx* c, int32_t rank) {
+    if (!c || rank < 0 || rank >= c->shard_world || !c->fo_open) return 0;
+    int lo, hi;
+    shard_range(c, rank, &lo, &hi);
+    return c->eng.shard_values(lo, hi);
+}
+
+static int32_t shard_xfer(hgx_ctx* c, int32_t rank, void* buf, int32_t on_device, bool to_buf) {
+    if (!c || rank < 0 || rank >= c->shard_world || (!buf && hgx_shard_values(c, rank) > 0)) return HGX_ERR_INVALID;
+    if (!c->fo_open) return HGX_OK;
+    DeviceGuard dg(c);
+    int lo, hi;
+    shard_range(c, rank, &lo, &hi);
+    return c->eng.shard_copy(lo, hi, buf, on_device != 0, to_buf) == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+int32_t hgx_shard_export(hgx_ctx* c, void* dst, int32_t dst_on_device) {
+    return c ? shard_xfer(c, c->shard_rank, dst, dst_on_device, true) : HGX_ERR_INVALID;
+}
+
+int32_t hgx_shard_import(hgx_ctx* c, int32_t src_rank, const void* src, int32_t src_on_device) {
+    if (c && src_rank == c->shard_rank) return HGX_OK;
+    return shard_xfer(c, src_rank, const_cast<void*>(src), src_on_device, false);
 }
 
 int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {

@@ -100,6 +100,8 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     n = n_part;
     C = G * n;
     sm = 2 * n / 3 + 1;   // hashgraph.go:63
+    shard_lo = 0;
+    shard_hi = C;
     nw = (n + 63) / 64;
     cap = std::max<int64_t>(cap_events, 1);
     const size_t P = (size_t)cap;
@@ -681,11 +683,16 @@ hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
 // ---- FindOrder ------------------------------------------------------------------
 hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
                               const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
+    HGX_TRY(find_order_begin(el, famous, ure, r0, max_unrecv, out));
+    return find_order_end(out);
+}
+
+// threshold and roundReceived (every chain), consensus timestamps of the shard's chains
+hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
+                                    const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
     out = OrderHost();
-    out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
-    out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
-    out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
-    out.blk_nil.assign((size_t)G * std::max(R, 1), 0);
+    fo_m = 0;
+    fo_cnt.assign(C, 0);
     if (R == 0 || E_div == 0 || max_unrecv == 0 || r0 >= R) return hipSuccess;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
@@ -707,22 +714,63 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     launch_round_received(stream, a, R, C, n, max_unrecv);
     kend(K_ROUND_RECEIVED, 0);
     HGX_TRY(hipMemcpyAsync(h_small, counters.p, 8, hipMemcpyDeviceToHost, stream));
-    std::vector<int32_t> cnt(C);
-    HGX_TRY(hipMemcpyAsync(cnt.data(), rcnt.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(fo_cnt.data(), rcnt.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
-    const int32_t m = h_small[0];
+    fo_m = h_small[0];
     out.panic = h_small[1] != 0;
-    out.m = m;
+    out.m = fo_m;
     int max_cnt = 0, unrecv = 0;
-    for (int c = 0; c < C; c++) {
-        max_cnt = std::max(max_cnt, cnt[c]);
-        unrecv += h_len_div[c] - h_fu[c];
-    }
+    for (int c = 0; c < C; c++) unrecv += h_len_div[c] - h_fu[c];
+    for (int c = shard_lo; c < shard_hi; c++) max_cnt = std::max(max_cnt, fo_cnt[c]);
     kadd_bytes(K_ROUND_RECEIVED, (double)unrecv * 16);
-    if (out.panic || m == 0) return collect_kernel_times();
+    if (out.panic || fo_m == 0) {
+        fo_m = 0;
+        return collect_kernel_times();
+    }
     kbeg(K_CTS);
-    launch_cts(stream, a, C, n, fd_ld, max_cnt);
-    kend(K_CTS, (double)m * (4.0 * n + 8.0 * n));
+    launch_cts(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt);
+    int64_t own = 0;
+    for (int c = shard_lo; c < shard_hi; c++) own += fo_cnt[c];
+    kend(K_CTS, (double)own * (4.0 * n + 8.0 * n));
+    return hipSuccess;
+}
+
+// the consensus timestamps of the events newly received on chains [lo, hi), chain-major
+// ([fu, fu + rcnt) of each chain): the values a shard exchanges
+int64_t Engine::shard_values(int lo, int hi) const {
+    int64_t k = 0;
+    for (int c = lo; c < hi && c < (int)fo_cnt.size(); c++) k += fo_cnt[c];
+    return k;
+}
+
+hipError_t Engine::shard_copy(int lo, int hi, void* buf, bool on_device, bool to_buf) {
+    const int64_t cnt = shard_values(lo, hi);
+    if (cnt == 0) return hipSuccess;
+    std::vector<int32_t> offs(C + 1, 0);   // exclusive scan of the counts over [lo, hi)
+    for (int c = lo; c < hi; c++) offs[c + 1] = offs[c] + fo_cnt[c];
+    if (sh_off.n < (size_t)C + 1) HGX_TRY(sh_off.alloc((size_t)C + 1));
+    HGX_TRY(hipMemcpyAsync(sh_off.p, offs.data(), (size_t)(C + 1) * 4, hipMemcpyHostToDevice, stream));
+    int64_t* dev = (int64_t*)buf;
+    if (!on_device) {
+        if (sh_buf.n < (size_t)cnt) HGX_TRY(sh_buf.alloc((size_t)cnt));
+        dev = sh_buf.p;
+        if (!to_buf) HGX_TRY(hipMemcpyAsync(dev, buf, (size_t)cnt * 8, hipMemcpyHostToDevice, stream));
+    }
+    launch_cts_shard_copy(stream, arrays(), lo, hi, sh_off.p, dev, to_buf ? 1 : 0);
+    if (!on_device && to_buf) HGX_TRY(hipMemcpyAsync(buf, dev, (size_t)cnt * 8, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+// sort by (graph, rr, cts, S), blocks
+hipError_t Engine::find_order_end(OrderHost& out) {
+    out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
+    out.blk_nil.assign((size_t)G * std::max(R, 1), 0);
+    const int32_t m = fo_m;
+    if (m == 0) return hipSuccess;
+    fo_m = 0;
+    DevArrays a = arrays();
     uint32_t* vals = nullptr;
     if (sort_small_ok(m)) {
         kbeg(K_SORT);
@@ -753,7 +801,7 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
     HGX_TRY(hipMemsetAsync(blk_nil.p, 0, (size_t)G * R, stream));
     launch_finish_order(stream, a, m, vals, R, n);
     launch_fu_advance(stream, a, C);
-    for (int c = 0; c < C; c++) h_fu[c] += cnt[c];
+    for (int c = 0; c < C; c++) h_fu[c] += fo_cnt[c];
     HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));

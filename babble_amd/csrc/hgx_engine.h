@@ -104,6 +104,16 @@ class Engine {
     hipError_t find_order(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
                           const std::vector<uint8_t>& ur_empty, int32_t r0, int max_unrecv, OrderHost& out);
     int32_t recv_round_lo(const RoundsHost& rh, int& max_unrecv) const;
+    // the same in two halves around the shard exchange of a row-sharded graph:
+    // begin = threshold, roundReceived, consensus timestamps of chains [shard_lo, shard_hi);
+    // end = sort and blocks
+    hipError_t find_order_begin(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
+                                const std::vector<uint8_t>& ur_empty, int32_t r0, int max_unrecv, OrderHost& out);
+    hipError_t find_order_end(OrderHost& out);
+    int64_t shard_values(int lo, int hi) const;   // newly received events of chains [lo, hi)
+    // their consensus timestamps to (to_buf) or from buf, a device or host pointer
+    hipError_t shard_copy(int lo, int hi, void* buf, bool on_device, bool to_buf);
+    int shard_lo = 0, shard_hi = 0;               // chains whose consensus timestamps this context computes
     // D2H of order[first, first+count) of the last find_order (async; then sync())
     hipError_t copy_order(int32_t* dst, int64_t first, int64_t count);
     hipError_t sync() { return hipStreamSynchronize(stream); }
@@ -148,6 +158,10 @@ class Engine {
     std::vector<int32_t> h_off;        // [C+1] chain slots (positions), fixed until a rebuild
     std::vector<int32_t> h_len_div;    // [C] chain lengths at the last divide_rounds
     std::vector<int32_t> h_fu;         // [C] events of each chain received so far (a prefix)
+    int32_t fo_m = 0;                  // events received by the FindOrder in progress
+    std::vector<int32_t> fo_cnt;       // [C] ... per chain
+    DBuf<int32_t> sh_off;              // shard exchange: chain offsets
+    DBuf<int64_t> sh_buf;              // ... and staging of host buffers
     // gid order
     DBuf<int32_t> g_creator, g_index, g_sp, g_op, g_ntx, g_rr, g_pos;
     DBuf<int64_t> g_ts, g_cts;

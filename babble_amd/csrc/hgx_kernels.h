@@ -130,8 +130,13 @@ void launch_threshold(hipStream_t s, const DevArrays& a, int r0, int R, int C, i
 void launch_round_received(hipStream_t s, const DevArrays& a, int R, int C, int n, int max_unrecv);
 void launch_fu_advance(hipStream_t s, const DevArrays& a, int C);           // fu += rcnt
 void launch_fu_count(hipStream_t s, const DevArrays& a, int64_t E);         // fu += received events (fu preset 0)
-// the newly received events [fu, fu + rcnt) of every chain (max_cnt = the largest rcnt)
-void launch_cts(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt);
+// the newly received events [fu, fu + rcnt) of chains [c_lo, c_lo + c_cnt) (max_cnt = the
+// largest rcnt among them)
+void launch_cts(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P, int max_cnt);
+// shard exchange: consensus timestamps of the newly received events of chains [lo, hi) to /
+// from a chain-major buffer (offs[c] = start of chain c)
+void launch_cts_shard_copy(hipStream_t s, const DevArrays& a, int lo, int hi, const int32_t* offs, int64_t* buf,
+                           int to_buf);
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);

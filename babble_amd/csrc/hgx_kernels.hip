@@ -903,8 +903,8 @@ __global__ void __launch_bounds__(256) k_cts_small(const int32_t* __restrict__ f
                                                    const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                    const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                    const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
-                                                   int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
-    const int gc = blockIdx.y;
+                                                   int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap, int c_lo) {
+    const int gc = c_lo + blockIdx.y;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= rcnt[gc]) return;
     const int g = gc / n;
@@ -953,7 +953,8 @@ __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu
                                                   const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
                                                   const uint8_t* __restrict__ fw, const int32_t* __restrict__ WLAT,
                                                   const CT* __restrict__ FDT, const int64_t* __restrict__ p_ts,
-                                                  int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap) {
+                                                  int64_t* __restrict__ p_cts, int C, int n, int64_t Pcap, int c_lo,
+                                                  int c_cnt) {
     constexpr int T = kCtsTile;
     constexpr int LD = T + 1;                     // row stride of vals (bank spread)
     constexpr int CPL = NPAD / 64;
@@ -968,7 +969,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu
     // i = tile i / C of chain i % C, so the blocks in flight cover every chain at about the
     // same time and their timestamp gathers (events of other chains at that time) share
     // lines in L2
-    const int tc = (int)(blockIdx.x % (unsigned)C), tt = (int)(blockIdx.x / (unsigned)C);
+    const int tc = c_lo + (int)(blockIdx.x % (unsigned)c_cnt), tt = (int)(blockIdx.x / (unsigned)c_cnt);
     const int64_t p0 = (int64_t)c_off[tc] + fu[tc] + (int64_t)tt * T;
     const int64_t pend = (int64_t)c_off[tc] + fu[tc] + rcnt[tc];
     if (threadIdx.x == 0) s_any = 0;
@@ -1642,13 +1643,15 @@ void launch_init_new(hipStream_t s, const DevArrays& a, int64_t E0, int64_t m, i
 }
 
 template <int NP, typename CT>
-static void cts_small_launch(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
-    hipLaunchKernelGGL((k_cts_small<NP, CT>), dim3(nblk(max_cnt, 256), C), dim3(256), 0, s, a.fu, a.rcnt, a.p_rr,
-                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
+static void cts_small_launch(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P,
+                             int max_cnt) {
+    hipLaunchKernelGGL((k_cts_small<NP, CT>), dim3(nblk(max_cnt, 256), c_cnt), dim3(256), 0, s, a.fu, a.rcnt, a.p_rr,
+                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P, c_lo);
 }
 
 template <int NPAD, typename CT>
-static void cts_tile_launch(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
+static void cts_tile_launch(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P,
+                            int max_cnt) {
     const size_t lds = (size_t)NPAD * (kCtsTile + 1) * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
@@ -1656,29 +1659,52 @@ static void cts_tile_launch(hipStream_t s, const DevArrays& a, int C, int n, int
                                   (int)lds);
         attr = true;
     }
-    const unsigned grid = (unsigned)((int64_t)C * ((max_cnt + kCtsTile - 1) / kCtsTile));
+    const unsigned grid = (unsigned)((int64_t)c_cnt * ((max_cnt + kCtsTile - 1) / kCtsTile));
     if (grid == 0) return;
     hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, a.fu, a.rcnt, a.p_rr,
-                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P);
+                       a.c_off, a.c_base, a.fw, a.WLAT, (const CT*)a.FDT, a.p_ts, a.p_cts, C, n, P, c_lo, c_cnt);
 }
 
 template <typename CT>
-static void launch_cts_t(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
-    if (n <= 4) cts_small_launch<4, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 8) cts_small_launch<8, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 16) cts_small_launch<16, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 32) cts_small_launch<32, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 64) cts_tile_launch<64, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 128) cts_tile_launch<128, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 256) cts_tile_launch<256, CT>(s, a, C, n, P, max_cnt);
-    else if (n <= 512) cts_tile_launch<512, CT>(s, a, C, n, P, max_cnt);
-    else cts_tile_launch<1024, CT>(s, a, C, n, P, max_cnt);
+static void launch_cts_t(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P,
+                         int max_cnt) {
+    if (n <= 4) cts_small_launch<4, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 8) cts_small_launch<8, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 16) cts_small_launch<16, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 32) cts_small_launch<32, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 64) cts_tile_launch<64, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 128) cts_tile_launch<128, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 256) cts_tile_launch<256, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else if (n <= 512) cts_tile_launch<512, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else cts_tile_launch<1024, CT>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
 }
 
-void launch_cts(hipStream_t s, const DevArrays& a, int C, int n, int64_t P, int max_cnt) {
-    if (max_cnt <= 0) return;
-    if (a.compact) launch_cts_t<uint16_t>(s, a, C, n, P, max_cnt);
-    else launch_cts_t<int32_t>(s, a, C, n, P, max_cnt);
+void launch_cts(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P, int max_cnt) {
+    if (max_cnt <= 0 || c_cnt <= 0) return;
+    if (a.compact) launch_cts_t<uint16_t>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+    else launch_cts_t<int32_t>(s, a, c_lo, c_cnt, C, n, P, max_cnt);
+}
+
+// consensus timestamps of the newly received events of chains [lo, hi), chain-major at
+// offs[c] (to_buf: p_cts -> buf, else buf -> p_cts): the shard exchange of a row-sharded graph
+__global__ void k_cts_shard_copy(int lo, const int32_t* __restrict__ c_off, const int32_t* __restrict__ fu,
+                                 const int32_t* __restrict__ rcnt, const int32_t* __restrict__ offs,
+                                 int64_t* __restrict__ p_cts, int64_t* __restrict__ buf, int to_buf) {
+    const int gc = lo + blockIdx.x;
+    const int cnt = rcnt[gc];
+    const int64_t p0 = (int64_t)c_off[gc] + fu[gc];
+    const int o = offs[gc];
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+        if (to_buf) buf[o + k] = p_cts[p0 + k];
+        else p_cts[p0 + k] = buf[o + k];
+    }
+}
+
+void launch_cts_shard_copy(hipStream_t s, const DevArrays& a, int lo, int hi, const int32_t* offs, int64_t* buf,
+                           int to_buf) {
+    if (hi <= lo) return;
+    hipLaunchKernelGGL(k_cts_shard_copy, dim3(hi - lo), dim3(256), 0, s, lo, a.c_off, a.fu, a.rcnt, offs, a.p_cts,
+                       buf, to_buf);
 }
 
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m) {

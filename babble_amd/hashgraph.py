@@ -115,6 +115,36 @@ class Hashgraph:
         """node/core.go:277-303"""
         self._call(self.L.hgx_run_consensus)
 
+    # ------------------------------------------------------------------ row-sharded graph
+    def set_shard(self, rank: int, world: int):
+        """One graph row-sharded over `world` ranks (hgx_set_shard)."""
+        if self.L.hgx_set_shard(self.ctx, rank, world) != 0:
+            raise ValueError("invalid shard")
+        self.shard = (rank, world)
+
+    def FindOrderSharded(self, all_gather):
+        """FindOrder of a row-sharded graph: begin, exchange of the shards' consensus timestamps,
+        end. all_gather(local: np.ndarray[int64], counts: list[int]) -> list of every rank's
+        array (torch.distributed over gloo, or over RCCL with device buffers)."""
+        rank, world = self.shard
+        self._call(self.L.hgx_find_order_begin)
+        counts = [int(self.L.hgx_shard_values(self.ctx, r)) for r in range(world)]
+        mine = np.zeros(counts[rank], np.int64)
+        if counts[rank] and self.L.hgx_shard_export(self.ctx, ptr(mine), 0) != 0:
+            raise HgxError(200, "hgx_shard_export failed")
+        parts = all_gather(mine, counts)
+        for r in range(world):
+            if r != rank and counts[r]:
+                a = np.ascontiguousarray(parts[r], np.int64)
+                if self.L.hgx_shard_import(self.ctx, r, ptr(a), 0) != 0:
+                    raise HgxError(200, "hgx_shard_import failed")
+        self._call(self.L.hgx_find_order_end)
+
+    def RunConsensusSharded(self, all_gather):
+        self.DivideRounds()
+        self.DecideFame()
+        self.FindOrderSharded(all_gather)
+
     def reset_consensus(self):
         """Fresh consensus state over the same resident events (Bootstrap replay)."""
         rc = self.L.hgx_reset_consensus(self.ctx)

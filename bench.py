@@ -283,6 +283,33 @@ def chunked_leg(h, dtr, tr, sync_limit, check):
     return res
 
 
+def p256_leg(count, steps, warmup, device):
+    """Side leg (second half): Event.Verify (hashgraph/event.go:142-152) of
+    `count` signatures over 6 creator keys (a sync batch), drawn from libcrypto's known answers
+    (tests/golden/p256_vectors.txt: valid, corrupted and bad-key rows), HBM-resident; device time
+    per (key tables + verify) launch from HIP events (hgx_p256_verify_bench); every result is
+    checked against libcrypto's."""
+    from babble_amd.hashgraph import p256_verify_bench
+    rows = []
+    with open(os.path.join(ROOT, "tests", "golden", "p256_vectors.txt")) as f:
+        for line in f:
+            pub, dg, r, s, exp, kok, _ = line.split()
+            rows.append((pub, dg, r, s, int(exp) if int(kok) else 2))
+    keys = sorted({r[0] for r in rows})
+    sel = np.random.default_rng(11).integers(0, len(rows), count)
+    kid = np.array([keys.index(rows[i][0]) for i in range(len(rows))], np.int32)[sel]
+    cols = [np.stack([np.frombuffer(bytes.fromhex(rows[i][c]), np.uint8) for i in range(len(rows))])[sel]
+            for c in (1, 2, 3)]
+    exp = np.array([r[4] for r in rows], np.uint8)[sel]
+    kb = np.stack([np.frombuffer(bytes.fromhex(k), np.uint8) for k in keys])
+    res = p256_verify_bench(kb, kid, *cols, warmup=max(1, warmup), iters=steps, device=device)
+    assert np.array_equal(res["out"], exp), "P-256 verify differs from libcrypto"
+    ms = res["ms_per_launch"]
+    return {"kernel": "k_p256_verify", "signatures": count, "keys": len(keys), "ms_per_launch": ms,
+            "verifies_per_s": count / (ms * 1e-3), "valid_fraction": float((exp == 1).mean()),
+            "check": "bit-exact vs libcrypto 3.0.2 (ECDSA_do_verify)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -421,6 +448,10 @@ def main():
                 result["ingest_sha256"] = ingest_leg(int(tr.E), args.steps, args.warmup, local_rank)
             except Exception as e:  # reported, never fatal
                 result["ingest_sha256"] = {"error": str(e)}
+            try:
+                result["ingest_p256_verify"] = p256_leg(1 << 20, args.steps, args.warmup, local_rank)
+            except Exception as e:  # reported, never fatal
+                result["ingest_p256_verify"] = {"error": str(e)}
         if G == 1 and not args.no_chunked:
             tcl = time.time()
             result["chunked_sync"] = chunked_leg(h, dtr, tr, args.sync_limit, not args.no_check)

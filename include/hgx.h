@@ -103,6 +103,23 @@ int32_t hgx_insert_events_device(hgx_ctx* ctx, const hgx_events* ev, int64_t cou
 int32_t hgx_divide_rounds(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_decide_fame(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_find_order(hgx_ctx* ctx, hgx_error* err);
+/* FindOrder in two halves (hgx_find_order = begin + end): begin = DecideRoundReceived and the
+ * consensus timestamps of the context's shard of chains; end = the ConsensusSorter order and
+ * the blocks. A row-sharded graph exchanges the shards' timestamps in between. */
+int32_t hgx_find_order_begin(hgx_ctx* ctx, hgx_error* err);
+int32_t hgx_find_order_end(hgx_ctx* ctx, hgx_error* err);
+/* One graph row-sharded over `world` ranks: every rank holds
+ * the whole DAG and runs the replicated phases (lastAncestors, firstDescendants, the round
+ * steps, fame, roundReceived); the consensus-timestamp medians of the events newly received
+ * are computed by the rank owning their creator (chains [C*rank/world, C*(rank+1)/world)) and
+ * all-gathered between hgx_find_order_begin and _end: hgx_shard_values(ctx, r) = how many int64
+ * values rank r contributes, hgx_shard_export writes this rank's, hgx_shard_import reads rank
+ * r's (device pointers on the context's device, e.g. RCCL buffers, or host pointers, e.g.
+ * gloo). hgx_find_order refuses a sharded context. */
+int32_t hgx_set_shard(hgx_ctx* ctx, int32_t rank, int32_t world);
+int64_t hgx_shard_values(hgx_ctx* ctx, int32_t rank);
+int32_t hgx_shard_export(hgx_ctx* ctx, void* dst, int32_t dst_on_device);
+int32_t hgx_shard_import(hgx_ctx* ctx, int32_t src_rank, const void* src, int32_t src_on_device);
 /* Core.RunConsensus (node/core.go:277-303): the three calls in sequence */
 int32_t hgx_run_consensus(hgx_ctx* ctx, hgx_error* err);
 /* Forget every consensus result but keep the inserted events resident in HBM:
