@@ -230,6 +230,33 @@ class Reducer:
     def sum(self, x):
         return x if self.dist is None else self._reduce(x, self.dist.ReduceOp.SUM)
 
+    def shard_exchange(self, h, world, rank):
+        """FindOrder of a row-sharded graph (hgx_find_order_begin / _end): the ranks' consensus
+        timestamps all-gathered in between, device buffers over RCCL (xGMI), host over gloo."""
+        import ctypes as C
+        import torch
+        err = C.create_string_buffer(256)
+        L = h.L
+        if L.hgx_find_order_begin(h.ctx, err):
+            raise SystemExit("hgx_find_order_begin failed")
+        counts = [int(L.hgx_shard_values(h.ctx, r)) for r in range(world)]
+        mx = max(1, max(counts))
+        on_dev = self.device != "cpu"
+        mine = torch.zeros(mx, dtype=torch.int64, device=self.device)
+        if counts[rank] and L.hgx_shard_export(h.ctx, C.c_void_p(mine.data_ptr()), 1 if on_dev else 0):
+            raise SystemExit("hgx_shard_export failed")
+        allv = torch.empty(world * mx, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(allv, mine)
+        if on_dev:
+            torch.cuda.synchronize()
+        for r in range(world):
+            if r != rank and counts[r]:
+                ptr_r = C.c_void_p(allv.data_ptr() + 8 * r * mx)
+                if L.hgx_shard_import(h.ctx, r, ptr_r, 1 if on_dev else 0):
+                    raise SystemExit("hgx_shard_import failed")
+        if L.hgx_find_order_end(h.ctx, err):
+            raise SystemExit("hgx_find_order_end failed")
+
 
 # SHA-256 compression in gfx950 lane instructions per 64-byte block (3-input v_bitop3/v_add3):
 # 64 rounds x (6 rotates + 2 xor3 + Ch + Maj + 4 adds) + 48 schedule words x (4 rotates + 2 shifts
@@ -310,6 +337,62 @@ def p256_leg(count, steps, warmup, device):
             "check": "bit-exact vs libcrypto 3.0.2 (ECDSA_do_verify)"}
 
 
+def device_of(local_rank):
+    """The rank's GPU; ranks beyond the visible devices share them (gloo rehearsals on one GPU)."""
+    try:
+        import torch
+        nd = torch.cuda.device_count()
+    except Exception:
+        nd = 0
+    return local_rank % nd if nd > 0 else local_rank
+
+
+def run_sharded(args, red, world, rank, local_rank):
+    """C3's north-star mode (BASELINE configs[2]): ONE graph row-sharded over the ranks. Every
+    rank holds the whole DAG (the same trace) and runs the replicated phases; the consensus
+    timestamps are computed per creator block and all-gathered (RCCL on GPUs). Strong scaling:
+    value = the graph's ordered events / the slowest rank's time."""
+    from babble_amd import trace
+    from babble_amd.hashgraph import DeviceTrace, Hashgraph
+    n, E, G, silent, stale, depth, desc = CONFIGS[args.config]
+    tr = trace.gossip(n, E, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
+    dev = device_of(local_rank)
+    h = Hashgraph(n, capacity=tr.E, device=dev)
+    h.set_shard(rank, world)
+    dtr = DeviceTrace(tr, device=dev)
+
+    def step():
+        h.clear()
+        h.insert_device(dtr)
+        h.DivideRounds()
+        h.DecideFame()
+        red.shard_exchange(h, world, rank)
+        return int(h.L.hgx_consensus_events_count(h.ctx, 0))
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    red.barrier()
+    t0 = time.perf_counter()
+    ordered = 0
+    for _ in range(args.steps):
+        ordered = step()
+    t_el = time.perf_counter() - t0
+    red.barrier()
+    t_max = red.max(t_el)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "consensus-ordered events/sec at N=256 peers (1 GPU and 8-GPU batched sims)",
+            "value": ordered * args.steps / t_max, "unit": "consensus-ordered events/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_max * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (seeded random-gossip trace, the same on every rank), resident in HBM",
+            "config": {"workload": desc, "config": args.config, "peers": n, "events": int(tr.E),
+                       "parallelism": f"row-sharded x{world}: consensus timestamps per creator block, "
+                                      f"all-gather over {'RCCL' if red.device != 'cpu' else 'gloo'}",
+                       "phase_ms_last_step": {k: round(float(v), 3) for k, v in h.phase_times().items()}}}),
+              flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -321,12 +404,19 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the full-size property checks")
     ap.add_argument("--no-chunked", action="store_true", help="skip the SyncLimit-chunked schedule leg")
     ap.add_argument("--sync-limit", type=int, default=1000)
+    ap.add_argument("--sharded", action="store_true",
+                    help="C3's mode: one graph row-sharded over the ranks (strong scaling) instead of replicas")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    red = Reducer(world, local_rank)
+    red = Reducer(world, local_rank, backend=args.backend)
+    if args.sharded:
+        if world < 2:
+            raise SystemExit("--sharded needs torch.distributed.run with >= 2 ranks")
+        return run_sharded(args, red, world, rank, local_rank)
 
     from babble_amd.hashgraph import DeviceTrace, Hashgraph
     n, E, G, *_ = CONFIGS[args.config]
