@@ -594,6 +594,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 HGX_TRY(hipGraphExecKernelNodeSetParams(sgr.exec, sgr.nodes[k], &kp));
             }
             kbeg(K_ROUND_SEARCH);
+            kstat[K_ROUND_SEARCH].launches += nb - 1;   // nb step kernels per replay
             HGX_TRY(hipGraphLaunch(sgr.exec, stream));
             kend(K_ROUND_SEARCH, 0);
             const int slot = launched & 1;

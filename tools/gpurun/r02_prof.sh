@@ -5,5 +5,5 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 CFG=${CFG:-c3}
 HGX_LIB=libhgx_prof.so timeout -k 10 200 python -u tools/phase_timing.py $CFG 1 > gpurun_out/prof_phases.log 2>&1 && \
 rm -rf /tmp/prof_k && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_k -o run -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-ingest --no-check > gpurun_out/prof_bench.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_k -o run -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked > gpurun_out/prof_bench.log 2>&1 && \
 python3 tools/rocpd_export.py stats /tmp/prof_k/run_results.db gpurun_out/prof_kernel_stats.csv
