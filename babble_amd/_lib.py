@@ -119,6 +119,8 @@ def lib():
     _sig(L, "hgx_find_order_begin", i32, [p, p])
     _sig(L, "hgx_find_order_end", i32, [p, p])
     _sig(L, "hgx_set_shard", i32, [p, i32, i32])
+    _sig(L, "hgx_reset", i32, [p, p, p, p, p])
+    _sig(L, "hgx_get_frame", i32, [p, p, i64, p, p, p, p, p, p, p, i64, p, p])
     _sig(L, "hgx_shard_values", i64, [p, i32])
     _sig(L, "hgx_shard_export", i32, [p, p, i32])
     _sig(L, "hgx_shard_import", i32, [p, i32, p, i32])

@@ -61,6 +61,7 @@ struct GraphOrder {
 struct GraphState {
     std::vector<int32_t> undecided{0};     // Hashgraph.UndecidedRounds, init []int{0} (hashgraph.go:64)
     int32_t queued_upto = -1;              // rounds <= this have RoundInfo.queued
+    std::vector<uint8_t> queued;           // [r] RoundInfo.queued after a Reset (rounds may appear out of order)
     bool has_lcr = false;
     int32_t lcr = 0;
     int32_t lcre = 0;
@@ -79,6 +80,7 @@ struct GraphState {
         fame.clear();
         round_events.clear();
         blocks.clear();
+        queued.clear();
     }
 };
 
@@ -112,6 +114,10 @@ struct hgx_ctx {
     bool fo_open = false;
     hgx::OrderHost fo;
     int32_t shard_rank = 0, shard_world = 1;
+    // Roots (root.go:62-67) after hgx_reset: Index, Round, Root.Y is an event outside the store
+    std::vector<int32_t> root_index, root_round;
+    std::vector<uint8_t> root_y_ext;
+    bool rooted = false;
 };
 
 static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
@@ -219,6 +225,9 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->last_gid.assign(c->C, -1);
     c->last_index.assign(c->C, -1);
     c->chain_gids.assign(c->C, {});
+    c->root_index.assign(c->C, -1);   // NewBaseRoot (root.go:69-76)
+    c->root_round.assign(c->C, -1);
+    c->root_y_ext.assign(c->C, 0);
     c->gs.assign(n_graphs, GraphState());
     c->order = std::vector<GraphOrder>(n_graphs);
     c->g_events.assign(n_graphs, 0);
@@ -359,7 +368,147 @@ int32_t hgx_clear(hgx_ctx* c) {
     c->divided = false;
     c->mirror_ok = c->chains_ok = false;
     c->rounds_cached = c->recv_cached = false;
+    if (c->rooted) {   // a fresh NewHashgraph has genesis roots
+        std::fill(c->root_index.begin(), c->root_index.end(), -1);
+        std::fill(c->root_round.begin(), c->root_round.end(), -1);
+        std::fill(c->root_y_ext.begin(), c->root_y_ext.end(), 0);
+        c->rooted = false;
+        if (c->eng.set_roots(c->root_round, c->root_y_ext) != hipSuccess) return HGX_ERR_DEVICE;
+    }
     return HGX_OK;
+}
+
+// ---- Reset (hashgraph.go:877-895, inmem_store.go:184-192) ---------------------------------
+// Store.Reset: new roots, the event / round / consensus caches and the participants'
+// RollingIndexes cleared, lastRound = -1 (the block cache is kept). Hashgraph.Reset:
+// UndeterminedEvents, UndecidedRounds (empty), PendingLoadedEvents, topologicalIndex and the
+// memo caches; LastConsensusRound, LastCommitedRoundEvents and ConsensusTransactions are kept.
+int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_round, const int32_t* root_y_is_event,
+                  hgx_error* err) {
+    if (!c || !root_index || !root_round || !root_y_is_event) {
+        set_err(err, HGX_ERR_INVALID, "hgx_reset: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    std::vector<int32_t> rr(root_round, root_round + c->C);
+    std::vector<uint8_t> ye(c->C);
+    bool rooted = false;
+    for (int p = 0; p < c->C; p++) {
+        ye[p] = root_y_is_event[p] ? 1 : 0;
+        if (rr[p] >= 0 || ye[p]) rooted = true;
+    }
+    if (rooted && c->G != 1) {
+        set_err(err, HGX_ERR_INVALID, "hgx_reset: roots need a single-graph context");
+        return HGX_ERR_INVALID;
+    }
+    if (rooted && c->n > 256) {
+        set_err(err, HGX_ERR_INVALID, "hgx_reset: roots need n <= 256 (the per-candidate round step)");
+        return HGX_ERR_INVALID;
+    }
+    if (c->eng.clear() != hipSuccess || c->eng.set_roots(rr, ye) != hipSuccess) return dev_err(err, hipErrorUnknown,
+                                                                                                  "hgx_reset");
+    c->root_index.assign(root_index, root_index + c->C);
+    c->root_round = rr;
+    c->root_y_ext = ye;
+    c->rooted = rooted;
+    std::fill(c->chain_len.begin(), c->chain_len.end(), 0);
+    std::fill(c->chain_base.begin(), c->chain_base.end(), 0);
+    std::fill(c->last_gid.begin(), c->last_gid.end(), -1);
+    std::fill(c->last_index.begin(), c->last_index.end(), -1);
+    for (int g = 0; g < c->G; g++) {
+        GraphState& s = c->gs[g];
+        s.undecided.clear();
+        s.queued_upto = -1;
+        s.queued.clear();
+        s.pending_loaded = s.undetermined = 0;
+        s.last_round = -1;
+        s.fame.clear();
+        s.round_events.clear();
+        for (Block& b : s.blocks) b.first = -1;   // kept (blockCache); their events are gone
+        c->order[g] = GraphOrder();
+    }
+    std::fill(c->g_events.begin(), c->g_events.end(), 0);
+    std::fill(c->g_loaded.begin(), c->g_loaded.end(), 0);
+    c->arena.used = 0;
+    c->E = c->E_div = 0;
+    c->divided = false;
+    c->mirror_ok = c->chains_ok = false;
+    c->rounds_cached = c->recv_cached = false;
+    return ok(err);
+}
+
+// forward declarations (per-event results, below)
+static int32_t ensure_rounds(hgx_ctx* c);
+static int32_t round_of(hgx_ctx* c, int64_t x);
+
+// ---- GetFrame (hashgraph.go:897-995) ---------------------------------------------------
+// Roots from LastConsensusRound's witnesses (and, for participants without one, from their
+// last event), the frame's events in topological order and the Root.Others entries of frame
+// events whose other-parent is not an earlier frame event. Encodings as in hgx.h.
+int32_t hgx_get_frame(hgx_ctx* c, int64_t* events, int64_t events_cap, int64_t* n_events, int64_t* root_x,
+                      int64_t* root_y, int32_t* root_index, int32_t* root_round, int64_t* others_event,
+                      int64_t* others_parent, int64_t others_cap, int64_t* n_others, hgx_error* err) {
+    if (!c || c->G != 1 || !n_events || !n_others || !root_x || !root_y || !root_index || !root_round) {
+        set_err(err, HGX_ERR_INVALID, "hgx_get_frame: bad arguments (single-graph contexts)");
+        return HGX_ERR_INVALID;
+    }
+    const GraphState& s = c->gs[0];
+    const int32_t lcr = s.has_lcr ? s.lcr : 0;
+    if (!c->divided || lcr < 0 || lcr > s.last_round || s.round_events[(size_t)lcr] == 0) {   // Store.GetRound
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(lcr) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    DeviceGuard dg(c);
+    if (ensure_rounds(c) || ensure_mirror(c) || ensure_chains(c)) return dev_err(err, hipErrorUnknown, "hgx_get_frame");
+    const int n = c->n, C = c->C;
+    std::vector<int64_t> evs;
+    std::vector<uint8_t> has(n, 0);
+    auto root_from = [&](int p, int64_t ev) {
+        root_x[p] = c->sp[(size_t)ev];
+        root_y[p] = c->op[(size_t)ev];
+        root_index[p] = c->index32[(size_t)ev] - 1;
+        root_round[p] = round_of(c, c->sp[(size_t)ev]);   // Round(Root.X outside the store) = -1
+    };
+    for (int p = 0; p < n; p++) {   // LastConsensusRound's witnesses
+        if (c->rh.wflag[(size_t)lcr * C + p] != 2) continue;
+        const int32_t k = c->rh.bm[(size_t)lcr * C + p];
+        const int64_t w = c->chain_gids[(size_t)p][(size_t)k];
+        has[p] = 1;
+        root_from(p, w);
+        for (size_t j = (size_t)k; j < c->chain_gids[(size_t)p].size(); j++) evs.push_back(c->chain_gids[(size_t)p][j]);
+    }
+    for (int p = 0; p < n; p++) {   // participants without a witness there: their last event
+        if (has[p]) continue;
+        if (c->chain_len[(size_t)p] == 0) {   // LastFrom is the Root: keep it
+            root_x[p] = -1;
+            root_y[p] = c->root_y_ext[(size_t)p] ? HGX_ROOT_Y : -1;
+            root_index[p] = c->root_index[(size_t)p];
+            root_round[p] = c->root_round[(size_t)p];
+            continue;
+        }
+        const int64_t ev = c->chain_gids[(size_t)p].back();
+        evs.push_back(ev);
+        root_from(p, ev);
+    }
+    std::sort(evs.begin(), evs.end());   // ByTopologicalOrder
+    std::vector<uint8_t> treated((size_t)c->E + 1, 0);
+    int64_t no = 0;
+    for (int64_t ev : evs) {
+        treated[(size_t)ev] = 1;
+        const int64_t op = c->op[(size_t)ev];
+        if (op == -1) continue;
+        if (!(op >= 0 && treated[(size_t)op]) && c->sp[(size_t)ev] != root_x[c->creator[(size_t)ev]]) {
+            if (no < others_cap && others_event && others_parent) {
+                others_event[no] = ev;
+                others_parent[no] = op;
+            }
+            no++;
+        }
+    }
+    *n_others = no;
+    *n_events = (int64_t)evs.size();
+    for (size_t k = 0; k < evs.size() && (int64_t)k < events_cap && events; k++) events[k] = evs[k];
+    return ok(err);
 }
 
 // ---- DivideRounds (hashgraph.go:616-646) -----------------------------------------
@@ -376,9 +525,6 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
     for (int g = 0; g < c->G; g++) {
         GraphState& s = c->gs[g];
         const int32_t LR = c->rh.last_round[g];
-        // rounds first seen in this call are queued in ascending order
-        for (int32_t r = s.queued_upto + 1; r <= LR; r++) s.undecided.push_back(r);
-        s.queued_upto = std::max(s.queued_upto, LR);
         s.last_round = LR;
         s.fame.resize((size_t)(LR + 1) * n, 0);
         // rounds below r_lo kept their boundaries (incremental DivideRounds)
@@ -391,6 +537,28 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
             }
             s.round_events[r] = (int32_t)cnt;
         }
+        if (!c->rooted) {
+            // rounds first seen in this call are queued in ascending order
+            for (int32_t r = s.queued_upto + 1; r <= LR; r++) s.undecided.push_back(r);
+            s.queued_upto = std::max(s.queued_upto, LR);
+            continue;
+        }
+        // after a Reset rounds start at the roots' rounds and can first appear out of order:
+        // queue the rounds with events not queued yet by their first event (DivideRounds
+        // walks UndeterminedEvents in insertion order, hashgraph.go:617-638)
+        s.queued.resize(LR + 1, 0);
+        std::vector<int32_t> first;
+        e = c->eng.round_first_gids(0, first);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_divide_rounds");
+        std::vector<std::pair<int32_t, int32_t>> fresh;
+        for (int32_t r = 0; r <= LR; r++)
+            if (!s.queued[r] && s.round_events[r] > 0) fresh.push_back({first[(size_t)r], r});
+        std::sort(fresh.begin(), fresh.end());
+        for (auto& fr : fresh) {
+            s.undecided.push_back(fr.second);
+            s.queued[(size_t)fr.second] = 1;
+        }
+        s.queued_upto = std::max(s.queued_upto, LR);
     }
     return ok(err);
 }
@@ -814,16 +982,17 @@ int32_t hgx_participant_event(hgx_ctx* c, int32_t p, int64_t index, int64_t* gid
     return ok(err);
 }
 
-// Store.GetRoot (inmem_store.go:155-161): the genesis Root (root.go:70-77) of every participant
+// Store.GetRoot (inmem_store.go:163-169): X = -1 (Root.X: "" for a genesis Root, else the
+// event named when hgx_reset installed it), Y = -1 ("") or HGX_ROOT_Y, Index, Round
 int32_t hgx_get_root(hgx_ctx* c, int32_t p, int64_t* x, int64_t* y, int32_t* index, int32_t* round, hgx_error* err) {
     if (!valid_participant(c, p)) {
         set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(p) + ", Not Found");
         return HGX_ERR_KEY_NOT_FOUND;
     }
     if (x) *x = -1;
-    if (y) *y = -1;
-    if (index) *index = -1;
-    if (round) *round = -1;
+    if (y) *y = c->root_y_ext[(size_t)p] ? HGX_ROOT_Y : -1;
+    if (index) *index = c->root_index[(size_t)p];
+    if (round) *round = c->root_round[(size_t)p];
     return ok(err);
 }
 
@@ -861,7 +1030,8 @@ int32_t hgx_wire_info(hgx_ctx* c, int64_t first, int64_t count, int32_t* self_pa
     for (int64_t k = 0; k < count; k++) {
         const size_t x = (size_t)(first + k);
         const int32_t sp = c->sp[x], op = c->op[x];
-        if (self_parent_index) self_parent_index[k] = sp >= 0 ? c->index32[(size_t)sp] : -1;
+        // a first event's self-parent is the Root: Root.Index (hashgraph.go:537-545)
+        if (self_parent_index) self_parent_index[k] = sp >= 0 ? c->index32[(size_t)sp] : c->root_index[(size_t)c->creator[x]];
         if (other_parent_creator) other_parent_creator[k] = op >= 0 ? c->creator[(size_t)op] : -1;
         if (other_parent_index) other_parent_index[k] = op >= 0 ? c->index32[(size_t)op] : -1;
     }
@@ -898,8 +1068,11 @@ static int32_t round_of(hgx_ctx* c, int64_t x) {
 }
 static int32_t witness_of(hgx_ctx* c, int64_t x) {   // Witness (hashgraph.go:265-282)
     if (x < 0 || x >= (int64_t)c->round_cache.size()) return 0;
-    if (c->sp[(size_t)x] == -1 && c->op[(size_t)x] == -1) return 1;
-    return round_of(c, x) > round_of(c, c->sp[(size_t)x]) ? 1 : 0;
+    // the creator's first event on its Root: SelfParent == Root.X && OtherParent == Root.Y
+    const int32_t sp = c->sp[(size_t)x], op = c->op[(size_t)x];
+    const bool yext = c->root_y_ext[(size_t)c->creator[(size_t)x]] != 0;
+    if (sp == -1 && ((op == -1 && !yext) || op == HGX_ROOT_Y)) return 1;
+    return round_of(c, x) > round_of(c, sp) ? 1 : 0;   // Round(Root.X) = -1
 }
 
 int32_t hgx_get_rounds(hgx_ctx* c, int64_t first, int64_t count, int32_t* round, int8_t* witness, int8_t* famous) {

@@ -124,6 +124,9 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
     HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
     HGX_TRY(c_old.alloc(C)); HGX_TRY(fu.alloc(C)); HGX_TRY(rcnt.alloc(C));
+    HGX_TRY(root_round_d.alloc(C)); HGX_TRY(root_y_ext_d.alloc(C));
+    HGX_TRY(hipMemsetAsync(root_round_d.p, 0xFF, (size_t)C * 4, stream));   // genesis: Round -1, Y ""
+    HGX_TRY(hipMemsetAsync(root_y_ext_d.p, 0, (size_t)C, stream));
     HGX_TRY(p_gid.alloc(PP)); HGX_TRY(p_chain.alloc(PP)); HGX_TRY(p_op.alloc(PP)); HGX_TRY(p_opu.alloc(PP));
     HGX_TRY(p_round.alloc(PP)); HGX_TRY(p_rr.alloc(PP)); HGX_TRY(p_ts.alloc(PP)); HGX_TRY(p_cts.alloc(PP));
     fd_ld = (Ppos + 1) & ~(int64_t)1;
@@ -253,6 +256,7 @@ InsertState Engine::insert_state() {
     st.succ = succ.p; st.first_none = first_none.p;
     st.last_gid = last_gid_d.p; st.last_index = last_index_d.p; st.chain_base = chain_base_d.p;
     st.fail = ins_fail.p; st.graph_loaded = graph_loaded_d.p;
+    st.root_y_ext = root_y_ext_d.p; st.rooted = rooted ? 1 : 0;
     return st;
 }
 
@@ -325,6 +329,29 @@ hipError_t Engine::clear() {
     E_div = 0;
     R = 0;
     laid_out = false;
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::set_roots(const std::vector<int32_t>& round, const std::vector<uint8_t>& y_ext) {
+    rooted = false;
+    root_gmax = -1;
+    for (int c = 0; c < C; c++) {
+        if (round[c] >= 0 || y_ext[c]) rooted = true;
+        root_gmax = std::max(root_gmax, round[c] + 1);
+    }
+    if (!rooted) root_gmax = -1;
+    HGX_TRY(hipMemcpyAsync(root_round_d.p, round.data(), (size_t)C * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(hipMemcpyAsync(root_y_ext_d.p, y_ext.data(), (size_t)C, hipMemcpyHostToDevice, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::round_first_gids(int32_t r0, std::vector<int32_t>& out) {
+    out.assign((size_t)std::max(0, R - r0), 0x7FFFFFFF);
+    if (R <= r0) return hipSuccess;
+    if (rfirst.n < (size_t)(R - r0)) HGX_TRY(rfirst.alloc((size_t)std::max(R - r0, 2 * (int)rfirst.n)));
+    HGX_TRY(hipMemsetAsync(rfirst.p, 0x7F, (size_t)(R - r0) * 4, stream));
+    launch_round_first_gid(stream, arrays(), r0, R, C, rfirst.p);
+    HGX_TRY(hipMemcpyAsync(out.data(), rfirst.p, (size_t)(R - r0) * 4, hipMemcpyDeviceToHost, stream));
     return hipStreamSynchronize(stream);
 }
 
@@ -490,6 +517,16 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     kbeg(K_FD_BUILD);
     launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
     kend(K_FD_BUILD, (double)(En - E0) * 2.0 * csz * n);
+    if (rooted) {   // root floors of every position (after a Reset)
+        if (n > 256) return hipErrorNotSupported;   // only k_round_k applies them
+        if (gfl.n < (size_t)Ppos) HGX_TRY(gfl.alloc((size_t)Ppos));
+        const size_t need = (size_t)(root_gmax + 1) * C;
+        if (gB.n < need) {
+            HGX_TRY(gB.alloc(need));
+            drop_step_graph();
+        }
+        launch_root_floor(stream, a, root_round_d.p, gfl.p, gB.p, root_gmax, C, n, max_len);
+    }
     if (rebuild) {   // events received before the rebuild (a prefix of every chain)
         HGX_TRY(hipMemsetAsync(fu.p, 0, (size_t)C * 4, stream));
         launch_fu_count(stream, a, En);
@@ -527,6 +564,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         A.p_gid = p_gid.p; A.g_coin = g_coin.p; A.FD8 = FD8.p; A.ovf = ovf.p;
         A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
         A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
+        A.gB = rooted ? gB.p : nullptr;
+        A.gmax = rooted ? root_gmax : -1;
         return A;
     };
     kbeg(K_ROUND_GATHER);
@@ -548,14 +587,17 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 HGX_TRY(ensure_round_cap(need));
                 a = arrays();
             }
-            if (!sgr.exec || sgr.kernel != round_kernel || sgr.compact != compact || sgr.nb != nb) {
+            const int kern = rooted ? 0 : round_kernel;   // root floors: per-candidate step only
+            const RoundArgs cur = round_args();
+            if (!sgr.exec || sgr.kernel != kern || sgr.compact != compact || sgr.nb != nb || sgr.args.gB != cur.gB ||
+                sgr.args.gmax != cur.gmax) {
                 sgr.drop();
-                sgr.args = round_args();
-                sgr.kernel = round_kernel;
+                sgr.args = cur;
+                sgr.kernel = kern;
                 sgr.compact = compact;
                 sgr.nb = nb;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                for (int k = 0; k < nb; k++) (void)launch_round_step(stream, sgr.args, k, round_kernel);
+                for (int k = 0; k < nb; k++) (void)launch_round_step(stream, sgr.args, k, kern);
                 HGX_TRY(hipStreamEndCapture(stream, &sgr.graph));
                 HGX_TRY(hipGraphInstantiate(&sgr.exec, sgr.graph, nullptr, nullptr, 0));
                 // the step nodes in launch order (a linear chain)

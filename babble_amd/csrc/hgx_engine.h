@@ -114,6 +114,13 @@ class Engine {
     // their consensus timestamps to (to_buf) or from buf, a device or host pointer
     hipError_t shard_copy(int lo, int hi, void* buf, bool on_device, bool to_buf);
     int shard_lo = 0, shard_hi = 0;               // chains whose consensus timestamps this context computes
+    // Roots (hgx_reset): per chain Root.Round and whether Root.Y is an event outside the store;
+    // genesis roots (Round -1, Y "") when not rooted
+    hipError_t set_roots(const std::vector<int32_t>& round, const std::vector<uint8_t>& y_ext);
+    bool rooted = false;
+    int root_gmax = -1;   // max Root.Round + 1 (rounds that root floors can force), -1 unrooted
+    // smallest gid of a witness of each round in [r0, R) (UndecidedRounds order after a Reset)
+    hipError_t round_first_gids(int32_t r0, std::vector<int32_t>& out);
     // D2H of order[first, first+count) of the last find_order (async; then sync())
     hipError_t copy_order(int32_t* dst, int64_t first, int64_t count);
     hipError_t sync() { return hipStreamSynchronize(stream); }
@@ -160,6 +167,8 @@ class Engine {
     std::vector<int32_t> h_fu;         // [C] events of each chain received so far (a prefix)
     int32_t fo_m = 0;                  // events received by the FindOrder in progress
     std::vector<int32_t> fo_cnt;       // [C] ... per chain
+    DBuf<int32_t> root_round_d, gfl, gB, rfirst;   // roots: [C], per position floor, [(gmax+1) x C], [R]
+    DBuf<uint8_t> root_y_ext_d;
     DBuf<int32_t> sh_off;              // shard exchange: chain offsets
     DBuf<int64_t> sh_buf;              // ... and staging of host buffers
     // gid order

@@ -76,6 +76,10 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
         if (ok) {
             const int oc = creator_of(op, E0, in, st);
             ok = oc >= 0 && oc < C && oc / n == cr / n;
+        } else {
+            // unknown other-parents only through the creator's Root (hashgraph.go:430-440):
+            // Root.X == SelfParent && Root.Y == OtherParent, or Root.Others[event] == OtherParent
+            ok = (op == kRootY && sp == -1 && st.root_y_ext[cr]) || (op == kRootOther && st.rooted);
         }
         if (!ok) code = INS_OTHER_PARENT;
     }

@@ -69,7 +69,12 @@ struct InsertState {
     int32_t *last_gid, *last_index, *chain_base;   // [C] per-chain state before / after the batch
     unsigned long long* fail;           // min over failing events of (k << 8 | code)
     unsigned long long* graph_loaded;   // [G] loaded events inserted (IsLoaded, event.go:119-126)
+    const uint8_t* root_y_ext;          // [C] Root.Y names an event outside the store (after hgx_reset)
+    int rooted;                         // a Reset installed roots (Root.Others codes accepted)
 };
+
+// other-parent codes for parents outside the store after a Reset (include/hgx.h)
+constexpr int64_t kRootY = -3, kRootOther = -4;
 
 // first-failure codes of the insert check (hgx_insert_events, hashgraph.go:356-401)
 enum InsertCode {
@@ -90,6 +95,11 @@ struct RoundArgs {
     int32_t *Bm, *WLA, *WFD, *p_round, *active, *lr;
     uint8_t *wflag, *wstat, *wcoin;
     uint64_t* Smat;
+    // Roots (after hgx_reset): gB[r][c] = first offset of chain c whose root floor reaches r
+    // (the event sees the first event of a chain whose Root.Round + 1 >= r), rounds r <= gmax;
+    // gmax = -1 without roots
+    const int32_t* gB;
+    int gmax;
 };
 
 int fd_tile_rows(int n, int compact);
@@ -116,6 +126,11 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r, int block
 hipError_t launch_round_k(hipStream_t s, const RoundArgs& A, int r);
 void launch_round_k_gather(hipStream_t s, const RoundArgs& A, int r);   // round r's rebased rows + ovf[r]
 int round_k_ndw(int n);
+// root floors (hgx_reset): per position G = max over chains i whose first event it sees of
+// Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
+void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,
+                       int gmax, int C, int n, int max_len);
+void launch_round_first_gid(hipStream_t s, const DevArrays& a, int r0, int R, int C, int32_t* first);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
 void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();     // -DHGX_STEP_PROF builds only

@@ -1422,6 +1422,48 @@ __global__ void k_gather_i32(int64_t E, const int32_t* __restrict__ src, const i
 }
 
 // ---------------------------------------------------------------------------------
+// root floors after a Reset (hashgraph.go:202-262 with Roots): an event that sees the first
+// event of chain i (Root.Round(i) + 1 by RoundInc's isRoot rule) has round >= Root.Round(i) + 1,
+// so R_{r+1} = {W'_r test} u {G >= r+1}, G(x) = max over those chains
+template <typename CT>
+__global__ void k_root_floor(const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
+                             const int32_t* __restrict__ c_base, const int32_t* __restrict__ root_round,
+                             const CT* __restrict__ LA, int32_t* __restrict__ gfl, int C, int n, int max_len) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)C * max_len) return;
+    const int c = (int)(t % C), k = (int)(t / C);
+    if (k >= c_len[c]) return;
+    const int g = c / n;
+    const int64_t p = (int64_t)c_off[c] + k;
+    int G = 0;
+    for (int i = 0; i < n; i++) {
+        const int gi = g * n + i;
+        const int32_t la = Coord<CT>::la(LA[(size_t)p * n + i]);
+        if (c_len[gi] > 0 && la >= c_base[gi]) G = max(G, root_round[gi] + 1);
+    }
+    gfl[p] = G;
+}
+
+__global__ void k_root_bound_init(int32_t* __restrict__ gB, const int32_t* __restrict__ c_len, int C, int gmax) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)(gmax + 1) * C) return;
+    gB[t] = c_len[t % C];
+}
+
+__global__ void k_root_bound(const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
+                             const int32_t* __restrict__ gfl, int32_t* __restrict__ gB, int C, int gmax,
+                             int max_len) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)C * max_len) return;
+    const int c = (int)(t % C), k = (int)(t / C);
+    if (k >= c_len[c]) return;
+    const int64_t p = (int64_t)c_off[c] + k;
+    const int gp = k > 0 ? gfl[p - 1] : -1;
+    const int G = min(gfl[p], gmax);
+    for (int r = gp + 1; r <= G; r++) gB[(size_t)r * C + c] = k;   // G is monotone along the chain
+}
+
+// ---------------------------------------------------------------------------------
 // order of a small received set (m <= kSortSmallMax, the incremental schedule's usual
 // case): one block bitonic-sorts (graph, rr, cts, S) in LDS, S compared from HBM only on
 // equal (graph, rr, cts) (consensus_sorter.go:36-51). Replaces the radix passes' ~40
@@ -1765,6 +1807,41 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
     hipLaunchKernelGGL(k_tiefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_cts, a.p_gid, a.g_S);
     *final_vals = va;
     *final_keys = ka;
+}
+
+void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,
+                       int gmax, int C, int n, int max_len) {
+    const int64_t work = (int64_t)C * max_len;
+    if (work <= 0 || gmax < 0) return;
+    if (a.compact)
+        hipLaunchKernelGGL(k_root_floor<uint16_t>, dim3(nblk(work, 256)), dim3(256), 0, s, a.c_off, a.c_len, a.c_base,
+                           root_round, (const uint16_t*)a.LA, gfl, C, n, max_len);
+    else
+        hipLaunchKernelGGL(k_root_floor<int32_t>, dim3(nblk(work, 256)), dim3(256), 0, s, a.c_off, a.c_len, a.c_base,
+                           root_round, (const int32_t*)a.LA, gfl, C, n, max_len);
+    hipLaunchKernelGGL(k_root_bound_init, dim3(nblk((int64_t)(gmax + 1) * C, 256)), dim3(256), 0, s, gB, a.c_len, C,
+                       gmax);
+    hipLaunchKernelGGL(k_root_bound, dim3(nblk(work, 256)), dim3(256), 0, s, a.c_off, a.c_len, gfl, gB, C, gmax,
+                       max_len);
+}
+
+// UndecidedRounds order of rounds first seen after a Reset: first[r - r0] = the smallest gid
+// of a witness of round r (the first event of its chain in the round has the chain's smallest
+// gid there)
+__global__ void k_round_first_gid(int r0, int R, int C, const int32_t* __restrict__ Bm, const uint8_t* __restrict__ wstat,
+                                  const int32_t* __restrict__ c_off, const int32_t* __restrict__ p_gid,
+                                  int32_t* __restrict__ first) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)(R - r0) * C) return;
+    const int r = r0 + (int)(t / C), c = (int)(t % C);
+    if (wstat[(size_t)r * C + c] != 2) return;
+    atomicMin(&first[r - r0], p_gid[c_off[c] + Bm[(size_t)r * C + c]]);
+}
+
+void launch_round_first_gid(hipStream_t s, const DevArrays& a, int r0, int R, int C, int32_t* first) {
+    if (R <= r0) return;
+    hipLaunchKernelGGL(k_round_first_gid, dim3(nblk((int64_t)(R - r0) * C, 256)), dim3(256), 0, s, r0, R, C, a.Bm,
+                       a.wstat, a.c_off, a.p_gid, first);
 }
 
 bool sort_small_ok(int32_t m) { return m <= kSortSmallMax; }

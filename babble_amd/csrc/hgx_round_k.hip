@@ -178,6 +178,8 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     // rebased row (written by the step that found the candidate), the flags and the bases
     const int b = A.Bm[(size_t)s * C + gc];
     const int len = A.c_len[gc], off = A.c_off[gc];
+    // root floor (after hgx_reset): offsets >= gk have round >= s+1 whatever they strongly see
+    const int gk = (s + 1 <= A.gmax) ? A.gB[(size_t)(s + 1) * C + gc] : len;
     const int j = cw * 64 + lane;        // this lane's candidate
     const int jj = j < n ? j : 0;
     uint32_t fd[HD];
@@ -407,7 +409,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         if (wh == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
             const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
             const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
-            const uint64_t m = __ballot(lane < np && (int)inc >= sm);
+            const uint64_t m = __ballot(lane < np && ((int)inc >= sm || kbase + lane >= gk));
             const int tot = __builtin_amdgcn_readlane((int)inc, 63);
             if (lane == 0) {
                 s_B[grp] = m ? (int)__builtin_ctzll(m) : -1;

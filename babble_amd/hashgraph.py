@@ -115,6 +115,36 @@ class Hashgraph:
         """node/core.go:277-303"""
         self._call(self.L.hgx_run_consensus)
 
+    # ------------------------------------------------------------------ Reset / GetFrame
+    ROOT_Y, ROOT_OTHER = -3, -4   # other-parent codes after a Reset (hgx.h)
+
+    def Reset(self, root_index, root_round, root_y_is_event):
+        """Hashgraph.Reset(roots) (hashgraph.go:877-895): per participant Root.Index, Root.Round and
+        whether Root.Y names an event. Then insert with self-parent -1 = Root.X and other-parent
+        ROOT_Y / ROOT_OTHER for parents outside the store."""
+        a = [np.ascontiguousarray(x, np.int32) for x in (root_index, root_round, root_y_is_event)]
+        err = hgx_error()
+        rc = self.L.hgx_reset(self.ctx, *[ptr(x) for x in a], C.byref(err))
+        _lib.check(rc, err)
+
+    def GetFrame(self):
+        """Hashgraph.GetFrame (hashgraph.go:897-995): roots (x, y, index, round per participant),
+        events (gids, topological order), others {event: other-parent}."""
+        C_ = self.n * self.G
+        ne, no = C.c_int64(), C.c_int64()
+        rx, ry = np.zeros(C_, np.int64), np.zeros(C_, np.int64)
+        ri, rr = np.zeros(C_, np.int32), np.zeros(C_, np.int32)
+        err = hgx_error()
+        cap = self.num_events() + 1
+        ev = np.zeros(cap, np.int64)
+        oe, op = np.zeros(cap, np.int64), np.zeros(cap, np.int64)
+        rc = self.L.hgx_get_frame(self.ctx, ptr(ev), cap, C.byref(ne), ptr(rx), ptr(ry), ptr(ri), ptr(rr), ptr(oe),
+                                  ptr(op), cap, C.byref(no), C.byref(err))
+        _lib.check(rc, err)
+        return dict(roots=[(int(rx[p]), int(ry[p]), int(ri[p]), int(rr[p])) for p in range(C_)],
+                    events=[int(x) for x in ev[:ne.value]],
+                    others={int(oe[k]): int(op[k]) for k in range(no.value)})
+
     # ------------------------------------------------------------------ row-sharded graph
     def set_shard(self, rank: int, world: int):
         """One graph row-sharded over `world` ranks (hgx_set_shard)."""

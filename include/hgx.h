@@ -55,6 +55,10 @@ enum {
 };
 
 #define HGX_UNKNOWN_PARENT (-2)
+/* After hgx_reset, other-parents outside the store that CheckOtherParent accepts through the
+ * creator's Root (hashgraph.go:430-440): */
+#define HGX_ROOT_Y (-3)       /* Root.Y (the creator's first event, self-parent = Root.X = -1) */
+#define HGX_ROOT_OTHER (-4)   /* Root.Others[event] (the caller checked the entry) */
 
 typedef struct {
     int32_t code;
@@ -130,6 +134,22 @@ int32_t hgx_reset_consensus(hgx_ctx* ctx);
  * the device allocations kept. */
 int32_t hgx_clear(hgx_ctx* ctx);
 
+/* ---- persistence: Reset / GetFrame (hashgraph.go:877-995, root.go) -------- */
+/* Hashgraph.Reset(roots): forget the events and rounds (keeping LastConsensusRound,
+ * LastCommitedRoundEvents, ConsensusTransactions and the blocks, like the reference) and
+ * install one Root per participant: Index, Round and whether Root.Y names an event (1) or is
+ * "" (0). Inserted events then name Root.X as self-parent -1 and Root.Y / Root.Others as
+ * HGX_ROOT_Y / HGX_ROOT_OTHER. Single-graph contexts with n <= 256. */
+int32_t hgx_reset(hgx_ctx* ctx, const int32_t* root_index, const int32_t* root_round, const int32_t* root_y_is_event,
+                  hgx_error* err);
+/* Hashgraph.GetFrame: per participant root_x / root_y (gid; -1 = the current Root.X / ""; 
+ * HGX_ROOT_Y / HGX_ROOT_OTHER as inserted), root_index, root_round; the frame's events (gids,
+ * topological order) and Root.Others pairs (event, other-parent). Counts are returned in full;
+ * arrays get the first `cap`. "<r>, Not Found" when LastConsensusRound's round is not stored. */
+int32_t hgx_get_frame(hgx_ctx* ctx, int64_t* events, int64_t events_cap, int64_t* n_events, int64_t* root_x,
+                      int64_t* root_y, int32_t* root_index, int32_t* root_round, int64_t* others_event,
+                      int64_t* others_parent, int64_t others_cap, int64_t* n_others, hgx_error* err);
+
 /* ---- Hashgraph state (hashgraph.go:15-37) --------------------------------- */
 int64_t hgx_num_events(hgx_ctx* ctx);
 int32_t hgx_super_majority(hgx_ctx* ctx);
@@ -173,7 +193,8 @@ int32_t hgx_participant_events(hgx_ctx* ctx, int32_t participant, int64_t skip, 
                                int64_t* count, hgx_error* err);
 /* ParticipantEvent(p, index) (caches.go:74-80): "<index>, Too Late" / "<index>, Not Found" */
 int32_t hgx_participant_event(hgx_ctx* ctx, int32_t participant, int64_t index, int64_t* gid, hgx_error* err);
-/* GetRoot (inmem_store.go:155-161): the genesis Root, X = Y = "" (-1), Index = Round = -1 */
+/* GetRoot (inmem_store.go:163-169): X = -1 (Root.X), Y = -1 ("") or HGX_ROOT_Y, Index, Round
+ * (the genesis Root: Index = Round = -1, or the one hgx_reset installed) */
 int32_t hgx_get_root(hgx_ctx* ctx, int32_t participant, int64_t* x, int64_t* y, int32_t* index, int32_t* round,
                      hgx_error* err);
 /* GetEvent (inmem_store.go:48-55): the DAG fields of an inserted event (bodies stay with the caller) */

@@ -102,6 +102,11 @@ struct hgo {
     vec64 tx_off; vec64 tx_len; uint8_t* txblob; int64_t txblob_n, txblob_cap;
     /* participant event caches (ParticipantEventsCache / RollingIndex without roll) */
     vec64* chain; int64_t* chain_base; int64_t* last_index;
+    /* Roots (root.go:62-67): Index, Round, and whether Y names an event outside the store
+       (genesis: X = Y = "", Index = Round = -1). Parent codes: self-parent -1 = Root.X; other
+       parent -1 = "", HGO_ROOT_Y = Root.Y (outside the store), HGO_ROOT_OTHER = the event's
+       Root.Others entry (outside the store) */
+    int32_t* root_index; int32_t* root_round; uint8_t* root_y_ext;
     /* Hashgraph fields (hashgraph.go:15-37) */
     vec64 undetermined;
     vec64 undecided;
@@ -123,6 +128,10 @@ hgo* hgo_new(int n) {
     h->chain_base = (int64_t*)calloc((size_t)n, sizeof(int64_t));
     h->last_index = (int64_t*)malloc((size_t)n * sizeof(int64_t));
     for (int i = 0; i < n; i++) h->last_index[i] = -1;  /* RollingIndex.lastIndex = -1 */
+    h->root_index = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    h->root_round = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    h->root_y_ext = (uint8_t*)calloc((size_t)n, 1);
+    for (int i = 0; i < n; i++) { h->root_index[i] = -1; h->root_round[i] = -1; }  /* NewBaseRoot */
     v_push(&h->undecided, 0);                          /* UndecidedRounds: []int{0} (:64) */
     h->last_round = -1;                                /* InmemStore.lastRound = -1 */
     hm_init(&h->ss_memo, 1 << 12);
@@ -139,6 +148,7 @@ void hgo_free(hgo* h) {
     free(h->tx_off.a); free(h->tx_len.a); free(h->txblob);
     for (int i = 0; i < h->n; i++) free(h->chain[i].a);
     free(h->chain); free(h->chain_base); free(h->last_index);
+    free(h->root_index); free(h->root_round); free(h->root_y_ext);
     free(h->undetermined.a); free(h->undecided.a);
     for (int64_t r = 0; r < h->rounds_cap; r++) { free(h->rounds[r].events.a); free(h->rounds[r].witnesses.a); }
     free(h->rounds);
@@ -226,12 +236,14 @@ int hgo_parent_round(hgo* h, int64_t x, int* is_root) {  /* :202-262 */
     if (known(h, x) && h->pr_known[x]) { *is_root = h->pr_root[x]; return h->pr_round[x]; }
     int res_round = -1, res_root = 0;                    /* NewBaseParentRoundInfo */
     if (!known(h, x)) { *is_root = 0; return -1; }
-    /* genesis Root: X = Y = "", Round = -1 */
+    const int c = h->creator[x];
+    const int rr0 = h->root_round[c];
     int spRound, spRoot, opRound = -1, opRoot = 0;
-    if (h->sp[x] == -1) { spRound = -1; spRoot = 1; }
+    if (h->sp[x] == -1) { spRound = rr0; spRoot = 1; }    /* SelfParent == Root.X */
     else { spRound = hgo_round(h, h->sp[x]); spRoot = 0; }
     if (known(h, h->op[x])) opRound = hgo_round(h, h->op[x]);
-    else if (h->op[x] == -1) { opRound = -1; opRoot = 1; }
+    else if ((h->op[x] == -1 && !h->root_y_ext[c]) || h->op[x] == HGO_ROOT_Y) { opRound = rr0; opRoot = 1; }
+    else if (h->op[x] == HGO_ROOT_OTHER) { opRound = rr0; opRoot = 0; }   /* Root.Others */
     res_round = spRound; res_root = spRoot;
     if (spRound < opRound) { res_round = opRound; res_root = opRoot; }
     h->pr_known[x] = 1; h->pr_round[x] = res_round; h->pr_root[x] = (uint8_t)res_root;
@@ -266,7 +278,8 @@ int hgo_round(hgo* h, int64_t x) {                       /* :320-339 (memoised) 
 
 int hgo_witness(hgo* h, int64_t x) {                     /* :265-282 */
     if (!known(h, x)) return 0;
-    if (h->sp[x] == -1 && h->op[x] == -1) return 1;
+    /* SelfParent == Root.X && OtherParent == Root.Y */
+    if (h->sp[x] == -1 && ((h->op[x] == -1 && !h->root_y_ext[h->creator[x]]) || h->op[x] == HGO_ROOT_Y)) return 1;
     return hgo_round(h, x) > hgo_round(h, h->sp[x]);
 }
 
@@ -302,11 +315,14 @@ int hgo_insert(hgo* h, int creator, int64_t index, int64_t sp, int64_t op, int64
         set_err(err, errlen, "CheckSelfParent: Self-parent not last known event by creator");
         return 100;
     }
-    /* CheckOtherParent (:423-445) */
+    /* CheckOtherParent (:423-445): unknown other-parents only through the creator's Root:
+       Root.X == SelfParent && Root.Y == OtherParent, or Root.Others[event] == OtherParent */
     if (op != -1 && !known(h, op)) {
-        /* Root.X == sp && Root.Y == op requires op == "" here; Root.Others is empty */
-        set_err(err, errlen, "CheckOtherParent: Other-parent not known");
-        return 101;
+        const int via_root = (op == HGO_ROOT_Y && sp == -1 && h->root_y_ext[creator]) || op == HGO_ROOT_OTHER;
+        if (!via_root) {
+            set_err(err, errlen, "CheckOtherParent: Other-parent not known");
+            return 101;
+        }
     }
     /* topologicalIndex++ (:373-374) is consumed even if SetEvent fails below */
     int64_t topo = h->topo_counter++;
@@ -338,9 +354,9 @@ int hgo_insert(hgo* h, int creator, int64_t index, int64_t sp, int64_t op, int64
     h->round_known[x] = 0; h->pr_known[x] = 0; h->famous[x] = 0; h->in_round[x] = 0;
     h->rr[x] = -1; h->cts[x] = 0;
     /* SetWireInfo (:532-567) */
-    h->w_spi[x] = (sp == -1) ? -1 /* root.Index */ : (int32_t)h->index[sp];
-    h->w_opc[x] = (op == -1) ? -1 : h->creator[op];
-    h->w_opi[x] = (op == -1) ? -1 : (int32_t)h->index[op];
+    h->w_spi[x] = (sp == -1) ? h->root_index[creator] : (int32_t)h->index[sp];
+    h->w_opc[x] = known(h, op) ? h->creator[op] : -1;
+    h->w_opi[x] = known(h, op) ? (int32_t)h->index[op] : -1;
     /* InitEventCoordinates (:448-499) */
     int32_t* la = h->la + x * n;
     int32_t* fd = h->fd + x * n;
@@ -375,6 +391,110 @@ int hgo_insert(hgo* h, int creator, int64_t index, int64_t sp, int64_t op, int64
     v_push(&h->undetermined, x);
     /* IsLoaded (event.go:119-126) */
     if (index == 0 || (!tx_nil && ntx > 0)) h->pending_loaded++;
+    return 0;
+}
+
+/* ---------------- Reset (hashgraph.go:877-895, inmem_store.go:184-192) ---------------- */
+int hgo_reset(hgo* h, const int32_t* root_index, const int32_t* root_round, const uint8_t* root_y_ext) {
+    /* Store.Reset: new roots; event, round and consensus caches and the participant
+       RollingIndexes cleared; lastRound = -1. The block cache is kept. */
+    for (int i = 0; i < h->n; i++) {
+        h->root_index[i] = root_index[i];
+        h->root_round[i] = root_round[i];
+        h->root_y_ext[i] = root_y_ext[i] ? 1 : 0;
+        h->chain[i].n = 0;
+        h->chain_base[i] = 0;
+        h->last_index[i] = -1;
+    }
+    h->E = 0;
+    for (int64_t r = 0; r < h->rounds_cap; r++) {
+        h->rounds[r].exists = 0; h->rounds[r].queued = 0;
+        h->rounds[r].events.n = 0; h->rounds[r].witnesses.n = 0;
+    }
+    h->last_round = -1;
+    hm_free(&h->ss_memo);
+    hm_init(&h->ss_memo, 1 << 12);
+    h->consensus.n = 0;
+    /* Hashgraph.Reset: UndeterminedEvents, UndecidedRounds (empty, not [0]), PendingLoadedEvents,
+       topologicalIndex and the memo caches; LastConsensusRound, LastCommitedRoundEvents and
+       ConsensusTransactions are kept */
+    h->undetermined.n = 0;
+    h->undecided.n = 0;
+    h->pending_loaded = 0;
+    h->topo_counter = 0;
+    return 0;
+}
+
+void hgo_get_root(hgo* h, int p, int32_t* index, int32_t* round, int* y_ext) {
+    *index = h->root_index[p];
+    *round = h->root_round[p];
+    *y_ext = h->root_y_ext[p];
+}
+
+/* ---------------- GetFrame (hashgraph.go:897-995) ----------------
+   Roots: X = the root event's self-parent (gid, or -1 = the participant's current Root.X),
+   Y = its other-parent (gid, -1 = "", HGO_ROOT_Y / HGO_ROOT_OTHER = outside the store as
+   inserted), Index = Index - 1, Round = Round(self-parent). Others: (event, other-parent)
+   pairs for frame events whose other-parent is not an earlier frame event. Events: gids in
+   topological (= insertion) order. Returns 0, or 1 (GetRound(LastConsensusRound) not found). */
+static int cmp_i64(const void* a, const void* b);
+
+int hgo_get_frame(hgo* h, int64_t* ev_out, int64_t ev_cap, int64_t* n_ev, int64_t* root_x, int64_t* root_y,
+                  int32_t* root_index, int32_t* root_round, int64_t* oth_ev, int64_t* oth_op, int64_t oth_cap,
+                  int64_t* n_oth) {
+    const int n = h->n;
+    const int lcr = h->has_lcr ? h->lcr : 0;
+    if (lcr < 0 || lcr >= h->rounds_cap || !h->rounds[lcr].exists) return 1;
+    vec64 evs = {0, 0, 0};
+    uint8_t* has_root = (uint8_t*)calloc((size_t)n, 1);
+    const vec64* ws = &h->rounds[lcr].witnesses;
+    for (int64_t k = 0; k < ws->n; k++) {
+        const int64_t w = ws->a[k];
+        const int c = h->creator[w];
+        v_push(&evs, w);
+        has_root[c] = 1;
+        root_x[c] = h->sp[w];
+        root_y[c] = h->op[w];
+        root_index[c] = (int32_t)(h->index[w] - 1);
+        root_round[c] = hgo_round(h, h->sp[w]);
+        /* ParticipantEvents(creator, w.Index()): the creator's events after w */
+        for (int64_t j = h->index[w] + 1 - h->chain_base[c]; j < h->chain[c].n; j++) v_push(&evs, h->chain[c].a[j]);
+    }
+    for (int p = 0; p < n; p++) {
+        if (has_root[p]) continue;
+        if (h->chain[p].n == 0) {   /* LastFrom is the Root: keep it */
+            root_x[p] = -1;
+            root_y[p] = h->root_y_ext[p] ? HGO_ROOT_Y : -1;
+            root_index[p] = h->root_index[p];
+            root_round[p] = h->root_round[p];
+        } else {
+            const int64_t ev = h->chain[p].a[h->chain[p].n - 1];
+            v_push(&evs, ev);
+            root_x[p] = h->sp[ev];
+            root_y[p] = h->op[ev];
+            root_index[p] = (int32_t)(h->index[ev] - 1);
+            root_round[p] = hgo_round(h, h->sp[ev]);
+        }
+    }
+    qsort(evs.a, (size_t)evs.n, sizeof(int64_t), cmp_i64);   /* ByTopologicalOrder */
+    uint8_t* treated = (uint8_t*)calloc((size_t)(h->E + 1), 1);
+    int64_t no = 0;
+    for (int64_t k = 0; k < evs.n; k++) {
+        const int64_t ev = evs.a[k];
+        treated[ev] = 1;
+        const int64_t op = h->op[ev];
+        if (op == -1) continue;
+        if (!(known(h, op) && treated[op]) && h->sp[ev] != root_x[h->creator[ev]]) {
+            if (no < oth_cap) { oth_ev[no] = ev; oth_op[no] = op; }
+            no++;
+        }
+    }
+    *n_oth = no;
+    *n_ev = evs.n;
+    for (int64_t k = 0; k < evs.n && k < ev_cap; k++) ev_out[k] = evs.a[k];
+    free(evs.a);
+    free(has_root);
+    free(treated);
     return 0;
 }
 

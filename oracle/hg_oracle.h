@@ -43,6 +43,18 @@ int64_t hgo_insert_batch(hgo* h, int64_t m, const int32_t* creator, const int64_
                          const int32_t* ntx, const int32_t* tx_nil, const uint8_t* tx_blob, const int32_t* tx_len,
                          int* rc, char* err, int errlen);
 
+/* other-parent codes for events whose other-parent is outside the store after a Reset
+   (CheckOtherParent through the creator's Root, hashgraph.go:430-440) */
+#define HGO_ROOT_Y (-3)      /* Root.Y */
+#define HGO_ROOT_OTHER (-4)  /* Root.Others[event] */
+/* Hashgraph.Reset(roots) (hashgraph.go:877-895): per participant Root.Index, Root.Round and
+   whether Root.Y names an event (1) or is "" (0); a first event's self-parent -1 is Root.X */
+int hgo_reset(hgo* h, const int32_t* root_index, const int32_t* root_round, const uint8_t* root_y_ext);
+void hgo_get_root(hgo* h, int p, int32_t* index, int32_t* round, int* y_ext);
+/* Hashgraph.GetFrame (hashgraph.go:897-995); see hg_oracle.c for the encodings */
+int hgo_get_frame(hgo* h, int64_t* ev_out, int64_t ev_cap, int64_t* n_ev, int64_t* root_x, int64_t* root_y,
+                  int32_t* root_index, int32_t* root_round, int64_t* oth_ev, int64_t* oth_op, int64_t oth_cap,
+                  int64_t* n_oth);
 int hgo_divide_rounds(hgo* h);                       /* hashgraph.go:616-646 */
 int hgo_decide_fame(hgo* h, char* err, int errlen);  /* hashgraph.go:649-730 */
 int hgo_decide_round_received(hgo* h, char* err, int errlen); /* :753-799 */

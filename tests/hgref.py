@@ -80,6 +80,10 @@ def oracle_lib():
     L.hgo_consensus_events.argtypes = [p, p, i64]
     L.hgo_consensus_events.restype = i64
     L.hgo_known.argtypes = [p, p]
+    L.hgo_reset.argtypes = [p, p, p, p]
+    L.hgo_reset.restype = i32
+    L.hgo_get_frame.argtypes = [p, p, i64, p, p, p, p, p, p, p, i64, p]
+    L.hgo_get_frame.restype = i32
     L.hgo_block.argtypes = [p, i64, p, p, p, p, p]
     L.hgo_block_tx.argtypes = [p, i64, i32, p, i64]
     L.hgo_block_tx.restype = i64
@@ -383,6 +387,27 @@ class Oracle:
         self.L.hgo_known(self.h, _ptr(out))
         return out
 
+    def reset(self, root_index, root_round, root_y_is_event):
+        """Hashgraph.Reset(roots) (hashgraph.go:877-895)."""
+        a = [np.ascontiguousarray(root_index, np.int32), np.ascontiguousarray(root_round, np.int32),
+             np.ascontiguousarray(root_y_is_event, np.uint8)]
+        return self.L.hgo_reset(self.h, *[_ptr(x) for x in a])
+
+    def get_frame(self):
+        """Hashgraph.GetFrame (hashgraph.go:897-995), the encodings of include/hgx.h hgx_get_frame."""
+        n, E = self.n, self.E()
+        ev, oe, op = np.zeros(E + 1, np.int64), np.zeros(E + 1, np.int64), np.zeros(E + 1, np.int64)
+        rx, ry = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        ri, rr = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        ne, no = C.c_int64(), C.c_int64()
+        rc = self.L.hgo_get_frame(self.h, _ptr(ev), E + 1, C.byref(ne), _ptr(rx), _ptr(ry), _ptr(ri), _ptr(rr),
+                                  _ptr(oe), _ptr(op), E + 1, C.byref(no))
+        if rc:
+            raise RuntimeError(f"hgo_get_frame: {rc}")
+        return dict(roots=[(int(rx[p]), int(ry[p]), int(ri[p]), int(rr[p])) for p in range(n)],
+                    events=[int(x) for x in ev[:ne.value]],
+                    others={int(oe[k]): int(op[k]) for k in range(no.value)})
+
     def blocks(self):
         res = []
         for b in range(self.L.hgo_num_blocks(self.h)):
@@ -518,3 +543,53 @@ class CoreSim:
 
     def consensus_hex(self, core) -> List[str]:
         return [self.events[self.l2g[core][int(x)]]["hex"] for x in self.backends[core].consensus_events()]
+
+
+# ----------------------------------------------------------------------------- Reset / frames
+ROOT_Y, ROOT_OTHER, UNKNOWN = -3, -4, -2
+
+
+def frame_root_arrays(frame):
+    """hgx_reset / hgo_reset arguments from a frame's roots."""
+    idx = [r[2] for r in frame["roots"]]
+    rnd = [r[3] for r in frame["roots"]]
+    yev = [0 if r[1] == -1 else 1 for r in frame["roots"]]
+    return idx, rnd, yev
+
+
+def remap_after_reset(t, order, frame, new=None):
+    """The source events `order` (source gids, topological) as a trace to insert into a
+    hashgraph reset with `frame`'s roots, parents resolved like InsertEvent does
+    (hashgraph.go:404-445): a parent already re-inserted -> its new gid; a self-parent equal to
+    the creator's Root.X -> -1; an other-parent equal to Root.Y -> ROOT_Y, or to the event's
+    Root.Others entry -> ROOT_OTHER; anything else -> UNKNOWN. `new` (source gid -> new gid)
+    carries over between calls. Returns (trace, new)."""
+    new = {} if new is None else new
+    base = len(new)
+    sp_new, op_new = [], []
+    for k, src in enumerate(order):
+        c = int(t.creator[src])
+        rx, ry = frame["roots"][c][0], frame["roots"][c][1]
+        sp, op = int(t.sp[src]), int(t.op[src])
+        sp_new.append(new[sp] if sp in new else (-1 if sp == rx else UNKNOWN))
+        if op == -1:
+            op_new.append(-1)
+        elif op in new:
+            op_new.append(new[op])
+        elif op == ry:
+            op_new.append(ROOT_Y)
+        elif frame["others"].get(src) == op:
+            op_new.append(ROOT_OTHER)
+        else:
+            op_new.append(UNKNOWN)
+        new[src] = base + k
+    sel = np.asarray(order, np.int64)
+    cols = dict(creator=t.creator[sel], index=t.index[sel], sp=np.array(sp_new, np.int64),
+                op=np.array(op_new, np.int64), ts=t.ts[sel], hash=t.hash[sel], s=t.s[sel], ntx=t.ntx[sel],
+                txnil=t.txnil[sel])
+    if hasattr(t, "tx_seq"):
+        sub = type(t)(t.n, tx_seq=t.tx_seq[sel], **cols)
+    else:
+        sub = Trace(n=t.n, txs=[t.txs[int(x)] for x in sel],
+                    names=[t.names[int(x)] for x in sel] if t.names else [], **cols)
+    return sub, new
