@@ -40,6 +40,10 @@ def ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+# void (*)(void* user, int32 graph, int64 b, int32 rr, int64 first, int32 n_events, int64 n_tx)
+COMMIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int64)
+
+
 def _sig(L, name, res, args):
     f = getattr(L, name, None)
     if f is None:
@@ -120,6 +124,7 @@ def lib():
     _sig(L, "hgx_find_order_end", i32, [p, p])
     _sig(L, "hgx_set_shard", i32, [p, i32, i32])
     _sig(L, "hgx_reset", i32, [p, p, p, p, p])
+    _sig(L, "hgx_set_commit_callback", i32, [p, C.c_void_p, p])
     _sig(L, "hgx_get_frame", i32, [p, p, i64, p, p, p, p, p, p, p, i64, p, p])
     _sig(L, "hgx_shard_values", i64, [p, i32])
     _sig(L, "hgx_shard_export", i32, [p, p, i32])

@@ -118,6 +118,9 @@ struct hgx_ctx {
     std::vector<int32_t> root_index, root_round;
     std::vector<uint8_t> root_y_ext;
     bool rooted = false;
+    // commitCh (hashgraph.go:848-854): called for every new block with transactions
+    hgx_commit_fn commit_fn = nullptr;
+    void* commit_user = nullptr;
 };
 
 static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
@@ -733,6 +736,8 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
             b.tx_nil = (oh.blk_nil[bi] && b.ntx == 0) ? 1 : 0;
             b.committed = b.ntx > 0 ? 1 : 0;   // commitCh only if len(Transactions) > 0
             s.blocks.push_back(b);
+            if (b.committed && c->commit_fn)   // commitCh <- block, in SetBlock order
+                c->commit_fn(c->commit_user, g, (int64_t)s.blocks.size() - 1, b.rr, b.first, b.nev, b.ntx);
             s.consensus_tx += b.ntx;
             s.pending_loaded -= oh.blk_loaded[bi];
             off += cnt;
@@ -1258,6 +1263,13 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
     c->eng.round_kernel = mode;
+    return HGX_OK;
+}
+
+int32_t hgx_set_commit_callback(hgx_ctx* c, hgx_commit_fn fn, void* user) {
+    if (!c) return HGX_ERR_INVALID;
+    c->commit_fn = fn;
+    c->commit_user = user;
     return HGX_OK;
 }
 

@@ -9,8 +9,9 @@
 // Arithmetic: 8 x 32-bit limbs, Montgomery multiplication (CIOS, v_mad_u64_u32) modulo p
 // (field) and modulo N (scalars, s^-1 by Fermat); Jacobian points, a = -3 doubling
 // (dbl-2001-b) and complete-case addition (add-2007-bl, doubling / infinity branches per
-// lane). u1 G + u2 Q by Straus with 4-bit windows over per-key tables [0..15]Q built once
-// per distinct key (a sync batch has few creators) and the same table for G. The final
+// lane). u1 G + u2 Q by Straus with 4-bit windows over per-key affine tables [1..15]Q built
+// once per distinct key (a sync batch has few creators) and the same table for G, so the
+// window additions are mixed Jacobian + affine (madd-2007-bl, 7M + 4S). The final
 // compare avoids the field inversion: X == r Z^2 or, when r + N < p, X == (r + N) Z^2.
 // Public keys that are not P-256 points (Go's elliptic.Unmarshal returns nil) give 2.
 #include <hip/hip_runtime.h>
@@ -51,6 +52,8 @@ __device__ constexpr uint32_t kGx[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0
                                         0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
 __device__ constexpr uint32_t kGy[8] = {0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u,
                                         0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
+__device__ constexpr uint32_t kPm2[8] = {0xFFFFFFFDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u,
+                                         0x00000000u, 0x00000000u, 0x00000001u, 0xFFFFFFFFu};
 __device__ constexpr uint32_t kNm2[8] = {0xFC63254Fu, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu,
                                          0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u, 0xFFFFFFFFu};
 
@@ -276,24 +279,72 @@ __device__ __forceinline__ void padd(Pt& o, const Pt& a, const Pt& b) {
     cpy(o.Z, Z3);
 }
 
-// table layout: [key][16][X | Y | Z] limbs (entry 0 = infinity)
-constexpr int kTabWords = 16 * 24;
-
-__device__ __forceinline__ void tab_load(Pt& p, const uint32_t* __restrict__ t) {
+// madd-2007-bl: Jacobian a + affine (x2, y2) (Z2 = 1), with the infinity / doubling cases
+__device__ __forceinline__ void pmadd(Pt& o, const Pt& a, const Fe x2, const Fe y2) {
+    if (is_zero(a.Z)) {
+        cpy(o.X, x2);
+        cpy(o.Y, y2);
+        cpy(o.Z, kOneP);
+        return;
+    }
+    Fe z1z1, u2, s2, t, H, r;
+    mmul<ModP>(z1z1, a.Z, a.Z);
+    mmul<ModP>(u2, x2, z1z1);
+    mmul<ModP>(t, a.Z, z1z1);
+    mmul<ModP>(s2, y2, t);
+    msub<ModP>(H, u2, a.X);
+    msub<ModP>(r, s2, a.Y);
+    if (is_zero(H)) {
+        if (is_zero(r)) {
+            pdbl(o, a);
+        } else {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        p.X[i] = t[i];
-        p.Y[i] = t[8 + i];
-        p.Z[i] = t[16 + i];
+            for (int i = 0; i < 8; i++) o.Z[i] = 0;
+        }
+        return;
+    }
+    Fe HH, I, J, V, X3, Y3;
+    mmul<ModP>(HH, H, H);
+    madd<ModP>(I, HH, HH);
+    madd<ModP>(I, I, I);            // 4 HH
+    mmul<ModP>(J, H, I);
+    madd<ModP>(r, r, r);            // 2 (S2 - Y1)
+    mmul<ModP>(V, a.X, I);
+    mmul<ModP>(X3, r, r);
+    msub<ModP>(X3, X3, J);
+    msub<ModP>(X3, X3, V);
+    msub<ModP>(X3, X3, V);
+    msub<ModP>(t, V, X3);
+    mmul<ModP>(Y3, r, t);
+    mmul<ModP>(t, a.Y, J);
+    madd<ModP>(t, t, t);
+    msub<ModP>(Y3, Y3, t);
+    madd<ModP>(t, a.Z, H);
+    mmul<ModP>(o.Z, t, t);
+    msub<ModP>(o.Z, o.Z, z1z1);
+    msub<ModP>(o.Z, o.Z, HH);
+    cpy(o.X, X3);
+    cpy(o.Y, Y3);
+}
+
+// a^(M - 2) (Montgomery form in and out), by square-and-multiply over a constant exponent
+template <class M>
+__device__ __forceinline__ void mpow_m2(Fe r, const Fe a, const uint32_t* e, const uint32_t* one) {
+    cpy(r, one);
+    for (int b = 255; b >= 0; b--) {
+        mmul<M>(r, r, r);
+        if ((e[b >> 5] >> (b & 31)) & 1u) mmul<M>(r, r, a);
     }
 }
 
-__device__ __forceinline__ void tab_store(uint32_t* __restrict__ t, const Pt& p) {
+// table layout: [key][16][x | y] affine limbs (Montgomery form), entry 0 unused
+constexpr int kTabWords = 16 * 16;
+
+__device__ __forceinline__ void tab_load(Fe x, Fe y, const uint32_t* __restrict__ t) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        t[i] = p.X[i];
-        t[8 + i] = p.Y[i];
-        t[16 + i] = p.Z[i];
+        x[i] = t[i];
+        y[i] = t[8 + i];
     }
 }
 
@@ -301,11 +352,14 @@ __device__ __forceinline__ void tab_store(uint32_t* __restrict__ t, const Pt& p)
 
 using namespace p256;
 
-// one thread per key (keys [0, nk): 65-byte uncompressed points; key nk: the base point G).
-// valid[k] = 1 when the key is a P-256 point (0x04 prefix, X, Y < p, Y^2 = X^3 - 3X + b).
+// one thread per (key, multiple j = 1..15) (keys [0, nk): 65-byte uncompressed points; key nk:
+// the base point G): [j]P by j - 1 additions, stored affine (x = X / Z^2, y = Y / Z^3; a valid
+// point of prime order has no multiple below 16 at infinity). valid[k] = 1 when the key is a
+// P-256 point (0x04 prefix, X, Y < p, Y^2 = X^3 - 3X + b).
 __global__ void __launch_bounds__(64) k_p256_tables(int nk, const uint8_t* __restrict__ keys65,
                                                     uint32_t* __restrict__ tab, uint8_t* __restrict__ valid) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = t / 15, j = 1 + t % 15;
     if (k > nk) return;
     Fe x, y;
     bool ok = true;
@@ -324,31 +378,35 @@ __global__ void __launch_bounds__(64) k_p256_tables(int nk, const uint8_t* __res
     mmul<ModP>(P.Y, y, kR2P);
     cpy(P.Z, kOneP);
     if (ok) {   // on the curve: y^2 == x^3 - 3x + b
-        Fe l, r, t;
+        Fe l, r, tt;
         mmul<ModP>(l, P.Y, P.Y);
-        mmul<ModP>(t, P.X, P.X);
-        mmul<ModP>(r, t, P.X);
+        mmul<ModP>(tt, P.X, P.X);
+        mmul<ModP>(r, tt, P.X);
         msub<ModP>(r, r, P.X);
         msub<ModP>(r, r, P.X);
         msub<ModP>(r, r, P.X);
         madd<ModP>(r, r, kBm);
         ok = eq(l, r);
     }
-    valid[k] = ok ? 1 : 0;
-    uint32_t* tk = tab + (size_t)k * kTabWords;
-    Pt inf;
-#pragma unroll
-    for (int i = 0; i < 8; i++) { inf.X[i] = 0; inf.Y[i] = 0; inf.Z[i] = 0; }
-    tab_store(tk, inf);
+    if (j == 1) valid[k] = ok ? 1 : 0;
     if (!ok) return;
-    tab_store(tk + 24, P);
+    uint32_t* tk = tab + (size_t)k * kTabWords;
     Pt acc = P;
-    for (int j = 2; j < 16; j++) {
+    for (int m = 2; m <= j; m++) {
         Pt nx;
         padd(nx, acc, P);
         acc = nx;
-        tab_store(tk + 24 * j, acc);
     }
+    Fe zi, zi2, tt;
+    mpow_m2<ModP>(zi, acc.Z, kPm2, kOneP);
+    mmul<ModP>(zi2, zi, zi);
+    mmul<ModP>(tt, acc.X, zi2);
+#pragma unroll
+    for (int i = 0; i < 8; i++) tk[16 * j + i] = tt[i];
+    mmul<ModP>(tt, zi2, zi);
+    mmul<ModP>(zi, acc.Y, tt);
+#pragma unroll
+    for (int i = 0; i < 8; i++) tk[16 * j + 8 + i] = zi[i];
 }
 
 __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, const int32_t* __restrict__ key_idx,
@@ -378,11 +436,7 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
     // w = s^-1 (Montgomery form), by s^(N-2)
     Fe sm, w, u1, u2;
     mmul<ModN>(sm, s, kR2N);
-    cpy(w, kOneN);
-    for (int b = 255; b >= 0; b--) {
-        mmul<ModN>(w, w, w);
-        if ((kNm2[b >> 5] >> (b & 31)) & 1u) mmul<ModN>(w, w, sm);
-    }
+    mpow_m2<ModN>(w, sm, kNm2, kOneN);
     mmul<ModN>(u1, e, w);   // e s^-1 (plain form)
     mmul<ModN>(u2, r, w);
     // Straus, 4-bit windows
@@ -391,27 +445,34 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
     Pt acc;
 #pragma unroll
     for (int q = 0; q < 8; q++) { acc.X[q] = 0; acc.Y[q] = 0; acc.Z[q] = 0; }
-    for (int wi = 63; wi >= 0; wi--) {
-        if (!is_zero(acc.Z)) {
-            for (int d = 0; d < 4; d++) {
-                Pt t2;
-                pdbl(t2, acc);
-                acc = t2;
+    // limbs outer (compile-time index: no dynamic register-array indexing), nibbles inner
+#pragma unroll
+    for (int li = 7; li >= 0; li--) {
+        const uint32_t w1 = u1[li], w2 = u2[li];
+        for (int sh = 28; sh >= 0; sh -= 4) {
+            if (!is_zero(acc.Z)) {
+                for (int d = 0; d < 4; d++) {
+                    Pt t2;
+                    pdbl(t2, acc);
+                    acc = t2;
+                }
             }
-        }
-        const uint32_t d1 = (u1[wi >> 3] >> (4 * (wi & 7))) & 15u;
-        const uint32_t d2 = (u2[wi >> 3] >> (4 * (wi & 7))) & 15u;
-        if (d1) {
-            Pt t, nx;
-            tab_load(t, tg + 24 * d1);
-            padd(nx, acc, t);
-            acc = nx;
-        }
-        if (d2) {
-            Pt t, nx;
-            tab_load(t, tq + 24 * d2);
-            padd(nx, acc, t);
-            acc = nx;
+            const uint32_t d1 = (w1 >> sh) & 15u;
+            const uint32_t d2 = (w2 >> sh) & 15u;
+            if (d1) {
+                Fe x, y;
+                Pt nx;
+                tab_load(x, y, tg + 16 * d1);
+                pmadd(nx, acc, x, y);
+                acc = nx;
+            }
+            if (d2) {
+                Fe x, y;
+                Pt nx;
+                tab_load(x, y, tq + 16 * d2);
+                pmadd(nx, acc, x, y);
+                acc = nx;
+            }
         }
     }
     if (is_zero(acc.Z)) {
@@ -445,7 +506,7 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
 size_t p256_table_bytes(int nk) { return (size_t)(nk + 1) * kTabWords * 4; }
 
 void launch_p256_tables(hipStream_t s, int nk, const uint8_t* keys65, uint32_t* tab, uint8_t* valid) {
-    hipLaunchKernelGGL(k_p256_tables, dim3((nk + 1 + 63) / 64), dim3(64), 0, s, nk, keys65, tab, valid);
+    hipLaunchKernelGGL(k_p256_tables, dim3(((nk + 1) * 15 + 63) / 64), dim3(64), 0, s, nk, keys65, tab, valid);
 }
 
 void launch_p256_verify(hipStream_t s, int64_t count, int nk, const int32_t* key_idx, const uint8_t* dig,

@@ -115,6 +115,20 @@ class Hashgraph:
         """node/core.go:277-303"""
         self._call(self.L.hgx_run_consensus)
 
+    def set_commit_callback(self, fn):
+        """commitCh (hashgraph.go:848-854): fn(graph, block, rr, first, n_events, n_tx) for every new
+        block with transactions, from inside FindOrder; None removes it."""
+        if fn is None:
+            self._commit_cb = None
+            rc = self.L.hgx_set_commit_callback(self.ctx, None, None)
+        else:
+            def tramp(_user, g, b, rr, first, nev, ntx):
+                fn(int(g), int(b), int(rr), int(first), int(nev), int(ntx))
+            self._commit_cb = _lib.COMMIT_FN(tramp)   # kept alive while registered
+            rc = self.L.hgx_set_commit_callback(self.ctx, C.cast(self._commit_cb, C.c_void_p), None)
+        if rc:
+            raise HgxError(rc, "hgx_set_commit_callback failed")
+
     # ------------------------------------------------------------------ Reset / GetFrame
     ROOT_Y, ROOT_OTHER = -3, -4   # other-parent codes after a Reset (hgx.h)
 

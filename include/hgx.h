@@ -174,6 +174,13 @@ int32_t hgx_consensus_events(hgx_ctx* ctx, int32_t graph, int64_t first, int64_t
 int64_t hgx_num_blocks(hgx_ctx* ctx, int32_t graph);
 int32_t hgx_block_info(hgx_ctx* ctx, int32_t graph, int64_t b, int32_t* round_received, int64_t* first,
                        int32_t* n_events, int64_t* n_tx, int32_t* tx_nil, int32_t* committed);
+/* commitCh (hashgraph.go:848-854, node/node.go:150-154 -> AppProxy.CommitBlock): fn is called
+ * from hgx_find_order for every new block with transactions, in SetBlock order, after the
+ * block's state is recorded (graph, block index b, RoundReceived, first position and number of
+ * its events in the graph's consensus order, transactions). NULL removes it. */
+typedef void (*hgx_commit_fn)(void* user, int32_t graph, int64_t b, int32_t round_received, int64_t first,
+                              int32_t n_events, int64_t n_tx);
+int32_t hgx_set_commit_callback(hgx_ctx* ctx, hgx_commit_fn fn, void* user);
 /* Store.GetBlock(rr) (inmem_store.go:163-169): index b of the block with RoundReceived rr,
  * else HGX_ERR_KEY_NOT_FOUND "<rr>, Not Found" */
 int32_t hgx_get_block(hgx_ctx* ctx, int32_t graph, int32_t round_received, int64_t* b, hgx_error* err);

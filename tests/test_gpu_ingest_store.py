@@ -354,3 +354,25 @@ def test_core_playbooks_as_the_shim_calls(plays):
             got = [cores[c]["hexes"][int(x)] for x in cores[c]["h"].ConsensusEvents()]
             assert got == so.consensus_hex(c), (fx, c)
             assert cores[c]["h"].LastConsensusRound() == so.backends[c].last_consensus_round()
+
+
+def test_commit_callback_like_commit_ch():
+    """hgx_set_commit_callback: commitCh sends (hashgraph.go:848-854) — every block with
+    transactions, in SetBlock order, over a chunked run; the callback reads the block's events."""
+    t = gtrace.gossip(8, 4000, 91, stale_prob=0.1, stale_depth=2)
+    h = _hg(8, cap=t.E)
+    got = []
+
+    def on_block(g, b, rr, first, nev, ntx):
+        order = h.ConsensusEvents(g)
+        txs = [t.tx_payload(int(x)) for x in order[first:first + nev]]
+        got.append((b, rr, ntx, sum(len(x) for x in txs)))
+
+    h.set_commit_callback(on_block)
+    for lo in range(0, t.E, 500):
+        h.insert_trace(t, lo, min(t.E, lo + 500))
+        h.RunConsensus()
+    blocks = h.Blocks()
+    want = [(i, b["rr"], b["ntx"], b["ntx"]) for i, b in enumerate(blocks) if b["ntx"] > 0]
+    assert got == want and len(got) > 3
+    h.set_commit_callback(None)
