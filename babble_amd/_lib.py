@@ -35,6 +35,12 @@ class hgx_events(C.Structure):
                  "ntx", "tx_nil")]
 
 
+class hgx_wire_events(C.Structure):
+    _fields_ = [(nm, C.c_void_p) for nm in
+                ("creator_id", "index", "self_parent_index", "other_parent_creator", "other_parent_index",
+                 "timestamp_ns", "hash", "sig_s", "ntx", "tx_nil")]
+
+
 def ptr(a: np.ndarray):
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(C.c_void_p)
@@ -124,6 +130,7 @@ def lib():
     _sig(L, "hgx_find_order_end", i32, [p, p])
     _sig(L, "hgx_set_shard", i32, [p, i32, i32])
     _sig(L, "hgx_reset", i32, [p, p, p, p, p])
+    _sig(L, "hgx_insert_wire_events", i32, [p, p, i64, p, p])
     _sig(L, "hgx_set_commit_callback", i32, [p, C.c_void_p, p])
     _sig(L, "hgx_get_frame", i32, [p, p, i64, p, p, p, p, p, p, p, i64, p, p])
     _sig(L, "hgx_shard_values", i64, [p, i32])

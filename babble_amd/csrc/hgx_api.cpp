@@ -333,6 +333,93 @@ int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64
     return finish_insert(c, out, n_inserted, err);
 }
 
+// Core.Sync's loop (node/core.go:199-211) over a SyncResponse's WireEvents: ReadWireInfo
+// (hashgraph.go:569-614, parents through Store.ParticipantEvent, which sees the events of the
+// batch inserted before) then InsertEvent(ev, false), stopping at the first error. Parents are
+// resolved on the host against the participants' RollingIndexes plus the batch so far ("as if
+// every earlier event was accepted", like the device insert); the prefix before the first
+// resolution error goes through the batched device insert, whose first failure comes first.
+int32_t hgx_insert_wire_events(hgx_ctx* c, const hgx_wire_events* w, int64_t count, int64_t* n_inserted,
+                               hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !w || count < 0 ||
+        (count > 0 && (!w->creator_id || !w->index || !w->self_parent_index || !w->other_parent_creator ||
+                       !w->other_parent_index || !w->timestamp_ns || !w->hash || !w->sig_s || !w->ntx || !w->tx_nil))) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_wire_events: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    if (ensure_chains(c)) return dev_err(err, hipErrorUnknown, "hgx_insert_wire_events");
+    const int64_t E0 = c->E;
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> pend((size_t)c->C);   // (index, gid) of the batch
+    // RollingIndex.GetItem over the participant's events plus the batch's (common/rolling_index.go:40-50)
+    auto participant_event = [&](int32_t p, int64_t idx, int64_t* gid, std::string& msg) -> int32_t {
+        if (p < 0 || p >= c->C) {   // ReverseParticipants miss: participantEvents[""] is nil
+            msg = "runtime error: invalid memory address or nil pointer dereference";
+            return HGX_ERR_PANIC;
+        }
+        const auto& pb = pend[(size_t)p];
+        const int64_t items = c->chain_len[(size_t)p] + (int64_t)pb.size();
+        const int64_t last = pb.empty() ? c->last_index[(size_t)p] : pb.back().first;
+        const int64_t oldest = last - items + 1;
+        if (idx < oldest) { msg = go_rune(idx) + ", Too Late"; return HGX_ERR_TOO_LATE; }
+        const int64_t f = idx - oldest;
+        if (f >= items) { msg = go_rune(idx) + ", Not Found"; return HGX_ERR_KEY_NOT_FOUND; }
+        const int64_t cl = c->chain_len[(size_t)p];
+        *gid = f < cl ? c->chain_gids[(size_t)p][(size_t)f] : pb[(size_t)(f - cl)].second;
+        return HGX_OK;
+    };
+    std::vector<int32_t> creator((size_t)count);
+    std::vector<int64_t> sp((size_t)count), op((size_t)count);
+    int64_t m = count;
+    int32_t rrc = HGX_OK;
+    std::string rmsg;
+    for (int64_t k = 0; k < count; k++) {
+        const int32_t cr = w->creator_id[k];
+        if (cr < 0 || cr >= c->C) {   // creator[2:] of "" (hashgraph.go:578-582)
+            m = k;
+            rrc = HGX_ERR_PANIC;
+            rmsg = "runtime error: slice bounds out of range [2:0]";
+            break;
+        }
+        int64_t s = -1, o = -1;
+        int32_t rc = HGX_OK;
+        if (w->self_parent_index[k] >= 0) rc = participant_event(cr, w->self_parent_index[k], &s, rmsg);
+        if (rc == HGX_OK && w->other_parent_index[k] >= 0)
+            rc = participant_event(w->other_parent_creator[k], w->other_parent_index[k], &o, rmsg);
+        if (rc != HGX_OK) {
+            m = k;
+            rrc = rc;
+            break;
+        }
+        creator[(size_t)k] = cr;
+        sp[(size_t)k] = s;
+        op[(size_t)k] = o;
+        pend[(size_t)cr].push_back({w->index[k], E0 + k});
+    }
+    const hgx_events ev{creator.data(), w->index, sp.data(), op.data(), w->timestamp_ns, w->hash, w->sig_s, w->ntx,
+                        w->tx_nil};
+    int64_t ins = 0;
+    const int32_t rc = m > 0 ? hgx_insert_events(c, &ev, m, &ins, err) : ok(err);
+    if (n_inserted) *n_inserted = ins;
+    if (ins > 0) {   // the host mirrors stay valid: append the accepted events (no O(E) rebuild per sync)
+        for (int64_t k = 0; k < ins; k++) {
+            c->creator.push_back(creator[(size_t)k]);
+            c->index32.push_back((int32_t)w->index[k]);
+            c->sp.push_back((int32_t)sp[(size_t)k]);
+            c->op.push_back((int32_t)op[(size_t)k]);
+            c->chain_gids[(size_t)creator[(size_t)k]].push_back((int32_t)(E0 + k));
+        }
+        c->mirror_ok = c->chains_ok = true;
+    }
+    if (rc != HGX_OK) return rc;
+    if (rrc != HGX_OK) {
+        set_err(err, rrc, rmsg);
+        return rrc;
+    }
+    return HGX_OK;
+}
+
 int32_t hgx_insert_events_device(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted,
                                  hgx_error* err) {
     if (n_inserted) *n_inserted = 0;

@@ -445,8 +445,7 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
     Pt acc;
 #pragma unroll
     for (int q = 0; q < 8; q++) { acc.X[q] = 0; acc.Y[q] = 0; acc.Z[q] = 0; }
-    // limbs outer (compile-time index: no dynamic register-array indexing), nibbles inner
-#pragma unroll
+    // limbs outer, nibbles inner
     for (int li = 7; li >= 0; li--) {
         const uint32_t w1 = u1[li], w2 = u2[li];
         for (int sh = 28; sh >= 0; sh -= 4) {

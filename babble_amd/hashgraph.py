@@ -66,6 +66,24 @@ class Hashgraph:
         _lib.check(rc, err)
         return n_ins.value
 
+    def insert_wire(self, creator_id, index, sp_index, op_creator, op_index, ts, hash32, s32, ntx, txnil) -> int:
+        """Core.Sync's loop over WireEvents (hgx_insert_wire_events): ReadWireInfo + InsertEvent(e, false)
+        per event; on the first error raises HgxError with .inserted = events inserted before it."""
+        a = [np.ascontiguousarray(creator_id, np.int32), np.ascontiguousarray(index, np.int64),
+             np.ascontiguousarray(sp_index, np.int64), np.ascontiguousarray(op_creator, np.int32),
+             np.ascontiguousarray(op_index, np.int64), np.ascontiguousarray(ts, np.int64),
+             np.ascontiguousarray(hash32, np.uint8), np.ascontiguousarray(s32, np.uint8),
+             np.ascontiguousarray(ntx, np.int32), np.ascontiguousarray(txnil, np.int32)]
+        ev = _lib.hgx_wire_events(*[ptr(x) for x in a])
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_wire_events(self.ctx, C.byref(ev), int(a[0].shape[0]), C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(rc, err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        return n_ins.value
+
     def insert_device(self, dt: "DeviceTrace", lo: int = 0, hi: Optional[int] = None) -> int:
         """Bulk InsertEvent of a trace already resident in HBM (hgx_insert_events_device)."""
         hi = dt.E if hi is None else hi

@@ -104,6 +104,26 @@ int32_t hgx_insert_events(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int
  * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */
 int32_t hgx_insert_events_device(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
                                  hgx_error* err);
+/* WireEvents (event.go:252-267) as a SyncResponse carries them (net/commands.go:10-15), the
+ * caller having decoded the JSON: the participants' ids instead of hashes. */
+typedef struct {
+    const int32_t* creator_id;            /* WireBody.CreatorID */
+    const int64_t* index;                 /* WireBody.Index */
+    const int64_t* self_parent_index;     /* WireBody.SelfParentIndex (-1: no self-parent) */
+    const int32_t* other_parent_creator;  /* WireBody.OtherParentCreatorID */
+    const int64_t* other_parent_index;    /* WireBody.OtherParentIndex (-1: "") */
+    const int64_t* timestamp_ns;
+    const uint8_t* hash;                  /* 32 bytes per event: the event id (Event.Hash) */
+    const uint8_t* sig_s;                 /* 32 bytes per event: S, big-endian */
+    const int32_t* ntx;
+    const int32_t* tx_nil;
+} hgx_wire_events;
+/* Core.Sync's insert loop (node/core.go:199-211) in one call: per event ReadWireInfo
+ * (hashgraph.go:569-614: parents through Store.ParticipantEvent, which sees the batch's earlier
+ * events) then InsertEvent(ev, false); stops at the first error with Go's string (the
+ * ReadWireInfo errors "<index>, Too Late" / "<index>, Not Found" included). */
+int32_t hgx_insert_wire_events(hgx_ctx* ctx, const hgx_wire_events* ev, int64_t count, int64_t* n_inserted,
+                               hgx_error* err);
 int32_t hgx_divide_rounds(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_decide_fame(hgx_ctx* ctx, hgx_error* err);
 int32_t hgx_find_order(hgx_ctx* ctx, hgx_error* err);

@@ -376,3 +376,85 @@ def test_commit_callback_like_commit_ch():
     want = [(i, b["rr"], b["ntx"], b["ntx"]) for i, b in enumerate(blocks) if b["ntx"] > 0]
     assert got == want and len(got) > 3
     h.set_commit_callback(None)
+
+
+def test_core_playbooks_through_wire_events(plays):
+    """node/core_test.go's playbooks with Core.Sync fed as the network delivers it: the sender's
+    WireEvents (hgx_wire_info = SetWireInfo) inserted by the receiver with hgx_insert_wire_events
+    (ReadWireInfo + InsertEvent per event, one call per sync), then the new head and RunConsensus.
+    Must equal the oracle-backed Core simulation."""
+    for fx in ("core_consensus", "core_ff"):
+        p = plays[fx]
+        n = p["n"]
+        fac = hgref.EventFactory(fx, n)
+        so = hgref.CoreSim(fx, n, lambda m: hgref.Oracle(m))
+        hexes = {}
+        cores = [dict(h=_hg(n, cap=4096), hexes=[], pool=[], head="", seq=0) for _ in range(n)]
+
+        def make(c, index, sp_hex, op_hex, txs):
+            e = fac.make(c, index, sp_hex, op_hex, txs, f"ev{len(hexes)}")
+            hexes[e["hex"]] = e
+            return e
+
+        def insert_local(core, e, sp, op):
+            core["h"].insert_arrays([e["creator"]], [e["index"]], [sp], [op], [e["ts"]],
+                                    np.frombuffer(e["hash"], np.uint8).reshape(1, 32),
+                                    np.frombuffer(e["s"], np.uint8).reshape(1, 32), [len(e["txs"] or [])],
+                                    [1 if e["txs"] is None else 0])
+            core["hexes"].append(e["hex"])
+
+        for i in range(n):
+            e = make(i, 0, "", "", None)
+            insert_local(cores[i], e, -1, -1)
+            cores[i]["head"] = e["hex"]
+        for frm, to, pl in p["playbook"]:
+            src, dst = cores[frm], cores[to]
+            known = dst["h"].Known()
+            lids = sorted(g for q in range(n) for g in src["h"].ParticipantEvents(q, int(known[q])))
+            spi, opc, opi = src["h"].wire_info()
+            if lids:
+                es = [hexes[src["hexes"][g]] for g in lids]
+                dst["h"].insert_wire([e["creator"] for e in es], [e["index"] for e in es], [int(spi[g]) for g in lids],
+                                     [int(opc[g]) for g in lids], [int(opi[g]) for g in lids], [e["ts"] for e in es],
+                                     np.stack([np.frombuffer(e["hash"], np.uint8) for e in es]),
+                                     np.stack([np.frombuffer(e["s"], np.uint8) for e in es]),
+                                     [len(e["txs"] or []) for e in es], [1 if e["txs"] is None else 0 for e in es])
+                dst["hexes"].extend(e["hex"] for e in es)
+            dst["pool"].extend(x.encode() for x in pl)
+            if lids or dst["pool"]:
+                other = hexes[src["hexes"][lids[-1]]]["hex"] if lids else ""
+                ne = make(to, dst["seq"] + 1, dst["head"], other, list(dst["pool"]))
+                insert_local(dst, ne, dst["hexes"].index(dst["head"]),
+                             dst["hexes"].index(other) if other else -1)
+                dst["head"], dst["seq"], dst["pool"] = ne["hex"], dst["seq"] + 1, []
+            dst["h"].RunConsensus()
+            so.sync_and_run(frm, to, [x.encode() for x in pl])
+        for c in range(n):
+            got = [cores[c]["hexes"][int(x)] for x in cores[c]["h"].ConsensusEvents()]
+            assert got == so.consensus_hex(c), (fx, c)
+
+
+def test_wire_events_errors_like_read_wire_info():
+    """ReadWireInfo errors stop Core.Sync after the events before them (hashgraph.go:586-598)."""
+    from babble_amd._lib import HgxError
+    n = 3
+    h = _hg(n, cap=64)
+    fac = hgref.EventFactory("wire", n)
+    evs = [fac.make(i, 0, "", "", [], f"g{i}") for i in range(n)]
+
+    def cols(rows):
+        return ([r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows], [r[3] for r in rows],
+                [r[4] for r in rows], [evs[0]["ts"]] * len(rows),
+                np.stack([np.frombuffer(evs[i % n]["hash"], np.uint8) for i in range(len(rows))]),
+                np.stack([np.frombuffer(evs[i % n]["s"], np.uint8) for i in range(len(rows))]),
+                [0] * len(rows), [0] * len(rows))
+    # (creator, index, sp index, op creator, op index): the genesis events, then 1's next event
+    # naming 0's event 0 (in the batch), then one naming an index 1 does not have
+    rows = [(0, 0, -1, -1, -1), (1, 0, -1, -1, -1), (1, 1, 0, 0, 0), (2, 0, -1, -1, -1), (2, 1, 0, 1, 7)]
+    with pytest.raises(HgxError) as ei:
+        h.insert_wire(*cols(rows))
+    assert ei.value.msg == "\x07, Not Found" and ei.value.inserted == 4
+    assert h.num_events() == 4
+    with pytest.raises(HgxError) as ei:   # a creator id the participants map does not have
+        h.insert_wire(*cols([(9, 0, -1, -1, -1)]))
+    assert ei.value.code == 300
