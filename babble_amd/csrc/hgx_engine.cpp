@@ -473,9 +473,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             if (chain_len[c] > h_len_div[c]) smin = std::min(smin, h_len_div[c] / seg);
         u0 = (int64_t)smin * C;
     }
-    if (la_chg.n < 2 * nunits) HGX_TRY(la_chg.grow_copy(std::max(2 * nunits, 2 * la_chg.n), 0, stream));
+    if (la_chg.n < nunits) {   // change stamps: new units start at 0, a stamp no sweep uses
+        const size_t old = la_chg.n;
+        HGX_TRY(la_chg.grow_copy(std::max(nunits, 2 * la_chg.n), old, stream));
+        HGX_TRY(hipMemsetAsync(la_chg.p + old, 0, (la_chg.n - old) * 4, stream));
+    }
     if (la_usum.n < nunits) HGX_TRY(la_usum.grow_copy(std::max(nunits, 2 * la_usum.n), la_usum.n, stream));
-    HGX_TRY(hipMemsetAsync(la_chg.p, 0, 2 * nunits, stream));   // no stale flags of an earlier call
     const int32_t* cold = rebuild ? nullptr : c_old.p;
     la_sweeps = 0;
     la_rows = 0;
@@ -483,17 +486,17 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // sweep k's counters in ring slot k % kLaRing; up to kLaAhead sweeps are queued
         // before the host reads the oldest one's "units changed" (a sweep after the one that
         // changed nothing finds no dirty unit and does nothing)
+        // dirty flags are sweep stamps (monotone over calls: stale ones never match), so a
+        // sweep is one kernel, one 8-byte read-back and one event
         int launched_s = 0;
+        HGX_TRY(hipMemsetAsync(counters.p + 8, 0, 16, stream));
         auto launch_sweep = [&]() -> hipError_t {
             const int slot = launched_s % kLaRing;
-            uint8_t* chg_prev = la_chg.p + (size_t)(launched_s & 1) * nunits;
-            uint8_t* chg_cur = la_chg.p + (size_t)((launched_s + 1) & 1) * nunits;
             int32_t* cnt = counters.p + 8 + 4 * slot;
-            HGX_TRY(hipMemsetAsync(chg_cur + u0, 0, nunits - (size_t)u0, stream));
-            HGX_TRY(hipMemsetAsync(cnt, 0, 16, stream));
+            int32_t* cnt_next = counters.p + 8 + 4 * ((launched_s + 1) % kLaRing);
             kbeg(K_LA_SWEEP);
-            launch_la_sweep(stream, a, C, n, max_len, seg, launched_s == 0 ? 1 : 0, chg_prev, chg_cur, la_usum.p, cnt,
-                            cold, u0);
+            launch_la_sweep(stream, a, C, n, max_len, seg, launched_s == 0 ? 1 : 0, la_chg.p, ++la_stamp, la_usum.p,
+                            cnt, cnt_next, cold, u0);
             kend(K_LA_SWEEP, 0);
             HGX_TRY(hipMemcpyAsync(h_small + 16 + 4 * slot, cnt, 8, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipEventRecord(la_ev[slot], stream));
@@ -646,13 +649,16 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             launched++;
             return hipSuccess;
         };
+        // a rebuild keeps two batches in flight; a resumed call usually ends within its first
+        // batch, so it waits for that batch's flag before queueing another
         HGX_TRY(launch_batch());
-        HGX_TRY(launch_batch());
+        if (rebuild) HGX_TRY(launch_batch());
         for (;;) {
             HGX_TRY(hipEventSynchronize(flag_ev[checked & 1]));
             const int more = h_small[checked & 1];
             checked++;
             if (!more) break;
+            if (launched == checked) HGX_TRY(launch_batch());   // no batch in flight
             HGX_TRY(launch_batch());
         }
     }

@@ -187,7 +187,8 @@ class Engine {
     DBuf<int32_t> c_off, c_len, c_base, c_old, fu, rcnt;
     // positions
     DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_round, p_rr;
-    DBuf<uint8_t> la_chg;   // [2 x units] ping-pong dirty flags of the lastAncestors sweeps
+    DBuf<int32_t> la_chg;   // [units] change stamps of the lastAncestors sweeps (sweep number)
+    int32_t la_stamp = 1;   // stamp of the last sweep launched (monotone over calls)
     DBuf<int64_t> la_usum;  // [units] sum of each unit's values (change detection)
     DBuf<int64_t> p_ts, p_cts;
     // coordinates

@@ -106,12 +106,13 @@ int fd_tile_rows(int n, int compact);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
 // (gids [E0, E))
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int seg);
-// one Gauss-Seidel sweep over the dirty units (all when `first`) from unit u0; out[0] +=
-// rows recomputed, out[1] += units whose values changed (marked in chg_cur; usum = per-unit
-// sums). c_old (incremental, else null): rows below c_old[c] are final and skipped.
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out, const int32_t* c_old,
-                     int64_t u0);
+// one Gauss-Seidel sweep over the dirty units (all when `first`) from unit u0: a unit is dirty
+// when its carry unit or an op unit has chg == stamp - 1, and gets chg = stamp when its values
+// change (usum = per-unit sums); out[0] += rows recomputed, out[1] += units changed; out_next
+// (the next sweep's counters) is zeroed. c_old (incremental, else null): rows below c_old[c]
+// are final and skipped.
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
+                     int32_t stamp, int64_t* usum, int32_t* out, int32_t* out_next, const int32_t* c_old, int64_t u0);
 // c_old (incremental, else null): only tiles from each chain's first new row; max_new = the
 // most new rows of one chain
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,

@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
 // never below its stored value and repeating sweeps until none changes anything
 // reaches the fixed point. A unit's rows can only change if one of its
 // inputs changed: the previous unit of its chain (the carry) or the unit of one of its
-// op rows; sweep t+1 recomputes only those (chg_prev), marking in chg_cur the units
+// op rows; sweep t+1 recomputes only those (stamp == t), marking with stamp t+1 the units
 // whose values changed. "Changed" is detected without reading the old rows: a unit's
 // values only grow, so they are unchanged iff their sum equals the stored sum usum[u].
 // Per recomputed row: read the op row, write the row (8n bytes).
@@ -188,10 +188,12 @@ template <int GS, int CPL, typename CT>
 __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
                            const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
-                           int nwd, int nseg, int seg, int first, const uint8_t* __restrict__ chg_prev,
-                           uint8_t* __restrict__ chg_cur, int64_t* __restrict__ usum, int32_t* __restrict__ out,
+                           int nwd, int nseg, int seg, int first, int32_t* __restrict__ chg, int32_t stamp,
+                           int64_t* __restrict__ usum, int32_t* __restrict__ out, int32_t* __restrict__ out_next,
                            const int32_t* __restrict__ c_old, int64_t u0) {
     typedef LaWord<CT> W;
+    // the next sweep's counters (its slot is not read before this sweep ends)
+    if (blockIdx.x == 0 && threadIdx.x == 0) { out_next[0] = 0; out_next[1] = 0; }
     const int lane = lane_id();
     const int gl = lane % GS;
     int rows = 0, nwr = 0;   // rows recomputed / units changed (counted by group lane 0)
@@ -211,10 +213,10 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
         if (c_old && k1 <= c_old[c]) continue;
         if (!first) {
             // dirty iff the carry unit or an op unit of one of its rows changed last sweep
-            bool d = (s > 0 && gl == 0) ? chg_prev[unit - C] != 0 : false;
+            bool d = (s > 0 && gl == 0) ? chg[unit - C] == stamp - 1 : false;
             for (int k = k0 + gl; k < k1; k += GS) {
                 const int u = p_opu[off + k];
-                d = d || (u >= 0 && chg_prev[u] != 0);
+                d = d || (u >= 0 && chg[u] == stamp - 1);
             }
             const uint64_t gm = group_mask(GS, lane / GS);
             if ((__ballot(d) & gm) == 0) continue;
@@ -265,7 +267,7 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
         if (gl == 0) {
             if (first || usum[unit] != sum) {
                 usum[unit] = sum;
-                chg_cur[unit] = 1;
+                chg[unit] = stamp;
                 nwr++;
             }
         }
@@ -1542,9 +1544,8 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
                        a.p_rr, a.p_cts, C, seg);
 }
 
-void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first,
-                     const uint8_t* chg_prev, uint8_t* chg_cur, int64_t* usum, int32_t* out, const int32_t* c_old,
-                     int64_t u0) {
+void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
+                     int32_t stamp, int64_t* usum, int32_t* out, int32_t* out_next, const int32_t* c_old, int64_t u0) {
     const int nseg = (max_len + seg - 1) / seg;
     if ((int64_t)nseg * C <= u0) return;
     const int nwd = a.compact ? n / 2 : n;
@@ -1553,7 +1554,7 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
         const int64_t threads = ((int64_t)nseg * C - u0) * GS;                                                \
         hipLaunchKernelGGL((k_la_sweep<GS, CPL, CT>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, \
                            s, (uint32_t*)a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nwd, nseg, seg, \
-                           first, chg_prev, chg_cur, usum, out, c_old, u0);                                   \
+                           first, chg, stamp, usum, out, out_next, c_old, u0);                                \
     }
 #define LA_LAUNCH(GS, CPL, NW)                                        \
     {                                                                 \
