@@ -1269,10 +1269,12 @@ int32_t hgx_witness(hgx_ctx* c, int64_t x) {
 // ---- instrumentation / knobs ----------------------------------------------------------
 int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
     if (!c || !out) return 0;
-    const int32_t m = std::min<int32_t>(cap, 10);
-    double v[10] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
+    const int32_t m = std::min<int32_t>(cap, 13);
+    double v[13] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
                     (double)c->eng.la_sweeps, (double)c->eng.R, (double)c->eng.compact,
-                    (double)c->eng.la_rows, c->eng.last_rebuild ? 1.0 : 0.0, (double)c->rh.r_lo};
+                    (double)c->eng.la_rows, c->eng.last_rebuild ? 1.0 : 0.0, (double)c->rh.r_lo,
+                    c->eng.la_wave_used ? 1.0 : 0.0, (double)c->eng.la_wave_fallbacks,
+                    (double)(c->eng.la_wave_used ? c->eng.la_wave_segs : 0)};
     for (int32_t i = 0; i < m; i++) out[i] = v[i];
     return m;
 }
@@ -1345,6 +1347,12 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
                                : hipSuccess;
     if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
     return e == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+int32_t hgx_set_la_kernel(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
+    c->eng.la_kernel = mode;
+    return HGX_OK;
 }
 
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {

@@ -87,6 +87,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     }
     hipDeviceProp_t prop;
     HGX_TRY(hipGetDeviceProperties(&prop, device));
+    num_cus = std::max(1, prop.multiProcessorCount);
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
         why = std::string("device is ") + prop.gcnArchName + ", libhgx is built for gfx950 (MI355X) only";
         return hipErrorInvalidDeviceFunction;
@@ -128,6 +129,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipMemsetAsync(root_round_d.p, 0xFF, (size_t)C * 4, stream));   // genesis: Round -1, Y ""
     HGX_TRY(hipMemsetAsync(root_y_ext_d.p, 0, (size_t)C, stream));
     HGX_TRY(p_gid.alloc(PP)); HGX_TRY(p_chain.alloc(PP)); HGX_TRY(p_op.alloc(PP)); HGX_TRY(p_opu.alloc(PP));
+    HGX_TRY(p_opk.alloc(PP));
     HGX_TRY(p_round.alloc(PP)); HGX_TRY(p_rr.alloc(PP)); HGX_TRY(p_ts.alloc(PP)); HGX_TRY(p_cts.alloc(PP));
     fd_ld = (Ppos + 1) & ~(int64_t)1;
     HGX_TRY(LA.alloc(PP * n));
@@ -192,7 +194,7 @@ DevArrays Engine::arrays() {
     a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p; a.g_txnil = g_txnil.p;
     a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p;
     a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
-    a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
+    a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_opk = p_opk.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
     a.LA = LA.p; a.FDT = FDT.p; a.compact = compact;
     a.Bm = Bm.p; a.wflag = wflag.p; a.wstat = wstat.p; a.wcoin = wcoin.p; a.WLA = WLA.p; a.WFD = WFD.p; a.WLAT = WLAT.p;
@@ -459,13 +461,20 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipEventRecord(ph0, stream));
     const int seg = kLaSeg;
     kbeg(K_LAYOUT);
-    launch_layout(stream, E0, En, a, C, seg);
+    launch_layout(stream, E0, En, a, C, n, seg);
     kend(K_LAYOUT, (double)(En - E0) * 64);
     // lastAncestors: fixed point from all -1 (new rows), dirty-tracked sweeps (k_la_sweep)
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
     int64_t u0 = 0;
-    if (rebuild) {
-        HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
+    la_wave_used = la_kernel == 0 && la_wave_ok(n, max_len);
+    // a rebuild of one large graph runs the wavefront on time segments in parallel (their
+    // rows are lower bounds), then a verify sweep and the dirty sweeps complete them
+    la_wave_segs = 1;
+    if (la_wave_used && rebuild && G == 1 && En >= (int64_t)kLaSegMinRows * C)
+        la_wave_segs = la_wave_segments(n, compact, num_cus, kLaMaxSegs);
+    if (rebuild) {   // (the exact wavefront writes every row it builds)
+        if (!la_wave_used || la_wave_segs > 1)
+            HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
     } else {
         launch_init_new(stream, a, E0, En - E0, n, fd_ld);
         int32_t smin = 0x7FFFFFFF;
@@ -482,7 +491,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     const int32_t* cold = rebuild ? nullptr : c_old.p;
     la_sweeps = 0;
     la_rows = 0;
-    {
+    auto run_sweeps = [&](int first_mode) -> hipError_t {
         // sweep k's counters in ring slot k % kLaRing; up to kLaAhead sweeps are queued
         // before the host reads the oldest one's "units changed" (a sweep after the one that
         // changed nothing finds no dirty unit and does nothing)
@@ -495,8 +504,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             int32_t* cnt = counters.p + 8 + 4 * slot;
             int32_t* cnt_next = counters.p + 8 + 4 * ((launched_s + 1) % kLaRing);
             kbeg(K_LA_SWEEP);
-            launch_la_sweep(stream, a, C, n, max_len, seg, launched_s == 0 ? 1 : 0, la_chg.p, ++la_stamp, la_usum.p,
-                            cnt, cnt_next, cold, u0);
+            launch_la_sweep(stream, a, C, n, max_len, seg, launched_s == 0 ? first_mode : 0, la_chg.p, ++la_stamp,
+                            la_usum.p, cnt, cnt_next, cold, u0);
             kend(K_LA_SWEEP, 0);
             HGX_TRY(hipMemcpyAsync(h_small + 16 + 4 * slot, cnt, 8, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipEventRecord(la_ev[slot], stream));
@@ -516,6 +525,22 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             if (changed == 0) break;
             if (la_sweeps > 100000) return hipErrorUnknown;
         }
+        return hipSuccess;
+    };
+    if (la_wave_used) {
+        // one dataflow pass (k_la_wave); its error flag is read with the phase clock below
+        HGX_TRY(hipMemsetAsync(counters.p + 6, 0, 4, stream));
+        kbeg(K_LA_SWEEP);
+        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6));
+        if (la_wave_segs > 1) HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6));
+        const double rows = (double)(En - E0);
+        kend(K_LA_SWEEP, rows * (3.0 * csz * n + 16));
+        HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
+        if (la_wave_segs > 1) HGX_TRY(run_sweeps(2));   // verify sweep + dirty sweeps (counted there)
+        la_sweeps++;
+        la_rows += (int64_t)rows;
+    } else {
+        HGX_TRY(run_sweeps(1));
     }
     kbeg(K_FD_BUILD);
     launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
@@ -538,6 +563,19 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     }
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
+    if (la_wave_used && h_small[48] != 0) {
+        // a wavefront lane gave up waiting (bounded spins): redo lastAncestors and the
+        // firstDescendants built from them with the sweeps
+        la_wave_used = false;
+        la_wave_fallbacks++;
+        if (rebuild) HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
+        else launch_init_new(stream, a, E0, En - E0, n, fd_ld);
+        HGX_TRY(run_sweeps(1));
+        launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
+        if (rooted) launch_root_floor(stream, a, root_round_d.p, gfl.p, gB.p, root_gmax, C, n, max_len);
+        HGX_TRY(hipEventRecord(ph1, stream));
+        HGX_TRY(hipEventSynchronize(ph1));
+    }
     float ms = 0;
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[0] = ms;

@@ -139,6 +139,14 @@ class Engine {
     bool last_rebuild = false;           // the last divide_rounds rebuilt the layout
     int32_t R = 0;
     int la_sweeps = 0;
+    int la_kernel = 0;            // 0 dataflow wavefront (k_la_wave) where it applies, 1 sweeps (hgx_set_la_kernel)
+    bool la_wave_used = false;    // the last DivideRounds built lastAncestors with k_la_wave
+    int la_wave_segs = 1;         // ... on this many time segments
+    int num_cus = 256;            // compute units of the device
+    static constexpr int kLaMaxSegs = 16;
+    static constexpr int kLaHeadRows = 64;   // rows per chain rebuilt at the start of each time segment
+    static constexpr int kLaSegMinRows = 512;   // time segments only when the graph has >= this many rows per chain
+    int64_t la_wave_fallbacks = 0;   // k_la_wave gave up and the sweeps redid the pass
     int compact = 0;             // coordinates of the last DivideRounds stored as uint16
     bool force_coord32 = false;  // hgx_set_coord_storage(1)
     int64_t la_rows = 0;   // rows recomputed over all sweeps of the last divide_rounds
@@ -186,7 +194,7 @@ class Engine {
     // chains
     DBuf<int32_t> c_off, c_len, c_base, c_old, fu, rcnt;
     // positions
-    DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_round, p_rr;
+    DBuf<int32_t> p_gid, p_chain, p_op, p_opu, p_opk, p_round, p_rr;
     DBuf<int32_t> la_chg;   // [units] change stamps of the lastAncestors sweeps (sweep number)
     int32_t la_stamp = 1;   // stamp of the last sweep launched (monotone over calls)
     DBuf<int64_t> la_usum;  // [units] sum of each unit's values (change detection)

@@ -8,6 +8,7 @@
 namespace hgx {
 
 constexpr int32_t kMaxI32 = 2147483647;
+constexpr int kOpkBits = 21;   // p_opk: op row bits (chains of up to 2^21 rows use k_la_wave)
 
 // Raw device pointers of one context (see hgx_engine.h for meaning/sizes).
 struct DevArrays {
@@ -21,6 +22,7 @@ struct DevArrays {
     const int32_t *c_off, *c_len, *c_base;
     // positions
     int32_t *p_gid, *p_chain, *p_op, *p_opu, *p_round, *p_rr;
+    int32_t* p_opk;   // (op chain within the graph << kOpkBits) | op row, -1 none (k_la_wave)
     int64_t *p_ts, *p_cts;
     // coordinates: int32_t, or uint16_t when `compact` (Coord<CT> in hgx_device.h)
     void *LA, *FDT;
@@ -103,14 +105,28 @@ struct RoundArgs {
 };
 
 int fd_tile_rows(int n, int compact);
-// gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows)
-// (gids [E0, E))
-void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int seg);
+// gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows),
+// p_opk = packed op chain and row (gids [E0, E))
+void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg);
+// lastAncestors of the new rows (from c_old[c], all rows when c_old is null) in ONE pass:
+// per (graph, 16-byte column block) a workgroup whose lanes own the chains and wait for
+// their op rows in an LDS ring. Needs n <= 896 and chains < 2^kOpkBits
+// rows. *err != 0 afterwards: a lane gave up waiting (bounded spins); LA is then incomplete.
+// nts > 1 (one graph, all rows): the rows split into nts gid segments built concurrently as
+// lower bounds (LA must hold none before); then (head > 0) the first `head` rows of each
+// chain in every segment but the first are rebuilt from the now final earlier segments, and
+// a verify sweep confirms or completes the rows.
+bool la_wave_ok(int n, int max_len);
+int la_wave_blocks(int n, int compact);   // column blocks per graph (workgroups per segment)
+int la_wave_segments(int n, int compact, int num_cus, int max_segs);   // time segments that fill the device
+hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
+                          int head, int32_t* err);
 // one Gauss-Seidel sweep over the dirty units (all when `first`) from unit u0: a unit is dirty
 // when its carry unit or an op unit has chg == stamp - 1, and gets chg = stamp when its values
 // change (usum = per-unit sums); out[0] += rows recomputed, out[1] += units changed; out_next
 // (the next sweep's counters) is zeroed. c_old (incremental, else null): rows below c_old[c]
-// are final and skipped.
+// are final and skipped. first == 2: verify sweep over rows holding lower bounds (every unit;
+// changed = some word grew).
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
                      int32_t stamp, int64_t* usum, int32_t* out, int32_t* out_next, const int32_t* c_old, int64_t u0);
 // c_old (incremental, else null): only tiles from each chain's first new row; max_new = the

@@ -35,17 +35,21 @@ __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __
                                            const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
                                            const int32_t* __restrict__ c_base, int32_t* __restrict__ p_gid,
                                            int32_t* __restrict__ p_chain, int32_t* __restrict__ p_op,
-                                           int32_t* __restrict__ p_opu, int64_t* __restrict__ p_ts,
-                                           int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int seg) {
+                                           int32_t* __restrict__ p_opu, int32_t* __restrict__ p_opk,
+                                           int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
+                                           int64_t* __restrict__ p_cts, int C, int n, int seg) {
     const int c = g_creator[gid];
     const int op = g_op[gid];
-    int opp = -1, opu = -1;
+    int opp = -1, opu = -1, opk = -1;
     if (op >= 0) {
         const int oc = g_creator[op];
         const int ok = g_index[op] - c_base[oc];
         opp = c_off[oc] + ok;
         opu = (ok / seg) * C + oc;   // lastAncestors unit of the op row (k_la_sweep)
+        // op chain within the graph | op row (k_la_wave; only used when rows < 2^kOpkBits)
+        opk = ((oc % n) << kOpkBits) | (ok & ((1 << kOpkBits) - 1));
     }
+    p_opk[p] = opk;
     p_gid[p] = (int32_t)gid;
     p_chain[p] = c;
     p_op[p] = opp;
@@ -62,8 +66,9 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
                                                 const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
                                                 int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
                                                 int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu,
-                                                int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
-                                                int64_t* __restrict__ p_cts, int C, int seg) {
+                                                int32_t* __restrict__ p_opk, int64_t* __restrict__ p_ts,
+                                                int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int n,
+                                                int seg) {
     __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
     __shared__ int32_t s_slot[kLayoutB];   // slot -> gid offset in the block
     __shared__ int32_t s_lo, s_hi;
@@ -89,7 +94,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
             const int p = c_off[c] + g_index[gid] - c_base[c];
             g_pos[gid] = p;
             layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
-                       p_opu, p_ts, p_rr, p_cts, C, seg);
+                       p_opu, p_opk, p_ts, p_rr, p_cts, C, n, seg);
         }
         return;
     }
@@ -133,7 +138,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
         const int c = g_creator[gid];
         const int p = c_off[c] + g_index[gid] - c_base[c];
         layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu,
-                   p_ts, p_rr, p_cts, C, seg);
+                   p_opk, p_ts, p_rr, p_cts, C, n, seg);
     }
 }
 
@@ -184,7 +189,10 @@ struct LaWord<uint16_t> {
 };
 
 // LA rows as 32-bit words: nwd words per row (n for int32, n/2 for compact storage).
-template <int GS, int CPL, typename CT>
+// VERIFY (with first): every unit is recomputed from rows that already hold lower bounds
+// (k_la_wave's time segments) and marked changed only where a word actually grew; unchanged
+// words are not rewritten.
+template <int GS, int CPL, typename CT, bool VERIFY>
 __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict__ p_op,
                            const int32_t* __restrict__ p_opu, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int C, int n,
@@ -233,8 +241,10 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
         // UB rows per batch: all their op-row loads are issued before the first use (one
         // memory round trip per batch; a whole 16-row unit when the rows are narrow)
         constexpr int UB = (CPL <= 2) ? 16 : (CPL <= 4 ? 8 : 4);
+        bool grew = false;   // VERIFY: some word of the unit grew
         for (int k = k0; k < k1; k += UB) {
             uint32_t opr[UB][CPL];
+            uint32_t cur[VERIFY ? UB : 1][CPL];
             int opp[UB];
 #pragma unroll
             for (int u = 0; u < UB; u++) opp[u] = (k + u < k1) ? p_op[off + k + u] : -1;
@@ -244,6 +254,8 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
                 for (int q = 0; q < CPL; q++) {
                     const int i = gl + GS * q;
                     opr[u][q] = (opp[u] >= 0 && i < nwd) ? LA[(size_t)opp[u] * nwd + i] : W::kNone;
+                    if constexpr (VERIFY)
+                        cur[u][q] = (k + u < k1 && i < nwd) ? LA[(size_t)(off + k + u) * nwd + i] : W::kNone;
                 }
             }
 #pragma unroll
@@ -254,7 +266,14 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
                         const int i = gl + GS * q;
                         const uint32_t v = W::set_own(W::wmax(carry[q], opr[u][q]), i, cl, base + k + u);
                         if (i < nwd) {
-                            LA[(size_t)(off + k + u) * nwd + i] = v;
+                            if constexpr (VERIFY) {
+                                if (v != cur[u][q]) {
+                                    LA[(size_t)(off + k + u) * nwd + i] = v;
+                                    grew = true;
+                                }
+                            } else {
+                                LA[(size_t)(off + k + u) * nwd + i] = v;
+                            }
                             sum += W::wsum(v);
                         }
                         carry[q] = v;
@@ -264,12 +283,13 @@ __global__ void k_la_sweep(uint32_t* __restrict__ LA, const int32_t* __restrict_
         }
         // group sum of the unit's values vs the stored one
         for (int o = 1; o < GS; o <<= 1) sum += __shfl_xor(sum, o);
+        if constexpr (VERIFY) grew = (__ballot(grew) & group_mask(GS, lane / GS)) != 0;
         if (gl == 0) {
-            if (first || usum[unit] != sum) {
-                usum[unit] = sum;
+            if (VERIFY ? grew : (first || usum[unit] != sum)) {
                 chg[unit] = stamp;
                 nwr++;
             }
+            usum[unit] = sum;
         }
     }
     if (GS < 64) {
@@ -1537,11 +1557,11 @@ __global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* _
 
 static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
 
-void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int seg) {
+void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
     if (E <= E0) return;
     hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
-                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_ts,
-                       a.p_rr, a.p_cts, C, seg);
+                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_opk,
+                       a.p_ts, a.p_rr, a.p_cts, C, n, seg);
 }
 
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
@@ -1549,12 +1569,16 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     const int nseg = (max_len + seg - 1) / seg;
     if ((int64_t)nseg * C <= u0) return;
     const int nwd = a.compact ? n / 2 : n;
-#define LA_LAUNCH_T(GS, CPL, CT)                                                                              \
+#define LA_LAUNCH_V(GS, CPL, CT, V)                                                                           \
     {                                                                                                         \
         const int64_t threads = ((int64_t)nseg * C - u0) * GS;                                                \
-        hipLaunchKernelGGL((k_la_sweep<GS, CPL, CT>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, \
+        hipLaunchKernelGGL((k_la_sweep<GS, CPL, CT, V>), dim3(std::min(nblk(threads, 256), 2048u)), dim3(256), 0, \
                            s, (uint32_t*)a.LA, a.p_op, a.p_opu, a.c_off, a.c_len, a.c_base, C, n, nwd, nseg, seg, \
-                           first, chg, stamp, usum, out, out_next, c_old, u0);                                \
+                           first ? 1 : 0, chg, stamp, usum, out, out_next, c_old, u0);                        \
+    }
+#define LA_LAUNCH_T(GS, CPL, CT)                                   \
+    {                                                              \
+        if (first == 2) LA_LAUNCH_V(GS, CPL, CT, true) else LA_LAUNCH_V(GS, CPL, CT, false) \
     }
 #define LA_LAUNCH(GS, CPL, NW)                                        \
     {                                                                 \
@@ -1563,6 +1587,7 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     HGX_DISPATCH_N(nwd, LA_LAUNCH);
 #undef LA_LAUNCH
 #undef LA_LAUNCH_T
+#undef LA_LAUNCH_V
 }
 
 int fd_tile_rows(int n, int compact) {

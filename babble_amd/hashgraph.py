@@ -410,17 +410,24 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(10, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 10)
+        out = np.zeros(13, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 13)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
-                    la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]))
+                    la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
+                    la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
         m = {"popc": 0, "vote": 1, "mfma": 2}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_fame_tally(self.ctx, m) != 0:
             raise ValueError(f"invalid fame tally {mode}")
+
+    def set_la_kernel(self, mode):
+        """DivideRounds lastAncestors: "wave" (default, one dataflow pass) or "sweep" (Gauss-Seidel)."""
+        m = {"wave": 0, "sweep": 1}[mode] if isinstance(mode, str) else int(mode)
+        if self.L.hgx_set_la_kernel(self.ctx, m) != 0:
+            raise ValueError(f"invalid lastAncestors kernel {mode}")
 
     def set_round_kernel(self, mode):
         """DivideRounds step (n <= 256): "candidate" (default) or "block" (block binary search)."""

@@ -305,7 +305,9 @@ int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_k
 /* per-phase device times (ms) of the last calls: coords, rounds, fame, order; then
  * LA sweeps, rounds, 1 if the coordinates were stored compact (uint16); then of the last
  * DivideRounds: lastAncestors rows recomputed, 1 if it rebuilt the layout (0: incremental),
- * the first round step it ran */
+ * the first round step it ran, 1 if the lastAncestors pass was the dataflow kernel; then
+ * the number of dataflow passes that gave up and were redone by the sweeps, and the time
+ * segments of the last dataflow pass (up to 13 values) */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
  * name of the kernel, summed device ms, launches, algorithmic bytes moved */
@@ -321,6 +323,10 @@ int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
 /* DecideFame vote tally: 0 = witness-tiled popcount (default), 1 = per-round popcount
  * kernel, 2 = witness-tiled int8 MFMA. Same results; for measurement. */
 int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
+/* DivideRounds lastAncestors: 0 = one dataflow pass per (graph, column block) where it
+ * applies (default: n <= 896, chains < 2^21 rows; hgx_la_wave.hip), 1 = Gauss-Seidel sweeps
+ * to the fixed point (hgx_kernels.hip). Same results. */
+int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds round step for n <= 256: 0 = one lane per candidate, 8-bit rebased compares
  * (default, hgx_round_k.hip), 1 = block binary search (hgx_rounds.hip). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
