@@ -1350,8 +1350,9 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
 }
 
 int32_t hgx_set_la_kernel(hgx_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
-    c->eng.la_kernel = mode;
+    if (!c || mode < 0 || mode > 1024) return HGX_ERR_INVALID;
+    c->eng.la_kernel = mode == 1 ? 1 : 0;
+    c->eng.la_segs_override = mode >= 2 ? mode : 0;
     return HGX_OK;
 }
 

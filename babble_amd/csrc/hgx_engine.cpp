@@ -471,10 +471,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // rows are lower bounds), then a verify sweep and the dirty sweeps complete them
     la_wave_segs = 1;
     if (la_wave_used && rebuild && G == 1 && En >= (int64_t)kLaSegMinRows * C)
-        la_wave_segs = la_wave_segments(n, compact, num_cus, kLaMaxSegs);
-    if (rebuild) {   // (the exact wavefront writes every row it builds)
-        if (!la_wave_used || la_wave_segs > 1)
-            HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
+        la_wave_segs = la_segs_override > 0 ? la_segs_override : la_wave_segments(n, compact, num_cus, kLaMaxSegs);
+    if (rebuild) {   // (the wavefront writes every row it builds before anything reads it)
+        if (!la_wave_used) HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
     } else {
         launch_init_new(stream, a, E0, En - E0, n, fd_ld);
         int32_t smin = 0x7FFFFFFF;
@@ -513,7 +512,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             return hipSuccess;
         };
         for (;;) {
-            while (launched_s < la_sweeps + kLaAhead) HGX_TRY(launch_sweep());
+            // a verify sweep usually finds nothing to redo: wait for it before queueing more
+            const int ahead = (first_mode == 2 && la_sweeps == 0) ? 1 : kLaAhead;
+            while (launched_s < la_sweeps + ahead) HGX_TRY(launch_sweep());
             const int slot = la_sweeps % kLaRing;
             HGX_TRY(hipEventSynchronize(la_ev[slot]));
             const int32_t rows = h_small[16 + 4 * slot], changed = h_small[16 + 4 * slot + 1];

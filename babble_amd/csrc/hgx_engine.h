@@ -142,6 +142,7 @@ class Engine {
     int la_kernel = 0;            // 0 dataflow wavefront (k_la_wave) where it applies, 1 sweeps (hgx_set_la_kernel)
     bool la_wave_used = false;    // the last DivideRounds built lastAncestors with k_la_wave
     int la_wave_segs = 1;         // ... on this many time segments
+    int la_segs_override = 0;     // > 0: time segments of a rebuild (hgx_set_la_kernel mode >= 2, measurement)
     int num_cus = 256;            // compute units of the device
     static constexpr int kLaMaxSegs = 16;
     static constexpr int kLaHeadRows = 64;   // rows per chain rebuilt at the start of each time segment

@@ -113,11 +113,11 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
 // their op rows in an LDS ring. Needs n <= 896 and chains < 2^kOpkBits
 // rows. *err != 0 afterwards: a lane gave up waiting (bounded spins); LA is then incomplete.
 // nts > 1 (one graph, all rows): the rows split into nts gid segments built concurrently as
-// lower bounds (LA must hold none before); then (head > 0) the first `head` rows of each
+// lower bounds (rows outside a segment count as none); then (head > 0) the first `head` rows of each
 // chain in every segment but the first are rebuilt from the now final earlier segments, and
 // a verify sweep confirms or completes the rows.
 bool la_wave_ok(int n, int max_len);
-int la_wave_blocks(int n, int compact);   // column blocks per graph (workgroups per segment)
+int la_wave_blocks(int n, int compact);   // column blocks of the time-segment passes (workgroups per segment)
 int la_wave_segments(int n, int compact, int num_cus, int max_segs);   // time segments that fill the device
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
                           int head, int32_t* err);

@@ -12,9 +12,9 @@
 // op depth (about 2.3 x the chain length on gossip traces) at one LDS hop per level.
 //
 // LDS per workgroup (n chains, ring of R rows per chain, queue of Q op descriptors):
-//   ring_d [R][n][DW]  op-row blocks, slot = row % R
-//   ring_t [R][n]      slot tags: the row held, -1 empty, -2 being rewritten (seqlock)
-//   q      [Q][n]      packed op descriptors (p_opk) of the rows ahead of each lane
+//   ring_d [R][NP][DW] op-row blocks, slot = row % R (NP = n rounded up to a power of two)
+//   ring_t [R][NP]     slot tags: the row held, -1 empty, -2 being rewritten (seqlock)
+//   q      [Q][NP]     packed op descriptors (p_opk) of the rows ahead of each lane
 //   lqv [n], prog [n], s_old [n], s_off [n], s_len [n]
 // One extra wave streams the op descriptors from HBM into q (the compute lanes never wait
 // on a global load in the steady state). A row whose op row already left the ring is read
@@ -93,7 +93,11 @@ __device__ __forceinline__ void settle(uint32_t (&v)[DW]) {
 template <int DW>
 __device__ __forceinline__ void ring_load(const uint32_t* p, uint32_t (&v)[DW]) {
     HGX_CB();
-    if constexpr (DW == 4) {
+    if constexpr (DW == 8) {
+        const uint4 x = *(const uint4*)p, y = *(const uint4*)(p + 4);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    } else if constexpr (DW == 4) {
         const uint4 x = *(const uint4*)p;
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
     } else if constexpr (DW == 2) {
@@ -107,14 +111,20 @@ __device__ __forceinline__ void ring_load(const uint32_t* p, uint32_t (&v)[DW]) 
 template <int DW>
 __device__ __forceinline__ void ring_store(uint32_t* p, const uint32_t (&v)[DW]) {
     HGX_CB();
-    if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+    if constexpr (DW == 8) {
+        *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+        *(uint4*)(p + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+    } else if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
     else if constexpr (DW == 2) *(uint2*)p = make_uint2(v[0], v[1]);
     else *p = v[0];
     HGX_CB();
 }
 template <int DW>
 __device__ __forceinline__ void row_store(uint32_t* p, const uint32_t (&v)[DW]) {
-    if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+    if constexpr (DW == 8) {
+        *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+        *(uint4*)(p + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+    } else if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
     else if constexpr (DW == 2) *(uint2*)p = make_uint2(v[0], v[1]);
     else *p = v[0];
 }
@@ -140,8 +150,9 @@ __device__ __forceinline__ int chain_lower_bound(const int32_t* __restrict__ p_g
 // loader lane (n <= 64 NLW J), CH descriptors per refill. MODE 0: all rows, exact;
 // 1 (incremental): rows from c_old, the rows below are final; 2 (time segments, one graph):
 // workgroup (segment ts, block) builds the rows with gids in [E ts / nts, E (ts + 1) / nts),
-// reading the earlier segments' rows from HBM as they are (lower bounds: LA was reset to
-// none and only ever grows), so its rows are lower bounds; 3 (segment heads, after 2):
+// taking every row before its segment as none, so its rows are lower bounds (it reads from
+// LA only its own rows whose ring slot moved on, so LA needs no reset); 3
+// (segment heads, after 2):
 // the first `head` rows of every chain in each segment again, now that the earlier
 // segments' tails hold their final values (a segment's lower bounds are wrong only near its
 // start: the missing knowledge is soon superseded by newer events). k_la_sweep's verify
@@ -152,13 +163,15 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
                                                   const int32_t* __restrict__ c_base,
                                                   const int32_t* __restrict__ c_old,
                                                   const int32_t* __restrict__ p_gid, int64_t E, int nts, int head,
-                                                  int n, int nwd, int nblk, int32_t* __restrict__ err) {
+                                                  int n, int lgnp, int nwd, int nblk, int32_t* __restrict__ err) {
     typedef LaW<CT> W;
     extern __shared__ uint32_t smem[];
-    uint32_t* ring_d = smem;                                     // [R][n][DW]
-    int32_t* ring_t = (int32_t*)(ring_d + (size_t)R * n * DW);   // [R][n]
-    int32_t* q = ring_t + R * n;                                 // [Q][n]
-    int32_t* lqv = q + Q * n;
+    // slot-major arrays with a power-of-two chain stride NP = 2^lgnp >= n (index = shifts)
+    const int NP = 1 << lgnp;
+    uint32_t* ring_d = smem;                                      // [R][NP][DW]
+    int32_t* ring_t = (int32_t*)(ring_d + (size_t)R * NP * DW);   // [R][NP]
+    int32_t* q = ring_t + R * NP;                                 // [Q][NP]
+    int32_t* lqv = q + Q * NP;
     int32_t* prog = lqv + n;
     int32_t* s_old = prog + n;
     int32_t* s_off = s_old + n;
@@ -168,7 +181,7 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
     const int c0 = g * n;
     const int wb = b * DW;   // first word of the block
     const int tid = threadIdx.x;
-    for (int t = tid; t < R * n; t += blockDim.x) ring_t[t] = kTagEmpty;
+    for (int t = tid; t < R * NP; t += blockDim.x) ring_t[t] = kTagEmpty;
     for (int t = tid; t < n; t += blockDim.x) {
         const int off = c_off[c0 + t], len = c_len[c0 + t];
         int o = 0, e = len;
@@ -224,7 +237,7 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
                 if (need[j]) {
                     const int i = l + 64 * NLW * j;
 #pragma unroll
-                    for (int t = 0; t < CH; t++) lds_st(&q[((unsigned)(lq[j] + t) % Q) * n + i], v[j][t]);
+                    for (int t = 0; t < CH; t++) lds_st(&q[(((unsigned)(lq[j] + t) % Q) << lgnp) + i], v[j][t]);
                     HGX_CB();
                     lds_st(&lqv[i], min(lq[j] + CH, s_len[i]));
                     any = true;
@@ -250,20 +263,22 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
     int k = s_old[i];
     uint32_t carry[DW];
 #pragma unroll
-    for (int w = 0; w < DW; w++) carry[w] = k > 0 ? LA[(size_t)(off + k - 1) * nwd + wb + w] : W::kNone;
+    for (int w = 0; w < DW; w++)
+        carry[w] = (k > 0 && MODE != 2) ? LA[(size_t)(off + k - 1) * nwd + wb + w] : W::kNone;
     settle(carry);
+    uint32_t* dst = LA + (size_t)(off + k) * nwd + wb;   // row k's block (advanced per row)
     // descriptor of row k: p_opk, or kNoDesc while the loader has not queued it
     int opv = kNoDesc;
     uint32_t idle = 0;
     while (k < len) {
         // one LDS round trip: the queue (rows k, k + 1) and the op row's ring slot
         const int lv = lds_ld(&lqv[i]);
-        const int q0 = lds_ld(&q[((unsigned)k % Q) * n + i]);
-        const int q1 = lds_ld(&q[((unsigned)(k + 1) % Q) * n + i]);
+        const int q0 = lds_ld(&q[(((unsigned)k % Q) << lgnp) + i]);
+        const int q1 = lds_ld(&q[(((unsigned)(k + 1) % Q) << lgnp) + i]);
         const bool has_op = opv >= 0;
         const int opc = has_op ? (opv >> kOpkBits) : 0;
         const int opk = has_op ? (opv & ((1 << kOpkBits) - 1)) : 0;
-        const int sl = ((unsigned)opk % R) * n + opc;
+        const int sl = (((unsigned)opk % R) << lgnp) + opc;
         int old = 0;
         int end = 0x7FFFFFFF;
         if constexpr (MODE != 0) old = lds_ld(&s_old[opc]);
@@ -281,14 +296,24 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
         // its producer drained that store before reusing the slot, and the load bypasses L1)
         const bool from_old = MODE != 0 && has_op && (opk < old || opk >= end);
         if (from_old || (has_op && !ready && t1 > opk)) {
-            uint32_t* src = LA + (size_t)(s_off[opc] + opk) * nwd + wb;
+            if (MODE == 2 && from_old) {
+                // an earlier segment's row: LA may still hold an earlier DivideRounds's row there;
+                // none is a lower bound (the head pass and the verify sweep complete it)
 #pragma unroll
-            for (int w = 0; w < DW; w++) od[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            settle(od);
+                for (int w = 0; w < DW; w++) od[w] = W::kNone;
+            } else {
+                uint32_t* src = LA + (size_t)(s_off[opc] + opk) * nwd + wb;
+#pragma unroll
+                for (int w = 0; w < DW; w++)
+                    od[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                settle(od);
+            }
             ready = true;
         }
+        const bool wave_idle = __ballot(ready) == 0;
         if (!ready) {
             if (opv == kNoDesc && lv > k) opv = q0;
+            if (wave_idle) __builtin_amdgcn_s_sleep(1);   // leave the SIMD to the other waves
             if (((++idle) & 4095) == 0 && (idle > kSpinCap || lds_ld(s_abort))) {
                 lds_st(s_abort, 1);
                 atomicOr(err, 1);
@@ -305,17 +330,14 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
         }
         // the store of row k - R (this slot's previous row) must be complete before the
         // slot is reused: at least R - 1 later stores of this lane were issued since
-        // (MODE 2 / 3 build lower bounds, completed by the verify sweep: a reader that finds
-        // a row not yet written reads an older lower bound, so they skip this wait)
-        if constexpr (MODE < 2) {
-            if constexpr (R >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        }
-        const int ws = ((unsigned)k % R) * n + i;
+        if constexpr (R >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        const int ws = (((unsigned)k % R) << lgnp) + i;
         lds_st(&ring_t[ws], kTagBusy);
         ring_store<DW>(ring_d + (size_t)ws * DW, v);
         lds_st(&ring_t[ws], k);
-        row_store<DW>(LA + (size_t)(off + k) * nwd + wb, v);
+        row_store<DW>(dst, v);
+        dst += nwd;
         lds_st(&prog[i], k + 1);
 #pragma unroll
         for (int w = 0; w < DW; w++) carry[w] = v[w];
@@ -330,7 +352,10 @@ hipError_t la_wave_launch1(hipStream_t s, const DevArrays& a, int G, int n, cons
                            int head, int32_t* err) {
     const int nwd = a.compact ? n / 2 : n;
     const int nblk = nwd / DW;
-    const size_t words = (size_t)R * n * DW + (size_t)R * n + (size_t)Q * n + 5 * (size_t)n + 1;
+    int lgnp = 0;
+    while ((1 << lgnp) < n) lgnp++;
+    const size_t np2 = (size_t)1 << lgnp;
+    const size_t words = np2 * (R * DW + R + Q) + 5 * (size_t)n + 1;
     auto kern = k_la_wave<CT, DW, R, Q, NLW, J, CH, MODE>;
     static bool attr_set = false;   // per instantiation
     if (!attr_set) {
@@ -340,7 +365,7 @@ hipError_t la_wave_launch1(hipStream_t s, const DevArrays& a, int G, int n, cons
     }
     const int threads = ((n + 63) & ~63) + 64 * NLW;
     hipLaunchKernelGGL(kern, dim3(G * nts * nblk), dim3(threads), words * 4, s, (uint32_t*)a.LA, a.p_opk, a.c_off,
-                       a.c_len, a.c_base, c_old, a.p_gid, E, nts, head, n, nwd, nblk, err);
+                       a.c_len, a.c_base, c_old, a.p_gid, E, nts, head, n, lgnp, nwd, nblk, err);
     return hipGetLastError();
 }
 template <typename CT, int DW, int R, int Q, int NLW, int J, int CH>
@@ -349,26 +374,38 @@ hipError_t la_wave_launch(hipStream_t s, const DevArrays& a, int G, int n, const
     if (c_old) return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 1>(s, a, G, n, c_old, E, 1, 0, err);
     return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 0>(s, a, G, n, nullptr, E, 1, 0, err);
 }
-// LDS: n * (R * DW + R + Q + 5) words <= 160 KB; DW divides the row's words
+// block width and ring sizes of the time-segment passes: one workgroup per CU (the passes
+// are issue-bound, so wider blocks share the per-row overhead over more coordinates)
+struct SegCfg {
+    int dw, r, q;
+};
+inline SegCfg seg_cfg(int n, int nwd) {
+    if (n <= 256) return {nwd % 8 == 0 ? 8 : (nwd % 4 == 0 ? 4 : 1), 8, 32};
+    if (n <= 512) return {nwd % 4 == 0 ? 4 : 1, 8, 16};
+    return {nwd % 2 == 0 ? 2 : 1, 8, 8};
+}
+// LDS: NP * (R * DW + R + Q) + 5 n words <= 160 KB (NP = n rounded up to a power of two); DW divides the row's words
 template <typename CT>
 hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
                             int head, int32_t* err) {
     const int nwd = a.compact ? n / 2 : n;
-    if (nts > 1) {   // time segments: smaller rings, so that two or more workgroups share a CU
-        if (head > 0) {
-            if (n <= 256) {
-                if (nwd % 4 == 0) return la_wave_launch1<CT, 4, 8, 32, 1, 4, 8, 3>(s, a, G, n, nullptr, E, nts, head, err);
-                return la_wave_launch1<CT, 1, 8, 32, 1, 4, 8, 3>(s, a, G, n, nullptr, E, nts, head, err);
-            }
-            if (n <= 512) return la_wave_launch1<CT, 1, 8, 16, 1, 8, 4, 3>(s, a, G, n, nullptr, E, nts, head, err);
-            return la_wave_launch1<CT, 1, 8, 16, 2, 8, 4, 3>(s, a, G, n, nullptr, E, nts, head, err);
-        }
+    if (nts > 1) {   // time segments: wider blocks, smaller rings (seg_cfg)
+        const SegCfg g = seg_cfg(n, nwd);
+#define SEG(DW_, R_, Q_, NLW_, J_, CH_)                                                                                \
+    return head > 0 ? la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 3>(s, a, G, n, nullptr, E, nts, head, err)      \
+                    : la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 2>(s, a, G, n, nullptr, E, nts, 0, err)
         if (n <= 256) {
-            if (nwd % 4 == 0) return la_wave_launch1<CT, 4, 8, 32, 1, 4, 8, 2>(s, a, G, n, nullptr, E, nts, 0, err);
-            return la_wave_launch1<CT, 1, 8, 32, 1, 4, 8, 2>(s, a, G, n, nullptr, E, nts, 0, err);
+            if (g.dw == 8) SEG(8, 8, 32, 1, 4, 8);
+            if (g.dw == 4) SEG(4, 8, 32, 1, 4, 8);
+            SEG(1, 8, 32, 1, 4, 8);
         }
-        if (n <= 512) return la_wave_launch1<CT, 1, 8, 16, 1, 8, 4, 2>(s, a, G, n, nullptr, E, nts, 0, err);
-        return la_wave_launch1<CT, 1, 8, 16, 2, 8, 4, 2>(s, a, G, n, nullptr, E, nts, 0, err);
+        if (n <= 512) {
+            if (g.dw == 4) SEG(4, 8, 16, 1, 8, 4);
+            SEG(1, 8, 16, 1, 8, 4);
+        }
+        if (g.dw == 2) SEG(2, 8, 8, 2, 8, 2);
+        SEG(1, 8, 8, 2, 8, 2);
+#undef SEG
     }
     if (n <= 128) {
         if (nwd % 4 == 0) return la_wave_launch<CT, 4, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err);
@@ -385,15 +422,16 @@ hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, con
 
 int la_wave_blocks(int n, int compact) {
     const int nwd = compact ? n / 2 : n;
-    return (n <= 256 && nwd % 4 == 0) ? nwd / 4 : nwd;
+    return nwd / seg_cfg(n, nwd).dw;
 }
 
 int la_wave_segments(int n, int compact, int num_cus, int max_segs) {
     // workgroups of the segment configuration per CU (LDS bound), times CUs, per column block
     const int nwd = compact ? n / 2 : n;
-    const int dw = (n <= 256 && nwd % 4 == 0) ? 4 : 1;
-    const int q = n <= 256 ? 32 : 16;
-    const size_t bytes = ((size_t)n * (8 * dw + 8 + q + 5) + 1) * 4;
+    const SegCfg g = seg_cfg(n, nwd);
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    const size_t bytes = ((size_t)np2 * (g.r * g.dw + g.r + g.q) + 5 * (size_t)n + 1) * 4;
     const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / bytes)));
     return std::max(1, std::min(max_segs, per_cu * num_cus / la_wave_blocks(n, compact)));
 }

@@ -325,7 +325,8 @@ int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
 int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds lastAncestors: 0 = one dataflow pass per (graph, column block) where it
  * applies (default: n <= 896, chains < 2^21 rows; hgx_la_wave.hip), 1 = Gauss-Seidel sweeps
- * to the fixed point (hgx_kernels.hip). Same results. */
+ * to the fixed point (hgx_kernels.hip), m >= 2 = the dataflow pass with m time segments on
+ * a rebuild (measurement). Same results. */
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds round step for n <= 256: 0 = one lane per candidate, 8-bit rebased compares
  * (default, hgx_round_k.hip), 1 = block binary search (hgx_rounds.hip). Same results. */

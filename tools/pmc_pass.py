@@ -15,7 +15,7 @@ from collections import defaultdict
 
 ROLES = {
     "layout": r"k_layout",
-    "la_sweep": r"k_la_sweep",
+    "la_sweep": r"k_la_sweep|k_la_wave",
     "fd_build": r"k_fd_build",
     "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin",
     "round_search": r"k_round_k<|k_round_step",

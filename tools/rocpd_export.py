@@ -3,6 +3,7 @@ summaries kept under profiles/:
 
   python tools/rocpd_export.py stats    <results.db> <kernel_stats.csv>
   python tools/rocpd_export.py counters <results.db> <out_counter_collection.csv>
+  python tools/rocpd_export.py trace    <results.db> <kernel_trace.csv> [name regex]
 
 stats: per kernel name Calls, TotalDurationNs, AverageNs, Percentage, MinNs, MaxNs, StdDev
 (the columns of rocprofv3 --stats). counters: one row per dispatch and counter
@@ -44,5 +45,20 @@ def counters(db, out):
             w.writerow(row)
 
 
+def trace(db, out, pattern=""):
+    """one row per dispatch in start order: name, start (ns from the first), duration (ns)"""
+    import re
+    con = sqlite3.connect(db)
+    rows = list(con.execute("select name, start, duration from kernels order by start"))
+    t0 = rows[0][1] if rows else 0
+    rx = re.compile(pattern) if pattern else None
+    with open(out, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Name", "StartNs", "DurationNs"])
+        for name, start, dur in rows:
+            if rx is None or rx.search(name):
+                w.writerow([name, int(start - t0), int(dur)])
+
+
 if __name__ == "__main__":
-    {"stats": stats, "counters": counters}[sys.argv[1]](sys.argv[2], sys.argv[3])
+    {"stats": stats, "counters": counters, "trace": trace}[sys.argv[1]](*sys.argv[2:])
