@@ -22,7 +22,11 @@
 // runs the exact int32 compare instead (same search, slower).
 //
 // The step also writes what the next step needs: the new candidate's rows (WLA, raw WFD,
-// rebased FD8) and its strongly-seen bitmask, DecideFame's S row (hashgraph.go:688-705).
+// rebased FD8), its strongly-seen bitmask (DecideFame's S row, hashgraph.go:688-705) and the
+// next step's probe window of this chain, already rebased (WinF): the step stages 2P raw rows,
+// so the window starting at its boundary is always in LDS. The next step then loads its window
+// from a fixed address together with the candidate rows, instead of waiting for its boundary
+// before it can address the rows (two dependent memory trips), and skips the conversion.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -69,37 +73,74 @@ void round_k_prof_dump() {}
 #endif
 
 constexpr int kWinP = 31;   // probes per window: K in [0, 31], 5 binary-search levels
+constexpr int kRawP = 2 * kWinP;   // raw rows staged: this window and the next step's
 
 // window row stride in dwords: even (8-byte reads) and == 2 mod 4, so that 32 lanes reading
 // 32 different rows at the same column hit 32 distinct bank pairs (MI355X_MICROARCH.md, LDS)
 __host__ __device__ constexpr int win_stride(int ndw) { return (ndw % 4 == 0) ? ndw + 2 : ndw + 4; }
+// one window image (LDS layout, whole 16-byte groups): the forwarded copy in WinF is the same
+__host__ __device__ constexpr int win_dwords(int ndw) { return (kWinP * win_stride(ndw) + 3) & ~3; }
+
+// LDS-DMA instruction counts of one wave, fixed at compile time (every lane active, sources
+// clamped into the valid range, destinations padded), so that explicit `s_waitcnt vmcnt(N)`
+// can wait for the loads issued before a staging and leave the staging in flight
+template <int NDW, int GW, int CSZ>
+struct RkDma {
+    static constexpr int WD = win_dwords(NDW);
+    static constexpr int KW = (WD + GW * 256 - 1) / (GW * 256);          // window image, 16 B per lane
+    static constexpr int RAWD = kRawP * NDW * CSZ;                        // raw dwords at n = 4 * NDW
+    static constexpr int KR16 = (RAWD + GW * 256 - 1) / (GW * 256);       // raw rows, 16 B per lane
+    static constexpr int KR4 = (RAWD + GW * 64 - 1) / (GW * 64);          // raw rows, 4 B per lane
+    static constexpr int CPI = (CSZ == 2) ? 4 : 2;                        // FD columns per instruction
+    static constexpr int KF = (4 * NDW + GW * CPI - 1) / (GW * CPI);      // FD columns
+    static constexpr int WIN_LDS = KW * GW * 256;                         // dwords
+    static constexpr int RAW_LDS = (KR16 * GW * 256 > KR4 * GW * 64) ? KR16 * GW * 256 : KR4 * GW * 64;
+    static constexpr int FDC_LDS = KF * GW * 65;                          // groups of 64 + 1 pad dword
+};
+
+// FD8 layout: per (parity, graph) the n candidate rows as [NDW / GWD][n][GWD] dwords, so that
+// the 64 lanes of a wave (64 candidates) load one GWD-dword group each from consecutive
+// addresses (row-major rows put every lane of a load on its own cache line: 64 lines per
+// instruction). GWD = 4 when a wave's share of a row (HD dwords) is whole 16-byte groups.
+__host__ __device__ constexpr int fd8_gwd(int hd) { return (hd % 4 == 0) ? 4 : 2; }
+__host__ __device__ inline size_t fd8_at(int par, int C, int n, int ndw, int gwd, int g, int j, int d) {
+    return (size_t)par * C * ndw + ((size_t)g * ndw / gwd + d / gwd) * n * gwd + (size_t)j * gwd + d % gwd;
+}
 
 struct RoundKLds {
     int win, raw, fdc, base, bm1, hist, total;
 };
 
 // one chain group's LDS: rebased byte window | raw LA rows | FD columns (stg) | bases | histogram
-__host__ __device__ inline RoundKLds round_k_lds(int n, int ndw, int csz, bool stg) {
+template <int NDW, int GW, int CSZ>
+__host__ __device__ inline RoundKLds round_k_lds(bool stg) {
+    typedef RkDma<NDW, GW, CSZ> D;
     RoundKLds L{};
     int o = 0;
     L.win = o;
-    o += kWinP * win_stride(ndw) * 4;
+    o += D::WIN_LDS * 4;
     L.raw = o;
-    if (stg) o += ((kWinP * n * csz + 15) / 16) * 16;
+    if (stg) o += D::RAW_LDS * 4;
     L.fdc = o;
-    if (stg) {   // FD columns in groups of one LDS-DMA instruction (64 dwords) + 1 pad dword
-        const int cpi = (csz == 2) ? 4 : 2;
-        o += ((n + cpi - 1) / cpi) * 65 * 4;
-    }
+    if (stg) o += D::FDC_LDS * 4;
     L.base = o;
-    o += n * 4;
+    o += 4 * NDW * 4;
     L.bm1 = o;
-    o += n * 4;
+    o += 4 * NDW * 4;
     L.hist = o;
     o += 32 * 4;
     L.total = (o + 15) & ~15;
     return L;
 }
+
+// s_waitcnt vmcnt(N) for a compile-time N; N > 63 (the counter's range) waits for more
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N < 63 ? N : 63) : "memory");
+}
+// workgroup barrier for LDS only: __syncthreads() would also wait for every outstanding
+// global load, the staging DMA included
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // HD dwords of an LDS row as plain ds_read_b64 (2 cycles, 256 B/clk, 64-bank rule), all in
 // flight before one wait. Left to itself the compiler fuses pairs into ds_read2_b64 (8 cycles,
@@ -130,6 +171,36 @@ __device__ __forceinline__ void lds_read_row(const uint32_t* p, uint32_t (&v)[HD
     }
 }
 
+// Loads the compiler does not see as loads: it would otherwise move the first use of a
+// uniform value (a readfirstlane) right behind its load and wait there, serialising the head
+// of the step. Their values exist only after ld_wait(), which waits for every load issued so
+// far (the compiler's own waits only get stronger from the extra outstanding loads).
+__device__ __forceinline__ int32_t ld_i32(const int32_t* p) {
+    int32_t v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ int64_t ld_i64(const int64_t* p) {
+    int64_t v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint4 ld_u32x4(const uint32_t* p) {
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint2 ld_u32x2(const uint32_t* p) {
+    uint2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) {
+    uint32_t v;
+    asm volatile("global_load_ubyte %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
 // CG waves of 64 candidates each; every candidate's row is split over H waves (coordinate
 // dwords [h*NDW/H, (h+1)*NDW/H)), whose partial counts meet in LDS once per search level, so
 // that two waves share each SIMD; GPB chain groups per block when a group is one wave.
@@ -143,6 +214,14 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     constexpr int FDW = P / 2 + 1;       // dwords per compact FD column (32 positions from an even start)
     constexpr int CW = (sizeof(CT) == 2) ? FDW : 32;   // dwords per staged FD column
     constexpr int CPI = 64 / CW;                        // FD columns per LDS-DMA wave instruction
+    typedef RkDma<NDW, GW, sizeof(CT) == 2 ? 2 : 4> D;
+    static_assert(D::CPI == CPI, "FD column groups");
+    constexpr int WD = D::WD;
+    // vector-memory instructions a wave issues between the boundary load and the staging
+    constexpr int GWD = fd8_gwd(HD);
+    constexpr int NFD8 = HD / GWD;
+    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256)
+    constexpr int NSMALL = 3 + 3 * BPT;
     static_assert(GPB == 1 || GW == 1, "several chain groups per block only with one-wave groups");
     static_assert(NDW % (2 * H) == 0, "row split");
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -157,7 +236,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     const int gc = blockIdx.x * GPB + grp;
     if (gc >= C) return;   // group-uniform; block barriers are only used when GPB == 1
     RK_PROF_BEGIN();
-    const RoundKLds L = round_k_lds(n, NDW, (int)sizeof(CT), STG);
+    const RoundKLds L = round_k_lds<NDW, GW, sizeof(CT) == 2 ? 2 : 4>(STG);
     uint8_t* gl = lds + (size_t)grp * L.total;
     uint32_t* win = (uint32_t*)(gl + L.win);
     CT* raw = (CT*)(gl + L.raw);
@@ -165,53 +244,72 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     int32_t* base = (int32_t*)(gl + L.base);
     int32_t* bm1 = (int32_t*)(gl + L.bm1);
     int32_t* hist = (int32_t*)(gl + L.hist);
-    auto gsync = [&]() {
-        if constexpr (GW == 1) wave_lds_fence();
-        else __syncthreads();
+    auto gsync = [&]() {   // LDS only: every wait for global loads is explicit
+        if constexpr (GW == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else lds_barrier();
     };
 
     const int g = gc / n, cl = gc % n;
     const int par = s & 1;
     const size_t wrow = (size_t)s * C + (size_t)g * n;
-    // every load that does not depend on this chain's boundary is issued first, so their
-    // latencies overlap the boundary load: the boundary, this lane's part of its candidate's
-    // rebased row (written by the step that found the candidate), the flags and the bases
-    const int b = A.Bm[(size_t)s * C + gc];
-    const int len = A.c_len[gc], off = A.c_off[gc];
-    // root floor (after hgx_reset): offsets >= gk have round >= s+1 whatever they strongly see
-    const int gk = (s + 1 <= A.gmax) ? A.gB[(size_t)(s + 1) * C + gc] : len;
+    // Every load of the step is issued before any is waited on, and none sits behind a branch:
+    // the boundary, the chain's extent and the forwarded window's tag first, then this lane's
+    // part of its candidate's rebased row (written by the step that found the candidate), the
+    // window the previous step forwarded (both at fixed addresses), the flags and the bases.
+    int64_t wtag = ld_i64(A.WinT + (size_t)par * C + gc);
+    int b = ld_i32(A.Bm + (size_t)s * C + gc);
+    int len = ld_i32(A.c_len + gc), off = ld_i32(A.c_off + gc);
     const int j = cw * 64 + lane;        // this lane's candidate
     const int jj = j < n ? j : 0;
     uint32_t fd[HD];
     {
-        const uint32_t* __restrict__ row = A.FD8 + ((size_t)par * C + (size_t)g * n + jj) * NDW + h * HD;
-        if constexpr (HD % 4 == 0) {
+        const uint32_t* __restrict__ row = A.FD8 + fd8_at(par, C, n, NDW, GWD, g, jj, h * HD);
+        if constexpr (GWD == 4) {
 #pragma unroll
             for (int d = 0; d < HD; d += 4) {
-                const uint4 v = *(const uint4*)(row + d);
+                const uint4 v = ld_u32x4(row + (size_t)(d / 4) * n * 4);
                 fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
             }
         } else {
 #pragma unroll
             for (int d = 0; d < HD; d += 2) {
-                const uint2 v = *(const uint2*)(row + d);
+                const uint2 v = ld_u32x2(row + (size_t)(d / 2) * n * 2);
                 fd[d] = v.x; fd[d + 1] = v.y;
             }
         }
     }
-    const uint8_t wfl = A.wflag[wrow + jj];
-    const int ovf_s = A.ovf[s];
-    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256)
+    {   // the forwarded window image, straight into LDS (fixed count, clamped sources)
+        const uint32_t* __restrict__ src = A.WinF + ((size_t)par * C + gc) * WD;
+#pragma unroll
+        for (int k = 0; k < D::KW; k++) {
+            const int c0 = wh * 256 + k * GW * 256;
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane * 4, WD - 4)), (lds_ptr_t)(win + c0),
+                                             16, 0, 0);
+        }
+    }
+    // root floor (after hgx_reset): offsets >= gk have round >= s+1 whatever they strongly see
+    // (gB is a valid array without roots too: an unconditional load)
+    const bool rootr = s + 1 <= A.gmax;
+    int gkv = ld_i32(A.gB + (rootr ? (size_t)(s + 1) * C + gc : 0));
+    uint32_t wfl = ld_u8(A.wflag + wrow + jj);
+    int ovf_s = ld_i32(A.ovf + s);
     int cbv[BPT], bmp[BPT], bmc[BPT];
+    const size_t prow = s > 0 ? wrow - C : wrow;
 #pragma unroll
     for (int u = 0; u < BPT; u++) {
         const int i = gt + u * GL;
         const int ii = i < n ? i : 0;
-        cbv[u] = A.c_base[g * n + ii];
-        bmp[u] = s > 0 ? A.Bm[wrow - C + ii] : 0;
-        bmc[u] = A.Bm[wrow + ii];
+        cbv[u] = ld_i32(A.c_base + g * n + ii);
+        bmp[u] = ld_i32(A.Bm + prow + ii);
+        bmc[u] = ld_i32(A.Bm + wrow + ii);
     }
+    wait_vm<NFD8 + D::KW + NSMALL>();   // the boundary, extent and tag have landed
+    asm volatile("" : "+v"(wtag), "+v"(b), "+v"(len), "+v"(off));
+    b = __builtin_amdgcn_readfirstlane(b);
+    len = __builtin_amdgcn_readfirstlane(len);
+    off = __builtin_amdgcn_readfirstlane(off);
     if (b >= len) {
+        __builtin_amdgcn_s_waitcnt(0);   // no LDS-DMA outlives the block
         if (gt == 0) {
             A.wstat[(size_t)s * C + gc] = 0;
             A.wflag[(size_t)(s + 1) * C + gc] = 0;
@@ -220,26 +318,17 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         return;
     }
 
-    // the window: raw LA rows [kbase, kbase+np) (contiguous) and, when staged, the window's
-    // FD columns (the new candidate's FD row comes from there), by LDS-DMA
+    // staging: raw LA rows [kbase, kbase + min(2P, len - kbase)) (contiguous; the window and
+    // the next step's) and the window's FD columns (the new candidate's FD row comes from
+    // there), by LDS-DMA with a fixed instruction count per wave; then wait for everything
+    // issued before it, leaving the staging in flight
     int fsh = 0;
-    auto stage = [&](int kbase, int np) {
+    auto stage_and_wait_rest = [&](int kbase, int np) {
         if constexpr (STG) {
-            const int nel = (int)((size_t)np * n * sizeof(CT) / 4);
+            const int nraw = min(kRawP, len - kbase);
+            const int nel = (int)((size_t)nraw * n * sizeof(CT) / 4);
             const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
             uint32_t* raw_w = (uint32_t*)raw;
-            if (((n * (int)sizeof(CT)) & 15) == 0) {
-                for (int c0 = wh * 256; c0 < nel; c0 += GW * 256) {
-                    const int t = c0 + lane * 4;
-                    if (t < nel)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 16, 0, 0);
-                }
-            } else {
-                for (int c0 = wh * 64; c0 < nel; c0 += GW * 64) {
-                    const int t = c0 + lane;
-                    if (t < nel) __builtin_amdgcn_global_load_lds((const void*)(src + t), (lds_ptr_t)(raw_w + c0), 4, 0, 0);
-                }
-            }
             // FD columns: one wave instruction stages CPI columns of CW dwords each (positions
             // [kbase, kbase+np) for int32; the 2*FDW positions from the even start below kbase for
             // uint16) into a 64-dword group; groups are 65 dwords apart (bank spread)
@@ -247,34 +336,56 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             const int pcol = lane % CW, icol = lane / CW;
             const uint32_t* __restrict__ fsrc;
             size_t cstride;
-            bool pok;
             if constexpr (sizeof(CT) == 4) {
-                fsrc = (const uint32_t*)A.FDT + off + kbase + pcol;
+                fsrc = (const uint32_t*)A.FDT + off + kbase + min(pcol, np - 1);
                 cstride = (size_t)A.Pcap;
-                pok = pcol < np;
             } else {
                 const int64_t p0 = (off + kbase) & ~1;
                 fsh = (off + kbase) & 1;
                 fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
                 cstride = (size_t)(A.Pcap / 2);
-                pok = true;
             }
-            for (int i0 = wh * CPI; i0 < n; i0 += GW * CPI) {
-                const int i = i0 + icol;
-                if (i < n && pok)
+            auto fd_cols = [&]() {
+#pragma unroll
+                for (int k = 0; k < D::KF; k++) {
+                    const int i0 = wh * CPI + k * GW * CPI;
+                    const int i = min(i0 + icol, n - 1);
                     __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride),
                                                      (lds_ptr_t)(fd_w + (size_t)(i0 / CPI) * 65), 4, 0, 0);
+                }
+            };
+            if (((n * (int)sizeof(CT)) & 15) == 0) {
+#pragma unroll
+                for (int k = 0; k < D::KR16; k++) {
+                    const int c0 = wh * 256 + k * GW * 256;
+                    __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane * 4, nel - 4)),
+                                                     (lds_ptr_t)(raw_w + c0), 16, 0, 0);
+                }
+                fd_cols();
+                wait_vm<D::KR16 + D::KF>();
+            } else {
+#pragma unroll
+                for (int k = 0; k < D::KR4; k++) {
+                    const int c0 = wh * 64 + k * GW * 64;
+                    __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane, nel - 1)),
+                                                     (lds_ptr_t)(raw_w + c0), 4, 0, 0);
+                }
+                fd_cols();
+                wait_vm<D::KR4 + D::KF>();
             }
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
         }
     };
-    auto la_at = [&](int kbase, int p, int i) -> int32_t {   // decoded lastAncestors of window row p
+    auto la_at = [&](int kbase, int p, int i) -> int32_t {   // decoded lastAncestors of staged row p
         if constexpr (STG) return Coord<CT>::la(raw[p * n + i]);
         else return Coord<CT>::la(((const CT*)A.LA)[(size_t)(off + kbase + p) * n + i]);
     };
-    // rebased byte window: (0x80 | LA') per coordinate, padding coordinates LA' = 0. A thread
-    // keeps one dword column d (4 coordinates, their bases in registers) over rows p.
+    // rebased byte rows: (0x80 | LA') per coordinate against bases bs[], padding coordinates
+    // LA' = 0, for staged rows [p0, p0 + np); a thread keeps one dword column d (4 coordinates,
+    // their bases in registers) over the rows and hands each word to put(p, d, word)
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    auto convert = [&](int kbase, int np) {
+    auto rebase_rows = [&](int kbase, int p0, int np, const int32_t* bs, auto&& put) {
         constexpr int RS = (GL >= NDW) ? GL / NDW : 1;   // rows per pass
         constexpr int NP = (P + RS - 1) / RS;              // passes (fixed trip count)
         for (int d = gt % NDW; d < NDW; d += GL) {
@@ -282,14 +393,14 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             if constexpr (STG && sizeof(CT) == 2) {
                 // packed: LA' = min(sat(raw - base), 126) on coordinate pairs (raw = LA + 1)
                 u16x2 b01 = {0, 0}, b23 = {0, 0};
-                if (i0 < n) b01 = u16x2{(unsigned short)base[i0], (unsigned short)base[i0 + 1]};
-                if (i0 + 2 < n) b23 = u16x2{(unsigned short)base[i0 + 2], (unsigned short)base[i0 + 3]};
+                if (i0 < n) b01 = u16x2{(unsigned short)bs[i0], (unsigned short)bs[i0 + 1]};
+                if (i0 + 2 < n) b23 = u16x2{(unsigned short)bs[i0 + 2], (unsigned short)bs[i0 + 3]};
                 const u16x2 cap = {126, 126};
 #pragma unroll
                 for (int u = 0; u < NP; u++) {
                     const int p = gt / NDW + u * RS;
                     if (p < np) {
-                        const uint32_t* rp = (const uint32_t*)(raw + p * n + i0);
+                        const uint32_t* rp = (const uint32_t*)(raw + (p0 + p) * n + i0);
                         const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
                         const u16x2 y01 = __builtin_elementwise_min(
                             __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
@@ -297,24 +408,24 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
                             __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
                         const uint32_t w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23),
                                                                  __builtin_bit_cast(uint32_t, y01), 0x06040200u);
-                        win[p * WS + d] = w | 0x80808080u;
+                        put(p, d, w | 0x80808080u);
                     }
                 }
             } else {
                 int32_t bq[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) bq[q] = (i0 + q < n) ? base[i0 + q] : 0;
+                for (int q = 0; q < 4; q++) bq[q] = (i0 + q < n) ? bs[i0 + q] : 0;
                 for (int p = gt / NDW; p < np; p += RS) {
                     uint32_t w = 0x80808080u;
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const int i = i0 + q;
                         if (i < n) {
-                            const int32_t x = la_at(kbase, p, i) - bq[q] + 1;
+                            const int32_t x = la_at(kbase, p0 + p, i) - bq[q] + 1;
                             w |= (uint32_t)min(max(x, 0), 126) << (8 * q);
                         }
                     }
-                    win[p * WS + d] = w;
+                    put(p, d, w);
                 }
             }
         }
@@ -334,31 +445,44 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         }
     };
 
-    int kbase = b, np = min(P, len - b), kstar = len, carried = 0, B = -1, K = P;
-    bool done = false;   // seen in an earlier window: seen at every later probe
-    // the first window's staging depends on the boundary only: issue it now, so the candidate
-    // rows and the bases are still in flight while it lands
-    stage(kbase, np);
+    // the forwarded window is this step's: same round, same first offset (tags are cleared at
+    // the start of every DivideRounds); exact rounds compare raw rows anyway
+    int kbase = b, np = min(P, len - b);
+    stage_and_wait_rest(kbase, np);   // everything before the staging has landed
+    asm volatile("" : "+v"(gkv), "+v"(wfl), "+v"(ovf_s));
+#pragma unroll
+    for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+#pragma unroll
+    for (int u = 0; u < BPT; u++) asm volatile("" : "+v"(cbv[u]), "+v"(bmp[u]), "+v"(bmc[u]));
+    const int gk = rootr ? gkv : len;
     const bool exact = ovf_s != 0;   // a candidate row of this round did not fit 8 bits
     const bool cand = j < n && wfl == 1;
+    const bool fwd = STG && !exact && wtag == (((int64_t)s << 32) | (int64_t)(uint32_t)b);
 #pragma unroll
     for (int u = 0; u < BPT; u++) {
         const int i = gt + u * GL;
         if (i < n) {
-            base[i] = cbv[u] + bmp[u];   // base(s): Index of round s-1's candidate on chain i
-            bm1[i] = cbv[u] + bmc[u];    // base(s+1)
+            base[i] = cbv[u] + (s > 0 ? bmp[u] : 0);   // base(s): Index of round s-1's candidate on chain i
+            bm1[i] = cbv[u] + bmc[u];                  // base(s+1)
         }
     }
     if (gt < 32) hist[gt] = 0;
     RK_PROF(0);
-    bool staged = true;
-    for (;;) {
-        if (!staged) stage(kbase, np);
-        staged = false;
-        __builtin_amdgcn_s_waitcnt(0);
-        gsync();
-        RK_PROF(1);
-        convert(kbase, np);
+
+    int kstar = len, carried = 0, B = -1, K = P;
+    bool done = false;     // seen in an earlier window: seen at every later probe
+    bool pending = true;   // staging issued and not yet waited for
+    for (int w_it = 0;; w_it++) {
+        if (w_it > 0) stage_and_wait_rest(kbase, np);   // a later window (rare)
+        if (w_it == 0 && fwd) {
+            RK_PROF(1);   // the window is in LDS; the raw rows land during the search
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+            pending = false;
+            gsync();
+            RK_PROF(1);
+            rebase_rows(kbase, 0, np, base, [&](int p, int d, uint32_t w) { win[p * WS + d] = w; });
+        }
         gsync();
         RK_PROF(2);
         // first probe of the window that strongly sees this lane's candidate (np: none);
@@ -432,6 +556,10 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             break;
         }
         np = min(P, len - kbase);
+        if (pending) {   // the forwarded window's staging lands before the next is issued
+            __builtin_amdgcn_s_waitcnt(0);
+            pending = false;
+        }
         gsync();
     }
 
@@ -448,6 +576,11 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         const uint64_t bits = __ballot(cand && K <= B);
         const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
         if (h == 0 && lane == 0 && cw < A.nw) A.Smat[srow + cw] = bits;
+        if (pending) {   // the raw rows and FD columns of a forwarded window's step
+            __builtin_amdgcn_s_waitcnt(0);
+            pending = false;
+            gsync();
+        }
         RK_PROF(6);
         // the new candidate's rows for round s+1
         const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
@@ -467,7 +600,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             else A.WFD[nrow + i] = f;
         }
         // rebased FD row (base(s+1) = Index of this round's candidates) for the next step
-        uint32_t* nfd = A.FD8 + ((size_t)(par ^ 1) * C + gc) * NDW;
+        uint32_t* nfd = A.FD8;
         bool of = false;
         for (int d = gt; d < NDW; d += GL) {
             uint32_t w = 0;
@@ -485,13 +618,22 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
                 }
                 w |= v << (8 * q);
             }
-            nfd[d] = w;
+            nfd[fd8_at(par ^ 1, C, n, NDW, GWD, g, cl, d)] = w;
         }
         if (of) A.ovf[s + 1] = 1;   // same value from every writer
         if (gt == 0) A.wflag[(size_t)(s + 1) * C + gc] = 1;
+        if constexpr (STG) {
+            // the next step's window of this chain: rows [kstar, kstar + np1) rebased to base(s+1)
+            // (pk <= P-1 and np1 <= P, so they lie in the 2P staged rows)
+            const int np1 = min(P, len - kstar);
+            uint32_t* dst = A.WinF + ((size_t)(par ^ 1) * C + gc) * WD;
+            rebase_rows(kbase, pk, np1, bm1, [&](int p, int d, uint32_t w) { dst[p * WS + d] = w; });
+            if (gt == 0) A.WinT[(size_t)(par ^ 1) * C + gc] = ((int64_t)(s + 1) << 32) | (int64_t)(uint32_t)kstar;
+        }
     } else if (gt == 0) {
         A.wflag[(size_t)(s + 1) * C + gc] = 0;
     }
+    if (pending) __builtin_amdgcn_s_waitcnt(0);   // no LDS-DMA outlives the block
     RK_PROF(5);
     RK_PROF_END();
 }
@@ -500,7 +642,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
 // round of an incremental DivideRounds), rebased to base(r) = c_base + Bm[r-1], from the
 // row-major WFD rows k_round_gather has just written (raw uint16 or int32 FD)
 template <typename CT>
-__global__ void k_round_k_gather(RoundArgs A, int ndw, int r) {
+__global__ void k_round_k_gather(RoundArgs A, int ndw, int gwd, int r) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)A.C * ndw) return;
     const int gc = (int)(t / ndw), d = (int)(t % ndw);
@@ -523,7 +665,7 @@ __global__ void k_round_k_gather(RoundArgs A, int ndw, int r) {
         }
         w |= v << (8 * q);
     }
-    A.FD8[((size_t)(r & 1) * C + gc) * ndw + d] = w;
+    A.FD8[fd8_at(r & 1, C, n, ndw, gwd, g, gc % n, d)] = w;
     if (of) A.ovf[r] = 1;
 }
 
@@ -534,10 +676,12 @@ int round_k_ndw(int n) {
     return p;
 }
 
+int round_k_win_dwords(int n) { return win_dwords(round_k_ndw(n)); }
+
 template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
 static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
     const void* f = (const void*)k_round_k<CT, NDW, CG, H, GPB, STG>;
-    const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), STG);
+    const RoundKLds L = round_k_lds<NDW, CG * H, sizeof(CT) == 2 ? 2 : 4>(STG);
     const size_t lds = (size_t)L.total * GPB;
     static bool attr = false;
     if (!attr) {
@@ -552,9 +696,23 @@ static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
 
 template <typename CT, int NDW, int CG, int H, int GPB>
 static hipError_t round_k_launch(hipStream_t st, const RoundArgs& A, int s) {
-    const RoundKLds L = round_k_lds(A.n, NDW, (int)sizeof(CT), true);
+    const RoundKLds L = round_k_lds<NDW, CG * H, sizeof(CT) == 2 ? 2 : 4>(true);
     if ((size_t)L.total * GPB <= 140 * 1024) return round_k_launch_v<CT, NDW, CG, H, GPB, true>(st, A, s);
     return round_k_launch_v<CT, NDW, CG, H, GPB, false>(st, A, s);
+}
+
+// a wave's share of a candidate row (dwords) in the configuration launch_round_k_t picks
+static int round_k_hd(int n, int C) {
+    const bool many = C >= 1024;
+    switch (round_k_ndw(n)) {
+        case 2: return 2;
+        case 4: return many ? 4 : 2;
+        case 8: return many ? 8 : 2;
+        case 16: return many ? 16 : 2;
+        case 32: return 8;
+        case 64: return 32;
+        default: return 2;
+    }
 }
 
 // one wave per chain, four chains per block, when chains are many (batched simulations);
@@ -579,12 +737,13 @@ hipError_t launch_round_k(hipStream_t st, const RoundArgs& A, int s) {
 
 void launch_round_k_gather(hipStream_t st, const RoundArgs& A, int r) {
     const int ndw = round_k_ndw(A.n);
+    const int gwd = fd8_gwd(round_k_hd(A.n, A.C));
     const int64_t work = (int64_t)A.C * ndw;
     if (work <= 0) return;
     if (A.compact)
-        hipLaunchKernelGGL(k_round_k_gather<uint16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, r);
+        hipLaunchKernelGGL(k_round_k_gather<uint16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, gwd, r);
     else
-        hipLaunchKernelGGL(k_round_k_gather<int32_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, r);
+        hipLaunchKernelGGL(k_round_k_gather<int32_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, A, ndw, gwd, r);
 }
 
 }  // namespace hgx
