@@ -598,21 +598,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(FD8.alloc(need));
             drop_step_graph();
         }
-        const size_t wneed = (size_t)2 * C * round_k_win_dwords(n);
-        if (WinF.n < wneed || WinT.n < (size_t)2 * C) {
-            HGX_TRY(WinF.alloc(wneed));
-            HGX_TRY(WinT.alloc((size_t)2 * C));
-            drop_step_graph();
-        }
-        // no forwarded window survives a call (its rows and bases may change in the next one)
-        HGX_TRY(hipMemsetAsync(WinT.p, 0xFF, (size_t)2 * C * 8, stream));
     }
     auto round_args = [&]() {
         RoundArgs A{};
         A.n = n; A.C = C; A.sm = sm; A.nw = nw; A.Pcap = fd_ld;
         A.c_len = c_len.p; A.c_off = c_off.p; A.c_base = c_base.p; A.LA = LA.p; A.FDT = FDT.p; A.compact = compact;
         A.p_gid = p_gid.p; A.g_coin = g_coin.p; A.FD8 = FD8.p; A.ovf = ovf.p;
-        A.WinF = WinF.p; A.WinT = WinT.p;
         A.Bm = Bm.p; A.WLA = WLA.p; A.WFD = WFD.p; A.p_round = p_round.p; A.active = active.p;
         A.lr = lr.p; A.wflag = wflag.p; A.wstat = wstat.p; A.wcoin = wcoin.p; A.Smat = Smat.p;
         A.gB = rooted ? gB.p : c_len.p;   // (any int array without roots: read, never used)

@@ -214,8 +214,6 @@ class Engine {
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<uint32_t> FD8;   // [2][C][ndw] rebased candidate rows (k_round_k)
-    DBuf<uint32_t> WinF;  // [2][C][win dwords] forwarded probe windows (k_round_k)
-    DBuf<int64_t> WinT;   // [2][C] their tags
     DBuf<int32_t> ovf;    // [r_cap + 2]
     DBuf<int8_t> fame;
     // order

@@ -91,10 +91,6 @@ struct RoundArgs {
     const int32_t *c_len, *c_off, *c_base, *p_gid;
     uint32_t* FD8;    // [2][C][ndw] candidate firstDescendants rebased to 8 bits (k_round_k, by round parity)
     int32_t* ovf;     // [rounds + 2] round r's candidate rows do not fit 8 bits: exact compares
-    // [2][C][round_k_win_dwords] the next step's rebased probe window of every chain, written by
-    // the step that found its boundary, tagged in WinT[2][C] with (round << 32 | first offset)
-    uint32_t* WinF;
-    int64_t* WinT;
     const void *LA, *FDT;   // int32_t or uint16_t (compact)
     int compact;
     const uint8_t* g_coin;
@@ -147,7 +143,6 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r, int block
 hipError_t launch_round_k(hipStream_t s, const RoundArgs& A, int r);
 void launch_round_k_gather(hipStream_t s, const RoundArgs& A, int r);   // round r's rebased rows + ovf[r]
 int round_k_ndw(int n);
-int round_k_win_dwords(int n);   // dwords of one forwarded window (WinF)
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,

@@ -22,11 +22,12 @@
 // runs the exact int32 compare instead (same search, slower).
 //
 // The step also writes what the next step needs: the new candidate's rows (WLA, raw WFD,
-// rebased FD8), its strongly-seen bitmask (DecideFame's S row, hashgraph.go:688-705) and the
-// next step's probe window of this chain, already rebased (WinF): the step stages 2P raw rows,
-// so the window starting at its boundary is always in LDS. The next step then loads its window
-// from a fixed address together with the candidate rows, instead of waiting for its boundary
-// before it can address the rows (two dependent memory trips), and skips the conversion.
+// rebased FD8) and its strongly-seen bitmask, DecideFame's S row (hashgraph.go:688-705).
+//
+// Memory: every step reads all candidates' rebased rows (64 KB at n = 256), written by the
+// previous step on every XCD. They are laid out so that a wave's 64 lanes (64 candidates) load
+// consecutive 16-byte groups (fd8_at); all head loads are issued before one explicit wait,
+// and barriers wait for LDS only, so no barrier drains the window staging early.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -73,13 +74,11 @@ void round_k_prof_dump() {}
 #endif
 
 constexpr int kWinP = 31;   // probes per window: K in [0, 31], 5 binary-search levels
-constexpr int kRawP = 2 * kWinP;   // raw rows staged: this window and the next step's
 
 // window row stride in dwords: even (8-byte reads) and == 2 mod 4, so that 32 lanes reading
 // 32 different rows at the same column hit 32 distinct bank pairs (MI355X_MICROARCH.md, LDS)
 __host__ __device__ constexpr int win_stride(int ndw) { return (ndw % 4 == 0) ? ndw + 2 : ndw + 4; }
-// one window image (LDS layout, whole 16-byte groups): the forwarded copy in WinF is the same
-__host__ __device__ constexpr int win_dwords(int ndw) { return (kWinP * win_stride(ndw) + 3) & ~3; }
+__host__ __device__ constexpr int win_dwords(int ndw) { return kWinP * win_stride(ndw); }
 
 // LDS-DMA instruction counts of one wave, fixed at compile time (every lane active, sources
 // clamped into the valid range, destinations padded), so that explicit `s_waitcnt vmcnt(N)`
@@ -87,13 +86,12 @@ __host__ __device__ constexpr int win_dwords(int ndw) { return (kWinP * win_stri
 template <int NDW, int GW, int CSZ>
 struct RkDma {
     static constexpr int WD = win_dwords(NDW);
-    static constexpr int KW = (WD + GW * 256 - 1) / (GW * 256);          // window image, 16 B per lane
-    static constexpr int RAWD = kRawP * NDW * CSZ;                        // raw dwords at n = 4 * NDW
+    static constexpr int RAWD = kWinP * NDW * CSZ;                        // raw dwords at n = 4 * NDW
     static constexpr int KR16 = (RAWD + GW * 256 - 1) / (GW * 256);       // raw rows, 16 B per lane
     static constexpr int KR4 = (RAWD + GW * 64 - 1) / (GW * 64);          // raw rows, 4 B per lane
     static constexpr int CPI = (CSZ == 2) ? 4 : 2;                        // FD columns per instruction
     static constexpr int KF = (4 * NDW + GW * CPI - 1) / (GW * CPI);      // FD columns
-    static constexpr int WIN_LDS = KW * GW * 256;                         // dwords
+    static constexpr int WIN_LDS = WD;                                    // dwords
     static constexpr int RAW_LDS = (KR16 * GW * 256 > KR4 * GW * 64) ? KR16 * GW * 256 : KR4 * GW * 64;
     static constexpr int FDC_LDS = KF * GW * 65;                          // groups of 64 + 1 pad dword
 };
@@ -180,11 +178,6 @@ __device__ __forceinline__ int32_t ld_i32(const int32_t* p) {
     asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
-__device__ __forceinline__ int64_t ld_i64(const int64_t* p) {
-    int64_t v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
 __device__ __forceinline__ uint4 ld_u32x4(const uint32_t* p) {
     uint4 v;
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
@@ -216,7 +209,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     constexpr int CPI = 64 / CW;                        // FD columns per LDS-DMA wave instruction
     typedef RkDma<NDW, GW, sizeof(CT) == 2 ? 2 : 4> D;
     static_assert(D::CPI == CPI, "FD column groups");
-    constexpr int WD = D::WD;
     // vector-memory instructions a wave issues between the boundary load and the staging
     constexpr int GWD = fd8_gwd(HD);
     constexpr int NFD8 = HD / GWD;
@@ -256,7 +248,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     // the boundary, the chain's extent and the forwarded window's tag first, then this lane's
     // part of its candidate's rebased row (written by the step that found the candidate), the
     // window the previous step forwarded (both at fixed addresses), the flags and the bases.
-    int64_t wtag = ld_i64(A.WinT + (size_t)par * C + gc);
     int b = ld_i32(A.Bm + (size_t)s * C + gc);
     int len = ld_i32(A.c_len + gc), off = ld_i32(A.c_off + gc);
     const int j = cw * 64 + lane;        // this lane's candidate
@@ -278,15 +269,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             }
         }
     }
-    {   // the forwarded window image, straight into LDS (fixed count, clamped sources)
-        const uint32_t* __restrict__ src = A.WinF + ((size_t)par * C + gc) * WD;
-#pragma unroll
-        for (int k = 0; k < D::KW; k++) {
-            const int c0 = wh * 256 + k * GW * 256;
-            __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane * 4, WD - 4)), (lds_ptr_t)(win + c0),
-                                             16, 0, 0);
-        }
-    }
     // root floor (after hgx_reset): offsets >= gk have round >= s+1 whatever they strongly see
     // (gB is a valid array without roots too: an unconditional load)
     const bool rootr = s + 1 <= A.gmax;
@@ -303,8 +285,8 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         bmp[u] = ld_i32(A.Bm + prow + ii);
         bmc[u] = ld_i32(A.Bm + wrow + ii);
     }
-    wait_vm<NFD8 + D::KW + NSMALL>();   // the boundary, extent and tag have landed
-    asm volatile("" : "+v"(wtag), "+v"(b), "+v"(len), "+v"(off));
+    wait_vm<NFD8 + NSMALL>();   // the boundary and the chain's extent have landed
+    asm volatile("" : "+v"(b), "+v"(len), "+v"(off));
     b = __builtin_amdgcn_readfirstlane(b);
     len = __builtin_amdgcn_readfirstlane(len);
     off = __builtin_amdgcn_readfirstlane(off);
@@ -325,7 +307,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     int fsh = 0;
     auto stage_and_wait_rest = [&](int kbase, int np) {
         if constexpr (STG) {
-            const int nraw = min(kRawP, len - kbase);
+            const int nraw = min(kWinP, len - kbase);
             const int nel = (int)((size_t)nraw * n * sizeof(CT) / 4);
             const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kbase) * n * sizeof(CT) / 4;
             uint32_t* raw_w = (uint32_t*)raw;
@@ -445,8 +427,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         }
     };
 
-    // the forwarded window is this step's: same round, same first offset (tags are cleared at
-    // the start of every DivideRounds); exact rounds compare raw rows anyway
     int kbase = b, np = min(P, len - b);
     stage_and_wait_rest(kbase, np);   // everything before the staging has landed
     asm volatile("" : "+v"(gkv), "+v"(wfl), "+v"(ovf_s));
@@ -457,7 +437,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     const int gk = rootr ? gkv : len;
     const bool exact = ovf_s != 0;   // a candidate row of this round did not fit 8 bits
     const bool cand = j < n && wfl == 1;
-    const bool fwd = STG && !exact && wtag == (((int64_t)s << 32) | (int64_t)(uint32_t)b);
 #pragma unroll
     for (int u = 0; u < BPT; u++) {
         const int i = gt + u * GL;
@@ -471,18 +450,12 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
 
     int kstar = len, carried = 0, B = -1, K = P;
     bool done = false;     // seen in an earlier window: seen at every later probe
-    bool pending = true;   // staging issued and not yet waited for
     for (int w_it = 0;; w_it++) {
         if (w_it > 0) stage_and_wait_rest(kbase, np);   // a later window (rare)
-        if (w_it == 0 && fwd) {
-            RK_PROF(1);   // the window is in LDS; the raw rows land during the search
-        } else {
-            __builtin_amdgcn_s_waitcnt(0);
-            pending = false;
-            gsync();
-            RK_PROF(1);
-            rebase_rows(kbase, 0, np, base, [&](int p, int d, uint32_t w) { win[p * WS + d] = w; });
-        }
+        __builtin_amdgcn_s_waitcnt(0);
+        gsync();
+        RK_PROF(1);
+        rebase_rows(kbase, 0, np, base, [&](int p, int d, uint32_t w) { win[p * WS + d] = w; });
         gsync();
         RK_PROF(2);
         // first probe of the window that strongly sees this lane's candidate (np: none);
@@ -556,10 +529,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             break;
         }
         np = min(P, len - kbase);
-        if (pending) {   // the forwarded window's staging lands before the next is issued
-            __builtin_amdgcn_s_waitcnt(0);
-            pending = false;
-        }
         gsync();
     }
 
@@ -576,11 +545,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         const uint64_t bits = __ballot(cand && K <= B);
         const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
         if (h == 0 && lane == 0 && cw < A.nw) A.Smat[srow + cw] = bits;
-        if (pending) {   // the raw rows and FD columns of a forwarded window's step
-            __builtin_amdgcn_s_waitcnt(0);
-            pending = false;
-            gsync();
-        }
         RK_PROF(6);
         // the new candidate's rows for round s+1
         const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
@@ -622,18 +586,9 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         }
         if (of) A.ovf[s + 1] = 1;   // same value from every writer
         if (gt == 0) A.wflag[(size_t)(s + 1) * C + gc] = 1;
-        if constexpr (STG) {
-            // the next step's window of this chain: rows [kstar, kstar + np1) rebased to base(s+1)
-            // (pk <= P-1 and np1 <= P, so they lie in the 2P staged rows)
-            const int np1 = min(P, len - kstar);
-            uint32_t* dst = A.WinF + ((size_t)(par ^ 1) * C + gc) * WD;
-            rebase_rows(kbase, pk, np1, bm1, [&](int p, int d, uint32_t w) { dst[p * WS + d] = w; });
-            if (gt == 0) A.WinT[(size_t)(par ^ 1) * C + gc] = ((int64_t)(s + 1) << 32) | (int64_t)(uint32_t)kstar;
-        }
     } else if (gt == 0) {
         A.wflag[(size_t)(s + 1) * C + gc] = 0;
     }
-    if (pending) __builtin_amdgcn_s_waitcnt(0);   // no LDS-DMA outlives the block
     RK_PROF(5);
     RK_PROF_END();
 }
@@ -675,8 +630,6 @@ int round_k_ndw(int n) {
     while (p < d) p *= 2;
     return p;
 }
-
-int round_k_win_dwords(int n) { return win_dwords(round_k_ndw(n)); }
 
 template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
 static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
