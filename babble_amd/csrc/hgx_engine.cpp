@@ -66,6 +66,7 @@ Engine::~Engine() {
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
     if (h_small) (void)hipHostFree(h_small);
+    if (h_flag) (void)hipHostFree(h_flag);
     for (auto e : flag_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : la_ev)
@@ -144,6 +145,8 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[1], hipEventDisableTiming));
     HGX_TRY(hipHostMalloc((void**)&h_small, 64 * sizeof(int32_t), hipHostMallocDefault));
+    HGX_TRY(hipHostMalloc((void**)&h_flag, 16 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    HGX_TRY(hipHostGetDevicePointer((void**)&d_flag, h_flag, 0));
     // rounds: initial guess, grown on demand
     const int lg = std::max(1, bitlen((uint64_t)n));
     // rounds of the largest graph: ~events per graph / (n log n) (SURVEY §8 estimate), x2
@@ -669,9 +672,15 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 }
                 if ((int)sgr.nodes.size() != nb) return hipErrorUnknown;
             }
+            const int slot = launched & 1;
+            // the batch's last step writes round + 1 into this slot's host-mapped flag when a
+            // chain still has events beyond its boundary (no D2H copy between the replays)
+            sgr.args_last[slot] = sgr.args;
+            sgr.args_last[slot].hflag = d_flag + slot;
+            h_flag[slot] = 0;
             for (int k = 0; k < nb; k++) {
                 sgr.round[k] = r_lo + launched * nb + k;
-                void* args[2] = {(void*)&sgr.args, (void*)&sgr.round[k]};
+                void* args[2] = {(void*)(k == nb - 1 ? &sgr.args_last[slot] : &sgr.args), (void*)&sgr.round[k]};
                 hipKernelNodeParams kp = sgr.params[k];
                 kp.kernelParams = args;
                 kp.extra = nullptr;
@@ -681,9 +690,6 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             kstat[K_ROUND_SEARCH].launches += nb - 1;   // nb step kernels per replay
             HGX_TRY(hipGraphLaunch(sgr.exec, stream));
             kend(K_ROUND_SEARCH, 0);
-            const int slot = launched & 1;
-            HGX_TRY(hipMemcpyAsync(h_small + slot, active.p + (r_lo + (launched + 1) * nb - 1), 4,
-                                   hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipEventRecord(flag_ev[slot], stream));
             launched++;
             return hipSuccess;
@@ -694,7 +700,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         if (rebuild) HGX_TRY(launch_batch());
         for (;;) {
             HGX_TRY(hipEventSynchronize(flag_ev[checked & 1]));
-            const int more = h_small[checked & 1];
+            const int more = __atomic_load_n(&h_flag[checked & 1], __ATOMIC_ACQUIRE);
             checked++;
             if (!more) break;
             if (launched == checked) HGX_TRY(launch_batch());   // no batch in flight

@@ -23,6 +23,7 @@ struct StepGraph {
     std::vector<hipGraphNode_t> nodes;   // the step nodes, in order
     std::vector<hipKernelNodeParams> params;
     RoundArgs args{};
+    RoundArgs args_last[2]{};   // the last step node's arguments: args + the host flag of a batch slot
     int kernel = -1, compact = -1, nb = 0;   // what the graph was captured for
     int32_t round[64] = {};
     void drop();
@@ -224,6 +225,8 @@ class Engine {
     DBuf<uint32_t> val_a, val_b, hist;
     DBuf<int64_t> minmax, blk_ntx;
     int32_t* h_small = nullptr;   // pinned scratch (flags)
+    int32_t* h_flag = nullptr;    // host-mapped, coherent: the round-step batches' "candidates left" flags
+    int32_t* d_flag = nullptr;    // its device address
     // timing
     hipEvent_t ph0 = nullptr, ph1 = nullptr;
     std::vector<hipEvent_t> kev;

@@ -102,6 +102,9 @@ struct RoundArgs {
     // gmax = -1 without roots
     const int32_t* gB;
     int gmax;
+    // last step node of a replayed batch only: host-mapped word set to round + 1 when a chain
+    // still has events beyond its boundary (the host polls it instead of a D2H copy)
+    int32_t* hflag;
 };
 
 int fd_tile_rows(int n, int compact);

@@ -536,7 +536,10 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     for (int k = b + gt; k < kstar; k += GL) A.p_round[off + k] = s;
     if (gt == 0) {
         A.wstat[(size_t)s * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) A.active[s] = 1;   // same value from every writer: a plain store
+        if (kstar < len) {   // same value from every writer: plain stores
+            A.active[s] = 1;
+            if (A.hflag) *A.hflag = s + 1;   // last step of a batch: the host's flag (mapped memory)
+        }
         A.Bm[(size_t)(s + 1) * C + gc] = kstar;
     }
     if (kstar < len) {

@@ -424,7 +424,10 @@ __global__ void __launch_bounds__(GPB * NWC * 64) k_round_step(RoundArgs A, int 
     for (int k = b + gt; k < kstar; k += NT) A.p_round[off + k] = r;
     if (gt == 0) {
         A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) A.active[r] = 1;   // same value from every writer: a plain store
+        if (kstar < len) {   // same value from every writer: plain stores
+            A.active[r] = 1;
+            if (A.hflag) *A.hflag = r + 1;   // last step of a batch: the host's flag
+        }
         A.Bm[(size_t)(r + 1) * C + gc] = kstar;
     }
     HGX_PROF(7);
@@ -657,7 +660,10 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_round_step_big(RoundArgs A, 
     for (int k = b + (int)threadIdx.x; k < kstar; k += blockDim.x) A.p_round[off + k] = r;
     if (threadIdx.x == 0) {
         A.wstat[(size_t)r * C + gc] = (kstar > b) ? 2 : 1;
-        if (kstar < len) A.active[r] = 1;   // same value from every writer: a plain store
+        if (kstar < len) {   // same value from every writer: plain stores
+            A.active[r] = 1;
+            if (A.hflag) *A.hflag = r + 1;   // last step of a batch: the host's flag
+        }
         A.Bm[(size_t)(r + 1) * C + gc] = kstar;
     }
     if (kstar < len) {
