@@ -1286,7 +1286,9 @@ int32_t hgx_kernel_stats(hgx_ctx* c, int32_t k, char* name, int32_t name_cap, do
                          double* bytes) {
     if (!c || k < 0 || k >= hgx::K_NUM) return HGX_ERR_INVALID;
     if (name && name_cap > 0) std::snprintf(name, (size_t)name_cap, "%s", kKernelNames[k]);
-    if (ms) *ms = c->eng.kstat[k].ms;
+    const hgx::KernelStat& ks = c->eng.kstat[k];
+    // summed device time of all launches, extrapolated from the timed sample
+    if (ms) *ms = (ks.timed > 0 && ks.timed < ks.launches) ? ks.ms * (double)ks.launches / (double)ks.timed : ks.ms;
     if (launches) *launches = c->eng.kstat[k].launches;
     if (bytes) *bytes = c->eng.kstat[k].bytes;
     return HGX_OK;

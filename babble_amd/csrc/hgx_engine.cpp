@@ -212,22 +212,26 @@ DevArrays Engine::arrays() {
 }
 
 // ---- per-kernel timing (only when time_kernels) ---------------------------------
-void Engine::kbeg(int k) {
-    kstat[k].launches++;
-    if (!((time_mask >> k) & 1u)) return;
+// count = launches the window covers (a hipGraph replay of round steps); sample = false
+// counts them without timing (a per-launch average from the timed sample: KernelStat.timed)
+void Engine::kbeg(int k, bool sample, int64_t count) {
+    kstat[k].launches += count;
+    if (!((time_mask >> k) & 1u) || !sample) return;
     while (kev.size() < kev_used + 2) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return;
+        // timing only (nothing on the host waits on them): no system-scope fences, so that the
+        // events bracketing every round-step replay cost the timed region as little as possible
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return;
         kev.push_back(e);
     }
     (void)hipEventRecord(kev[kev_used], stream);
-    kopen.push_back({k, kev_used, 0});
+    kopen.push_back({k, kev_used, 0, count});
     kev_used += 2;
 }
 
 void Engine::kend(int k, double bytes) {
     kstat[k].bytes += bytes;
-    if (!((time_mask >> k) & 1u) || kopen.empty()) return;
+    if (!((time_mask >> k) & 1u) || kopen.empty() || kopen.back().k != k) return;
     Open& o = kopen.back();
     o.bytes = bytes;
     (void)hipEventRecord(kev[o.e0 + 1], stream);
@@ -245,7 +249,10 @@ hipError_t Engine::collect_kernel_times() {
     HGX_TRY(hipStreamSynchronize(stream));
     for (const Open& o : kopen) {
         float ms = 0;
-        if (hipEventElapsedTime(&ms, kev[o.e0], kev[o.e0 + 1]) == hipSuccess) kstat[o.k].ms += ms;
+        if (hipEventElapsedTime(&ms, kev[o.e0], kev[o.e0 + 1]) == hipSuccess) {
+            kstat[o.k].ms += ms;
+            kstat[o.k].timed += o.count;
+        }
     }
     kopen.clear();
     kev_used = 0;
@@ -686,10 +693,11 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 kp.extra = nullptr;
                 HGX_TRY(hipGraphExecKernelNodeSetParams(sgr.exec, sgr.nodes[k], &kp));
             }
-            kbeg(K_ROUND_SEARCH);
-            kstat[K_ROUND_SEARCH].launches += nb - 1;   // nb step kernels per replay
+            // nb step kernels per replay; one replay in 4 is bracketed by timing events
+            const bool sample = (launched & 3) == 0;
+            kbeg(K_ROUND_SEARCH, sample, nb);
             HGX_TRY(hipGraphLaunch(sgr.exec, stream));
-            kend(K_ROUND_SEARCH, 0);
+            if (sample) kend(K_ROUND_SEARCH, 0);
             HGX_TRY(hipEventRecord(flag_ev[slot], stream));
             launched++;
             return hipSuccess;

@@ -35,8 +35,9 @@ enum KernelId {
 };
 
 struct KernelStat {
-    double ms = 0;        // summed device time (HIP events around each launch)
+    double ms = 0;        // summed device time (HIP events around the timed launches)
     int64_t launches = 0;
+    int64_t timed = 0;    // launches inside HIP-event windows (the round steps time a sample of replays)
     double bytes = 0;     // algorithmic bytes summed over launches
 };
 
@@ -164,7 +165,7 @@ class Engine {
    private:
     hipError_t ensure_round_cap(int32_t need);
     InsertState insert_state();
-    void kbeg(int k);
+    void kbeg(int k, bool sample = true, int64_t count = 1);
     void kend(int k, double bytes);
     void kadd_bytes(int k, double bytes);
     hipError_t collect_kernel_times();
@@ -230,7 +231,7 @@ class Engine {
     // timing
     hipEvent_t ph0 = nullptr, ph1 = nullptr;
     std::vector<hipEvent_t> kev;
-    struct Open { int k; size_t e0; double bytes; };
+    struct Open { int k; size_t e0; double bytes; int64_t count; };
     std::vector<Open> kopen;
     size_t kev_used = 0;
 };

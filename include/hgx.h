@@ -310,7 +310,8 @@ int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_k
  * segments of the last dataflow pass (up to 13 values) */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
- * name of the kernel, summed device ms, launches, algorithmic bytes moved */
+ * name of the kernel, summed device ms (the round steps time one hipGraph replay in four and
+ * scale the sample to every launch), launches, algorithmic bytes moved */
 int32_t hgx_kernel_stats(hgx_ctx* ctx, int32_t k, char* name, int32_t name_cap, double* ms, int64_t* launches,
                          double* bytes);
 int32_t hgx_reset_stats(hgx_ctx* ctx);
