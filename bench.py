@@ -423,8 +423,9 @@ def main():
     t0 = time.time()
     tr, G = make_trace(args.config, rank)
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
-    h = Hashgraph(n, capacity=tr.E, device=local_rank, n_graphs=G)
-    dtr = DeviceTrace(tr, device=local_rank)   # resident in HBM before the clock starts
+    dev = device_of(local_rank)   # one GPU per rank (ranks share a GPU only in gloo rehearsals)
+    h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
+    dtr = DeviceTrace(tr, device=dev)   # resident in HBM before the clock starts
 
     def step():
         h.clear()
@@ -541,11 +542,11 @@ def main():
         }
         if not args.no_ingest:
             try:
-                result["ingest_sha256"] = ingest_leg(int(tr.E), args.steps, args.warmup, local_rank)
+                result["ingest_sha256"] = ingest_leg(int(tr.E), args.steps, args.warmup, dev)
             except Exception as e:  # reported, never fatal
                 result["ingest_sha256"] = {"error": str(e)}
             try:
-                result["ingest_p256_verify"] = p256_leg(1 << 20, args.steps, args.warmup, local_rank)
+                result["ingest_p256_verify"] = p256_leg(1 << 20, args.steps, args.warmup, dev)
             except Exception as e:  # reported, never fatal
                 result["ingest_p256_verify"] = {"error": str(e)}
         if G == 1 and not args.no_chunked:
@@ -560,7 +561,7 @@ def main():
             ts = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
             base, o = cpu_baseline(ts, n, desc)
             result["cpu_baseline"] = base
-            checks["prefix_parity"] = prefix_parity(ts, o, local_rank)
+            checks["prefix_parity"] = prefix_parity(ts, o, dev)
             log(f"[rank {rank}] prefix parity ({sample} events) bit-exact")
         print(json.dumps(result), flush=True)
     if red.dist is not None:
