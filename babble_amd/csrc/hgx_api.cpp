@@ -491,10 +491,6 @@ int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_rou
         set_err(err, HGX_ERR_INVALID, "hgx_reset: roots need a single-graph context");
         return HGX_ERR_INVALID;
     }
-    if (rooted && c->n > 256) {
-        set_err(err, HGX_ERR_INVALID, "hgx_reset: roots need n <= 256 (the per-candidate round step)");
-        return HGX_ERR_INVALID;
-    }
     if (c->eng.clear() != hipSuccess || c->eng.set_roots(rr, ye) != hipSuccess) return dev_err(err, hipErrorUnknown,
                                                                                                   "hgx_reset");
     c->root_index.assign(root_index, root_index + c->C);

@@ -557,7 +557,6 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
     kend(K_FD_BUILD, (double)(En - E0) * 2.0 * csz * n);
     if (rooted) {   // root floors of every position (after a Reset)
-        if (n > 256) return hipErrorNotSupported;   // only k_round_k applies them
         if (gfl.n < (size_t)Ppos) HGX_TRY(gfl.alloc((size_t)Ppos));
         const size_t need = (size_t)(root_gmax + 1) * C;
         if (gB.n < need) {

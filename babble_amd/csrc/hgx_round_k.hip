@@ -197,7 +197,7 @@ __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) {
 // CG waves of 64 candidates each; every candidate's row is split over H waves (coordinate
 // dwords [h*NDW/H, (h+1)*NDW/H)), whose partial counts meet in LDS once per search level, so
 // that two waves share each SIMD; GPB chain groups per block when a group is one wave.
-template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
+template <typename CT, int NDW, int CG, int H, int GPB, bool STG, int NCH>
 __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int s) {
     constexpr int P = kWinP;
     constexpr int GW = CG * H;           // waves of one chain group
@@ -212,10 +212,11 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     // vector-memory instructions a wave issues between the boundary load and the staging
     constexpr int GWD = fd8_gwd(HD);
     constexpr int NFD8 = HD / GWD;
-    constexpr int BPT = (256 + GL - 1) / GL;   // base coordinates per thread (n <= 256)
-    constexpr int NSMALL = 3 + 3 * BPT;
+    constexpr int BPT = (4 * NDW + GL - 1) / GL;   // base coordinates per thread (n <= 4 NDW)
+    constexpr int NSMALL = 2 + 3 * BPT;   // after the candidate rows: root floor, ovf, bases
     static_assert(GPB == 1 || GW == 1, "several chain groups per block only with one-wave groups");
     static_assert(NDW % (2 * H) == 0, "row split");
+    static_assert(NCH == 1 || (GPB == 1 && NCH <= 12), "candidate chunks: one chain group per block");
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ int s_B[GPB], s_tot[GPB];
@@ -250,30 +251,34 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     // window the previous step forwarded (both at fixed addresses), the flags and the bases.
     int b = ld_i32(A.Bm + (size_t)s * C + gc);
     int len = ld_i32(A.c_len + gc), off = ld_i32(A.c_off + gc);
-    const int j = cw * 64 + lane;        // this lane's candidate
-    const int jj = j < n ? j : 0;
-    uint32_t fd[HD];
-    {
-        const uint32_t* __restrict__ row = A.FD8 + fd8_at(par, C, n, NDW, GWD, g, jj, h * HD);
+    // candidates come in NCH chunks of 64 * CG (one chunk unless n > 256): lane (cw, lane) holds
+    // candidate ch * 64 * CG + jl of chunk ch, coordinate dwords [h * HD, (h + 1) * HD) of its row
+    const int jl = cw * 64 + lane;
+    auto load_chunk = [&](int ch, uint32_t (&dst)[HD], uint32_t& wf) {
+        const int jc = ch * 64 * CG + jl;
+        const int jcc = jc < n ? jc : 0;
+        const uint32_t* __restrict__ row = A.FD8 + fd8_at(par, C, n, NDW, GWD, g, jcc, h * HD);
         if constexpr (GWD == 4) {
 #pragma unroll
             for (int d = 0; d < HD; d += 4) {
                 const uint4 v = ld_u32x4(row + (size_t)(d / 4) * n * 4);
-                fd[d] = v.x; fd[d + 1] = v.y; fd[d + 2] = v.z; fd[d + 3] = v.w;
+                dst[d] = v.x; dst[d + 1] = v.y; dst[d + 2] = v.z; dst[d + 3] = v.w;
             }
         } else {
 #pragma unroll
             for (int d = 0; d < HD; d += 2) {
                 const uint2 v = ld_u32x2(row + (size_t)(d / 2) * n * 2);
-                fd[d] = v.x; fd[d + 1] = v.y;
+                dst[d] = v.x; dst[d + 1] = v.y;
             }
         }
-    }
+        wf = ld_u8(A.wflag + wrow + jcc);
+    };
+    uint32_t fd[HD], wfl;
+    load_chunk(0, fd, wfl);
     // root floor (after hgx_reset): offsets >= gk have round >= s+1 whatever they strongly see
     // (gB is a valid array without roots too: an unconditional load)
     const bool rootr = s + 1 <= A.gmax;
     int gkv = ld_i32(A.gB + (rootr ? (size_t)(s + 1) * C + gc : 0));
-    uint32_t wfl = ld_u8(A.wflag + wrow + jj);
     int ovf_s = ld_i32(A.ovf + s);
     int cbv[BPT], bmp[BPT], bmc[BPT];
     const size_t prow = s > 0 ? wrow - C : wrow;
@@ -285,7 +290,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         bmp[u] = ld_i32(A.Bm + prow + ii);
         bmc[u] = ld_i32(A.Bm + wrow + ii);
     }
-    wait_vm<NFD8 + NSMALL>();   // the boundary and the chain's extent have landed
+    wait_vm<NFD8 + 1 + NSMALL>();   // the boundary and the chain's extent have landed
     asm volatile("" : "+v"(b), "+v"(len), "+v"(off));
     b = __builtin_amdgcn_readfirstlane(b);
     len = __builtin_amdgcn_readfirstlane(len);
@@ -418,11 +423,11 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             return part;
         } else {
             int* pcb = pc + (it & 1) * (H * 64 * CG);
-            pcb[h * 64 * CG + j] = (int)part;
+            pcb[h * 64 * CG + jl] = (int)part;
             gsync();
             uint32_t t = 0;
 #pragma unroll
-            for (int q = 0; q < H; q++) t += (uint32_t)pcb[q * 64 * CG + j];
+            for (int q = 0; q < H; q++) t += (uint32_t)pcb[q * 64 * CG + jl];
             return t;
         }
     };
@@ -436,7 +441,6 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     for (int u = 0; u < BPT; u++) asm volatile("" : "+v"(cbv[u]), "+v"(bmp[u]), "+v"(bmc[u]));
     const int gk = rootr ? gkv : len;
     const bool exact = ovf_s != 0;   // a candidate row of this round did not fit 8 bits
-    const bool cand = j < n && wfl == 1;
 #pragma unroll
     for (int u = 0; u < BPT; u++) {
         const int i = gt + u * GL;
@@ -448,8 +452,12 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     if (gt < 32) hist[gt] = 0;
     RK_PROF(0);
 
-    int kstar = len, carried = 0, B = -1, K = P;
-    bool done = false;     // seen in an earlier window: seen at every later probe
+    int kstar = len, carried = 0, B = -1;
+    // per chunk (bit / 5-bit field ch): the lane's candidate exists, was seen in an earlier
+    // window (seen at every later probe), and its first seeing probe K in the current window
+    uint32_t cand_bits = 0, done_bits = 0;
+    uint64_t k_bits = 0;
+    uint32_t fdn[NCH > 1 ? HD : 1], wfln = 0;   // the next chunk's rows, in flight during a search
     for (int w_it = 0;; w_it++) {
         if (w_it > 0) stage_and_wait_rest(kbase, np);   // a later window (rare)
         __builtin_amdgcn_s_waitcnt(0);
@@ -458,50 +466,73 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         rebase_rows(kbase, 0, np, base, [&](int p, int d, uint32_t w) { win[p * WS + d] = w; });
         gsync();
         RK_PROF(2);
-        // first probe of the window that strongly sees this lane's candidate (np: none);
-        // probes past the window's end count as seeing (keeps the predicate monotone)
-        int lo = 0, hi = P;
-        if (!exact) {
-            uint32_t f[HD];
+#pragma unroll 1
+        for (int ch = 0; ch < NCH; ch++) {
+            if (ch * 64 * CG >= n) break;   // (block-uniform) no candidate in this chunk
+            if constexpr (NCH > 1) {
+                if (ch > 0 || w_it > 0) {
+                    if (ch == 0) load_chunk(0, fdn, wfln);   // a later window: the first chunk again
+                    __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-            for (int d = 0; d < HD; d++) f[d] = cand ? fd[d] : 0x7F7F7F7Fu;
-#pragma unroll
-            for (int it = 0; it < 5; it++) {
-                const int mid = (lo + hi) >> 1;
-                const uint32_t* row = win + mid * WS + h * HD;
-                uint32_t v[HD];
-                lds_read_row<HD>(row, v);
-                uint32_t c4[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int d = 0; d < HD; d++) c4[d & 3] += __builtin_popcount((v[d] - f[d]) & 0x80808080u);
-                uint32_t cnt = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-                cnt = combine(cnt, it);
-                const bool seen = done || mid >= np || ((int)cnt >= sm && !(j == cl && kbase + mid == b));
-                if (seen) hi = mid; else lo = mid + 1;
-            }
-        } else {
-            // exact int32 compares against the raw candidate row (rounds flagged by the producer)
-            const int i_lo = h * HD * 4, i_hi = min(n, (h + 1) * HD * 4);
-            for (int it = 0; it < 5; it++) {
-                const int mid = (lo + hi) >> 1;
-                uint32_t cnt = 0;
-                if (cand && !done && mid < np) {
-                    for (int i = i_lo; i < i_hi; i++) {
-                        const int32_t fdv = (sizeof(CT) == 2)
-                                                ? Coord<uint16_t>::fd(((const uint16_t*)A.WFD)[(wrow + jj) * n + i])
-                                                : A.WFD[(wrow + jj) * n + i];
-                        const int32_t lav = min(la_at(kbase, mid, i), kMaxI32 - 1);
-                        cnt += lav >= fdv ? 1u : 0u;
+                    for (int d = 0; d < HD; d++) {
+                        asm volatile("" : "+v"(fdn[d]));
+                        fd[d] = fdn[d];
                     }
+                    asm volatile("" : "+v"(wfln));
+                    wfl = wfln;
                 }
-                cnt = combine(cnt, it);
-                const bool seen = done || mid >= np || (cand && (int)cnt >= sm && !(j == cl && kbase + mid == b));
-                if (seen) hi = mid; else lo = mid + 1;
+                if (ch + 1 < NCH) load_chunk(ch + 1, fdn, wfln);
             }
+            const int jc = ch * 64 * CG + jl;
+            const bool cand = jc < n && wfl == 1;
+            if (cand) cand_bits |= 1u << ch;
+            const bool done = (done_bits >> ch) & 1u;
+            // first probe of the window that strongly sees this lane's candidate (np: none);
+            // probes past the window's end count as seeing (keeps the predicate monotone)
+            int lo = 0, hi = P;
+            if (!exact) {
+#pragma unroll
+                for (int d = 0; d < HD; d++) fd[d] = cand ? fd[d] : 0x7F7F7F7Fu;   // never seen
+#pragma unroll
+                for (int it = 0; it < 5; it++) {
+                    const int mid = (lo + hi) >> 1;
+                    const uint32_t* row = win + mid * WS + h * HD;
+                    uint32_t v[HD];
+                    lds_read_row<HD>(row, v);
+                    uint32_t c4[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int d = 0; d < HD; d++) c4[d & 3] += __builtin_popcount((v[d] - fd[d]) & 0x80808080u);
+                    uint32_t cnt = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+                    cnt = combine(cnt, it);
+                    const bool seen = done || mid >= np || ((int)cnt >= sm && !(jc == cl && kbase + mid == b));
+                    if (seen) hi = mid; else lo = mid + 1;
+                }
+            } else {
+                // exact int32 compares against the raw candidate row (rounds flagged by the producer)
+                const int i_lo = h * HD * 4, i_hi = min(n, (h + 1) * HD * 4);
+                const size_t jrow = (wrow + (jc < n ? jc : 0)) * n;
+                for (int it = 0; it < 5; it++) {
+                    const int mid = (lo + hi) >> 1;
+                    uint32_t cnt = 0;
+                    if (cand && !done && mid < np) {
+                        for (int i = i_lo; i < i_hi; i++) {
+                            const int32_t fdv = (sizeof(CT) == 2) ? Coord<uint16_t>::fd(((const uint16_t*)A.WFD)[jrow + i])
+                                                                  : A.WFD[jrow + i];
+                            const int32_t lav = min(la_at(kbase, mid, i), kMaxI32 - 1);
+                            cnt += lav >= fdv ? 1u : 0u;
+                        }
+                    }
+                    cnt = combine(cnt, it);
+                    const bool seen = done || mid >= np || (cand && (int)cnt >= sm && !(jc == cl && kbase + mid == b));
+                    if (seen) hi = mid; else lo = mid + 1;
+                }
+            }
+            const int K = lo;
+            k_bits = (k_bits & ~(31ull << (5 * ch))) | ((uint64_t)K << (5 * ch));
+            // earlier windows' candidates are in `carried`
+            if (h == 0 && K < np && cand && !done) atomicAdd(&hist[K], 1);
         }
-        K = lo;
         RK_PROF(3);
-        if (h == 0 && K < np && cand && !done) atomicAdd(&hist[K], 1);   // earlier windows are in `carried`
         gsync();
         if (wh == 0) {   // boundary: first probe where #{K <= p} (+ candidates seen earlier) >= SM
             const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
@@ -521,7 +552,9 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             break;
         }
         carried = s_tot[grp];
-        done = done || (cand && K < np);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ch++)
+            if (((cand_bits >> ch) & 1u) && (int)((k_bits >> (5 * ch)) & 31u) < np) done_bits |= 1u << ch;
         if (gt < 32) hist[gt] = 0;
         kbase += np;
         if (kbase >= len) {
@@ -545,9 +578,15 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
     if (kstar < len) {
         const int pk = kstar - kbase;   // inside the staged window
         // S row of the boundary event: the candidates it strongly sees (bit j of word j/64)
-        const uint64_t bits = __ballot(cand && K <= B);
         const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
-        if (h == 0 && lane == 0 && cw < A.nw) A.Smat[srow + cw] = bits;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ch++) {   // (seen in an earlier window: seen at B)
+            const bool sb = ((cand_bits >> ch) & 1u) &&
+                            (((done_bits >> ch) & 1u) || (int)((k_bits >> (5 * ch)) & 31u) <= B);
+            const uint64_t bits = __ballot(sb);
+            const int wd = ch * CG + cw;
+            if (h == 0 && lane == 0 && wd < A.nw) A.Smat[srow + wd] = bits;
+        }
         RK_PROF(6);
         // the new candidate's rows for round s+1
         const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
@@ -634,9 +673,9 @@ int round_k_ndw(int n) {
     return p;
 }
 
-template <typename CT, int NDW, int CG, int H, int GPB, bool STG>
+template <typename CT, int NDW, int CG, int H, int GPB, bool STG, int NCH>
 static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
-    const void* f = (const void*)k_round_k<CT, NDW, CG, H, GPB, STG>;
+    const void* f = (const void*)k_round_k<CT, NDW, CG, H, GPB, STG, NCH>;
     const RoundKLds L = round_k_lds<NDW, CG * H, sizeof(CT) == 2 ? 2 : 4>(STG);
     const size_t lds = (size_t)L.total * GPB;
     static bool attr = false;
@@ -646,15 +685,15 @@ static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
         attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
-    hipLaunchKernelGGL((k_round_k<CT, NDW, CG, H, GPB, STG>), dim3(grid), dim3(64 * CG * H * GPB), lds, st, A, s);
+    hipLaunchKernelGGL((k_round_k<CT, NDW, CG, H, GPB, STG, NCH>), dim3(grid), dim3(64 * CG * H * GPB), lds, st, A, s);
     return hipGetLastError();
 }
 
-template <typename CT, int NDW, int CG, int H, int GPB>
+template <typename CT, int NDW, int CG, int H, int GPB, int NCH = 1>
 static hipError_t round_k_launch(hipStream_t st, const RoundArgs& A, int s) {
     const RoundKLds L = round_k_lds<NDW, CG * H, sizeof(CT) == 2 ? 2 : 4>(true);
-    if ((size_t)L.total * GPB <= 140 * 1024) return round_k_launch_v<CT, NDW, CG, H, GPB, true>(st, A, s);
-    return round_k_launch_v<CT, NDW, CG, H, GPB, false>(st, A, s);
+    if ((size_t)L.total * GPB <= 140 * 1024) return round_k_launch_v<CT, NDW, CG, H, GPB, true, NCH>(st, A, s);
+    return round_k_launch_v<CT, NDW, CG, H, GPB, false, NCH>(st, A, s);
 }
 
 // a wave's share of a candidate row (dwords) in the configuration launch_round_k_t picks
@@ -667,6 +706,8 @@ static int round_k_hd(int n, int C) {
         case 16: return many ? 16 : 2;
         case 32: return 8;
         case 64: return 32;
+        case 128: return 32;
+        case 256: return 64;
         default: return 2;
     }
 }
@@ -683,7 +724,10 @@ static hipError_t launch_round_k_t(hipStream_t st, const RoundArgs& A, int s) {
         case 16: return many ? round_k_launch<CT, 16, 1, 1, 4>(st, A, s) : round_k_launch<CT, 16, 1, 8, 1>(st, A, s);
         case 32: return round_k_launch<CT, 32, 2, 4, 1>(st, A, s);
         case 64: return round_k_launch<CT, 64, 4, 2, 1>(st, A, s);
-        default: return hipErrorInvalidValue;   // n > 256: k_round_step_big
+        // n > 256: the candidates in chunks of 128 (4 / 8 chunks), rows split over 4 waves
+        case 128: return round_k_launch<CT, 128, 2, 4, 1, 4>(st, A, s);
+        case 256: return round_k_launch<CT, 256, 2, 4, 1, 8>(st, A, s);
+        default: return hipErrorInvalidValue;
     }
 }
 

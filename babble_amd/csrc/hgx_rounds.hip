@@ -749,7 +749,7 @@ static hipError_t launch_round_step_t(hipStream_t s, const RoundArgs& A, int kst
 }
 
 hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep, int block_search) {
-    if (!block_search && A.n <= 256) return launch_round_k(s, A, kstep);
+    if (!block_search && A.n <= 1024) return launch_round_k(s, A, kstep);
     return A.compact ? launch_round_step_t<uint16_t>(s, A, kstep) : launch_round_step_t<int32_t>(s, A, kstep);
 }
 

@@ -159,7 +159,7 @@ int32_t hgx_clear(hgx_ctx* ctx);
  * LastCommitedRoundEvents, ConsensusTransactions and the blocks, like the reference) and
  * install one Root per participant: Index, Round and whether Root.Y names an event (1) or is
  * "" (0). Inserted events then name Root.X as self-parent -1 and Root.Y / Root.Others as
- * HGX_ROOT_Y / HGX_ROOT_OTHER. Single-graph contexts with n <= 256. */
+ * HGX_ROOT_Y / HGX_ROOT_OTHER. Single-graph contexts. */
 int32_t hgx_reset(hgx_ctx* ctx, const int32_t* root_index, const int32_t* root_round, const int32_t* root_y_is_event,
                   hgx_error* err);
 /* Hashgraph.GetFrame: per participant root_x / root_y (gid; -1 = the current Root.X / ""; 
@@ -329,8 +329,9 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
  * to the fixed point (hgx_kernels.hip), m >= 2 = the dataflow pass with m time segments on
  * a rebuild (measurement). Same results. */
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
-/* DivideRounds round step for n <= 256: 0 = one lane per candidate, 8-bit rebased compares
- * (default, hgx_round_k.hip), 1 = block binary search (hgx_rounds.hip). Same results. */
+/* DivideRounds round step: 0 = one lane per candidate, 8-bit rebased compares (default,
+ * hgx_round_k.hip; candidates in chunks of 128 above n = 256), 1 = block binary search
+ * (hgx_rounds.hip; per-candidate search over streamed rows above n = 256). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds schedule: 1 = incremental (default: a call after more InsertEvents extends
  * lastAncestors/firstDescendants for the new events only and resumes the round steps at the

@@ -34,6 +34,7 @@ def _run_chunked(t, chunk, incremental=True, cap=None, graphs=1, stats=None):
     (64, 12000, 42, 333, 0, 0.25),     # stale other-parents
     (128, 20000, 45, 1000, 20, 0.0),   # silent peers (chains that never grow)
     (256, 40000, 43, 1000, 0, 0.0),    # C3's n, compact coordinates
+    (600, 30000, 47, 2000, 150, 0.2),  # n > 256: candidate chunks, silent and stale peers
     (16, 2000, 44, 1, 0, 0.1),         # one event per call
     (5, 900, 46, 17, 1, 0.3)])
 def test_chunked_matches_oracle(n, E, seed, chunk, silent, stale):

@@ -108,8 +108,8 @@ GOSSIP = [
     (16, 4000, 6, 0, 0.0), (16, 4000, 7, 5, 0.5), (32, 6000, 8, 0, 0.0), (64, 12000, 9, 0, 0.0),
     (64, 12000, 10, 21, 0.2), (100, 15000, 11, 0, 0.0), (128, 20000, 12, 0, 0.0), (2, 300, 13, 0, 0.0),
     (1, 64, 14, 0, 0.0), (200, 20000, 15, 60, 0.0), (256, 30000, 16, 0, 0.0),
-    # n > 256: the per-candidate round step (k_round_step_big)
-    (300, 24000, 17, 0, 0.0), (512, 24000, 18, 100, 0.2), (1024, 16000, 19, 300, 0.0)]
+    # n > 256: the per-candidate step with the candidates in chunks of 128
+    (300, 24000, 17, 0, 0.0), (512, 24000, 18, 100, 0.2), (1024, 16000, 19, 300, 0.0), (1000, 30000, 20, 330, 0.3)]
 
 
 @pytest.mark.parametrize("n,E,seed,silent,stale", GOSSIP)
@@ -119,9 +119,11 @@ def test_gossip_batch(n, E, seed, silent, stale):
 
 
 @pytest.mark.parametrize("n,E,seed,silent,stale", [(4, 1024, 1, 0, 0.0), (7, 1500, 5, 2, 0.4), (64, 12000, 10, 21, 0.2),
-                                                   (128, 20000, 12, 0, 0.0), (256, 30000, 16, 0, 0.0)])
+                                                   (128, 20000, 12, 0, 0.0), (256, 30000, 16, 0, 0.0),
+                                                   (300, 24000, 17, 0, 0.0), (1024, 16000, 19, 300, 0.0)])
 def test_gossip_block_search_round_kernel(n, E, seed, silent, stale):
-    """The block binary-search round step (hgx_set_round_kernel(ctx, 1)) against the oracle."""
+    """The block binary-search round step (hgx_set_round_kernel(ctx, 1); k_round_step_big
+    above n = 256) against the oracle."""
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
     compare(run_gpu(t, round_kernel="block"), hgref.oracle_run(t), t, hashes=False)
 

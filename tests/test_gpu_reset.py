@@ -70,7 +70,7 @@ def test_reset_errors():
 
 
 @pytest.mark.parametrize("n,E,seed,chunks", [(4, 1500, 71, 3), (16, 6000, 72, 4), (64, 20000, 73, 2),
-                                             (256, 40000, 74, 2)])
+                                             (256, 40000, 74, 2), (512, 40000, 75, 2)])
 def test_gossip_fast_forward_from_frame(n, E, seed, chunks):
     t = gtrace.gossip(n, E, seed)
     K = E // 2
