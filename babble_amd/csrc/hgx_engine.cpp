@@ -648,8 +648,15 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 sgr.compact = compact;
                 sgr.nb = nb;
                 HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                for (int k = 0; k < nb; k++) (void)launch_round_step(stream, sgr.args, k, kern);
-                HGX_TRY(hipStreamEndCapture(stream, &sgr.graph));
+                hipError_t le = hipSuccess;   // a failed launch ends the capture, then is reported
+                for (int k = 0; k < nb && le == hipSuccess; k++) le = launch_round_step(stream, sgr.args, k, kern);
+                const hipError_t ce = hipStreamEndCapture(stream, &sgr.graph);
+                if (le != hipSuccess) {
+                    if (ce == hipSuccess && sgr.graph) (void)hipGraphDestroy(sgr.graph);
+                    sgr.graph = nullptr;
+                    return le;
+                }
+                HGX_TRY(ce);
                 HGX_TRY(hipGraphInstantiate(&sgr.exec, sgr.graph, nullptr, nullptr, 0));
                 // the step nodes in launch order (a linear chain)
                 size_t nn = 0;

@@ -377,18 +377,38 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
         constexpr int NP = (P + RS - 1) / RS;              // passes (fixed trip count)
         for (int d = gt % NDW; d < NDW; d += GL) {
             const int i0 = 4 * d;
-            if constexpr (STG && sizeof(CT) == 2) {
-                // packed: LA' = min(sat(raw - base), 126) on coordinate pairs (raw = LA + 1)
+            if constexpr (sizeof(CT) == 2) {
+                // packed: LA' = min(sat(raw - base), 126) on coordinate pairs (raw = LA + 1); the raw
+                // rows from LDS (staged) or straight from HBM (big n: the rows do not fit in LDS)
                 u16x2 b01 = {0, 0}, b23 = {0, 0};
                 if (i0 < n) b01 = u16x2{(unsigned short)bs[i0], (unsigned short)bs[i0 + 1]};
                 if (i0 + 2 < n) b23 = u16x2{(unsigned short)bs[i0 + 2], (unsigned short)bs[i0 + 3]};
                 const u16x2 cap = {126, 126};
+                uint32_t g01[STG ? 1 : NP], g23[STG ? 1 : NP];
+                if constexpr (!STG) {   // every pass's HBM loads in flight before the first is used
+                    const int ic = i0 < n ? i0 : 0;
+#pragma unroll
+                    for (int u = 0; u < NP; u++) {
+                        const int p = min(gt / NDW + u * RS, np - 1);   // (n even: dword-aligned pairs)
+                        const uint32_t* rp =
+                            (const uint32_t*)((const CT*)A.LA + (size_t)(off + kbase + p0 + p) * n + ic);
+                        g01[u] = rp[0];
+                        g23[u] = rp[i0 + 2 < n ? 1 : 0];
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < NP; u++) {
                     const int p = gt / NDW + u * RS;
                     if (p < np) {
-                        const uint32_t* rp = (const uint32_t*)(raw + (p0 + p) * n + i0);
-                        const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
+                        uint32_t r01 = 0u, r23 = 0u;
+                        if constexpr (STG) {
+                            const uint32_t* rp = (const uint32_t*)(raw + (p0 + p) * n + i0);
+                            r01 = i0 < n ? rp[0] : 0u;
+                            r23 = i0 + 2 < n ? rp[1] : 0u;
+                        } else if (i0 < n) {
+                            r01 = g01[u];
+                            r23 = i0 + 2 < n ? g23[u] : 0u;
+                        }
                         const u16x2 y01 = __builtin_elementwise_min(
                             __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
                         const u16x2 y23 = __builtin_elementwise_min(
@@ -490,6 +510,8 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
             // first probe of the window that strongly sees this lane's candidate (np: none);
             // probes past the window's end count as seeing (keeps the predicate monotone)
             int lo = 0, hi = P;
+            // a wave whose 64 candidates are all absent (silent chains) only keeps the barriers
+            const bool wave_cand = __ballot(cand) != 0;
             if (!exact) {
 #pragma unroll
                 for (int d = 0; d < HD; d++) fd[d] = cand ? fd[d] : 0x7F7F7F7Fu;   // never seen
@@ -497,11 +519,19 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
                 for (int it = 0; it < 5; it++) {
                     const int mid = (lo + hi) >> 1;
                     const uint32_t* row = win + mid * WS + h * HD;
-                    uint32_t v[HD];
-                    lds_read_row<HD>(row, v);
                     uint32_t c4[4] = {0, 0, 0, 0};
+                    if (wave_cand) {
+                    // big n (several chunks, the next chunk's rows in flight): the row in two halves,
+                    // fewer live registers (one block of 16 waves per CU)
+                    constexpr int RH = (NCH > 1 && HD >= 32) ? HD / 2 : HD;
 #pragma unroll
-                    for (int d = 0; d < HD; d++) c4[d & 3] += __builtin_popcount((v[d] - fd[d]) & 0x80808080u);
+                    for (int r0 = 0; r0 < HD; r0 += RH) {
+                        uint32_t v[RH];
+                        lds_read_row<RH>(row + r0, v);
+#pragma unroll
+                        for (int d = 0; d < RH; d++) c4[d & 3] += __builtin_popcount((v[d] - fd[r0 + d]) & 0x80808080u);
+                    }
+                    }
                     uint32_t cnt = (c4[0] + c4[1]) + (c4[2] + c4[3]);
                     cnt = combine(cnt, it);
                     const bool seen = done || mid >= np || ((int)cnt >= sm && !(jc == cl && kbase + mid == b));
@@ -599,12 +629,15 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
                 return ((const CT*)A.FDT)[(size_t)i * A.Pcap + off + kstar];
             }
         };
+        int32_t* fdrow = (int32_t*)win;   // not staged: the row's gathered values, read twice below
         for (int i = gt; i < n; i += GL) {
             A.WLA[nrow + i] = la_at(kbase, pk, i);
             const CT f = fd_raw(i);
+            if constexpr (!STG) fdrow[i] = (int32_t)f;
             if constexpr (sizeof(CT) == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
             else A.WFD[nrow + i] = f;
         }
+        if constexpr (!STG) gsync();
         // rebased FD row (base(s+1) = Index of this round's candidates) for the next step
         uint32_t* nfd = A.FD8;
         bool of = false;
@@ -615,7 +648,7 @@ __global__ void __launch_bounds__(64 * CG * H * GPB) k_round_k(RoundArgs A, int 
                 const int i = 4 * d + q;
                 uint32_t v = 127u;
                 if (i < n) {
-                    const int32_t f = Coord<CT>::fd(fd_raw(i));
+                    const int32_t f = Coord<CT>::fd(STG ? fd_raw(i) : (CT)fdrow[i]);
                     if (f != kMaxI32) {
                         const int32_t x = f - bm1[i] + 1;
                         if (x > 126) of = true;
@@ -680,7 +713,7 @@ static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
     const size_t lds = (size_t)L.total * GPB;
     static bool attr = false;
     if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
@@ -707,7 +740,7 @@ static int round_k_hd(int n, int C) {
         case 32: return 8;
         case 64: return 32;
         case 128: return 32;
-        case 256: return 64;
+        case 256: return 32;
         default: return 2;
     }
 }
@@ -724,9 +757,9 @@ static hipError_t launch_round_k_t(hipStream_t st, const RoundArgs& A, int s) {
         case 16: return many ? round_k_launch<CT, 16, 1, 1, 4>(st, A, s) : round_k_launch<CT, 16, 1, 8, 1>(st, A, s);
         case 32: return round_k_launch<CT, 32, 2, 4, 1>(st, A, s);
         case 64: return round_k_launch<CT, 64, 4, 2, 1>(st, A, s);
-        // n > 256: the candidates in chunks of 128 (4 / 8 chunks), rows split over 4 waves
+        // n > 256: the candidates in chunks of 128 (4 / 8 chunks), rows split over 4 / 8 waves
         case 128: return round_k_launch<CT, 128, 2, 4, 1, 4>(st, A, s);
-        case 256: return round_k_launch<CT, 256, 2, 4, 1, 8>(st, A, s);
+        case 256: return round_k_launch<CT, 256, 2, 8, 1, 8>(st, A, s);
         default: return hipErrorInvalidValue;
     }
 }
