@@ -476,7 +476,22 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // lastAncestors: fixed point from all -1 (new rows), dirty-tracked sweeps (k_la_sweep)
     const size_t nunits = (size_t)((max_len + seg - 1) / seg) * C;
     int64_t u0 = 0;
-    la_wave_used = la_kernel == 0 && la_wave_ok(n, max_len);
+    // above 896 chains a workgroup cannot give every chain a lane: one graph gets lanes for
+    // the chains that have events only (silent peers have none)
+    int la_na = n;
+    const int32_t* la_map = nullptr;
+    if (n > 896 && G == 1) {
+        h_lmap.clear();
+        for (int c = 0; c < C; c++)
+            if (chain_len[c] > 0) h_lmap.push_back(c);
+        la_na = (int)h_lmap.size();
+        if (la_na <= 896) {
+            if (la_lmap.n < (size_t)std::max(1, la_na)) HGX_TRY(la_lmap.alloc((size_t)n));
+            HGX_TRY(hipMemcpyAsync(la_lmap.p, h_lmap.data(), (size_t)la_na * 4, hipMemcpyHostToDevice, stream));
+            la_map = la_lmap.p;
+        }
+    }
+    la_wave_used = la_kernel == 0 && la_wave_ok(n, max_len, la_na) && (n <= 896 || la_map);
     // a rebuild of one large graph runs the wavefront on time segments in parallel (their
     // rows are lower bounds), then a verify sweep and the dirty sweeps complete them
     la_wave_segs = 1;
@@ -542,8 +557,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // one dataflow pass (k_la_wave); its error flag is read with the phase clock below
         HGX_TRY(hipMemsetAsync(counters.p + 6, 0, 4, stream));
         kbeg(K_LA_SWEEP);
-        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6));
-        if (la_wave_segs > 1) HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6));
+        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na));
+        if (la_wave_segs > 1)
+            HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6, la_map, la_na));
         const double rows = (double)(En - E0);
         kend(K_LA_SWEEP, rows * (3.0 * csz * n + 16));
         HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));

@@ -216,6 +216,8 @@ class Engine {
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<uint32_t> FD8;   // [2][C][ndw] rebased candidate rows (k_round_k)
+    DBuf<int32_t> la_lmap;          // k_la_wave lanes -> chains with events (one graph, n > 896)
+    std::vector<int32_t> h_lmap;
     DBuf<int32_t> ovf;    // [r_cap + 2]
     DBuf<int8_t> fame;
     // order

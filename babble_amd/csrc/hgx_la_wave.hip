@@ -163,7 +163,8 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
                                                   const int32_t* __restrict__ c_base,
                                                   const int32_t* __restrict__ c_old,
                                                   const int32_t* __restrict__ p_gid, int64_t E, int nts, int head,
-                                                  int n, int lgnp, int nwd, int nblk, int32_t* __restrict__ err) {
+                                                  int n, int lgnp, int nwd, int nblk, int32_t* __restrict__ err,
+                                                  const int32_t* __restrict__ lmap, int na) {
     typedef LaW<CT> W;
     extern __shared__ uint32_t smem[];
     // slot-major arrays with a power-of-two chain stride NP = 2^lgnp >= n (index = shifts)
@@ -199,7 +200,10 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
     }
     if (tid == 0) *s_abort = 0;
     __syncthreads();
-    const int ncw = (n + 63) & ~63;   // compute lanes (whole waves); the last NLW waves load
+    // compute lanes (whole waves): one per chain, or per chain with events (lmap); the last NLW
+    // waves load (they walk every chain: those without events have nothing to load)
+    const int nl = lmap ? na : n;
+    const int ncw = (nl + 63) & ~63;
     if (tid >= ncw) {
         // ---- loader wave: op descriptors of rows [lqv, lqv + CH) of each owned chain -> q
         // (its per-chain state lives in LDS: lqv is written by this wave only)
@@ -251,9 +255,9 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
         }
         return;
     }
-    // ---- compute lane i: chain c0 + i, rows [s_old[i], len)
-    const int i = tid;
-    if (i >= n) return;
+    // ---- compute lane: chain c0 + i, rows [s_old[i], len)
+    if (tid >= nl) return;
+    const int i = lmap ? lmap[tid] : tid;
     const int len = s_len[i];
     const int off = s_off[i];
     int own0 = c_base[c0 + i];   // Index of the chain's row 0
@@ -349,7 +353,7 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
 namespace {
 template <typename CT, int DW, int R, int Q, int NLW, int J, int CH, int MODE>
 hipError_t la_wave_launch1(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                           int head, int32_t* err) {
+                           int head, int32_t* err, const int32_t* lmap, int na) {
     const int nwd = a.compact ? n / 2 : n;
     const int nblk = nwd / DW;
     int lgnp = 0;
@@ -363,16 +367,17 @@ hipError_t la_wave_launch1(hipStream_t s, const DevArrays& a, int G, int n, cons
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const int threads = ((n + 63) & ~63) + 64 * NLW;
+    const int threads = (((lmap ? na : n) + 63) & ~63) + 64 * NLW;
+    if (threads > 1024 || (lmap && G != 1)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3(G * nts * nblk), dim3(threads), words * 4, s, (uint32_t*)a.LA, a.p_opk, a.c_off,
-                       a.c_len, a.c_base, c_old, a.p_gid, E, nts, head, n, lgnp, nwd, nblk, err);
+                       a.c_len, a.c_base, c_old, a.p_gid, E, nts, head, n, lgnp, nwd, nblk, err, lmap, na);
     return hipGetLastError();
 }
 template <typename CT, int DW, int R, int Q, int NLW, int J, int CH>
 hipError_t la_wave_launch(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E,
-                          int32_t* err) {
-    if (c_old) return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 1>(s, a, G, n, c_old, E, 1, 0, err);
-    return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 0>(s, a, G, n, nullptr, E, 1, 0, err);
+                          int32_t* err, const int32_t* lmap, int na) {
+    if (c_old) return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 1>(s, a, G, n, c_old, E, 1, 0, err, lmap, na);
+    return la_wave_launch1<CT, DW, R, Q, NLW, J, CH, 0>(s, a, G, n, nullptr, E, 1, 0, err, lmap, na);
 }
 // block width and ring sizes of the time-segment passes: one workgroup per CU (the passes
 // are issue-bound, so wider blocks share the per-row overhead over more coordinates)
@@ -387,13 +392,14 @@ inline SegCfg seg_cfg(int n, int nwd) {
 // LDS: NP * (R * DW + R + Q) + 5 n words <= 160 KB (NP = n rounded up to a power of two); DW divides the row's words
 template <typename CT>
 hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                            int head, int32_t* err) {
+                            int head, int32_t* err, const int32_t* lmap, int na) {
     const int nwd = a.compact ? n / 2 : n;
     if (nts > 1) {   // time segments: wider blocks, smaller rings (seg_cfg)
         const SegCfg g = seg_cfg(n, nwd);
 #define SEG(DW_, R_, Q_, NLW_, J_, CH_)                                                                                \
-    return head > 0 ? la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 3>(s, a, G, n, nullptr, E, nts, head, err)      \
-                    : la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 2>(s, a, G, n, nullptr, E, nts, 0, err)
+    return head > 0 ? la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 3>(s, a, G, n, nullptr, E, nts, head, err, lmap, \
+                                                                          na)                                          \
+                    : la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 2>(s, a, G, n, nullptr, E, nts, 0, err, lmap, na)
         if (n <= 256) {
             if (g.dw == 8) SEG(8, 8, 32, 1, 4, 8);
             if (g.dw == 4) SEG(4, 8, 32, 1, 4, 8);
@@ -408,15 +414,18 @@ hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, con
 #undef SEG
     }
     if (n <= 128) {
-        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err);
-        return la_wave_launch<CT, 1, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err);
+        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err, lmap, na);
+        return la_wave_launch<CT, 1, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err, lmap, na);
     }
     if (n <= 256) {
-        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err);
-        return la_wave_launch<CT, 1, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err);
+        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err, lmap, na);
+        return la_wave_launch<CT, 1, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err, lmap, na);
     }
-    if (n <= 512) return la_wave_launch<CT, 1, 16, 32, 1, 8, 8>(s, a, G, n, c_old, E, err);
-    return la_wave_launch<CT, 1, 8, 16, 2, 8, 4>(s, a, G, n, c_old, E, err);
+    if (n <= 512) return la_wave_launch<CT, 1, 16, 32, 1, 8, 8>(s, a, G, n, c_old, E, err, lmap, na);
+    // n > 512: 8-byte blocks and an 8-row ring (one workgroup per CU: half the workgroups of
+    // 4-byte blocks, which ran in two generations)
+    if (nwd % 2 == 0) return la_wave_launch<CT, 2, 8, 8, 2, 8, 2>(s, a, G, n, c_old, E, err, lmap, na);
+    return la_wave_launch<CT, 1, 8, 16, 2, 8, 4>(s, a, G, n, c_old, E, err, lmap, na);
 }
 }  // namespace
 
@@ -437,13 +446,15 @@ int la_wave_segments(int n, int compact, int num_cus, int max_segs) {
 }
 
 // one workgroup holds every chain of a graph plus the loader waves (<= 1024 threads)
-bool la_wave_ok(int n, int max_len) { return n >= 1 && n <= 896 && max_len < (1 << kOpkBits); }
+bool la_wave_ok(int n, int max_len, int n_active) {
+    return n >= 1 && n <= 1024 && n_active <= 896 && max_len < (1 << kOpkBits);
+}
 
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                          int head, int32_t* err) {
+                          int head, int32_t* err, const int32_t* lmap, int na) {
     if (nts > 1 && (G != 1 || c_old)) return hipErrorInvalidValue;
-    return a.compact ? la_wave_dispatch<uint16_t>(s, a, G, n, c_old, E, nts, head, err)
-                     : la_wave_dispatch<int32_t>(s, a, G, n, c_old, E, nts, head, err);
+    return a.compact ? la_wave_dispatch<uint16_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na)
+                     : la_wave_dispatch<int32_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na);
 }
 
 }  // namespace hgx

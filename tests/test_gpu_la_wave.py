@@ -1,7 +1,8 @@
 """The dataflow lastAncestors pass (k_la_wave, hgx_la_wave.hip) against the Gauss-Seidel
 sweeps (k_la_sweep) and the oracle: identical coordinates on sampled events and identical
 consensus on the whole DAG, for both coordinate storages, batched graphs, odd n, n > 256
-(4-byte column blocks) and incremental calls (rows of earlier calls read from HBM)."""
+(4-byte column blocks), n > 896 (lanes for the chains with events only) and incremental calls
+(rows of earlier calls read from HBM)."""
 import numpy as np
 import pytest
 
@@ -44,7 +45,9 @@ def _same_results(h1, h2, graph=0):
 
 CASES = [(4, 1024, 1, 0, 0.0), (5, 800, 4, 1, 0.0), (16, 4000, 7, 5, 0.5), (64, 12000, 10, 21, 0.2),
          (100, 15000, 11, 0, 0.0), (256, 30000, 16, 0, 0.0), (300, 24000, 17, 0, 0.0), (512, 24000, 18, 100, 0.2),
-         (896, 14000, 20, 0, 0.0)]
+         (896, 14000, 20, 0, 0.0),
+         # n > 896: lanes only for the chains with events (silent peers have none)
+         (1024, 16000, 19, 300, 0.0), (1000, 20000, 22, 330, 0.3)]
 
 
 @pytest.mark.parametrize("n,E,seed,silent,stale", CASES)
@@ -76,11 +79,11 @@ def test_wave_int32_coordinates(n, E, seed):
 
 
 @pytest.mark.parametrize("n,E,seed,chunk", [(4, 1024, 21, 64), (5, 700, 23, 13), (16, 4000, 24, 333),
-                                            (64, 12000, 25, 1000), (256, 30000, 26, 2500)])
+                                            (64, 12000, 25, 1000), (256, 30000, 26, 2500), (1024, 20000, 27, 4000)])
 def test_wave_incremental_calls(n, E, seed, chunk):
     """Chunked RunConsensus: every call's pass starts at the chains' first new rows and reads
     the op rows of earlier calls from HBM."""
-    t = gtrace.gossip(n, E, seed, stale_prob=0.3, stale_depth=4)
+    t = gtrace.gossip(n, E, seed, stale_prob=0.3, stale_depth=4, n_silent=300 if n > 896 else 0)
     hw = _run(t, "wave", chunk=chunk)
     pt = hw.phase_times()
     assert pt["la_wave"] == 1 and pt["la_wave_fallbacks"] == 0 and pt["rebuild"] == 0, pt
