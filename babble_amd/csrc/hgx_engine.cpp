@@ -613,10 +613,14 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     HGX_TRY(hipEventRecord(ph0, stream));
     HGX_TRY(ensure_round_cap(r_lo + 2 * kStepBatch + 2));
     a = arrays();
-    HGX_TRY(hipMemsetAsync(lr.p, 0xFF, (size_t)G * 4, stream));
-    if (r_lo == 0) HGX_TRY(hipMemsetAsync(Bm.p, 0, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(active.p + r_lo, 0, (size_t)(r_cap + 1 - r_lo) * 4, stream));
-    HGX_TRY(hipMemsetAsync(ovf.p + r_lo, 0, (size_t)(r_cap + 2 - r_lo) * 4, stream));
+    {   // one launch for the round tables' resets
+        FillRange fr[4] = {{lr.p, (uint32_t)((size_t)G * 4), 0xFF},
+                           {active.p + r_lo, (uint32_t)((size_t)(r_cap + 1 - r_lo) * 4), 0},
+                           {ovf.p + r_lo, (uint32_t)((size_t)(r_cap + 2 - r_lo) * 4), 0},
+                           {Bm.p, (uint32_t)((size_t)C * 4), 0}};
+        launch_fill_many(stream, fr, r_lo == 0 ? 4 : 3);
+        HGX_TRY(hipGetLastError());
+    }
     {
         const size_t need = (size_t)2 * C * round_k_ndw(n);
         if (FD8.n < need) {
@@ -737,10 +741,19 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_batch());
         }
     }
-    launch_last_round(stream, r_lo + launched * nb, G, C, n, wstat.p, lr.p);
+    // rounds below r_lo are unchanged and every round up to a graph's last one has witnesses,
+    // so only [r_lo, R) is scanned: last = max(that, min(previous last, r_lo - 1))
+    const int r_scan = rebuild ? 0 : r_lo;
+    const std::vector<int32_t> prev_last = out.last_round;
+    launch_last_round(stream, r_scan, r_lo + launched * nb, G, C, n, wstat.p, lr.p);
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));
+    if (r_scan > 0)
+        for (int g = 0; g < G; g++) {
+            const int32_t pl = g < (int)prev_last.size() ? prev_last[g] : -1;
+            out.last_round[g] = std::max(out.last_round[g], std::min(pl, r_scan - 1));
+        }
     int32_t mx = -1;
     for (int g = 0; g < G; g++) mx = std::max(mx, out.last_round[g]);
     R = mx + 1;
@@ -832,8 +845,11 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     launch_wla_transpose(stream, a, r0, R, G, C, n);
     launch_threshold(stream, a, r0, R, C, n);
     kend(K_THRESHOLD, 0);
-    HGX_TRY(hipMemsetAsync(counters.p, 0, 8, stream));
-    HGX_TRY(hipMemsetAsync(rcnt.p, 0, (size_t)C * 4, stream));
+    {
+        FillRange fr[2] = {{counters.p, 8, 0}, {rcnt.p, (uint32_t)((size_t)C * 4), 0}};
+        launch_fill_many(stream, fr, 2);
+        HGX_TRY(hipGetLastError());
+    }
     kbeg(K_ROUND_RECEIVED);
     launch_round_received(stream, a, R, C, n, max_unrecv);
     kend(K_ROUND_RECEIVED, 0);
@@ -919,10 +935,14 @@ hipError_t Engine::find_order_end(OrderHost& out) {
                          (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
                                                     : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
     }
-    HGX_TRY(hipMemsetAsync(blk_cnt.p, 0, (size_t)G * R * 4, stream));
-    HGX_TRY(hipMemsetAsync(blk_loaded.p, 0, (size_t)G * R * 4, stream));
-    HGX_TRY(hipMemsetAsync(blk_ntx.p, 0, (size_t)G * R * 8, stream));
-    HGX_TRY(hipMemsetAsync(blk_nil.p, 0, (size_t)G * R, stream));
+    {   // one launch for the per-(graph, rr) block tables
+        FillRange fr[4] = {{blk_cnt.p, (uint32_t)((size_t)G * R * 4), 0},
+                           {blk_loaded.p, (uint32_t)((size_t)G * R * 4), 0},
+                           {blk_ntx.p, (uint32_t)((size_t)G * R * 8), 0},
+                           {blk_nil.p, (uint32_t)((size_t)G * R), 0}};
+        launch_fill_many(stream, fr, 4);
+        HGX_TRY(hipGetLastError());
+    }
     launch_finish_order(stream, a, m, vals, R, n);
     launch_fu_advance(stream, a, C);
     for (int c = 0; c < C; c++) h_fu[c] += fo_cnt[c];

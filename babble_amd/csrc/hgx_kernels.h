@@ -107,6 +107,15 @@ struct RoundArgs {
     int32_t* hflag;
 };
 
+// several small device ranges set to a byte value in one launch (instead of one memset each)
+struct FillRange {
+    void* p;          // 4-byte aligned
+    uint32_t bytes;
+    uint8_t value;
+};
+constexpr int kFillMax = 8;
+void launch_fill_many(hipStream_t s, const FillRange* r, int count);
+
 int fd_tile_rows(int n, int compact);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows),
 // p_opk = packed op chain and row (gids [E0, E))
@@ -154,7 +163,7 @@ void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_ro
                        int gmax, int C, int n, int max_len);
 void launch_round_first_gid(hipStream_t s, const DevArrays& a, int r0, int R, int C, int32_t* first);
 // lr[g] = max round with a witness in graph g over the first R round steps (lr preset to -1)
-void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
+void launch_last_round(hipStream_t s, int rs, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();     // -DHGX_STEP_PROF builds only
 void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA

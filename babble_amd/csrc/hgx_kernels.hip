@@ -1557,6 +1557,32 @@ __global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* _
 
 static inline unsigned nblk(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
 
+struct FillArgs {
+    FillRange r[kFillMax];
+    int count;
+};
+__global__ void __launch_bounds__(256) k_fill_many(FillArgs f) {
+    const FillRange r = f.r[blockIdx.y];
+    const uint32_t v4 = 0x01010101u * r.value;
+    uint32_t* p = (uint32_t*)r.p;
+    const uint32_t nw = r.bytes / 4;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nw; t += gridDim.x * blockDim.x) p[t] = v4;
+    if (blockIdx.x == 0 && threadIdx.x < (r.bytes & 3u)) ((uint8_t*)r.p)[nw * 4 + threadIdx.x] = r.value;
+}
+
+void launch_fill_many(hipStream_t s, const FillRange* r, int count) {
+    if (count <= 0) return;
+    FillArgs f{};
+    uint32_t mx = 0;
+    for (int i = 0; i < count && i < kFillMax; i++) {
+        f.r[i] = r[i];
+        mx = std::max(mx, r[i].bytes);
+    }
+    f.count = std::min(count, kFillMax);
+    const unsigned bx = std::max(1u, std::min(256u, (mx / 4 + 255) / 256));
+    hipLaunchKernelGGL(k_fill_many, dim3(bx, f.count), dim3(256), 0, s, f);
+}
+
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
     if (E <= E0) return;
     hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_op, a.g_ts,

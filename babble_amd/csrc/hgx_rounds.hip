@@ -755,13 +755,13 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int kstep, int b
 
 
 
-// lastRound per graph after the round steps: the largest r < R with a witness
-// (wstat 2) in any chain of graph g. Grid (G, ceil(R / 64)).
-__global__ void __launch_bounds__(256) k_last_round(int R, int C, int n, const uint8_t* __restrict__ wstat,
+// lastRound per graph after the round steps: the largest r in [rs, R) with a witness
+// (wstat 2) in any chain of graph g. Grid (G, ceil((R - rs) / 64)).
+__global__ void __launch_bounds__(256) k_last_round(int rs, int R, int C, int n, const uint8_t* __restrict__ wstat,
                                                     int32_t* __restrict__ lr) {
     __shared__ int32_t s_max[4];
     const int g = blockIdx.x;
-    const int r0 = blockIdx.y * 64;
+    const int r0 = rs + blockIdx.y * 64;
     int m = -1;
     for (int t = threadIdx.x; t < 64 * n; t += blockDim.x) {
         const int r = r0 + t / n, i = t % n;
@@ -776,9 +776,9 @@ __global__ void __launch_bounds__(256) k_last_round(int R, int C, int n, const u
     }
 }
 
-void launch_last_round(hipStream_t s, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr) {
-    if (R <= 0) return;
-    hipLaunchKernelGGL(k_last_round, dim3(G, (R + 63) / 64), dim3(256), 0, s, R, C, n, wstat, lr);
+void launch_last_round(hipStream_t s, int rs, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr) {
+    if (R <= rs) return;
+    hipLaunchKernelGGL(k_last_round, dim3(G, (R - rs + 63) / 64), dim3(256), 0, s, rs, R, C, n, wstat, lr);
 }
 
 
