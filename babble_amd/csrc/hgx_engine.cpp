@@ -41,9 +41,10 @@ hipError_t DBuf<T>::grow_copy(size_t count, size_t keep, hipStream_t s) {
 
 template <typename T>
 void DBuf<T>::release() {
-    if (p) (void)hipFree(p);
+    if (p && own) (void)hipFree(p);
     p = nullptr;
     n = 0;
+    own = true;
 }
 
 template struct DBuf<int32_t>;
@@ -66,6 +67,8 @@ Engine::~Engine() {
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
     if (h_small) (void)hipHostFree(h_small);
+    if (h_ins) (void)hipHostFree(h_ins);
+    if (h_cpar) (void)hipHostFree(h_cpar);
     if (h_flag) (void)hipHostFree(h_flag);
     for (auto e : flag_ev)
         if (e) (void)hipEventDestroy(e);
@@ -116,16 +119,25 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(g_txnil.alloc(P));
     // insert state: no claims, no events per creator
     HGX_TRY(succ.alloc(P)); HGX_TRY(first_none.alloc(C));
-    HGX_TRY(last_gid_d.alloc(C)); HGX_TRY(last_index_d.alloc(C)); HGX_TRY(chain_base_d.alloc(C));
-    HGX_TRY(ins_fail.alloc(1)); HGX_TRY(graph_loaded_d.alloc(G));
+    ins_gl_off = ((size_t)3 * C + 1) & ~(size_t)1;
+    HGX_TRY(ins_blk.alloc(ins_gl_off + (size_t)2 * G));
+    last_gid_d.view(ins_blk.p, C);
+    last_index_d.view(ins_blk.p + C, C);
+    chain_base_d.view(ins_blk.p + 2 * C, C);
+    graph_loaded_d.view((unsigned long long*)(ins_blk.p + ins_gl_off), G);
+    HGX_TRY(ins_fail.alloc(1));
+    HGX_TRY(hipHostMalloc((void**)&h_ins, ins_blk.n * sizeof(int32_t), hipHostMallocDefault));
+    HGX_TRY(cpar_blk.alloc((size_t)3 * C));
+    HGX_TRY(hipHostMalloc((void**)&h_cpar, (size_t)3 * C * sizeof(int32_t), hipHostMallocDefault));
     HGX_TRY(hipMemsetAsync(succ.p, 0xFF, P * 4, stream));
     HGX_TRY(hipMemsetAsync(first_none.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(last_index_d.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
-    HGX_TRY(c_off.alloc(C + 1)); HGX_TRY(c_len.alloc(C)); HGX_TRY(c_base.alloc(C));
-    HGX_TRY(c_old.alloc(C)); HGX_TRY(fu.alloc(C)); HGX_TRY(rcnt.alloc(C));
+    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 8, stream));   // last_gid, last_index
+    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (ins_blk.n - (size_t)2 * C) * 4, stream));   // chain_base, graph_loaded
+    HGX_TRY(c_off.alloc(C + 1));
+    c_len.view(cpar_blk.p, C);
+    c_base.view(cpar_blk.p + C, C);
+    c_old.view(cpar_blk.p + 2 * C, C);
+    HGX_TRY(fu.alloc(C)); HGX_TRY(rcnt.alloc(C));
     HGX_TRY(root_round_d.alloc(C)); HGX_TRY(root_y_ext_d.alloc(C));
     HGX_TRY(hipMemsetAsync(root_round_d.p, 0xFF, (size_t)C * 4, stream));   // genesis: Round -1, Y ""
     HGX_TRY(hipMemsetAsync(root_y_ext_d.p, 0, (size_t)C, stream));
@@ -323,20 +335,21 @@ hipError_t Engine::insert(const InsertIn& in, int64_t count, InsertOut& out) {
     out.last_index.resize(C);
     out.chain_base.resize(C);
     out.graph_loaded.resize(G);
-    HGX_TRY(hipMemcpyAsync(out.last_gid.data(), last_gid_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.last_index.data(), last_index_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.chain_base.data(), chain_base_d.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.graph_loaded.data(), graph_loaded_d.p, (size_t)G * 8, hipMemcpyDeviceToHost, stream));
-    return hipStreamSynchronize(stream);
+    // one copy of the whole block into pinned memory, then the host mirrors
+    HGX_TRY(hipMemcpyAsync(h_ins, ins_blk.p, ins_blk.n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    std::memcpy(out.last_gid.data(), h_ins, (size_t)C * 4);
+    std::memcpy(out.last_index.data(), h_ins + C, (size_t)C * 4);
+    std::memcpy(out.chain_base.data(), h_ins + 2 * C, (size_t)C * 4);
+    std::memcpy(out.graph_loaded.data(), h_ins + ins_gl_off, (size_t)G * 8);
+    return hipSuccess;
 }
 
 hipError_t Engine::clear() {
     if (E > 0) HGX_TRY(hipMemsetAsync(succ.p, 0xFF, (size_t)E * 4, stream));
     HGX_TRY(hipMemsetAsync(first_none.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(last_index_d.p, 0xFF, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (size_t)C * 4, stream));
-    HGX_TRY(hipMemsetAsync(graph_loaded_d.p, 0, (size_t)G * 8, stream));
+    HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 8, stream));   // last_gid, last_index
+    HGX_TRY(hipMemsetAsync(chain_base_d.p, 0, (ins_blk.n - (size_t)2 * C) * 4, stream));   // chain_base, graph_loaded
     E = 0;
     E_div = 0;
     R = 0;
@@ -443,9 +456,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     } else {
         last_rebuild = false;
     }
-    HGX_TRY(hipMemcpyAsync(c_len.p, chain_len.data(), C * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(c_base.p, chain_base.data(), C * 4, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(c_old.p, h_len_div.data(), C * 4, hipMemcpyHostToDevice, stream));
+    // c_len | c_base | c_old in one copy from pinned staging (the previous call's copy has
+    // completed: every call synchronizes before returning)
+    std::memcpy(h_cpar, chain_len.data(), (size_t)C * 4);
+    std::memcpy(h_cpar + C, chain_base.data(), (size_t)C * 4);
+    std::memcpy(h_cpar + 2 * C, h_len_div.data(), (size_t)C * 4);
+    HGX_TRY(hipMemcpyAsync(cpar_blk.p, h_cpar, (size_t)3 * C * 4, hipMemcpyHostToDevice, stream));
     // first round whose step can change: the lowest round of the last old event of a chain
     // that got new events (every boundary below it is among old events)
     int32_t r_lo = 0;

@@ -45,9 +45,16 @@ template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
+    bool own = true;   // false: a view into another buffer (never freed here)
     hipError_t alloc(size_t count);
     hipError_t grow_copy(size_t count, size_t keep, hipStream_t s);
     void release();
+    void view(T* q, size_t count) {   // point into a block owned elsewhere
+        release();
+        p = q;
+        n = count;
+        own = false;
+    }
     ~DBuf() { release(); }
 };
 
@@ -188,6 +195,13 @@ class Engine {
     DBuf<uint8_t> g_S, g_coin, g_loaded, g_txnil;
     // insert state (hgx_insert.hip)
     DBuf<uint32_t> succ, first_none;
+    // small per-call tables in one block each, so that one copy moves them (views below):
+    // [last_gid | last_index | chain_base | graph_loaded (8-byte)] read back after every insert
+    // batch, [c_len | c_base | c_old] written before every DivideRounds
+    DBuf<int32_t> ins_blk, cpar_blk;
+    int32_t* h_ins = nullptr;    // pinned staging of ins_blk
+    int32_t* h_cpar = nullptr;   // pinned staging of cpar_blk
+    size_t ins_gl_off = 0;       // graph_loaded's offset in ins_blk (int32 units, even)
     DBuf<int32_t> last_gid_d, last_index_d, chain_base_d;
     DBuf<unsigned long long> ins_fail, graph_loaded_d;
     // host-batch staging (hgx_insert_events)

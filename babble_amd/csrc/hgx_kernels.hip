@@ -1499,6 +1499,7 @@ __global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* _
                                                      const uint8_t* __restrict__ g_S, int n,
                                                      uint32_t* __restrict__ out) {
     __shared__ uint64_t khi[kSortSmallMax], klo[kSortSmallMax];
+    __shared__ uint64_t ks[kSortSmallMax];   // S's first 8 bytes, big-endian: the tie-break, almost always
     __shared__ int32_t kv[kSortSmallMax];
     int NP = 1;
     while (NP < m) NP <<= 1;
@@ -1507,18 +1508,27 @@ __global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* _
             const int p = list[i];
             khi[i] = ((uint64_t)(uint32_t)(p_chain[p] / n) << 32) | (uint64_t)(uint32_t)p_rr[p];
             klo[i] = (uint64_t)p_cts[p] ^ 0x8000000000000000ull;
+            const uint8_t* sp = g_S + (size_t)p_gid[p] * 32;
+            uint64_t h = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) h = (h << 8) | sp[k];
+            ks[i] = h;
             kv[i] = p;
         } else {   // padding sorts last
             khi[i] = ~0ull;
             klo[i] = ~0ull;
+            ks[i] = ~0ull;
             kv[i] = -1;
         }
     }
     __syncthreads();
+    // equal (graph, rr, timestamp) runs are ordered by S (256-bit big-endian): the prefix in LDS
+    // decides unless two signatures share 8 bytes (then the rows are read from HBM)
     auto less = [&](int a, int b) -> bool {   // element a before element b
         if (khi[a] != khi[b]) return khi[a] < khi[b];
         if (klo[a] != klo[b]) return klo[a] < klo[b];
         if (kv[a] < 0 || kv[b] < 0) return kv[b] < 0 && kv[a] >= 0;
+        if (ks[a] != ks[b]) return ks[a] < ks[b];
         return cmp_s(g_S + (size_t)p_gid[kv[a]] * 32, g_S + (size_t)p_gid[kv[b]] * 32) < 0;
     };
     for (int k = 2; k <= NP; k <<= 1) {
@@ -1528,10 +1538,10 @@ __global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* _
                 const int l = i + j;
                 const bool up = (i & k) == 0;
                 if (up ? less(l, i) : less(i, l)) {
-                    const uint64_t h = khi[i], o = klo[i];
+                    const uint64_t h = khi[i], o = klo[i], q = ks[i];
                     const int32_t v = kv[i];
-                    khi[i] = khi[l]; klo[i] = klo[l]; kv[i] = kv[l];
-                    khi[l] = h; klo[l] = o; kv[l] = v;
+                    khi[i] = khi[l]; klo[i] = klo[l]; ks[i] = ks[l]; kv[i] = kv[l];
+                    khi[l] = h; klo[l] = o; ks[l] = q; kv[l] = v;
                 }
             }
             __syncthreads();
