@@ -67,6 +67,7 @@ Engine::~Engine() {
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
     if (h_small) (void)hipHostFree(h_small);
+    if (h_stage) (void)hipHostFree(h_stage);
     if (h_ins) (void)hipHostFree(h_ins);
     if (h_cpar) (void)hipHostFree(h_cpar);
     if (h_flag) (void)hipHostFree(h_flag);
@@ -256,6 +257,47 @@ void Engine::kadd_bytes(int k, double bytes) {
         if (it->k == k) { it->bytes += bytes; break; }
 }
 
+hipError_t Engine::stage_reserve(size_t bytes) {
+    const size_t need = stage_used + ((bytes + 63) & ~(size_t)63);
+    if (need <= stage_cap) return hipSuccess;
+    // grow: nothing staged may still be in flight, and staged D2H data is copied out first
+    HGX_TRY(hipStreamSynchronize(stream));
+    size_t cap = std::max(need, std::max((size_t)1 << 20, 2 * stage_cap));
+    uint8_t* q = nullptr;
+    HGX_TRY(hipHostMalloc((void**)&q, cap, hipHostMallocDefault));
+    if (h_stage) {
+        std::memcpy(q, h_stage, stage_used);
+        (void)hipHostFree(h_stage);
+    }
+    h_stage = q;
+    stage_cap = cap;
+    return hipSuccess;
+}
+
+hipError_t Engine::stage_h2d(void* dev, const void* host, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    HGX_TRY(stage_reserve(bytes));
+    uint8_t* h = h_stage + stage_used;
+    std::memcpy(h, host, bytes);
+    stage_used += (bytes + 63) & ~(size_t)63;
+    return hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, stream);
+}
+
+hipError_t Engine::stage_d2h(void* host, const void* dev, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    HGX_TRY(stage_reserve(bytes));
+    stage_out.push_back({host, stage_used, bytes});
+    uint8_t* h = h_stage + stage_used;
+    stage_used += (bytes + 63) & ~(size_t)63;
+    return hipMemcpyAsync(h, dev, bytes, hipMemcpyDeviceToHost, stream);
+}
+
+void Engine::stage_flush() {
+    for (const StagedD2H& d : stage_out) std::memcpy(d.dst, h_stage + d.off, d.bytes);
+    stage_out.clear();
+    stage_used = 0;
+}
+
 hipError_t Engine::collect_kernel_times() {
     if (kopen.empty()) return hipSuccess;
     HGX_TRY(hipStreamSynchronize(stream));
@@ -427,6 +469,8 @@ hipError_t Engine::reserve_rounds(int32_t rounds) {
 // the coordinate storage changes, or after reset_received / reserve_rounds / clear.
 hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_len,
                                  const std::vector<int32_t>& chain_base, RoundsHost& out) {
+    stage_out.clear();   // every earlier call synchronized: the staging is free
+    stage_used = 0;
     int32_t max_index = -1;
     int new_max_len = 0;
     for (int c = 0; c < C; c++) {
@@ -780,12 +824,11 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
     const size_t b0 = (size_t)out.r_lo * C;
-    HGX_TRY(hipMemcpyAsync(out.bm.data() + b0, Bm.p + b0, out.bm.size() * 4 - b0 * 4, hipMemcpyDeviceToHost, stream));
-    if (R > out.r_lo)
-        HGX_TRY(hipMemcpyAsync(out.wflag.data() + b0, wstat.p + b0, out.wflag.size() - b0, hipMemcpyDeviceToHost,
-                               stream));
+    HGX_TRY(stage_d2h(out.bm.data() + b0, Bm.p + b0, out.bm.size() * 4 - b0 * 4));
+    if (R > out.r_lo) HGX_TRY(stage_d2h(out.wflag.data() + b0, wstat.p + b0, out.wflag.size() - b0));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
+    stage_flush();
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[1] = ms;
     step_prof_dump();   // -DHGX_STEP_PROF builds only
@@ -815,6 +858,8 @@ int32_t Engine::recv_round_lo(const RoundsHost& rh, int& max_unrecv) const {
 
 // ---- DecideFame -----------------------------------------------------------------
 hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
+    stage_out.clear();   // every earlier call synchronized: the staging is free
+    stage_used = 0;
     fame_out.assign((size_t)R * C, 0);
     r0 = std::max(r0, 0);
     if (R <= r0) return hipSuccess;
@@ -824,9 +869,10 @@ hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
     launch_fame(stream, a, r0, R, C, n, nw, sm, G, fame_tally);
     kend(K_FAME, 0);
     const size_t o = (size_t)r0 * C;
-    HGX_TRY(hipMemcpyAsync(fame_out.data() + o, fame.p + o, fame_out.size() - o, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(stage_d2h(fame_out.data() + o, fame.p + o, fame_out.size() - o));
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
+    stage_flush();
     float ms = 0;
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[2] = ms;
@@ -843,6 +889,8 @@ hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<
 // threshold and roundReceived (every chain), consensus timestamps of the shard's chains
 hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
                                     const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
+    stage_out.clear();   // every earlier call synchronized: the staging is free
+    stage_used = 0;
     out = OrderHost();
     fo_m = 0;
     fo_cnt.assign(C, 0);
@@ -850,9 +898,9 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
     const size_t o = (size_t)r0 * C;
-    HGX_TRY(hipMemcpyAsync(elig.p, el.data(), (size_t)G * R, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(fw.p + o, famous.data() + o, (size_t)R * C - o, hipMemcpyHostToDevice, stream));
-    HGX_TRY(hipMemcpyAsync(ur_empty.p, ure.data(), (size_t)G, hipMemcpyHostToDevice, stream));
+    HGX_TRY(stage_h2d(elig.p, el.data(), (size_t)G * R));
+    HGX_TRY(stage_h2d(fw.p + o, famous.data() + o, (size_t)R * C - o));
+    HGX_TRY(stage_h2d(ur_empty.p, ure.data(), (size_t)G));
     if (WLAT.n < (size_t)R * C * n) {   // grown geometrically: R grows by a round or two per call
         HGX_TRY(WLAT.alloc(std::max((size_t)R * C * n + (size_t)C * n, 2 * WLAT.n)));
         a = arrays();
@@ -870,8 +918,9 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     launch_round_received(stream, a, R, C, n, max_unrecv);
     kend(K_ROUND_RECEIVED, 0);
     HGX_TRY(hipMemcpyAsync(h_small, counters.p, 8, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(fo_cnt.data(), rcnt.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(stage_d2h(fo_cnt.data(), rcnt.p, (size_t)C * 4));
     HGX_TRY(hipStreamSynchronize(stream));
+    stage_flush();
     fo_m = h_small[0];
     out.panic = h_small[1] != 0;
     out.m = fo_m;

@@ -242,6 +242,16 @@ class Engine {
     DBuf<uint32_t> val_a, val_b, hist;
     DBuf<int64_t> minmax, blk_ntx;
     int32_t* h_small = nullptr;   // pinned scratch (flags)
+    // pinned staging of the per-call host tables (DMA instead of pageable copies): a cursor per
+    // phase; D2H copies land here and are handed out by stage_flush() after the phase's sync
+    uint8_t* h_stage = nullptr;
+    size_t stage_cap = 0, stage_used = 0;
+    struct StagedD2H { void* dst; size_t off, bytes; };
+    std::vector<StagedD2H> stage_out;
+    hipError_t stage_reserve(size_t bytes);
+    hipError_t stage_h2d(void* dev, const void* host, size_t bytes);
+    hipError_t stage_d2h(void* host, const void* dev, size_t bytes);
+    void stage_flush();   // after the stream synchronized: copy the D2H tables out, reset the cursor
     int32_t* h_flag = nullptr;    // host-mapped, coherent: the round-step batches' "candidates left" flags
     int32_t* d_flag = nullptr;    // its device address
     // timing
