@@ -814,11 +814,11 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
     const int i = r0 + (int)(item / C), gd = (int)(item % C);
     const int g = gd / n;
     if (!elig[(size_t)g * R + i]) return;
-    __shared__ uint32_t whist[4][256];
+    __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
     const int lane = lane_id();
     const size_t base = (size_t)i * C + (size_t)g * n;
     const size_t row = ((size_t)i * C + gd) * n;
-    uint64_t v[CPL];
+    uint32_t v[CPL];   // int32 order as u32: sign bit flipped
     bool ok[CPL];
     int m = 0;
 #pragma unroll
@@ -826,13 +826,13 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
         const int c = lane + 64 * q;
         ok[q] = c < n && fw[base + c];
         const int32_t x = ok[q] ? WLAT[row + c] : 0;
-        v[q] = (uint64_t)(int64_t)x ^ 0x8000000000000000ull;
+        v[q] = (uint32_t)x ^ 0x80000000u;
         m += __popcll(__ballot(ok[q]));
     }
     int32_t res = -1;
     if (m > 0) {   // (m/2)-th largest = (m-1-m/2)-th smallest
-        const uint64_t u = wave_select_kth<CPL>(v, ok, m - 1 - m / 2, whist[(threadIdx.x >> 6) & 3]);
-        res = (int32_t)(int64_t)(u ^ 0x8000000000000000ull);
+        const uint32_t u = wave_select_kth32<CPL>(v, ok, m - 1 - m / 2, whist[(threadIdx.x >> 6) & 3]);
+        res = (int32_t)(u ^ 0x80000000u);
     }
     if (lane == 0) T[(size_t)i * C + gd] = res;
 }
