@@ -396,36 +396,53 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     // positions of a chunk carries the owner forward; then one coalesced store per 64
     // positions. (A per-lane store loop measured 9 stores and ~76 VALU per (tile, d),
     // VALU-issue-bound at 6.2 ms for c3.)
-    // Per-d values are wave-uniform: readfirstlane keeps them (and the chunk loop) in SGPRs.
+    // Per-d values are wave-uniform (SGPRs, and so is the chunk loop). The per-d scalars of up to 64 of the wave's chains are read in one LDS batch (lane q
+    // holds chain d0 + nwaves*q) and taken with readlane, and the next chain's tile column is
+    // read while the current one is written: no dependent LDS round trip per chain.
     int32_t* slot = (int32_t*)(tw + (FT + 1) * ldw) + 64 * wave;
     const int ownv = base_c + k0;
-    for (int d = wave; d < n; d += nwaves) {
-        const int len_d = __builtin_amdgcn_readfirstlane(m_len[d]);
-        if (len_d == 0) continue;
-        const int base_d = __builtin_amdgcn_readfirstlane(m_base[d]);
-        const int off_d = __builtin_amdgcn_readfirstlane(m_off[d]);
-        int lo = (k0 > 0) ? __builtin_amdgcn_readfirstlane(K::la(tile[d])) : base_d - 1;
-        if (lo < base_d - 1) lo = base_d - 1;
-        const int vmax = base_d + len_d - 1;
-        const int hi_val = (rows > 0) ? __builtin_amdgcn_readfirstlane(K::la(tile[rows * ld + d])) : lo;
-        const int hi = last ? vmax : min(hi_val, vmax);
-        CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
-        const int v = (lane < rows) ? min(max(K::la(tile[(lane + 1) * ld + d]), lo), vmax) : hi_val;
-        // first position of this lane's range = previous lane's v + 1 (lane 0: lo + 1)
-        const int start = __builtin_amdgcn_update_dpp(lo, v, 0x138, 0xf, 0xf, false) + 1;   // wave_shr:1
-        const bool own = lane < rows && v >= start;
-        const int vlast = max(lo, min(hi_val, vmax));   // end of the tile's last range
-        int carry = -1;
-        for (int j0 = lo + 1; j0 <= hi; j0 += 64) {   // scalar loop
-            slot[lane] = -1;
-            wave_lds_fence();
-            if (own && (unsigned)(start - j0) < 64u) slot[start - j0] = lane;
-            // past the last row (last tile only): none = MaxInt32, sentinel owner 64
-            if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 64;
-            wave_lds_fence();
-            const int o = max(wave_incl_max(slot[lane]), carry);
-            carry = __builtin_amdgcn_readlane(o, 63);
-            if (j0 + lane <= hi) out[j0 + lane] = K::enc_fd(o < rows ? ownv + o : kMaxI32);
+    for (int d0 = wave; d0 < n; d0 += nwaves * 64) {
+        const int dq = d0 + nwaves * lane;
+        int q_len = 0, q_base = 0, q_off = 0, q_lo = 0, q_hv = 0;
+        if (dq < n) {
+            q_len = m_len[dq];
+            q_base = m_base[dq];
+            q_off = m_off[dq];
+            q_lo = (k0 > 0) ? K::la(tile[dq]) : q_base - 1;
+            if (rows > 0) q_hv = K::la(tile[rows * ld + dq]);
+        }
+        const int nq = min(64, (n - d0 + nwaves - 1) / nwaves);
+        int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0]) : 0;
+        for (int q = 0; q < nq; q++) {
+            const int vraw = vnext;
+            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + nwaves * (q + 1)]);
+            const int len_d = __builtin_amdgcn_readlane(q_len, q);
+            if (len_d == 0) continue;
+            const int base_d = __builtin_amdgcn_readlane(q_base, q);
+            const int off_d = __builtin_amdgcn_readlane(q_off, q);
+            int lo = __builtin_amdgcn_readlane(q_lo, q);
+            if (lo < base_d - 1) lo = base_d - 1;
+            const int vmax = base_d + len_d - 1;
+            const int hi_val = (rows > 0) ? __builtin_amdgcn_readlane(q_hv, q) : lo;
+            const int hi = last ? vmax : min(hi_val, vmax);
+            CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
+            const int v = (lane < rows) ? min(max(vraw, lo), vmax) : hi_val;
+            // first position of this lane's range = previous lane's v + 1 (lane 0: lo + 1)
+            const int start = __builtin_amdgcn_update_dpp(lo, v, 0x138, 0xf, 0xf, false) + 1;   // wave_shr:1
+            const bool own = lane < rows && v >= start;
+            const int vlast = max(lo, min(hi_val, vmax));   // end of the tile's last range
+            int carry = -1;
+            for (int j0 = lo + 1; j0 <= hi; j0 += 64) {   // scalar loop
+                slot[lane] = -1;
+                wave_lds_fence();
+                if (own && (unsigned)(start - j0) < 64u) slot[start - j0] = lane;
+                // past the last row (last tile only): none = MaxInt32, sentinel owner 64
+                if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 64;
+                wave_lds_fence();
+                const int o = max(wave_incl_max(slot[lane]), carry);
+                carry = __builtin_amdgcn_readlane(o, 63);
+                if (j0 + lane <= hi) out[j0 + lane] = K::enc_fd(o < rows ? ownv + o : kMaxI32);
+            }
         }
     }
 }
