@@ -701,13 +701,54 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     };
     kbeg(K_ROUND_GATHER);
     launch_round_gather(stream, a, r_lo, C, n, fd_ld);   // W'_{r_lo}: round 0 = first event of every chain
-    launch_round_k_gather(stream, round_args(), r_lo);   // ... rebased for the per-candidate step
     kend(K_ROUND_GATHER, (double)C * n * 16);
     int launched = 0, checked = 0;
+    // the persistent recurrence (hgx_round_p.hip): every round in one launch; r_done = rounds
+    // [r_lo, r_done) written (the last one empty)
+    int32_t r_done = -1;
+    auto run_persistent = [&]() -> hipError_t {
+        const int ndw = round_k_ndw(n);
+        if (FD8p.n < (size_t)2 * C * ndw) HGX_TRY(FD8p.alloc((size_t)2 * C * ndw));
+        if (rp_gran.n < (size_t)4 * C) HGX_TRY(rp_gran.alloc((size_t)4 * C));
+        if (rp_st.n < 4) HGX_TRY(rp_st.alloc(4));
+        HGX_TRY(hipMemsetAsync(rp_gran.p, 0, (size_t)4 * C * 8, stream));   // no tag survives a call
+        int32_t s = r_lo;
+        for (int init = 1;; init = 0) {
+            if (r_cap - 1 <= s + 1) {
+                HGX_TRY(ensure_round_cap(s + 64));
+                a = arrays();
+            }
+            HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
+            kbeg(K_ROUND_SEARCH);
+            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, s, r_cap - 1, init, num_cus));
+            kend(K_ROUND_SEARCH, 0);
+            HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+            round_p_runs++;
+            round_p_ovf += h_small[59];
+            if (h_small[56] != 0) return hipErrorLaunchTimeOut;   // a workgroup gave up waiting
+            s = h_small[57];
+            if (h_small[58]) {
+                r_done = s + 1;
+                return hipSuccess;
+            }
+        }
+    };
+    if (!rooted && round_kernel == 0 && round_p_ok(n, C, num_cus)) {
+        const hipError_t pe = run_persistent();
+        if (pe != hipSuccess) {
+            // redo the rounds with the per-launch steps (a timed-out launch left partial rows)
+            (void)hipGetLastError();
+            if (pe != hipErrorLaunchTimeOut && pe != hipErrorCooperativeLaunchTooLarge) return pe;
+            round_p_fallbacks++;
+            r_done = -1;
+        }
+    }
+    if (r_done < 0) launch_round_k_gather(stream, round_args(), r_lo);   // W'_{r_lo} rebased for k_round_k
     // a rebuild replays kStepBatch steps per hipGraph; a resumed call (a few rounds) kStepBatchSmall
     StepGraph& sgr = step_g[rebuild ? 0 : 1];
     const int nb = rebuild ? kStepBatch : kStepBatchSmall;
-    {   // n <= 1024 (hgx_create's limit)
+    if (r_done < 0) {   // n <= 1024 (hgx_create's limit)
         // nb step nodes replayed as one hipGraph; before each replay the nodes' round
         // arguments are rewritten (hipGraphExecKernelNodeSetParams), so a step knows its
         // round without a dependent device load. Batch i+1 is queued before the host looks
@@ -718,7 +759,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 HGX_TRY(ensure_round_cap(need));
                 a = arrays();
             }
-            const int kern = rooted ? 0 : round_kernel;   // root floors: per-candidate step only
+            const int kern = (rooted || round_kernel != 1) ? 0 : 1;   // root floors: per-candidate step only
             const RoundArgs cur = round_args();
             if (!sgr.exec || sgr.kernel != kern || sgr.compact != compact || sgr.nb != nb || sgr.args.gB != cur.gB ||
                 sgr.args.gmax != cur.gmax) {
@@ -805,7 +846,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // so only [r_lo, R) is scanned: last = max(that, min(previous last, r_lo - 1))
     const int r_scan = rebuild ? 0 : r_lo;
     const std::vector<int32_t> prev_last = out.last_round;
-    launch_last_round(stream, r_scan, r_lo + launched * nb, G, C, n, wstat.p, lr.p);
+    launch_last_round(stream, r_scan, r_done >= 0 ? r_done : r_lo + launched * nb, G, C, n, wstat.p, lr.p);
     out.last_round.assign(G, -1);
     HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
     HGX_TRY(hipStreamSynchronize(stream));

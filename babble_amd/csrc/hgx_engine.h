@@ -166,7 +166,10 @@ class Engine {
     KernelStat kstat[K_NUM];
     uint32_t time_mask = 0;   // kernels (bit = KernelId) timed with HIP events
     int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
-    int round_kernel = 0;     // 0 per-candidate step (hgx_round_k.hip), 1 block-search step (hgx_set_round_kernel)
+    int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence where it applies (hgx_round_p.hip),
+                              // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
+    int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
+    int64_t round_p_ovf = 0;   // candidate rows the persistent launches counted exactly (over 8 bits)
     int dev = 0;
 
    private:
@@ -230,6 +233,9 @@ class Engine {
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<uint32_t> FD8;   // [2][C][ndw] rebased candidate rows (k_round_k)
+    DBuf<uint32_t> FD8p;  // [2][C][ndw] the same, row-major (k_round_p)
+    DBuf<uint64_t> rp_gran;   // [4][C] k_round_p hand-off granules
+    DBuf<int32_t> rp_st;      // k_round_p status: abort, rounds done, finished
     DBuf<int32_t> la_lmap;          // k_la_wave lanes -> chains with events (one graph, n > 896)
     std::vector<int32_t> h_lmap;
     DBuf<int32_t> ovf;    // [r_cap + 2]

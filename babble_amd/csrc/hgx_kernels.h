@@ -157,6 +157,14 @@ hipError_t launch_round_step(hipStream_t s, const RoundArgs& A, int r, int block
 hipError_t launch_round_k(hipStream_t s, const RoundArgs& A, int r);
 void launch_round_k_gather(hipStream_t s, const RoundArgs& A, int r);   // round r's rebased rows + ovf[r]
 int round_k_ndw(int n);
+// persistent round recurrence (hgx_round_p.hip): one resident workgroup per chain runs rounds
+// [r0, r_end) in one launch (init: W'_{r0}'s rebased rows and hand-off granules first, from
+// the WFD rows of launch_round_gather). status[0] != 0: a workgroup gave up waiting (bounded
+// spins), the rounds must be redone per launch; status[1] = the round it stopped at; status[2]
+// = 1 when W'_{status[1]} is empty (no round status[1]).
+bool round_p_ok(int n, int C, int num_cus);
+hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status, int r0,
+                          int r_end, int init, int num_cus);
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,

@@ -1,0 +1,574 @@
+// Persistent round recurrence: one resident workgroup per chain runs every round of a
+// DivideRounds in ONE launch (RoundInc, hashgraph.go:285-305; StronglySee :170-198;
+// DivideRounds :616-646). DESIGN.md §3.3.
+//
+// Round s of chain c finds Bm[s+1][c] = the first offset k >= Bm[s][c] whose event strongly
+// sees >= SM candidates of W'_s (the first event of each chain with round >= s), exactly as
+// k_round_k does (same per-candidate binary search over a window of 31 probe rows, same 8-bit
+// SWAR compare, same K(w) histogram). What changes is how the rounds are chained:
+//  * the workgroup of chain c stays resident for all rounds. Its own boundary is the start of
+//    its next window, so the window's raw lastAncestors rows and firstDescendants columns are
+//    staged by LDS-DMA right after the boundary is known, while the other chains finish;
+//  * the only data a round needs from other workgroups is W'_s: for each chain its boundary
+//    and its candidate's rebased firstDescendants row. The producer (the workgroup that found
+//    the candidate) stores the row write-through (sc1), drains it, then stores an 8-byte
+//    granule {tag = s + 1, boundary | flags} write-through; a consumer wave polls the granules
+//    of ITS candidates (sc1 loads), then loads their rows (sc1 loads) and searches at once: a
+//    wave whose candidates arrived early searches while the last producers still run. This is
+//    the first row of the hand-off table in MI355X_MICROARCH.md (§Workgroup dispatch): one
+//    signalling lane per storing workgroup after its wave's vmcnt(0), an sc1 poll, sc1 stores
+//    and loads of every handed-off byte, one workgroup per CU, hipMalloc memory;
+//  * no grid barrier and no kernel boundary per round; every wait is bounded (s_memrealtime),
+//    a workgroup that gives up raises the abort word, every workgroup then leaves, and the
+//    host reruns the rounds with the per-launch step (k_round_k).
+// A candidate row that does not fit 8 bits is flagged in its granule and that candidate alone
+// is counted with exact int32 compares (k_round_k flags the whole round instead).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "hgx_device.h"
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kRpP = 31;       // probes per window (K in [0, 31], 5 binary-search levels)
+constexpr int kRpSlots = 4;    // granule ring slots (a slot is rewritten 4 rounds later)
+constexpr uint32_t kRpEx = 1u << 31, kRpOv = 1u << 30, kRpBm = (1u << 30) - 1;
+
+// ---- write-through hand-off primitives (MI355X_MICROARCH.md, Valid forms, row 1) ----------
+__device__ __forceinline__ uint64_t rp_ld_gran(const uint64_t* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 load
+}
+__device__ __forceinline__ void rp_st_gran(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);      // sc1 store
+}
+__device__ __forceinline__ void rp_st_sc1(uint32_t* p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t rp_ld_abort(const int32_t* p) {
+    return (uint32_t)__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rp_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void rp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// HD dwords of this lane's part of a candidate row, sc1 loads (every load of handed-off bytes)
+template <int HD>
+__device__ __forceinline__ void rp_ld_row(const uint32_t* p, uint32_t (&v)[HD]) {
+    if constexpr (HD >= 4) {
+#pragma unroll
+        for (int k = 0; k < HD / 4; k++) {
+            uint4 x;
+            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(x) : "v"(p + 4 * k) : "memory");
+            v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
+        }
+    } else if constexpr (HD == 2) {
+        uint2 x;
+        asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(x) : "v"(p) : "memory");
+        v[0] = x.x; v[1] = x.y;
+    } else {
+        uint32_t x;
+        asm volatile("global_load_dword %0, %1, off sc1" : "=v"(x) : "v"(p) : "memory");
+        v[0] = x;
+    }
+}
+
+// HD dwords of an LDS row, all reads in flight before one wait (16-byte reads when HD % 4 == 0)
+template <int HD>
+__device__ __forceinline__ void rp_lds_row(const uint32_t* p, uint32_t (&v)[HD]) {
+    const uint32_t a = (uint32_t)(uintptr_t)p;
+    if constexpr (HD % 4 == 0) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 r[HD / 4];
+#pragma unroll
+        for (int k = 0; k < HD / 4; k++) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[k]) : "v"(a), "i"(16 * k));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < HD / 4; k++) {
+            asm volatile("" : "+v"(r[k]));
+            v[4 * k] = r[k].x; v[4 * k + 1] = r[k].y; v[4 * k + 2] = r[k].z; v[4 * k + 3] = r[k].w;
+        }
+    } else if constexpr (HD == 2) {
+        uint64_t r;
+        asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(a));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(r));
+        v[0] = (uint32_t)r; v[1] = (uint32_t)(r >> 32);
+    } else {
+        uint32_t r;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(a));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(r));
+        v[0] = r;
+    }
+}
+
+// sum over the Q adjacent lanes of a candidate (DPP: quad_perm xor 1, xor 2, half-row mirror)
+template <int Q>
+__device__ __forceinline__ uint32_t rp_combine(uint32_t x) {
+    if constexpr (Q >= 2) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);
+    if constexpr (Q >= 4) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false);
+    if constexpr (Q >= 8) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xf, 0xf, false);
+    return x;
+}
+
+// geometry of one instantiation: n <= 4 NDW chains per graph; candidate j's row is split over
+// Q adjacent lanes (HD dwords each); T threads
+template <typename CT, int NDW, int Q>
+struct RpCfg {
+    static constexpr int NC = 4 * NDW;
+    static constexpr int HD = NDW / Q;
+    static constexpr int T = (NC * Q < 64) ? 64 : NC * Q;
+    static constexpr int NW = T / 64;
+    static constexpr int WS = NDW + 4;                         // 8-bit window row stride (dwords, == 4 mod 16)
+    static constexpr int CSZ = (int)sizeof(CT);
+    static constexpr int RAW_DW = kRpP * NC * CSZ / 4;          // raw window rows (dwords) at n = NC
+    static constexpr int KR16 = (RAW_DW + NW * 256 - 1) / (NW * 256);   // 16-byte DMA per lane
+    static constexpr int KR4 = (RAW_DW + NW * 64 - 1) / (NW * 64);      // 4-byte DMA per lane
+    static constexpr int RAW_LDS = (KR16 * NW * 256 > KR4 * NW * 64 ? KR16 * NW * 256 : KR4 * NW * 64);   // dwords
+    static constexpr int CW = (CSZ == 2) ? 16 : 32;             // dwords per staged FD column (32 positions)
+    static constexpr int CPI = 64 / CW;                          // FD columns per DMA instruction
+    static constexpr int KF = (NC + NW * CPI - 1) / (NW * CPI);
+    static constexpr int FDC_LDS = KF * NW * 65;                 // dwords: groups of 64 + 1 pad
+    // LDS carve (bytes, 16-aligned)
+    static constexpr int O_WIN = 0;
+    static constexpr int O_RAW0 = O_WIN + ((kRpP * WS * 4 + 15) & ~15);
+    static constexpr int O_RAW1 = O_RAW0 + RAW_LDS * 4;
+    static constexpr int O_FDC0 = O_RAW1 + RAW_LDS * 4;
+    static constexpr int O_FDC1 = O_FDC0 + ((FDC_LDS * 4 + 15) & ~15);
+    static constexpr int O_CB = O_FDC1 + ((FDC_LDS * 4 + 15) & ~15);   // c_base[NC]
+    static constexpr int O_CO = O_CB + NC * 4;                           // c_off[NC]
+    static constexpr int O_BM0 = O_CO + NC * 4;                          // Bm of the candidates, by round parity
+    static constexpr int O_BM1 = O_BM0 + NC * 4;
+    static constexpr int O_HIST = O_BM1 + NC * 4;                        // 32 bins
+    static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits (NC / 32 words)
+    static constexpr int O_MISC = O_SB + ((NC / 32 + 4) * 4 + 15 & ~15); // [0] B, [1] tot, [2] any, [3] fail
+    static constexpr int USED = O_MISC + 64;
+    // at least 82 KB: one workgroup per CU (the hand-off rule's geometry), whatever fits
+    static constexpr int LDS = USED > 84 * 1024 ? USED : 84 * 1024;
+};
+
+struct RoundPArgs {
+    RoundArgs A;
+    uint32_t* FD8p;     // [2][C][ndw] rebased candidate rows, row-major (parity = round & 1)
+    uint64_t* gran;     // [kRpSlots][C]
+    int32_t* st;        // [0] abort, [1] the round it stopped at, [2] 1: W'_{st[1]} empty, [3] rows over 8 bits
+    int r0, r_end;      // rounds [r0, r_end) at most
+    long long tmo;      // one wait's budget in s_memrealtime ticks (100 MHz)
+};
+
+template <typename CT, int NDW, int Q>
+__global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round_p(RoundPArgs P) {
+    typedef RpCfg<CT, NDW, Q> K;
+    constexpr int HD = K::HD, T = K::T, WS = K::WS, CW = K::CW, CPI = K::CPI;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const RoundArgs& A = P.A;
+    const int n = A.n, C = A.C, sm = A.sm;
+    const int t = threadIdx.x, lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int gc = blockIdx.x, g = gc / n, cl = gc % n, g0 = g * n;
+    const int j = t / Q, q = t % Q;              // candidate slot and row part of this lane
+    const bool jv = j < n && t < K::NC * Q;      // a real chain of the graph
+    uint32_t* win = (uint32_t*)(lds + K::O_WIN);
+    int32_t* cbase = (int32_t*)(lds + K::O_CB);
+    int32_t* coff = (int32_t*)(lds + K::O_CO);
+    int32_t* hist = (int32_t*)(lds + K::O_HIST);
+    uint32_t* sbits = (uint32_t*)(lds + K::O_SB);
+    int32_t* misc = (int32_t*)(lds + K::O_MISC);
+
+    const int len = A.c_len[gc], off = A.c_off[gc];
+    for (int i = t; i < n; i += T) {
+        cbase[i] = A.c_base[g0 + i];
+        coff[i] = A.c_off[g0 + i];
+        // Bm of round r0 - 1 (bases of round r0's window), written by earlier launches
+        ((int32_t*)(lds + (((P.r0 - 1) & 1) ? K::O_BM1 : K::O_BM0)))[i] = P.r0 > 0 ? A.Bm[(size_t)(P.r0 - 1) * C + g0 + i] : 0;
+    }
+    int b = A.Bm[(size_t)P.r0 * C + gc];
+
+    // ---- staging of a window [kb, kb + 31) into buffer `buf` (LDS-DMA, fixed counts per wave)
+    int fsh_buf[2] = {0, 0};
+    auto stage = [&](int kb, int buf) {
+        const int nraw = min(kRpP, len - kb);
+        uint32_t* raw_w = (uint32_t*)(lds + (buf ? K::O_RAW1 : K::O_RAW0));
+        const int nel = (int)((size_t)nraw * n * K::CSZ / 4);   // dwords
+        const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kb) * n * K::CSZ / 4;
+        if (((n * K::CSZ) & 15) == 0) {
+#pragma unroll
+            for (int k = 0; k < K::KR16; k++) {
+                const int c0 = wave * 256 + k * K::NW * 256;
+                __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane * 4, nel - 4)),
+                                                 (lds_ptr_t)(raw_w + c0), 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K::KR4; k++) {
+                const int c0 = wave * 64 + k * K::NW * 64;
+                __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane, nel - 1)),
+                                                 (lds_ptr_t)(raw_w + c0), 4, 0, 0);
+            }
+        }
+        // firstDescendants columns at positions [off + kb, off + kb + 32) (uint16: from the even
+        // position below), 65-dword groups of CPI columns
+        uint32_t* fd_w = (uint32_t*)(lds + (buf ? K::O_FDC1 : K::O_FDC0));
+        const int pcol = lane % CW, icol = lane / CW;
+        const int64_t Pc = A.Pcap;
+        const uint32_t* __restrict__ fsrc;
+        size_t cstride, lim;
+        if constexpr (K::CSZ == 4) {
+            fsrc = (const uint32_t*)A.FDT + off + kb + pcol;
+            cstride = (size_t)Pc;
+            lim = (size_t)n * Pc - 1 - (size_t)(off + kb + pcol);
+        } else {
+            const int64_t p0 = (off + kb) & ~1;
+            fsh_buf[buf] = (off + kb) & 1;
+            fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
+            cstride = (size_t)(Pc / 2);
+            lim = (size_t)n * (Pc / 2) - 1 - (size_t)(p0 / 2 + pcol);
+        }
+#pragma unroll
+        for (int k = 0; k < K::KF; k++) {
+            const int i0 = wave * CPI + k * K::NW * CPI;
+            const int i = min(i0 + icol, n - 1);
+            const size_t o = min((size_t)i * cstride, lim);
+            __builtin_amdgcn_global_load_lds((const void*)(fsrc + o), (lds_ptr_t)(fd_w + (size_t)(i0 / CPI) * 65), 4, 0, 0);
+        }
+    };
+    auto fd_at = [&](int buf, int i, int pk) -> CT {   // staged FD of coordinate i at window probe pk
+        const uint32_t* fd_w = (const uint32_t*)(lds + (buf ? K::O_FDC1 : K::O_FDC0));
+        const int col = (i / CPI) * 65 + (i % CPI) * CW;
+        if constexpr (K::CSZ == 2) return ((const CT*)fd_w)[2 * col + fsh_buf[buf] + pk];
+        else return (CT)fd_w[col + pk];
+    };
+    auto raw_at = [&](int buf, int p, int i) -> CT {
+        return ((const CT*)(lds + (buf ? K::O_RAW1 : K::O_RAW0)))[p * n + i];
+    };
+    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the staged rows [0, np)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    auto rebase = [&](int buf, int np, const int32_t* bmp) {
+        constexpr int RS = T / NDW > 0 ? T / NDW : 1;   // rows per pass
+        for (int d = t % NDW; d < NDW; d += T) {
+            const int i0 = 4 * d;
+            int32_t bq[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) bq[u] = (i0 + u < n) ? cbase[i0 + u] + bmp[i0 + u] : 0;
+            for (int p = t / NDW; p < np; p += RS) {
+                uint32_t w;
+                if constexpr (K::CSZ == 2) {
+                    const uint32_t* rp = (const uint32_t*)(lds + (buf ? K::O_RAW1 : K::O_RAW0)) + (p * n + i0) / 2;
+                    const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
+                    const u16x2 b01 = {(unsigned short)bq[0], (unsigned short)bq[1]};
+                    const u16x2 b23 = {(unsigned short)bq[2], (unsigned short)bq[3]};
+                    const u16x2 cap = {126, 126};
+                    const u16x2 y01 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
+                    const u16x2 y23 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
+                    w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23), __builtin_bit_cast(uint32_t, y01), 0x06040200u) |
+                        0x80808080u;
+                } else {
+                    w = 0x80808080u;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (i0 + u < n) {
+                            const int32_t x = Coord<CT>::la(raw_at(buf, p, i0 + u)) - bq[u] + 1;
+                            w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
+                        }
+                    }
+                }
+                win[p * WS + d] = w;
+            }
+        }
+    };
+
+    int cur = 0;
+    if (b < len) stage(b, 0);
+    const long long t_start = __builtin_amdgcn_s_memrealtime();
+    int s = P.r0;
+    bool failed = false;
+    for (;; s++) {
+        if (s >= P.r_end) break;   // capacity: the host continues from round s
+        const int32_t* bm_prev = (const int32_t*)(lds + (((s - 1) & 1) ? K::O_BM1 : K::O_BM0));
+        int32_t* bm_cur = (int32_t*)(lds + ((s & 1) ? K::O_BM1 : K::O_BM0));
+        const bool have = b < len;   // block-uniform
+        int kb = b, np = have ? min(kRpP, len - b) : 0;
+        // (a) this round's window (staged at the end of the previous round), rebased to base(s)
+        rp_vm_drain();
+        if (t < 32) hist[t] = 0;
+        if (t == 0) { misc[2] = 0; misc[3] = 0; }
+        if (t < K::NC / 32 + 1) sbits[t] = 0;
+        __syncthreads();
+        if (have) rebase(cur, np, bm_prev);
+        rp_lds_barrier();
+
+        // (b) poll the granules of this lane's candidate (W'_s, tag s + 1), then its row
+        const uint64_t* gp = P.gran + (size_t)(s % kRpSlots) * C + g0 + (jv ? j : 0);
+        uint64_t gv = 0;
+        bool wfail = false;
+        {
+            const long long tw = __builtin_amdgcn_s_memrealtime();
+            for (int spins = 0;; spins++) {
+                gv = jv ? rp_ld_gran(gp) : ((uint64_t)(uint32_t)(s + 1) << 32);
+                if (__all((uint32_t)(gv >> 32) == (uint32_t)(s + 1))) break;
+                if ((spins & 31) == 31) {
+                    const long long now = __builtin_amdgcn_s_memrealtime();
+                    if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const uint32_t gval = (uint32_t)gv;
+        const bool cand = jv && !wfail && (gval & kRpEx);
+        const bool ov = cand && (gval & kRpOv);
+        const int bmj = (int)(gval & kRpBm);
+        if (jv && q == 0 && !wfail) bm_cur[j] = bmj;
+        uint32_t fd[HD];
+        if (cand && have) {
+            rp_ld_row<HD>(P.FD8p + ((size_t)(s & 1) * C + g0 + j) * NDW + q * HD, fd);
+        } else {
+#pragma unroll
+            for (int d = 0; d < HD; d++) fd[d] = 0x7F7F7F7Fu;   // never seen
+        }
+        if (wfail && lane == 0) misc[3] = 1;
+        if (cand && q == 0) misc[2] = 1;   // (same value from every writer)
+        rp_vm_drain();
+#pragma unroll
+        for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+
+        // (c) search, window after window until the boundary is found (a later window is rare)
+        int kstar = len, B = -1, K_last = kRpP, carried = 0;
+        bool done = false;
+        const bool wave_cand = __any(cand) && have;
+        const bool wave_ov = __any(ov) && have;
+        for (int w_it = 0; have; w_it++) {
+            int lo = 0, hi = kRpP;
+            if (wave_cand) {
+#pragma unroll 1
+                for (int it = 0; it < 5; it++) {
+                    const int mid = (lo + hi) >> 1;
+                    uint32_t cnt = 0;
+                    if (!ov) {
+                        uint32_t v[HD];
+                        rp_lds_row<HD>(win + mid * WS + q * HD, v);
+#pragma unroll
+                        for (int d = 0; d < HD; d++) cnt += __builtin_popcount((v[d] - fd[d]) & 0x80808080u);
+                    } else if (!done && mid < np) {
+                        // exact int32 compares of this part of the row (hashgraph.go:191-197)
+                        const int i_lo = q * HD * 4, i_hi = min(n, (q + 1) * HD * 4);
+                        const size_t pos = (size_t)coff[j] + bmj;
+                        for (int i = i_lo; i < i_hi; i++) {
+                            const int32_t fdv = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + pos]);
+                            const int32_t lav = min(Coord<CT>::la(raw_at(cur, mid, i)), kMaxI32 - 1);
+                            cnt += lav >= fdv ? 1u : 0u;
+                        }
+                    }
+                    (void)wave_ov;
+                    cnt = rp_combine<Q>(cnt);
+                    const bool seen = done || mid >= np || ((int)cnt >= sm && !(j == cl && kb + mid == b));
+                    if (seen) hi = mid; else lo = mid + 1;
+                }
+            }
+            const int Kw = lo;
+            if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
+            rp_lds_barrier();
+            if (wave == 0) {   // boundary: first probe where #{K <= p} (+ seen in earlier windows) >= SM
+                const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
+                const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
+                const uint64_t m = __ballot(lane < np && (int)inc >= sm);
+                const int tot = __builtin_amdgcn_readlane((int)inc, 63);
+                if (lane == 0) { misc[0] = m ? (int)__builtin_ctzll(m) : -1; misc[1] = tot; }
+            }
+            rp_lds_barrier();
+            B = misc[0];
+            K_last = Kw;
+            if (B >= 0 || misc[2] == 0 || misc[3] != 0) {
+                if (B >= 0) kstar = kb + B;
+                break;
+            }
+            // no boundary in this window: the next one (synchronous staging)
+            carried = misc[1];
+            if (cand && Kw < np) done = true;
+            kb += np;
+            if (kb >= len) break;
+            np = min(kRpP, len - kb);
+            if (t < 32) hist[t] = 0;
+            rp_lds_barrier();
+            stage(kb, cur);
+            rp_vm_drain();
+            __syncthreads();
+            rebase(cur, np, bm_prev);
+            rp_lds_barrier();
+        }
+        if (!have) rp_lds_barrier();   // the pollers' any / fail words
+        if (misc[3] != 0) { failed = true; break; }
+        if (misc[2] == 0) break;       // W'_s is empty: no round s (every workgroup of the graph agrees)
+
+        // (d) publish W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s]), then the granule
+        const bool nx = kstar < len;
+        const int pk = kstar - kb;
+        if (wave == 0) {
+            bool of = false;
+            if (nx) {
+                uint32_t* dst = P.FD8p + ((size_t)((s + 1) & 1) * C + gc) * NDW;
+                for (int d = lane; d < NDW; d += 64) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int i = 4 * d + u;
+                        uint32_t v = 127u;
+                        if (i < n) {
+                            const int32_t f = Coord<CT>::fd(fd_at(cur, i, pk));
+                            if (f != kMaxI32) {
+                                const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
+                                if (x > 126) of = true;
+                                else v = (uint32_t)x;
+                            }
+                        }
+                        w |= v << (8 * u);
+                    }
+                    rp_st_sc1(dst + d, w);
+                }
+            }
+            of = __any(of);
+            rp_vm_drain();   // this wave stored every byte of the row
+            if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
+            if (lane == 0)
+                rp_st_gran(P.gran + (size_t)((s + 1) % kRpSlots) * C + gc,
+                           ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u));
+        }
+        // (e) the round's other outputs (read by later launches: plain stores)
+        if (have) {
+            for (int k = b + t; k < kstar; k += T) A.p_round[off + k] = s;
+            if (nx && cand && q == 0 && (done || K_last <= B)) atomicOr(&sbits[j >> 5], 1u << (j & 31));
+        }
+        if (t == 0) {
+            A.wstat[(size_t)s * C + gc] = have ? ((kstar > b) ? 2 : 1) : 0;
+            A.wflag[(size_t)(s + 1) * C + gc] = nx ? 1 : 0;
+            A.Bm[(size_t)(s + 1) * C + gc] = kstar;
+            if (nx) A.active[s] = 1;
+        }
+        if (nx) {
+            const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
+            for (int i = t; i < n; i += T) {
+                A.WLA[nrow + i] = Coord<CT>::la(raw_at(cur, pk, i));
+                const CT f = fd_at(cur, i, pk);
+                if constexpr (K::CSZ == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
+                else A.WFD[nrow + i] = f;
+            }
+            rp_lds_barrier();
+            const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
+            for (int wd = t; wd < A.nw; wd += T)
+                A.Smat[srow + wd] = (uint64_t)sbits[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sbits[2 * wd + 1] : 0) << 32);
+        }
+        // (f) the next round's window, staged while the other chains finish
+        b = kstar;
+        cur ^= 1;
+        __syncthreads();   // every read of this round's LDS is done
+        if (b < len) stage(b, cur);
+    }
+    rp_vm_drain();   // no LDS-DMA outlives the workgroup
+    if (failed) {
+        if (t == 0) __hip_atomic_store((gu32*)P.st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (t == 0) {
+        if (s < P.r_end) {   // W'_s empty: round s has no events (the per-launch step's outputs)
+            A.wstat[(size_t)s * C + gc] = 0;
+            A.wflag[(size_t)(s + 1) * C + gc] = 0;
+            A.Bm[(size_t)(s + 1) * C + gc] = len;
+            if (gc == 0) { P.st[2] = 1; }
+        }
+        if (gc == 0) P.st[1] = s;
+    }
+    (void)t_start;
+}
+
+// W'_{r} rows (row-major, rebased to base(r)) and their granules before the first launch of
+// a DivideRounds, from the WFD rows k_round_gather wrote. One workgroup per chain.
+template <typename CT>
+__global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
+    const RoundArgs& A = P.A;
+    const int gc = blockIdx.x, n = A.n, C = A.C, g = gc / n, r = P.r0;
+    const int b = A.Bm[(size_t)r * C + gc];
+    const bool have = b < A.c_len[gc];
+    bool of = false;
+    const CT* __restrict__ row = (const CT*)A.WFD + ((size_t)r * C + gc) * n;
+    for (int d = threadIdx.x; d < ndw; d += 64) {
+        uint32_t w = 0;
+        for (int u = 0; u < 4; u++) {
+            const int i = 4 * d + u;
+            uint32_t v = 127u;
+            if (have && i < n) {
+                const int32_t f = Coord<CT>::fd(row[i]);
+                if (f != kMaxI32) {
+                    const int32_t bs = A.c_base[g * n + i] + (r > 0 ? A.Bm[(size_t)(r - 1) * C + g * n + i] : 0);
+                    const int32_t x = f - bs + 1;
+                    if (x > 126) of = true;
+                    else v = (uint32_t)x;
+                }
+            }
+            w |= v << (8 * u);
+        }
+        P.FD8p[((size_t)(r & 1) * C + gc) * ndw + d] = w;
+    }
+    of = __any(of);
+    if (threadIdx.x == 0)
+        P.gran[(size_t)(r % kRpSlots) * C + gc] =
+            ((uint64_t)(uint32_t)(r + 1) << 32) | (uint32_t)b | (have ? kRpEx : 0u) | (of ? kRpOv : 0u);
+}
+
+template <typename CT, int NDW, int Q>
+static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus) {
+    typedef RpCfg<CT, NDW, Q> K;
+    const void* f = (const void*)k_round_p<CT, NDW, Q>;
+    static bool attr = false;
+    static int per_cu = 0;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+        if (e != hipSuccess) return e;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, K::T, K::LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    // every workgroup must be resident at once (they wait for each other): one per CU
+    if (per_cu < 1 || P.A.C > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL((k_round_p<CT, NDW, Q>), dim3(P.A.C), dim3(K::T), K::LDS, st, P);
+    return hipGetLastError();
+}
+
+template <typename CT>
+static hipError_t rp_launch_t(hipStream_t st, const RoundPArgs& P, int num_cus) {
+    switch (round_k_ndw(P.A.n)) {
+        case 2: return rp_launch<CT, 2, 2>(st, P, num_cus);
+        case 4: return rp_launch<CT, 4, 4>(st, P, num_cus);
+        case 8: return rp_launch<CT, 8, 2>(st, P, num_cus);
+        case 16: return rp_launch<CT, 16, 4>(st, P, num_cus);
+        case 32: return rp_launch<CT, 32, 4>(st, P, num_cus);
+        case 64: return rp_launch<CT, 64, 4>(st, P, num_cus);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool round_p_ok(int n, int C, int num_cus) { return n >= 1 && n <= 256 && C <= num_cus; }
+
+hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
+                          int r0, int r_end, int init, int num_cus) {
+    RoundPArgs P{};
+    P.A = A;
+    P.FD8p = FD8p;
+    P.gran = gran;
+    P.st = status;
+    P.r0 = r0;
+    P.r_end = r_end;
+    P.tmo = 5000000;   // 50 ms per wait (a round takes microseconds)
+    if (init) {
+        if (A.compact) hipLaunchKernelGGL(k_round_p_init<uint16_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
+        else hipLaunchKernelGGL(k_round_p_init<int32_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return A.compact ? rp_launch_t<uint16_t>(st, P, num_cus) : rp_launch_t<int32_t>(st, P, num_cus);
+}
+
+}  // namespace hgx

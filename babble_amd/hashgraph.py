@@ -410,12 +410,13 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(13, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 13)
+        out = np.zeros(16, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 16)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
                     la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
-                    la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]))
+                    la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]),
+                    round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
@@ -430,8 +431,10 @@ class Hashgraph:
             raise ValueError(f"invalid lastAncestors kernel {mode}")
 
     def set_round_kernel(self, mode):
-        """DivideRounds step (n <= 256): "candidate" (default) or "block" (block binary search)."""
-        m = {"candidate": 0, "block": 1}[mode] if isinstance(mode, str) else int(mode)
+        """DivideRounds rounds: "auto" (default: the persistent recurrence where it applies, else
+        per-round "candidate" launches), "block" (block binary search per round) or "candidate"
+        (one launch per round, one lane per candidate)."""
+        m = {"auto": 0, "persistent": 0, "block": 1, "candidate": 2}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
 

@@ -307,7 +307,9 @@ int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_k
  * DivideRounds: lastAncestors rows recomputed, 1 if it rebuilt the layout (0: incremental),
  * the first round step it ran, 1 if the lastAncestors pass was the dataflow kernel; then
  * the number of dataflow passes that gave up and were redone by the sweeps, and the time
- * segments of the last dataflow pass (up to 13 values) */
+ * segments of the last dataflow pass; then the persistent round launches so far and the
+ * DivideRounds calls whose persistent launch gave up and were redone per round, and the
+ * candidate rows it counted with exact compares (over 8 bits) (up to 16 values) */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
  * name of the kernel, summed device ms (the round steps time one hipGraph replay in four and
@@ -329,9 +331,12 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
  * to the fixed point (hgx_kernels.hip), m >= 2 = the dataflow pass with m time segments on
  * a rebuild (measurement). Same results. */
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
-/* DivideRounds round step: 0 = one lane per candidate, 8-bit rebased compares (default,
- * hgx_round_k.hip; candidates in chunks of 128 above n = 256), 1 = block binary search
- * (hgx_rounds.hip; per-candidate search over streamed rows above n = 256). Same results. */
+/* DivideRounds rounds: 0 = default: the persistent recurrence (hgx_round_p.hip, one resident
+ * workgroup per chain runs every round in one launch) where it applies (n <= 256, at most one
+ * chain per compute unit, no roots), otherwise one launch per round of mode 2;
+ * 1 = block binary search per round (hgx_rounds.hip; per-candidate search over streamed rows
+ * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
+ * (hgx_round_k.hip; candidates in chunks of 128 above n = 256). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds schedule: 1 = incremental (default: a call after more InsertEvents extends
  * lastAncestors/firstDescendants for the new events only and resumes the round steps at the
