@@ -76,6 +76,9 @@ def lib():
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_insert_events_device", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_reset_consensus", i32, [p])
+    _sig(L, "hgx_save", i32, [p, C.c_char_p, E])
+    _sig(L, "hgx_checksum", u64, [p, i64])
+    _sig(L, "hgx_bootstrap", i32, [p, C.c_char_p, E])
     _sig(L, "hgx_clear", i32, [p])
     for nm in ("hgx_divide_rounds", "hgx_decide_fame", "hgx_find_order", "hgx_run_consensus"):
         _sig(L, nm, i32, [p, E])

@@ -468,6 +468,181 @@ int32_t hgx_clear(hgx_ctx* c) {
     return HGX_OK;
 }
 
+// ---- checkpoint file + Bootstrap (hashgraph.go:1008-1037, badger_store.go:345-386) ----------
+// Format: include/hgx.h. The file is the replay log Bootstrap needs: the events in topological
+// (gid) order with the columns consensus reads, plus the roots of a context after a Reset.
+static const char kCkptMagic[8] = {'H', 'G', 'X', 'C', 'K', 'P', 'T', '1'};
+
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+uint64_t hgx_checksum(const void* data, int64_t bytes) {
+    return fnv1a(14695981039346656037ull, data, bytes > 0 && data ? (size_t)bytes : 0);
+}
+
+namespace {
+struct CkptWriter {
+    FILE* f;
+    uint64_t h = 14695981039346656037ull;
+    bool ok = true;
+    void put(const void* p, size_t n) {
+        if (!ok || n == 0) return;
+        h = fnv1a(h, p, n);
+        ok = std::fwrite(p, 1, n, f) == n;
+    }
+};
+struct CkptReader {
+    std::vector<uint8_t> buf;
+    size_t pos = 0;
+    bool get(void* p, size_t n) {
+        if (buf.size() - pos < n) return false;
+        if (n) std::memcpy(p, buf.data() + pos, n);
+        pos += n;
+        return true;
+    }
+};
+}  // namespace
+
+int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
+    if (!c || !path) {
+        set_err(err, HGX_ERR_INVALID, "hgx_save: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    std::vector<int32_t> creator, index, sp, op, ntx;
+    std::vector<int64_t> ts;
+    std::vector<uint8_t> S, coin, nil;
+    hipError_t e = c->eng.get_columns(creator, index, sp, op, ts, S, coin, ntx, nil);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_save");
+    const int64_t E = (int64_t)creator.size();
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) {
+        set_err(err, HGX_ERR_INVALID, std::string("hgx_save: cannot open ") + tmp);
+        return HGX_ERR_INVALID;
+    }
+    CkptWriter w{f};
+    const uint32_t version = 1;
+    const int32_t flags = c->rooted ? 1 : 0;
+    w.put(kCkptMagic, 8);
+    w.put(&version, 4);
+    w.put(&c->n, 4);
+    w.put(&c->G, 4);
+    w.put(&flags, 4);
+    w.put(&E, 8);
+    if (c->rooted) {
+        w.put(c->root_index.data(), (size_t)c->C * 4);
+        w.put(c->root_round.data(), (size_t)c->C * 4);
+        std::vector<uint8_t> y(c->root_y_ext.begin(), c->root_y_ext.end());
+        y.resize(((size_t)c->C + 3) & ~(size_t)3, 0);
+        w.put(y.data(), y.size());
+    }
+    std::vector<int64_t> wide((size_t)E);
+    w.put(creator.data(), (size_t)E * 4);
+    for (auto* col : {&index, &sp, &op}) {
+        for (int64_t i = 0; i < E; i++) wide[(size_t)i] = (*col)[(size_t)i];
+        w.put(wide.data(), (size_t)E * 8);
+    }
+    w.put(ts.data(), (size_t)E * 8);
+    w.put(S.data(), (size_t)E * 32);
+    w.put(coin.data(), (size_t)E);
+    w.put(ntx.data(), (size_t)E * 4);
+    w.put(nil.data(), (size_t)E);
+    const uint64_t sum = w.h;
+    w.put(&sum, 8);
+    const bool ok_w = w.ok && std::fflush(f) == 0;
+    std::fclose(f);
+    if (!ok_w || std::rename(tmp.c_str(), path) != 0) {
+        std::remove(tmp.c_str());
+        set_err(err, HGX_ERR_INVALID, std::string("hgx_save: write failed: ") + path);
+        return HGX_ERR_INVALID;
+    }
+    return ok(err);
+}
+
+int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
+    if (!c || !path) {
+        set_err(err, HGX_ERR_INVALID, "hgx_bootstrap: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    auto bad = [&](const std::string& why) {
+        set_err(err, HGX_ERR_INVALID, "hgx_bootstrap: " + why);
+        return HGX_ERR_INVALID;
+    };
+    if (c->E != 0) return bad("the context already holds events (Bootstrap runs on a fresh Hashgraph)");
+    CkptReader r;
+    {
+        FILE* f = std::fopen(path, "rb");
+        if (!f) return bad(std::string("cannot open ") + path);
+        uint8_t tmp[1 << 16];
+        size_t got;
+        while ((got = std::fread(tmp, 1, sizeof tmp, f)) > 0) r.buf.insert(r.buf.end(), tmp, tmp + got);
+        std::fclose(f);
+    }
+    if (r.buf.size() < 8 + 4 + 12 + 8 + 8) return bad("truncated file");
+    uint64_t stored = 0;
+    std::memcpy(&stored, r.buf.data() + r.buf.size() - 8, 8);
+    if (fnv1a(14695981039346656037ull, r.buf.data(), r.buf.size() - 8) != stored) return bad("checksum mismatch");
+    char magic[8];
+    uint32_t version = 0;
+    int32_t n = 0, G = 0, flags = 0;
+    int64_t E = 0;
+    r.get(magic, 8);
+    r.get(&version, 4);
+    r.get(&n, 4);
+    r.get(&G, 4);
+    r.get(&flags, 4);
+    r.get(&E, 8);
+    if (std::memcmp(magic, kCkptMagic, 8) != 0) return bad("not a checkpoint file");
+    if (version != 1) return bad("unsupported version " + std::to_string(version));
+    if (n != c->n || G != c->G)
+        return bad("file has " + std::to_string(G) + " x " + std::to_string(n) + " participants, the context " +
+                   std::to_string(c->G) + " x " + std::to_string(c->n));
+    const size_t Ez = (size_t)E, Cz = (size_t)c->C;
+    const size_t need = (flags & 1 ? Cz * 8 + ((Cz + 3) & ~(size_t)3) : 0) + Ez * (4 + 8 * 4 + 32 + 1 + 4 + 1) + 8;
+    if (E < 0 || r.buf.size() - r.pos != need) return bad("truncated file");
+    if (E > c->eng.cap) return bad("the file has " + std::to_string(E) + " events, the context's capacity is " +
+                                   std::to_string(c->eng.cap));
+    if (flags & 1) {
+        std::vector<int32_t> ri(Cz), rr(Cz), ry(Cz);
+        std::vector<uint8_t> y((Cz + 3) & ~(size_t)3);
+        r.get(ri.data(), Cz * 4);
+        r.get(rr.data(), Cz * 4);
+        r.get(y.data(), y.size());
+        for (size_t p = 0; p < Cz; p++) ry[p] = y[p];
+        const int32_t rc = hgx_reset(c, ri.data(), rr.data(), ry.data(), err);
+        if (rc) return rc;
+    }
+    std::vector<int32_t> creator(Ez), ntx(Ez), nil(Ez);
+    std::vector<int64_t> index(Ez), sp(Ez), op(Ez), ts(Ez);
+    std::vector<uint8_t> S(Ez * 32), coin(Ez), nil8(Ez), hash(Ez * 32, 0);
+    r.get(creator.data(), Ez * 4);
+    r.get(index.data(), Ez * 8);
+    r.get(sp.data(), Ez * 8);
+    r.get(op.data(), Ez * 8);
+    r.get(ts.data(), Ez * 8);
+    r.get(S.data(), Ez * 32);
+    r.get(coin.data(), Ez);
+    r.get(ntx.data(), Ez * 4);
+    r.get(nil8.data(), Ez);
+    for (size_t i = 0; i < Ez; i++) {
+        hash[32 * i + 16] = coin[i] ? 1 : 0;   // the byte middleBit reads (hashgraph.go:1039-1048)
+        nil[i] = nil8[i];
+    }
+    hgx_events ev{creator.data(), index.data(), sp.data(), op.data(), ts.data(), hash.data(), S.data(), ntx.data(),
+                  nil.data()};
+    int64_t inserted = 0;
+    int32_t rc = hgx_insert_events(c, &ev, E, &inserted, err);
+    if (rc) return rc;
+    return hgx_run_consensus(c, err);
+}
+
 // ---- Reset (hashgraph.go:877-895, inmem_store.go:184-192) ---------------------------------
 // Store.Reset: new roots, the event / round / consensus caches and the participants'
 // RollingIndexes cleared, lastRound = -1 (the block cache is kept). Hashgraph.Reset:

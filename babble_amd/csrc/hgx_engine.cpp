@@ -436,6 +436,25 @@ hipError_t Engine::get_events(std::vector<int32_t>& creator, std::vector<int32_t
     return hipStreamSynchronize(stream);
 }
 
+hipError_t Engine::get_columns(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
+                               std::vector<int32_t>& op, std::vector<int64_t>& ts, std::vector<uint8_t>& S,
+                               std::vector<uint8_t>& coin, std::vector<int32_t>& ntx, std::vector<uint8_t>& txnil) {
+    HGX_TRY(get_events(creator, index, sp, op));
+    const size_t e = (size_t)E;
+    ts.resize(e);
+    S.resize(e * 32);
+    coin.resize(e);
+    ntx.resize(e);
+    txnil.resize(e);
+    if (e == 0) return hipSuccess;
+    HGX_TRY(hipMemcpyAsync(ts.data(), g_ts.p, e * 8, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(S.data(), g_S.p, e * 32, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(coin.data(), g_coin.p, e, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(ntx.data(), g_ntx.p, e * 4, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipMemcpyAsync(txnil.data(), g_txnil.p, e, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
 hipError_t Engine::get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil) {
     uint8_t nil = 0;
     HGX_TRY(hipMemcpyAsync(ts, g_ts.p + gid, 8, hipMemcpyDeviceToHost, stream));

@@ -105,6 +105,10 @@ class Engine {
     hipError_t get_events(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
                           std::vector<int32_t>& op);
     hipError_t get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil);
+    // every column of the inserted events (gid order) for a checkpoint (hgx_save)
+    hipError_t get_columns(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
+                           std::vector<int32_t>& op, std::vector<int64_t>& ts, std::vector<uint8_t>& S,
+                           std::vector<uint8_t>& coin, std::vector<int32_t>& ntx, std::vector<uint8_t>& txnil);
     hipError_t divide_rounds(int64_t E, const std::vector<int32_t>& chain_len,
                              const std::vector<int32_t>& chain_base, RoundsHost& out);
     // fame of the witnesses of rounds >= r0 (the first undecided round); rows below stay 0

@@ -341,7 +341,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         bool done = false;
         const bool wave_cand = __any(cand) && have;
         const bool wave_ov = __any(ov) && have;
-        for (int w_it = 0; have; w_it++) {
+        for (;have;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
 #pragma unroll 1

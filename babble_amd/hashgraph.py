@@ -11,6 +11,7 @@ marshals arrays.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -132,6 +133,16 @@ class Hashgraph:
     def RunConsensus(self):
         """node/core.go:277-303"""
         self._call(self.L.hgx_run_consensus)
+
+    def save(self, path: str):
+        """Checkpoint of the resident events (hgx_save; the BadgerStore's topological event log,
+        badger_store.go:309-343). Format: include/hgx.h, babble_amd/checkpoint.py."""
+        self._call(lambda ctx, e: self.L.hgx_save(ctx, os.fsencode(path), e))
+
+    def Bootstrap(self, path: str):
+        """Hashgraph.Bootstrap (hashgraph.go:1008-1037) from a checkpoint file: replay the events
+        in topological order, then DivideRounds / DecideFame / FindOrder once (hgx_bootstrap)."""
+        self._call(lambda ctx, e: self.L.hgx_bootstrap(ctx, os.fsencode(path), e))
 
     def set_commit_callback(self, fn):
         """commitCh (hashgraph.go:848-854): fn(graph, block, rr, first, n_events, n_tx) for every new

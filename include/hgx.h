@@ -154,6 +154,28 @@ int32_t hgx_reset_consensus(hgx_ctx* ctx);
  * the device allocations kept. */
 int32_t hgx_clear(hgx_ctx* ctx);
 
+/* ---- persistence: checkpoint file + Bootstrap (hashgraph.go:1008-1037) ----- */
+/* The reference persists the DAG in its BadgerStore (events under topological-index keys,
+ * badger_store.go:103-125, 309-343) and Hashgraph.Bootstrap replays them in topological order
+ * through InsertEvent, then runs DivideRounds / DecideFame / FindOrder once
+ * (dbTopologicalEvents, badger_store.go:345-386). The equivalent here is a binary SoA file of
+ * the resident events in gid (= topological) order, little-endian:
+ *   "HGXCKPT1" | u32 version 1 | i32 n | i32 graphs | i32 flags (1 = rooted) | i64 E
+ *   | rooted: i32 root_index[C], i32 root_round[C], u8 root_y_is_event[C], zero pad to 4
+ *   | i32 creator[E] | i64 index[E] | i64 self_parent[E] | i64 other_parent[E]
+ *   | i64 timestamp_ns[E] | u8 sig_s[E][32] | u8 coin[E] (Event.Hash byte 16 != 0)
+ *   | i32 ntx[E] | u8 tx_nil[E] | u64 FNV-1a of every preceding byte
+ * (C = graphs * n). It holds what consensus reads; bodies and signatures stay with the caller,
+ * as in hgx_insert_events. hgx_save writes it (atomically: a temporary file renamed over
+ * `path`). hgx_bootstrap = Bootstrap on a fresh context (no events inserted): checks the file
+ * (magic, version, n, graphs, checksum: HGX_ERR_INVALID "<reason>"), installs the roots of a
+ * rooted file (hgx_reset), inserts every event in order (hgx_insert_events; its Go error if one
+ * is rejected) and runs the three consensus calls once (hgx_run_consensus). */
+int32_t hgx_save(hgx_ctx* ctx, const char* path, hgx_error* err);
+/* the file's checksum: 64-bit FNV-1a of `bytes` bytes (host function, no device) */
+uint64_t hgx_checksum(const void* data, int64_t bytes);
+int32_t hgx_bootstrap(hgx_ctx* ctx, const char* path, hgx_error* err);
+
 /* ---- persistence: Reset / GetFrame (hashgraph.go:877-995, root.go) -------- */
 /* Hashgraph.Reset(roots): forget the events and rounds (keeping LastConsensusRound,
  * LastCommitedRoundEvents, ConsensusTransactions and the blocks, like the reference) and
