@@ -304,6 +304,14 @@ static int32_t finish_insert(hgx_ctx* c, const hgx::InsertOut& out, int64_t* n_i
             rc = HGX_ERR_SKIPPED_INDEX;
             msg = "SetEvent: " + go_rune(out.fail_index) + ", Skipped Index";
             break;
+        case hgx::INS_BAD_SIG:
+            rc = HGX_ERR_SIGNATURE;
+            msg = "Invalid signature";
+            break;
+        case hgx::INS_BAD_KEY:   // elliptic.Unmarshal returned nil; ecdsa.Verify dereferences it
+            rc = HGX_ERR_PANIC;
+            msg = "runtime error: invalid memory address or nil pointer dereference";
+            break;
         default:
             rc = HGX_ERR_INVALID;
             msg = "hgx_insert_events: index out of int32 range";
@@ -331,6 +339,60 @@ int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64
     hipError_t e = c->eng.insert(in, count, out);
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events");
     return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_set_participant_keys(hgx_ctx* c, const uint8_t* keys65, hgx_error* err) {
+    if (!c || !keys65) {
+        set_err(err, HGX_ERR_INVALID, "hgx_set_participant_keys: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    const hipError_t e = c->eng.set_keys(keys65);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_set_participant_keys");
+    return ok(err);
+}
+
+static int32_t insert_verified(hgx_ctx* c, const hgx_events* ev, const uint8_t* digest32, const uint8_t* sig_r32,
+                               int64_t count, int64_t* n_inserted, hgx_error* err, bool on_device) {
+    const char* who = on_device ? "hgx_insert_events_verified_device" : "hgx_insert_events_verified";
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !ev || count < 0 ||
+        (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
+                       !ev->hash || !ev->sig_s || !ev->ntx || !ev->tx_nil || !digest32 || !sig_r32)) ||
+        (on_device && (((uintptr_t)ev->sig_s & 15) || ((uintptr_t)ev->hash & 15)))) {
+        set_err(err, HGX_ERR_INVALID, std::string(who) + ": bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    if (!c->eng.keys_set) {
+        set_err(err, HGX_ERR_INVALID, std::string(who) + ": participant keys not set");
+        return HGX_ERR_INVALID;
+    }
+    hgx::InsertIn in{};
+    const uint8_t *dd = digest32, *dr = sig_r32;
+    if (on_device) {
+        in.creator = ev->creator; in.index = ev->index; in.sp = ev->self_parent; in.op = ev->other_parent;
+        in.ts = ev->timestamp_ns; in.hash = ev->hash; in.S = ev->sig_s; in.ntx = ev->ntx; in.nil = ev->tx_nil;
+    } else if (count > 0) {
+        hipError_t e = c->eng.stage_host(ev->creator, ev->index, ev->self_parent, ev->other_parent, ev->timestamp_ns,
+                                         ev->hash, ev->sig_s, ev->ntx, ev->tx_nil, count, in);
+        if (e == hipSuccess) e = c->eng.stage_sig(digest32, sig_r32, count, &dd, &dr);
+        if (e != hipSuccess) return dev_err(err, e, who);
+    }
+    hgx::InsertOut out;
+    const hipError_t e = c->eng.insert_verified(in, dd, dr, count, out);
+    if (e != hipSuccess) return dev_err(err, e, who);
+    return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_insert_events_verified(hgx_ctx* c, const hgx_events* ev, const uint8_t* digest32, const uint8_t* sig_r32,
+                                   int64_t count, int64_t* n_inserted, hgx_error* err) {
+    return insert_verified(c, ev, digest32, sig_r32, count, n_inserted, err, false);
+}
+
+int32_t hgx_insert_events_verified_device(hgx_ctx* c, const hgx_events* ev, const uint8_t* digest32,
+                                          const uint8_t* sig_r32, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    return insert_verified(c, ev, digest32, sig_r32, count, n_inserted, err, true);
 }
 
 // Core.Sync's loop (node/core.go:199-211) over a SyncResponse's WireEvents: ReadWireInfo

@@ -350,7 +350,52 @@ hipError_t Engine::stage_host(const int32_t* creator, const int64_t* index, cons
     return hipSuccess;
 }
 
+hipError_t Engine::set_keys(const uint8_t* keys65) {
+    HGX_TRY(pk_keys.alloc((size_t)C * 65 + 1));
+    HGX_TRY(pk_valid.alloc((size_t)C + 1));
+    HGX_TRY(pk_tab.alloc(p256_table_bytes(C) / 4 + 1));
+    HGX_TRY(hipMemcpyAsync(pk_keys.p, keys65, (size_t)C * 65, hipMemcpyHostToDevice, stream));
+    launch_p256_tables(stream, C, pk_keys.p, pk_tab.p, pk_valid.p);
+    HGX_TRY(hipGetLastError());
+    HGX_TRY(hipStreamSynchronize(stream));
+    keys_set = true;
+    return hipSuccess;
+}
+
+hipError_t Engine::stage_sig(const uint8_t* digest, const uint8_t* r, int64_t count, const uint8_t** d_digest,
+                             const uint8_t** d_r) {
+    const size_t c = (size_t)count * 32;
+    if (st_dig.n < c) HGX_TRY(st_dig.alloc(c));
+    if (st_r.n < c) HGX_TRY(st_r.alloc(c));
+    if (c) {
+        HGX_TRY(hipMemcpyAsync(st_dig.p, digest, c, hipMemcpyHostToDevice, stream));
+        HGX_TRY(hipMemcpyAsync(st_r.p, r, c, hipMemcpyHostToDevice, stream));
+    }
+    *d_digest = st_dig.p;
+    *d_r = st_r.p;
+    return hipSuccess;
+}
+
+hipError_t Engine::insert_verified(const InsertIn& in, const uint8_t* digest, const uint8_t* r, int64_t count,
+                                   InsertOut& out) {
+    if (!keys_set) return hipErrorNotReady;
+    if (count > 0) {
+        if (pk_out.n < (size_t)count) HGX_TRY(pk_out.alloc((size_t)count));
+        if (ins_fail_sig.n < 1) HGX_TRY(ins_fail_sig.alloc(1));
+        HGX_TRY(hipMemsetAsync(ins_fail_sig.p, 0xFF, 8, stream));
+        // Event.Verify of the whole batch (hgx_p256.hip; key = the creator's), then its first failure
+        launch_p256_verify(stream, count, C, in.creator, digest, r, in.S, pk_tab.p, pk_valid.p, pk_out.p);
+        launch_insert_sig_first(stream, count, C, in.creator, pk_out.p, ins_fail_sig.p);
+        HGX_TRY(hipGetLastError());
+    }
+    return insert_impl(in, count, out, count > 0 ? ins_fail_sig.p : nullptr);
+}
+
 hipError_t Engine::insert(const InsertIn& in, int64_t count, InsertOut& out) {
+    return insert_impl(in, count, out, nullptr);
+}
+
+hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig) {
     out = InsertOut();
     const int64_t E0 = E;
     InsertState st = insert_state();
@@ -358,10 +403,14 @@ hipError_t Engine::insert(const InsertIn& in, int64_t count, InsertOut& out) {
         HGX_TRY(hipMemsetAsync(ins_fail.p, 0xFF, 8, stream));
         launch_insert_claim(stream, count, E0, cap, C, in, st);
         launch_insert_check(stream, count, E0, cap, C, n, in, st);
-        unsigned long long fail = 0;
+        unsigned long long fail = 0, fsig = ~0ull;
         HGX_TRY(hipMemcpyAsync(h_small, ins_fail.p, 8, hipMemcpyDeviceToHost, stream));
+        if (fail_sig) HGX_TRY(hipMemcpyAsync(h_small + 2, fail_sig, 8, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
         std::memcpy(&fail, h_small, 8);
+        if (fail_sig) std::memcpy(&fsig, h_small + 2, 8);
+        // Verify comes first in InsertEvent: at the same event the signature's failure wins
+        if ((fsig >> 8) <= (fail >> 8) && fsig != ~0ull) fail = fsig;
         const int64_t m_ok = (fail == ~0ull) ? count : (int64_t)(fail >> 8);
         out.accepted = m_ok;
         out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
@@ -729,9 +778,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         const int ndw = round_k_ndw(n);
         if (FD8p.n < (size_t)2 * C * ndw) HGX_TRY(FD8p.alloc((size_t)2 * C * ndw));
         if (rp_gran.n < (size_t)4 * C) HGX_TRY(rp_gran.alloc((size_t)4 * C));
-        if (rp_st.n < 4) HGX_TRY(rp_st.alloc(4));
+        if (rp_st.n < (size_t)4 + G) HGX_TRY(rp_st.alloc((size_t)4 + G));
+        int32_t* fin = rp_st.p + 4;
         HGX_TRY(hipMemsetAsync(rp_gran.p, 0, (size_t)4 * C * 8, stream));   // no tag survives a call
-        int32_t s = r_lo;
+        HGX_TRY(hipMemsetAsync(fin, 0xFF, (size_t)G * 4, stream));          // no graph finished yet
+        int32_t s = r_lo, last = -1;
+        int finished = 0;
         for (int init = 1;; init = 0) {
             if (r_cap - 1 <= s + 1) {
                 HGX_TRY(ensure_round_cap(s + 64));
@@ -739,18 +791,23 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             }
             HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
             kbeg(K_ROUND_SEARCH);
-            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, s, r_cap - 1, init, num_cus));
+            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, init, num_cus));
             kend(K_ROUND_SEARCH, 0);
             HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipStreamSynchronize(stream));
             round_p_runs++;
             round_p_ovf += h_small[59];
             if (h_small[56] != 0) return hipErrorLaunchTimeOut;   // a workgroup gave up waiting
-            s = h_small[57];
-            if (h_small[58]) {
-                r_done = s + 1;
-                return hipSuccess;
+            last = std::max(last, h_small[57]);
+            finished += h_small[58];
+            if (finished >= G) {
+                r_done = last + 1;
+                // graphs that finished earlier: empty rows up to the last round (k_last_round,
+                // fame and the host copies read every graph's rows of every round)
+                launch_round_p_tail(stream, round_args(), fin, last);
+                return hipGetLastError();
             }
+            s = h_small[57];   // the round tables' capacity: continue from there
         }
     };
     if (!rooted && round_kernel == 0 && round_p_ok(n, C, num_cus)) {
@@ -880,6 +937,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     out.R = R;
     out.r_lo = std::min(r_lo, R);
     launch_wcoin(stream, a, out.r_lo, R, C);
+    HGX_TRY(hipGetLastError());
     // the host copies keep the rows below r_lo
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
@@ -925,9 +983,11 @@ hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
     if (R <= r0) return hipSuccess;
     DevArrays a = arrays();
     HGX_TRY(hipEventRecord(ph0, stream));
+    HGX_TRY(hipGetLastError());   // (an error left by DivideRounds' launches surfaces there, not here)
     kbeg(K_FAME);
     launch_fame(stream, a, r0, R, C, n, nw, sm, G, fame_tally);
     kend(K_FAME, 0);
+    HGX_TRY(hipGetLastError());
     const size_t o = (size_t)r0 * C;
     HGX_TRY(stage_d2h(fame_out.data() + o, fame.p + o, fame_out.size() - o));
     HGX_TRY(hipEventRecord(ph1, stream));

@@ -96,6 +96,15 @@ class Engine {
     // InsertEvent for `count` events whose columns are device pointers (hgx_insert_events_device)
     // or host pointers staged to HBM first (hgx_insert_events); validation and append on the GPU.
     hipError_t insert(const InsertIn& in, int64_t count, InsertOut& out);
+    // the same with Event.Verify first (hashgraph.go:356-363): digest (EventBody.Hash) and R per
+    // event, S = in.S, key = the creator's (set_keys); device pointers
+    hipError_t insert_verified(const InsertIn& in, const uint8_t* digest, const uint8_t* r, int64_t count,
+                               InsertOut& out);
+    hipError_t stage_sig(const uint8_t* digest, const uint8_t* r, int64_t count, const uint8_t** d_digest,
+                         const uint8_t** d_r);
+    // participants' public keys (65 bytes each, C of them): device window tables built once
+    hipError_t set_keys(const uint8_t* keys65);
+    bool keys_set = false;
     hipError_t stage_host(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
                           const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                           const int32_t* nil, int64_t count, InsertIn& in);
@@ -178,6 +187,7 @@ class Engine {
 
    private:
     hipError_t ensure_round_cap(int32_t need);
+    hipError_t insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig);
     InsertState insert_state();
     void kbeg(int k, bool sample = true, int64_t count = 1);
     void kend(int k, double bytes);
@@ -214,7 +224,11 @@ class Engine {
     // host-batch staging (hgx_insert_events)
     DBuf<int32_t> st_creator, st_ntx, st_nil;
     DBuf<int64_t> st_index, st_sp, st_op, st_ts;
-    DBuf<uint8_t> st_hash, st_S;
+    DBuf<uint8_t> st_hash, st_S, st_dig, st_r;
+    // signatures (Event.Verify): keys, window tables, per-event results, first failure
+    DBuf<uint8_t> pk_keys, pk_valid, pk_out;
+    DBuf<uint32_t> pk_tab;
+    DBuf<unsigned long long> ins_fail_sig;
     // chains
     DBuf<int32_t> c_off, c_len, c_base, c_old, fu, rcnt;
     // positions

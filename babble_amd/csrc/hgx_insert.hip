@@ -185,6 +185,29 @@ void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const 
     if (m_ok > 0) hipLaunchKernelGGL(k_insert_commit, dim3(grid), dim3(256), 0, s, m_ok, E0, n, in, st);
 }
 
+// Event.Verify's place in InsertEvent (hashgraph.go:356-363): the smallest event of the batch
+// whose signature failed (k << 8 | code, like the parent checks' first-failure word). A creator
+// id outside the participants has no key here; the reference verifies it with the key it
+// carries and then fails CheckSelfParent, which k_insert_check reports.
+__global__ void __launch_bounds__(256) k_insert_sig_first(int64_t m, int C, const int32_t* __restrict__ creator,
+                                                          const uint8_t* __restrict__ vout,
+                                                          unsigned long long* __restrict__ fail) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long w = ~0ull;
+    if (k < m) {
+        const int cr = creator[k];
+        const uint8_t v = vout[k];
+        if (cr >= 0 && cr < C && v != 1) w = ((unsigned long long)k << 8) | (v == 2 ? INS_BAD_KEY : INS_BAD_SIG);
+    }
+    w = wave_min_u64(w);
+    if (lane_id() == 0 && w != ~0ull) atomicMin(fail, w);
+}
+
+void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* creator, const uint8_t* vout,
+                             unsigned long long* fail) {
+    if (m > 0) hipLaunchKernelGGL(k_insert_sig_first, dim3(nblocks(m)), dim3(256), 0, s, m, C, creator, vout, fail);
+}
+
 void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
                            const InsertState& st) {
     if (m > m_ok)

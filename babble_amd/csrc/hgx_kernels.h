@@ -81,7 +81,8 @@ constexpr int64_t kRootY = -3, kRootOther = -4;
 // first-failure codes of the insert check (hgx_insert_events, hashgraph.go:356-401)
 enum InsertCode {
     INS_OK = 0, INS_KEY_NOT_FOUND = 1, INS_SELF_PARENT = 2, INS_OTHER_PARENT = 3, INS_CAPACITY = 4,
-    INS_PASSED_INDEX = 5, INS_SKIPPED_INDEX = 6, INS_INDEX_RANGE = 7
+    INS_PASSED_INDEX = 5, INS_SKIPPED_INDEX = 6, INS_INDEX_RANGE = 7,
+    INS_BAD_SIG = 8, INS_BAD_KEY = 9   // Event.Verify: invalid signature / creator key not a P-256 point
 };
 
 // arguments of the round step (hgx_rounds.hip)
@@ -160,11 +161,14 @@ int round_k_ndw(int n);
 // persistent round recurrence (hgx_round_p.hip): one resident workgroup per chain runs rounds
 // [r0, r_end) in one launch (init: W'_{r0}'s rebased rows and hand-off granules first, from
 // the WFD rows of launch_round_gather). status[0] != 0: a workgroup gave up waiting (bounded
-// spins), the rounds must be redone per launch; status[1] = the round it stopped at; status[2]
-// = 1 when W'_{status[1]} is empty (no round status[1]).
+// spins), the rounds must be redone per launch; status[1] = the largest round a graph stopped
+// at; status[2] = graphs that found W'_s empty in this launch (fin[g] = that s; fin preset to
+// -1 per DivideRounds, a finished graph's workgroups leave at once in a later launch).
+// launch_round_p_tail writes the empty rows of rounds (fin[g], r_last] of every graph.
 bool round_p_ok(int n, int C, int num_cus);
-hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status, int r0,
-                          int r_end, int init, int num_cus);
+hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
+                          int32_t* fin, int r0, int r_end, int init, int num_cus);
+void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, int r_last);
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,
@@ -174,6 +178,7 @@ void launch_round_first_gid(hipStream_t s, const DevArrays& a, int r0, int R, in
 void launch_last_round(hipStream_t s, int rs, int R, int G, int C, int n, const uint8_t* wstat, int32_t* lr);
 void step_prof_dump();     // -DHGX_STEP_PROF builds only
 void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
+void round_p_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
 // rounds [r0, R) (r0 = the first undecided round)
 void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n, int nw, int sm, int G, int tally);
@@ -215,5 +220,8 @@ void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int 
 void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st);
 void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
                            const InsertState& st);
+// verify results vout[k] (1 valid, 0 invalid, 2 key not a point) -> *fail = min (k << 8 | code)
+void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* creator, const uint8_t* vout,
+                             unsigned long long* fail);
 
 }  // namespace hgx

@@ -41,6 +41,41 @@ constexpr int kRpP = 31;       // probes per window (K in [0, 31], 5 binary-sear
 constexpr int kRpSlots = 4;    // granule ring slots (a slot is rewritten 4 rounds later)
 constexpr uint32_t kRpEx = 1u << 31, kRpOv = 1u << 30, kRpBm = (1u << 30) - 1;
 
+// Optional phase clocks (-DHGX_STEP_PROF, build variant "prof"): thread 0 of each workgroup adds
+// s_memtime deltas per phase of every round, flushed once at the end of the launch.
+#ifdef HGX_STEP_PROF
+__device__ unsigned long long hgx_rp_prof[8];
+#define RP_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define RP_PROF(i)                                                \
+    do {                                                          \
+        if (threadIdx.x == 0) {                                   \
+            const long long _t = clock64();                       \
+            _pa[i] += (unsigned long long)(_t - _pt);             \
+            _pt = _t;                                             \
+            if ((i) == 6) _pa[7] += 1;                            \
+        }                                                         \
+    } while (0)
+#define RP_PROF_END()                                                              \
+    do {                                                                           \
+        if (threadIdx.x == 0)                                                      \
+            for (int _i = 0; _i < 8; _i++)                                         \
+                if (_pa[_i]) atomicAdd(&hgx_rp_prof[_i], _pa[_i]);                 \
+    } while (0)
+void round_p_prof_dump() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
+    fprintf(stderr, "[hgx] k_round_p phases (clk sums, thread 0): window+rebase %llu poll %llu rows %llu search %llu "
+            "boundary %llu publish %llu outputs %llu | block-rounds %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
+}
+#else
+#define RP_PROF_BEGIN() (void)0
+#define RP_PROF(i) (void)0
+#define RP_PROF_END() (void)0
+void round_p_prof_dump() {}
+#endif
+
 // ---- write-through hand-off primitives (MI355X_MICROARCH.md, Valid forms, row 1) ----------
 __device__ __forceinline__ uint64_t rp_ld_gran(const uint64_t* p) {
     return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 load
@@ -157,7 +192,9 @@ struct RoundPArgs {
     RoundArgs A;
     uint32_t* FD8p;     // [2][C][ndw] rebased candidate rows, row-major (parity = round & 1)
     uint64_t* gran;     // [kRpSlots][C]
-    int32_t* st;        // [0] abort, [1] the round it stopped at, [2] 1: W'_{st[1]} empty, [3] rows over 8 bits
+    int32_t* st;        // [0] abort, [1] max over graphs of the round each stopped at, [2] graphs that
+                        // finished (W'_s empty) in this launch, [3] rows counted exactly (over 8 bits)
+    int32_t* fin;       // [G] the round at which graph g found W'_s empty (-1: not yet, this call)
     int r0, r_end;      // rounds [r0, r_end) at most
     long long tmo;      // one wait's budget in s_memrealtime ticks (100 MHz)
 };
@@ -180,6 +217,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     uint32_t* sbits = (uint32_t*)(lds + K::O_SB);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
 
+    if (P.fin[g] >= 0) return;   // the graph finished in an earlier launch of this DivideRounds
     const int len = A.c_len[gc], off = A.c_off[gc];
     for (int i = t; i < n; i += T) {
         cbase[i] = A.c_base[g0 + i];
@@ -282,9 +320,15 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
     };
 
+    // vector-memory instructions stage() issues per wave (explicit waits leave them in flight)
+    const bool dma16 = ((n * K::CSZ) & 15) == 0;
+    auto wait_all_but_dma = [&]() {   // every earlier memory operation of this wave but the staging
+        if (dma16) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K::KR16 + K::KF < 63 ? K::KR16 + K::KF : 63) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K::KR4 + K::KF < 63 ? K::KR4 + K::KF : 63) : "memory");
+    };
+    RP_PROF_BEGIN();
     int cur = 0;
     if (b < len) stage(b, 0);
-    const long long t_start = __builtin_amdgcn_s_memrealtime();
     int s = P.r0;
     bool failed = false;
     for (;; s++) {
@@ -293,31 +337,37 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         int32_t* bm_cur = (int32_t*)(lds + ((s & 1) ? K::O_BM1 : K::O_BM0));
         const bool have = b < len;   // block-uniform
         int kb = b, np = have ? min(kRpP, len - b) : 0;
-        // (a) this round's window (staged at the end of the previous round), rebased to base(s)
-        rp_vm_drain();
+        // (a) the first poll of this lane's candidate granule (W'_s, tag s + 1) goes out first and
+        // is in flight while this round's window (staged at the end of the previous round, before
+        // the poll) lands and is rebased to base(s). Every lane issues it (a clamped address for
+        // the lanes past n), so the vmcnt below covers exactly the staging.
+        const uint64_t* gp = P.gran + (size_t)(s % kRpSlots) * C + g0 + (jv ? j : 0);
+        uint64_t gv = rp_ld_gran(gp);
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // this wave's staging has landed
         if (t < 32) hist[t] = 0;
         if (t == 0) { misc[2] = 0; misc[3] = 0; }
         if (t < K::NC / 32 + 1) sbits[t] = 0;
-        __syncthreads();
+        rp_lds_barrier();
         if (have) rebase(cur, np, bm_prev);
         rp_lds_barrier();
+        RP_PROF(0);
 
-        // (b) poll the granules of this lane's candidate (W'_s, tag s + 1), then its row
-        const uint64_t* gp = P.gran + (size_t)(s % kRpSlots) * C + g0 + (jv ? j : 0);
-        uint64_t gv = 0;
+        // (b) poll until every candidate of this wave is published, then load their rows
         bool wfail = false;
         {
             const long long tw = __builtin_amdgcn_s_memrealtime();
             for (int spins = 0;; spins++) {
-                gv = jv ? rp_ld_gran(gp) : ((uint64_t)(uint32_t)(s + 1) << 32);
+                if (!jv) gv = (uint64_t)(uint32_t)(s + 1) << 32;
                 if (__all((uint32_t)(gv >> 32) == (uint32_t)(s + 1))) break;
                 if ((spins & 31) == 31) {
                     const long long now = __builtin_amdgcn_s_memrealtime();
                     if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);
+                gv = rp_ld_gran(gp);
             }
         }
+        RP_PROF(1);
         const uint32_t gval = (uint32_t)gv;
         const bool cand = jv && !wfail && (gval & kRpEx);
         const bool ov = cand && (gval & kRpOv);
@@ -335,13 +385,13 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         rp_vm_drain();
 #pragma unroll
         for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+        RP_PROF(2);
 
         // (c) search, window after window until the boundary is found (a later window is rare)
         int kstar = len, B = -1, K_last = kRpP, carried = 0;
         bool done = false;
         const bool wave_cand = __any(cand) && have;
-        const bool wave_ov = __any(ov) && have;
-        for (;have;) {
+        for (; have;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
 #pragma unroll 1
@@ -363,7 +413,6 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                             cnt += lav >= fdv ? 1u : 0u;
                         }
                     }
-                    (void)wave_ov;
                     cnt = rp_combine<Q>(cnt);
                     const bool seen = done || mid >= np || ((int)cnt >= sm && !(j == cl && kb + mid == b));
                     if (seen) hi = mid; else lo = mid + 1;
@@ -372,6 +421,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             const int Kw = lo;
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
             rp_lds_barrier();
+            RP_PROF(3);
             if (wave == 0) {   // boundary: first probe where #{K <= p} (+ seen in earlier windows) >= SM
                 const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
                 const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
@@ -401,42 +451,49 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             rp_lds_barrier();
         }
         if (!have) rp_lds_barrier();   // the pollers' any / fail words
+        RP_PROF(4);
         if (misc[3] != 0) { failed = true; break; }
         if (misc[2] == 0) break;       // W'_s is empty: no round s (every workgroup of the graph agrees)
 
-        // (d) publish W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s]), then the granule
+        // (d) publish W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s]), written
+        // through by wave 0; every wave then stages the next window (buffer cur ^ 1: the outputs
+        // below still read buffer cur); wave 0 drains its row stores, not the staging, and stores
+        // the granule
         const bool nx = kstar < len;
         const int pk = kstar - kb;
-        if (wave == 0) {
-            bool of = false;
-            if (nx) {
-                uint32_t* dst = P.FD8p + ((size_t)((s + 1) & 1) * C + gc) * NDW;
-                for (int d = lane; d < NDW; d += 64) {
-                    uint32_t w = 0;
+        bool of = false;
+        if (wave == 0 && nx) {
+            uint32_t* dst = P.FD8p + ((size_t)((s + 1) & 1) * C + gc) * NDW;
+            for (int d = lane; d < NDW; d += 64) {
+                uint32_t w = 0;
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const int i = 4 * d + u;
-                        uint32_t v = 127u;
-                        if (i < n) {
-                            const int32_t f = Coord<CT>::fd(fd_at(cur, i, pk));
-                            if (f != kMaxI32) {
-                                const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
-                                if (x > 126) of = true;
-                                else v = (uint32_t)x;
-                            }
+                for (int u = 0; u < 4; u++) {
+                    const int i = 4 * d + u;
+                    uint32_t v = 127u;
+                    if (i < n) {
+                        const int32_t f = Coord<CT>::fd(fd_at(cur, i, pk));
+                        if (f != kMaxI32) {
+                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
+                            if (x > 126) of = true;
+                            else v = (uint32_t)x;
                         }
-                        w |= v << (8 * u);
                     }
-                    rp_st_sc1(dst + d, w);
+                    w |= v << (8 * u);
                 }
+                rp_st_sc1(dst + d, w);
             }
+        }
+        if (nx) stage(kstar, cur ^ 1);
+        if (wave == 0) {
             of = __any(of);
-            rp_vm_drain();   // this wave stored every byte of the row
-            if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
+            if (nx) wait_all_but_dma();   // the row stores are done (the staging went out after them)
+            else rp_vm_drain();
             if (lane == 0)
                 rp_st_gran(P.gran + (size_t)((s + 1) % kRpSlots) * C + gc,
                            ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u));
+            if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
+        RP_PROF(5);
         // (e) the round's other outputs (read by later launches: plain stores)
         if (have) {
             for (int k = b + t; k < kstar; k += T) A.p_round[off + k] = s;
@@ -461,13 +518,13 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             for (int wd = t; wd < A.nw; wd += T)
                 A.Smat[srow + wd] = (uint64_t)sbits[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sbits[2 * wd + 1] : 0) << 32);
         }
-        // (f) the next round's window, staged while the other chains finish
         b = kstar;
         cur ^= 1;
-        __syncthreads();   // every read of this round's LDS is done
-        if (b < len) stage(b, cur);
+        rp_lds_barrier();   // every read of this round's LDS is done
+        RP_PROF(6);
     }
     rp_vm_drain();   // no LDS-DMA outlives the workgroup
+    RP_PROF_END();
     if (failed) {
         if (t == 0) __hip_atomic_store((gu32*)P.st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -477,11 +534,13 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             A.wstat[(size_t)s * C + gc] = 0;
             A.wflag[(size_t)(s + 1) * C + gc] = 0;
             A.Bm[(size_t)(s + 1) * C + gc] = len;
-            if (gc == 0) { P.st[2] = 1; }
+            if (cl == 0) {
+                P.fin[g] = s;
+                atomicAdd(&P.st[2], 1);
+            }
         }
-        if (gc == 0) P.st[1] = s;
+        if (cl == 0) atomicMax(&P.st[1], s);
     }
-    (void)t_start;
 }
 
 // W'_{r} rows (row-major, rebased to base(r)) and their granules before the first launch of
@@ -552,13 +611,31 @@ static hipError_t rp_launch_t(hipStream_t st, const RoundPArgs& P, int num_cus) 
 
 bool round_p_ok(int n, int C, int num_cus) { return n >= 1 && n <= 256 && C <= num_cus; }
 
+// rounds (fin[g], r_last] of the graphs that finished before r_last: empty rows, as the
+// per-launch step writes them for every chain of every round
+__global__ void k_round_p_tail(RoundArgs A, const int32_t* __restrict__ fin, int r_last) {
+    const int gc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gc >= A.C) return;
+    const int len = A.c_len[gc];
+    for (int r = fin[gc / A.n] + 1; r <= r_last; r++) {
+        A.wstat[(size_t)r * A.C + gc] = 0;
+        A.wflag[(size_t)(r + 1) * A.C + gc] = 0;
+        A.Bm[(size_t)(r + 1) * A.C + gc] = len;
+    }
+}
+
+void launch_round_p_tail(hipStream_t st, const RoundArgs& A, const int32_t* fin, int r_last) {
+    hipLaunchKernelGGL(k_round_p_tail, dim3((A.C + 255) / 256), dim3(256), 0, st, A, fin, r_last);
+}
+
 hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                          int r0, int r_end, int init, int num_cus) {
+                          int32_t* fin, int r0, int r_end, int init, int num_cus) {
     RoundPArgs P{};
     P.A = A;
     P.FD8p = FD8p;
     P.gran = gran;
     P.st = status;
+    P.fin = fin;
     P.r0 = r0;
     P.r_end = r_end;
     P.tmo = 5000000;   // 50 ms per wait (a round takes microseconds)

@@ -790,6 +790,7 @@ void step_prof_dump() {
     for (int i = 0; i < 8; i++) fprintf(stderr, " %d:%llu", i, h[i]);
     fprintf(stderr, "\n");
     round_k_prof_dump();
+    round_p_prof_dump();
 }
 #else
 void step_prof_dump() {}

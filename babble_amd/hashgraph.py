@@ -67,6 +67,51 @@ class Hashgraph:
         _lib.check(rc, err)
         return n_ins.value
 
+    def set_participant_keys(self, keys65):
+        """Participants' public keys (C x 65 bytes, participant id order) for Event.Verify."""
+        k = np.ascontiguousarray(keys65, np.uint8).reshape(-1, 65)
+        self._call(lambda ctx, e: self.L.hgx_set_participant_keys(ctx, ptr(k), e))
+
+    def insert_verified(self, t, digest32, r32, lo: int = 0, hi: Optional[int] = None) -> int:
+        """InsertEvent with Event.Verify (hgx_insert_events_verified): events [lo, hi) of a trace,
+        their body digests and signature R (S = the trace's S column). Raises HgxError on the first
+        rejected event, with .inserted = events inserted before it."""
+        hi = t.E if hi is None else hi
+        sl = slice(lo, hi)
+        a = dict(creator=np.ascontiguousarray(t.creator[sl], np.int32), index=np.ascontiguousarray(t.index[sl], np.int64),
+                 sp=np.ascontiguousarray(t.sp[sl], np.int64), op=np.ascontiguousarray(t.op[sl], np.int64),
+                 ts=np.ascontiguousarray(t.ts[sl], np.int64), h=np.ascontiguousarray(t.hash[sl], np.uint8),
+                 s=np.ascontiguousarray(t.s[sl], np.uint8), ntx=np.ascontiguousarray(t.ntx[sl], np.int32),
+                 nil=np.ascontiguousarray(t.txnil[sl], np.int32),
+                 d=np.ascontiguousarray(np.asarray(digest32)[sl], np.uint8),
+                 r=np.ascontiguousarray(np.asarray(r32)[sl], np.uint8))
+        ev = hgx_events(ptr(a["creator"]), ptr(a["index"]), ptr(a["sp"]), ptr(a["op"]), ptr(a["ts"]),
+                        ptr(a["h"]), ptr(a["s"]), ptr(a["ntx"]), ptr(a["nil"]))
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_events_verified(self.ctx, C.byref(ev), ptr(a["d"]), ptr(a["r"]), hi - lo,
+                                               C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        return n_ins.value
+
+    def insert_verified_device(self, dt: "DeviceTrace", d_digest, d_r, lo: int = 0, hi: Optional[int] = None) -> int:
+        """The same with every column resident in HBM (d_digest / d_r: device addresses of 32-byte rows)."""
+        hi = dt.E if hi is None else hi
+        ev = dt.events(lo, hi)
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_events_verified_device(self.ctx, C.byref(ev), C.c_void_p(int(d_digest) + 32 * lo),
+                                                      C.c_void_p(int(d_r) + 32 * lo), hi - lo, C.byref(n_ins),
+                                                      C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        return n_ins.value
+
     def insert_wire(self, creator_id, index, sp_index, op_creator, op_index, ts, hash32, s32, ntx, txnil) -> int:
         """Core.Sync's loop over WireEvents (hgx_insert_wire_events): ReadWireInfo + InsertEvent(e, false)
         per event; on the first error raises HgxError with .inserted = events inserted before it."""
@@ -489,6 +534,37 @@ class Hashgraph:
 
     def reset_stats(self):
         self.L.hgx_reset_stats(self.ctx)
+
+
+class DeviceBuffer:
+    """A host array copied to a buffer from hgx_device_alloc (libhgx's own HIP runtime)."""
+
+    def __init__(self, a: np.ndarray, device: int = 0):
+        self.L = _lib.lib()
+        self.device = device
+        a = np.ascontiguousarray(a)
+        self.nbytes = a.nbytes
+        self.p = C.c_void_p()
+        if self.L.hgx_device_alloc(device, max(1, a.nbytes), C.byref(self.p)) != 0:
+            raise HgxError(200, "hgx_device_alloc failed")
+        if a.nbytes and self.L.hgx_device_copy(device, self.p, ptr(a), a.nbytes, 1) != 0:
+            self.close()
+            raise HgxError(200, "hgx_device_copy failed")
+
+    @property
+    def addr(self) -> int:
+        return int(self.p.value or 0)
+
+    def close(self):
+        if getattr(self, "p", None) is not None and self.p.value:
+            self.L.hgx_device_free(self.device, self.p)
+            self.p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class DeviceTrace:

@@ -4,11 +4,16 @@
 Workload (BASELINE.json metric "consensus-ordered events/sec at N=256 peers"): one synthetic
 random-gossip hashgraph per GPU (configs[2]: 256 peers, 10M events, fits one MI355X), seeded
 per rank (weak scaling: independent 256-peer simulations, no data-path collective --
-DESIGN.md §6). The trace is resident in HBM before the clock starts. A step is one whole
-pass of the hot path, from the first event append to the order in host memory:
+DESIGN.md §6). The trace is in host RAM when the clock starts. A step is one whole pass of
+the hot path, from the first event append to the order in host memory:
 
-    hgx_clear -> hgx_insert_events_device (InsertEvent for every event: parent/index
-    validation + append, on the GPU) -> DivideRounds -> DecideFame -> FindOrder
+    hgx_clear -> hgx_insert_events (the event columns copied to HBM, InsertEvent for every
+    event: parent/index validation + append, on the GPU) -> DivideRounds -> DecideFame
+    -> FindOrder
+
+Side legs on the same line: the step with the columns already in HBM (hbm_resident), the
+SyncLimit-chunked schedule (chunked_sync), event ids (ingest_sha256), signature checks
+(ingest_p256_verify), and the InsertEvent pass with Event.Verify (insert_verify).
 
 After the timed steps (outside the clock) the run is checked: the GPU against the CPU oracle
 on a prefix of the same trace (every output, bit-exact), and the full-size result against
@@ -121,10 +126,23 @@ def prefix_parity(t, o, device):
             raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: {k} {a[k]} != {b[k]}")
     if [(x["rr"], x["ntx"], x["tx_nil"], x["committed"]) for x in a["blocks"]] != [tuple(x[:4]) for x in b["blocks"]]:
         raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: blocks")
+    # block hashes: SHA256(json(Block)) over the GPU order's transactions (block.go:26-53)
+    from babble_amd.hashgraph import block_hash
+    order = h.ConsensusEvents()
+    gh = []
+    for blk in h.Blocks():
+        txs = []
+        for g in order[blk["first"]:blk["first"] + blk["n_events"]]:
+            txs.extend(t.txs(int(g)) or [])
+        gh.append(block_hash(blk["rr"], txs, blk["tx_nil"]))
+    if gh != [x[4] for x in b["blocks"]]:
+        raise SystemExit(f"PARITY FAILURE on the {t.E}-event prefix: block hashes")
     h.close()
     return {"events": int(t.E), "ordered": int(len(b["order"])), "rounds": int(b["last_round"]) + 1,
+            "blocks": len(gh),
             "outputs": "round, witness, fame, round received, consensus timestamp, order, UndecidedRounds, "
-                       "LastConsensusRound, LastCommitedRoundEvents, counters, blocks", "result": "bit-exact"}
+                       "LastConsensusRound, LastCommitedRoundEvents, counters, blocks, block hashes",
+            "result": "bit-exact"}
 
 
 def full_size_checks(h, tr, G):
@@ -284,18 +302,18 @@ def ingest_leg(count, steps, warmup, device):
                          "blocks_per_launch": r["blocks"]}}
 
 
-def chunked_leg(h, dtr, tr, sync_limit, check):
+def chunked_leg(h, tr, sync_limit, check):
     """The real caller's schedule: Core.Sync inserts at most SyncLimit events
     (cmd/babble/main.go:83-85) and Core.RunConsensus follows every sync (node/core.go:190-303);
     the incremental DivideRounds/FindOrder work on the new events only. Wall clock over the
-    whole trace, inputs resident in HBM."""
+    whole trace; every sync's events come from host memory, as Core hands them over."""
     h.clear()
     h.set_kernel_timing(False)
     calls, worst = 0, 0.0
     t0 = time.perf_counter()
     for lo in range(0, tr.E, sync_limit):
         c0 = time.perf_counter()
-        h.insert_device(dtr, lo, min(tr.E, lo + sync_limit))
+        h.insert_trace(tr, lo, min(tr.E, lo + sync_limit))
         h.RunConsensus()
         worst = max(worst, time.perf_counter() - c0)
         calls += 1
@@ -425,31 +443,34 @@ def main():
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
     dev = device_of(local_rank)   # one GPU per rank (ranks share a GPU only in gloo rehearsals)
     h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
-    dtr = DeviceTrace(tr, device=dev)   # resident in HBM before the clock starts
 
     def step():
+        """from the first event append (the trace in host RAM, as the caller holds
+        it: the H2D copy of every event column is inside the step) to the order in host memory."""
         h.clear()
-        h.insert_device(dtr)
+        h.insert_trace(tr)
         h.DivideRounds()
         h.DecideFame()
         h.FindOrder()
         return sum(int(h.L.hgx_consensus_events_count(h.ctx, g)) for g in range(G))
 
-    # warmup: every kernel timed with HIP events, to rank the kernels
-    h.set_kernel_timing(True)
-    h.reset_stats()
+    h.set_kernel_timing(False)
     for w in range(max(1, args.warmup)):
         tw = time.time()
         ordered = step()
         log(f"[rank {rank}] warmup {w}: {ordered} ordered in {time.time() - tw:.2f}s  {h.phase_times()}")
-    ks_w = h.kernel_stats()
-    nw = max(1, args.warmup)
-    dom = max(ks_w, key=lambda k: ks_w[k]["ms"])   # ranked on the warmup passes
-    log(f"[rank {rank}] kernel profile (warmup, ms per pass): " +
+    # the kernels ranked on one post-warmup pass with every launch timed (HIP events on the
+    # context stream; no first-touch costs): the per-kernel table and the dominant kernel
+    h.set_kernel_timing(True)
+    h.reset_stats()
+    step()
+    ks_w, nw = h.kernel_stats(), 1
+    dom = max(ks_w, key=lambda k: ks_w[k]["ms"])
+    log(f"[rank {rank}] kernel profile (ms per pass / launches): " +
         ", ".join(f"{k}={v['ms'] / nw:.2f}/{v['launches'] // nw}" for k, v in
                   sorted(ks_w.items(), key=lambda kv: -kv[1]['ms'])))
 
-    # timed region: the dominant kernel alone is instrumented (HIP events on the context stream)
+    # timed region: the dominant kernel alone is instrumented
     h.set_kernel_timing(dom)
     h.reset_stats()
     red.barrier()
@@ -463,22 +484,23 @@ def main():
     total_all = red.sum(total)
     ks = h.kernel_stats()
     phases = h.phase_times()
-    # one more (untimed) pass with every kernel timed: the per-kernel table of the bench line
-    # (the warmup pass also pays first-touch costs)
-    h.set_kernel_timing(True)
-    h.reset_stats()
-    step()
-    ks_w, nw = h.kernel_stats(), 1
     h.set_kernel_timing(False)
 
-    # PCIe-inclusive variant: the same step with the trace in host memory
-    tp = time.perf_counter()
-    h.clear()
-    h.insert_trace(tr)
-    h.DivideRounds()
-    h.DecideFame()
-    h.FindOrder()
-    t_pcie = time.perf_counter() - tp
+    # side leg: the same step with the event columns already resident in HBM (no H2D)
+    dtr = DeviceTrace(tr, device=dev)
+
+    def step_hbm():
+        h.clear()
+        h.insert_device(dtr)
+        h.DivideRounds()
+        h.DecideFame()
+        h.FindOrder()
+
+    step_hbm()
+    th = time.perf_counter()
+    for _ in range(args.steps):
+        step_hbm()
+    t_hbm = (time.perf_counter() - th) / args.steps
 
     checks = {"full_size": "skipped"}
     if not args.no_check:
@@ -499,7 +521,7 @@ def main():
         dom_ms = r["ms"] / max(1, args.steps)
         dom_bytes = kernel_bytes(dom, n, tr.E, m_pass, phases["compact"])
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and dom_bytes else 0.0
-        traffic = None
+        traffic, valu = None, None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
             try:
@@ -507,6 +529,20 @@ def main():
                 traffic = tj.get("bytes_per_pass") if isinstance(tj, dict) else None
             except Exception:
                 traffic = None
+        vf = os.path.join(ROOT, "profiles", f"valu_{args.config}.json")
+        if os.path.exists(vf):
+            try:
+                vj = json.load(open(vf)).get(dom)
+                if isinstance(vj, dict) and vj.get("valu_insts_per_pass"):
+                    lane_ops = 64.0 * vj["valu_insts_per_pass"]
+                    v_ach = lane_ops / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else 0.0
+                    valu = {"achieved": v_ach, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                            "frac": v_ach / VALU_PEAK_TOPS, "valu_insts_per_pass": vj["valu_insts_per_pass"],
+                            "frac_profiled": vj.get("frac_profiled"),
+                            "source": f"profiles/valu_{args.config}.json (rocprofv3 --pmc SQ_INSTS_VALU, "
+                                      "64 lanes per wave instruction, over this line's ms_per_pass)"}
+            except Exception:
+                valu = None
         result = {
             "metric": "consensus-ordered events/sec at N=256 peers (1 GPU and 8-GPU batched sims)",
             "value": total_all / t_max,
@@ -519,25 +555,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded random-gossip traces, synthetic event ids/signatures), resident in HBM",
+            "data": "synthetic (seeded random-gossip traces, synthetic event ids/signatures), in host RAM at "
+                    "the start of every step (hgx_insert_events copies the columns to HBM inside the step)",
             "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
                        "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
                        "ordered_events_per_step_per_gpu": int(m_pass),
-                       "step": "clear + InsertEvent (device validation) + DivideRounds + DecideFame + FindOrder",
+                       "step": "clear + InsertEvent (H2D of the event columns + device validation) + DivideRounds "
+                               "+ DecideFame + FindOrder, order in host memory",
                        "parallelism": f"replicas x{world} (seed-sharded)",
                        "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
                        "dominant_kernel": dom},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "ms_per_pass": dom_ms, "launches_per_pass": r["launches"] // max(1, args.steps),
-                         "algorithmic_bytes_per_pass": dom_bytes,
+                         "algorithmic_bytes_per_pass": dom_bytes, "valu": valu,
                          "note": "per pass: SURVEY 8(d) bytes of the kernel's role over all its launches / "
-                                 "its summed device time; traffic = PMC bytes per pass (profiles/)"},
+                                 "its summed device time (HIP events on the context stream, timed steps); "
+                                 "traffic = PMC bytes per pass (profiles/traffic_<cfg>.json: FETCH_SIZE x2 only "
+                                 "for wide streaming kernels, Infinity-Cache hits included); valu = VALU issue "
+                                 "rate from SQ_INSTS_VALU (profiles/valu_<cfg>.json)"},
             "kernels_per_pass": per_pass,
-            "host_insert_pcie": {"value": total // max(1, args.steps) / t_pcie, "unit": "consensus-ordered events/s",
-                                 "ms_per_step": t_pcie * 1e3,
-                                 "note": "the same step with the trace in host memory (H2D of every event "
-                                         "column inside the timed step); not the headline"},
+            "hbm_resident": {"value": total // max(1, args.steps) / t_hbm, "unit": "consensus-ordered events/s",
+                             "ms_per_step": t_hbm * 1e3,
+                             "note": "the same step with the event columns already in HBM (hgx_insert_events_device, "
+                                     "no H2D inside the step); not the headline"},
             "checks": checks,
         }
         if not args.no_ingest:
@@ -551,7 +592,7 @@ def main():
                 result["ingest_p256_verify"] = {"error": str(e)}
         if G == 1 and not args.no_chunked:
             tcl = time.time()
-            result["chunked_sync"] = chunked_leg(h, dtr, tr, args.sync_limit, not args.no_check)
+            result["chunked_sync"] = chunked_leg(h, tr, args.sync_limit, not args.no_check)
             log(f"[rank {rank}] chunked schedule: {result['chunked_sync']['calls']} calls in "
                 f"{time.time() - tcl:.1f}s")
         if world == 1 and not args.no_cpu_baseline:

@@ -50,6 +50,7 @@ enum {
     HGX_ERR_OTHER_PARENT = 101, /* "CheckOtherParent: Other-parent not known" hashgraph.go:370,441 */
     HGX_ERR_INVALID = 102,      /* bad argument to the C ABI itself */
     HGX_ERR_CAPACITY = 103,     /* context capacity exceeded */
+    HGX_ERR_SIGNATURE = 104,    /* "Invalid signature" hashgraph.go:358-363 (Event.Verify false) */
     HGX_ERR_DEVICE = 200,       /* HIP error / no gfx950 device */
     HGX_ERR_PANIC = 300         /* the reference would panic here (e.g. UndecidedRounds[0] on empty) */
 };
@@ -104,6 +105,25 @@ int32_t hgx_insert_events(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int
  * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */
 int32_t hgx_insert_events_device(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
                                  hgx_error* err);
+/* Participants' public keys for Event.Verify: C = graphs * n_participants entries of 65 bytes
+ * (Body.Creator: the uncompressed P-256 point 0x04|X|Y, participant id order). The device
+ * window tables are built once here. A key that is not a P-256 point is accepted; an event it
+ * signs then fails as in the reference, where elliptic.Unmarshal returns nil and
+ * ecdsa.Verify dereferences it: HGX_ERR_PANIC "runtime error: invalid memory address or nil
+ * pointer dereference". */
+int32_t hgx_set_participant_keys(hgx_ctx* ctx, const uint8_t* keys65, hgx_error* err);
+/* InsertEvent including Event.Verify (hashgraph.go:356-363, event.go:142-152): every event's
+ * signature (R = sig_r32, S = ev->sig_s, 32 bytes big-endian each) is checked on the device
+ * against its creator's key (hgx_set_participant_keys) and its body digest digest32
+ * (EventBody.Hash: SHA-256 of the body JSON, event.go:48-54; hgx_sha256_batch computes it),
+ * in the same data-parallel pass as the parent checks. The batch stops at the first failing
+ * event; at one event the signature's failure ("Invalid signature", HGX_ERR_SIGNATURE) comes
+ * before its parent checks, as in the reference. Host pointers (copied to HBM), or device
+ * pointers (_device). HGX_ERR_INVALID "participant keys not set" without keys. */
+int32_t hgx_insert_events_verified(hgx_ctx* ctx, const hgx_events* ev, const uint8_t* digest32, const uint8_t* sig_r32,
+                                   int64_t count, int64_t* n_inserted, hgx_error* err);
+int32_t hgx_insert_events_verified_device(hgx_ctx* ctx, const hgx_events* ev, const uint8_t* digest32,
+                                          const uint8_t* sig_r32, int64_t count, int64_t* n_inserted, hgx_error* err);
 /* WireEvents (event.go:252-267) as a SyncResponse carries them (net/commands.go:10-15), the
  * caller having decoded the JSON: the participants' ids instead of hashes. */
 typedef struct {

@@ -14,6 +14,7 @@
  *                          expected = 1 valid / 0 invalid; key_ok = 0 when the public key is
  *                          not a P-256 point (Go's elliptic.Unmarshal returns nil)
  *   p256_ref check <file>  re-verify every line with libcrypto; exit 0 iff all agree
+ *   p256_ref sign <n_keys> <in> <out>  test signatures (derived keys) for a batch of digests
  *
  * Build: gcc -O2 -o oracle/_ref/p256_ref oracle/p256_ref.c -lcrypto  (oracle/Makefile)
  */
@@ -186,7 +187,60 @@ static int check(const char* path) {
     return (bad || lines == 0) ? 1 : 0;
 }
 
+/* sign <n_keys> <in> <out>: test signatures for libhgx's verified insert (tests/).
+ * Keys are derived, not random: private key k = SHA-256("hgx test key" | k) mod N.
+ * in = records {u32 key, u8 digest[32]}; out = n_keys public keys (65 B each), then per
+ * record R and S (32 B big-endian each) from ECDSA_do_sign (random nonces). */
+static int sign_file(int nk, const char* in, const char* out) {
+    FILE* fi = fopen(in, "rb");
+    FILE* fo = fopen(out, "wb");
+    if (!fi || !fo || nk <= 0) return 1;
+    const EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_X9_62_prime256v1);
+    const BIGNUM* N = EC_GROUP_get0_order(grp);
+    EC_KEY** keys = (EC_KEY**)calloc((size_t)nk, sizeof(EC_KEY*));
+    BN_CTX* ctx = BN_CTX_new();
+    for (int k = 0; k < nk; k++) {
+        uint8_t seed[16 + 4], h[32], pub[65];
+        memcpy(seed, "hgx test key \0\0\0", 16);
+        memcpy(seed + 16, &k, 4);
+        SHA256(seed, sizeof seed, h);
+        BIGNUM* d = BN_bin2bn(h, 32, NULL);
+        BN_mod(d, d, N, ctx);
+        if (BN_is_zero(d)) BN_one(d);
+        keys[k] = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+        EC_POINT* Q = EC_POINT_new(grp);
+        EC_POINT_mul(grp, Q, d, NULL, NULL, ctx);
+        EC_KEY_set_private_key(keys[k], d);
+        EC_KEY_set_public_key(keys[k], Q);
+        EC_POINT_point2oct(grp, Q, POINT_CONVERSION_UNCOMPRESSED, pub, 65, NULL);
+        fwrite(pub, 1, 65, fo);
+        EC_POINT_free(Q);
+        BN_free(d);
+    }
+    uint32_t key;
+    uint8_t dg[32], r[32], sg[32];
+    int rc = 0;
+    while (fread(&key, 4, 1, fi) == 1 && fread(dg, 1, 32, fi) == 32) {
+        if ((int)key >= nk) { rc = 2; break; }
+        ECDSA_SIG* sig = ECDSA_do_sign(dg, 32, keys[key]);
+        const BIGNUM *br, *bs;
+        ECDSA_SIG_get0(sig, &br, &bs);
+        put_bn(br, r);
+        put_bn(bs, sg);
+        fwrite(r, 1, 32, fo);
+        fwrite(sg, 1, 32, fo);
+        ECDSA_SIG_free(sig);
+    }
+    for (int k = 0; k < nk; k++) EC_KEY_free(keys[k]);
+    free(keys);
+    BN_CTX_free(ctx);
+    fclose(fi);
+    fclose(fo);
+    return rc;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 5 && !strcmp(argv[1], "sign")) return sign_file(atoi(argv[2]), argv[3], argv[4]);
     if (argc == 3 && !strcmp(argv[1], "gen")) return gen(argv[2]);
     if (argc == 3 && !strcmp(argv[1], "check")) return check(argv[2]);
     fprintf(stderr, "usage: p256_ref gen|check <file>\n");

@@ -447,6 +447,29 @@ def gossip_payload(creator: int, seq: int) -> bytes:
     return b"p%03d tx %08d" % (creator, seq)
 
 
+def sign_batch(n_keys: int, key_idx, digests):
+    """ECDSA P-256 signatures from libcrypto (oracle/p256_ref sign: derived keys, random nonces)
+    for digests[i] under key key_idx[i]. Returns (public keys [n_keys, 65], r [m, 32], s [m, 32])."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "p256_ref")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    key_idx = np.asarray(key_idx, np.uint32)
+    digests = np.ascontiguousarray(digests, np.uint8).reshape(-1, 32)
+    m = len(key_idx)
+    rec = np.zeros(m, dtype=[("k", "<u4"), ("d", "u1", 32)])
+    rec["k"], rec["d"] = key_idx, digests
+    with tempfile.TemporaryDirectory() as td:
+        fi, fo = os.path.join(td, "in"), os.path.join(td, "out")
+        rec.tofile(fi)
+        subprocess.check_call([exe, "sign", str(n_keys), fi, fo])
+        out = np.fromfile(fo, np.uint8)
+    keys = out[:65 * n_keys].reshape(n_keys, 65)
+    rs = out[65 * n_keys:].reshape(m, 64)
+    return keys, np.ascontiguousarray(rs[:, :32]), np.ascontiguousarray(rs[:, 32:])
+
+
 def oracle_run(t: Trace, chunk: Optional[int] = None) -> Oracle:
     """Insert a trace and run consensus: batch (Bootstrap-style, hashgraph.go:1008-1037)
     or every `chunk` inserted events (Core.RunConsensus after each sync)."""

@@ -1,6 +1,10 @@
 """HBM bytes per consensus pass per kernel role from two rocprofv3 PMC passes over
 `tools/phase_timing.py <cfg> 1` (one reset + DivideRounds + DecideFame + FindOrder):
-FETCH_SIZE (KB, x2 gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE (KB).
+FETCH_SIZE (KB) + WRITE_SIZE (KB). MI355X_MICROARCH.md (HBM): FETCH_SIZE reports half the
+bytes of a WIDE COALESCED STREAMING read (16 B per lane), so only the streaming roles
+(STREAMING below) get the x2 correction; gathers and hand-off reads are counted as read.
+FETCH_SIZE comes from the L2's memory-side requests: Infinity-Cache hits are included, so
+the figure is L2-miss traffic, an upper bound on HBM bytes.
 
   python tools/pmc_pass.py <fetch_counters.csv> <write_counters.csv> <out.json>
 
@@ -18,13 +22,17 @@ ROLES = {
     "la_sweep": r"k_la_sweep|k_la_wave",
     "fd_build": r"k_fd_build",
     "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin",
-    "round_search": r"k_round_k<|k_round_step",
+    "round_search": r"k_round_k<|k_round_step|k_round_p<",
     "fame": r"k_fame",
     "threshold": r"k_threshold|k_wla_transpose",
     "round_received": r"k_round_received",
     "cts_median": r"k_cts",
     "order_sort": r"k_radix|k_sort_small|k_tie|k_keys|k_scan|k_minmax|k_finish_order",
 }
+
+
+# roles whose reads are wide coalesced streams (16-byte lanes or LDS-DMA rows)
+STREAMING = {"layout", "la_sweep", "fd_build", "order_sort"}
 
 
 def load(path, counter):
@@ -44,10 +52,12 @@ def main():
         w = [v for k, vs in wr.items() if re.search(rx, k) for v in vs]
         if not f:
             continue
-        fetch = 2.0 * 1024.0 * sum(f)
+        corr = 2.0 if role in STREAMING else 1.0
+        fetch = corr * 1024.0 * sum(f)
         write = 1024.0 * sum(w)
-        res[role] = {"bytes_per_pass": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
-                     "dispatches": len(f), "bytes_per_launch": (fetch + write) / len(f)}
+        res[role] = {"bytes_per_pass": fetch + write, "fetch_bytes": fetch, "fetch_correction": corr,
+                     "write_bytes": write, "dispatches": len(f), "bytes_per_launch": (fetch + write) / len(f),
+                     "note": "L2 memory-side traffic (Infinity-Cache hits included)"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
