@@ -700,7 +700,9 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
     hgx_events ev{creator.data(), index.data(), sp.data(), op.data(), ts.data(), hash.data(), S.data(), ntx.data(),
                   nil.data()};
     int64_t inserted = 0;
+    c->eng.others_trust = true;   // Root.Others codes were checked when the events were first inserted
     int32_t rc = hgx_insert_events(c, &ev, E, &inserted, err);
+    c->eng.others_trust = false;
     if (rc) return rc;
     return hgx_run_consensus(c, err);
 }
@@ -728,8 +730,9 @@ int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_rou
         set_err(err, HGX_ERR_INVALID, "hgx_reset: roots need a single-graph context");
         return HGX_ERR_INVALID;
     }
-    if (c->eng.clear() != hipSuccess || c->eng.set_roots(rr, ye) != hipSuccess) return dev_err(err, hipErrorUnknown,
-                                                                                                  "hgx_reset");
+    if (c->eng.clear() != hipSuccess || c->eng.set_roots(rr, ye) != hipSuccess ||
+        c->eng.set_root_others(nullptr, 0) != hipSuccess)
+        return dev_err(err, hipErrorUnknown, "hgx_reset");
     c->root_index.assign(root_index, root_index + c->C);
     c->root_round = rr;
     c->root_y_ext = ye;
@@ -1033,6 +1036,9 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
         if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
         c->arena.used = base_off + (size_t)total;
     }
+    // committed blocks (graph, block index): commitCh receives them once the graph state
+    // (counters, pending, undetermined) is final for this call
+    std::vector<std::pair<int, int64_t>> commits;
     for (int g = 0; g < G; g++) {
         const int64_t mg = seg_len[g];
         if (mg == 0) continue;
@@ -1056,13 +1062,16 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
             b.tx_nil = (oh.blk_nil[bi] && b.ntx == 0) ? 1 : 0;
             b.committed = b.ntx > 0 ? 1 : 0;   // commitCh only if len(Transactions) > 0
             s.blocks.push_back(b);
-            if (b.committed && c->commit_fn)   // commitCh <- block, in SetBlock order
-                c->commit_fn(c->commit_user, g, (int64_t)s.blocks.size() - 1, b.rr, b.first, b.nev, b.ntx);
+            if (b.committed && c->commit_fn) commits.push_back({g, (int64_t)s.blocks.size() - 1});
             s.consensus_tx += b.ntx;
             s.pending_loaded -= oh.blk_loaded[bi];
             off += cnt;
         }
         s.undetermined -= mg;
+    }
+    for (const auto& gb : commits) {   // commitCh <- block, in SetBlock order
+        const Block& b = c->gs[gb.first].blocks[(size_t)gb.second];
+        c->commit_fn(c->commit_user, gb.first, gb.second, b.rr, b.first, b.nev, b.ntx);
     }
     return ok(err);
 }
@@ -1592,9 +1601,30 @@ int32_t hgx_set_la_kernel(hgx_ctx* c, int32_t mode) {
     return HGX_OK;
 }
 
+int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t count, hgx_error* err) {
+    if (!c || count < 0 || (count > 0 && !event_hash32)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_set_root_others: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (!c->rooted && count > 0) {
+        set_err(err, HGX_ERR_INVALID, "hgx_set_root_others: no roots installed (hgx_reset)");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    const hipError_t e = c->eng.set_root_others(event_hash32, count);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_set_root_others");
+    return ok(err);
+}
+
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
     c->eng.round_kernel = mode;
+    return HGX_OK;
+}
+
+int32_t hgx_set_cts_kernel(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
+    c->eng.cts_kernel = mode;
     return HGX_OK;
 }
 

@@ -3,6 +3,7 @@
 #include "hgx_engine.h"
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -323,6 +324,7 @@ InsertState Engine::insert_state() {
     st.last_gid = last_gid_d.p; st.last_index = last_index_d.p; st.chain_base = chain_base_d.p;
     st.fail = ins_fail.p; st.graph_loaded = graph_loaded_d.p;
     st.root_y_ext = root_y_ext_d.p; st.rooted = rooted ? 1 : 0;
+    st.others = others_d.p; st.n_others = n_others; st.others_trust = others_trust ? 1 : 0;
     return st;
 }
 
@@ -458,6 +460,23 @@ hipError_t Engine::set_roots(const std::vector<int32_t>& round, const std::vecto
     if (!rooted) root_gmax = -1;
     HGX_TRY(hipMemcpyAsync(root_round_d.p, round.data(), (size_t)C * 4, hipMemcpyHostToDevice, stream));
     HGX_TRY(hipMemcpyAsync(root_y_ext_d.p, y_ext.data(), (size_t)C, hipMemcpyHostToDevice, stream));
+    return hipStreamSynchronize(stream);
+}
+
+// Root.Others keys (event ids, 32 bytes each): sorted as 4 big-endian words for k_insert_check
+hipError_t Engine::set_root_others(const uint8_t* keys32, int64_t count) {
+    std::vector<std::array<uint64_t, 4>> k((size_t)count);
+    for (int64_t i = 0; i < count; i++)
+        for (int w = 0; w < 4; w++) {
+            uint64_t x = 0;
+            for (int b = 0; b < 8; b++) x = (x << 8) | keys32[32 * i + 8 * w + b];
+            k[(size_t)i][w] = x;
+        }
+    std::sort(k.begin(), k.end());
+    k.erase(std::unique(k.begin(), k.end()), k.end());
+    n_others = (int64_t)k.size();
+    if (others_d.n < (size_t)std::max<int64_t>(1, 4 * n_others)) HGX_TRY(others_d.alloc((size_t)std::max<int64_t>(1, 4 * n_others)));
+    if (n_others) HGX_TRY(hipMemcpyAsync(others_d.p, k.data(), (size_t)n_others * 32, hipMemcpyHostToDevice, stream));
     return hipStreamSynchronize(stream);
 }
 
@@ -1053,7 +1072,8 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
         return collect_kernel_times();
     }
     kbeg(K_CTS);
-    launch_cts(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt);
+    if (cts_kernel != 0 || !launch_cts_pipe(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt))
+        launch_cts(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt);
     int64_t own = 0;
     for (int c = shard_lo; c < shard_hi; c++) own += fo_cnt[c];
     kend(K_CTS, (double)own * (4.0 * n + 8.0 * n));

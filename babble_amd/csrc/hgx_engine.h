@@ -139,6 +139,8 @@ class Engine {
     // Roots (hgx_reset): per chain Root.Round and whether Root.Y is an event outside the store;
     // genesis roots (Round -1, Y "") when not rooted
     hipError_t set_roots(const std::vector<int32_t>& round, const std::vector<uint8_t>& y_ext);
+    hipError_t set_root_others(const uint8_t* keys32, int64_t count);   // Root.Others keys (event ids)
+    bool others_trust = false;   // checkpoint replay: Root.Others codes accepted without a key
     bool rooted = false;
     int root_gmax = -1;   // max Root.Round + 1 (rounds that root floors can force), -1 unrooted
     // smallest gid of a witness of each round in [r0, R) (UndecidedRounds order after a Reset)
@@ -181,6 +183,7 @@ class Engine {
     int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
     int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence where it applies (hgx_round_p.hip),
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
+    int cts_kernel = 0;       // hgx_set_cts_kernel: 0 pipelined resident blocks where they apply (hgx_cts.hip), 1 per-tile
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
     int64_t round_p_ovf = 0;   // candidate rows the persistent launches counted exactly (over 8 bits)
     int dev = 0;
@@ -204,6 +207,8 @@ class Engine {
     std::vector<int32_t> fo_cnt;       // [C] ... per chain
     DBuf<int32_t> root_round_d, gfl, gB, rfirst;   // roots: [C], per position floor, [(gmax+1) x C], [R]
     DBuf<uint8_t> root_y_ext_d;
+    DBuf<uint64_t> others_d;   // [n_others][4] sorted Root.Others keys
+    int64_t n_others = 0;
     DBuf<int32_t> sh_off;              // shard exchange: chain offsets
     DBuf<int64_t> sh_buf;              // ... and staging of host buffers
     // gid order

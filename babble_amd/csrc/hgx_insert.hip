@@ -52,6 +52,28 @@ __device__ __forceinline__ int64_t index_of(int64_t x, int64_t E0, const InsertI
 }
 
 // Checks in the reference's order: creator known (LastFrom -> KeyNotFound), self-parent,
+// Root.Others has an entry for the event with id h (the keys are sorted 32-byte strings)
+__device__ bool others_has(const InsertState& st, const uint8_t* h) {
+    uint64_t q[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint64_t x = 0;
+        for (int b = 0; b < 8; b++) x = (x << 8) | h[8 * w + b];
+        q[w] = x;
+    }
+    int64_t lo = 0, hi = st.n_others;
+    while (lo < hi) {   // first key >= q
+        const int64_t mid = (lo + hi) >> 1;
+        const uint64_t* kk = st.others + 4 * mid;
+        int cmp = 0;
+        for (int w = 0; w < 4 && cmp == 0; w++) cmp = kk[w] < q[w] ? -1 : kk[w] > q[w] ? 1 : 0;
+        if (cmp < 0) lo = mid + 1; else hi = mid;
+    }
+    if (lo >= st.n_others) return false;
+    const uint64_t* kk = st.others + 4 * lo;
+    return kk[0] == q[0] && kk[1] == q[1] && kk[2] == q[2] && kk[3] == q[3];
+}
+
 // other-parent (genesis Root only: "" or a known event of the same graph), capacity,
 // then the RollingIndex rules of SetEvent.
 __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int64_t cap, int C, int n, InsertIn in,
@@ -79,7 +101,8 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
         } else {
             // unknown other-parents only through the creator's Root (hashgraph.go:430-440):
             // Root.X == SelfParent && Root.Y == OtherParent, or Root.Others[event] == OtherParent
-            ok = (op == kRootY && sp == -1 && st.root_y_ext[cr]) || (op == kRootOther && st.rooted);
+            ok = (op == kRootY && sp == -1 && st.root_y_ext[cr]) ||
+                 (op == kRootOther && st.rooted && (st.others_trust || others_has(st, in.hash + 32 * k)));
         }
         if (!ok) code = INS_OTHER_PARENT;
     }

@@ -8,6 +8,7 @@
 namespace hgx {
 
 constexpr int32_t kMaxI32 = 2147483647;
+constexpr int32_t kWlatNotFamous = -2147483647 - 1;   // WLAT row of a witness that is not famous
 constexpr int kOpkBits = 21;   // p_opk: op row bits (chains of up to 2^21 rows use k_la_wave)
 
 // Raw device pointers of one context (see hgx_engine.h for meaning/sizes).
@@ -72,7 +73,10 @@ struct InsertState {
     unsigned long long* fail;           // min over failing events of (k << 8 | code)
     unsigned long long* graph_loaded;   // [G] loaded events inserted (IsLoaded, event.go:119-126)
     const uint8_t* root_y_ext;          // [C] Root.Y names an event outside the store (after hgx_reset)
-    int rooted;                         // a Reset installed roots (Root.Others codes accepted)
+    int rooted;                         // a Reset installed roots
+    const uint64_t* others;             // [n_others][4] Root.Others keys (event ids as 4 big-endian words, sorted)
+    int64_t n_others;
+    int others_trust;                   // accept every Root.Others code (checkpoint replay)
 };
 
 // other-parent codes for parents outside the store after a Reset (include/hgx.h)
@@ -192,6 +196,10 @@ void launch_fu_count(hipStream_t s, const DevArrays& a, int64_t E);         // f
 // the newly received events [fu, fu + rcnt) of chains [c_lo, c_lo + c_cnt) (max_cnt = the
 // largest rcnt among them)
 void launch_cts(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P, int max_cnt);
+// the same, pipelined (hgx_cts.hip): resident blocks, three tiles' loads in flight; false when
+// it does not apply (cts_pipe_ok) and nothing was launched
+bool cts_pipe_ok(int n, int C);
+bool launch_cts_pipe(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P, int max_cnt);
 // shard exchange: consensus timestamps of the newly received events of chains [lo, hi) to /
 // from a chain-major buffer (offs[c] = start of chain c)
 void launch_cts_shard_copy(hipStream_t s, const DevArrays& a, int lo, int hi, const int32_t* offs, int64_t* buf,

@@ -800,8 +800,10 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
 // WLAT[i][g][d][c] = WLA[i][g][c][d]: per round, the lastAncestors of the candidates
 // transposed so that "which witnesses of round i see chain d up to index j" is one
 // contiguous row (k_threshold, k_cts_*). 64 x 64 tiles through LDS; eligible rounds only.
+// The famous flag is folded in: the row of a witness that is not famous (or no witness) holds
+// kWlatNotFamous, below every Index and every lastAncestors value (-1 = sees none of d).
 __global__ void __launch_bounds__(256) k_wla_transpose(int R, int r0, int G, int C, int n,
-                                                       const uint8_t* __restrict__ elig,
+                                                       const uint8_t* __restrict__ elig, const uint8_t* __restrict__ fw,
                                                        const int32_t* __restrict__ WLA, int32_t* __restrict__ WLAT) {
     __shared__ int32_t t[64][65];
     const int ig = blockIdx.y, i = r0 + ig / G, g = ig % G;
@@ -810,7 +812,8 @@ __global__ void __launch_bounds__(256) k_wla_transpose(int R, int r0, int G, int
     const size_t base = ((size_t)i * C + (size_t)g * n) * n;
     for (int k = threadIdx.x; k < 64 * 64; k += 256) {
         const int r = k >> 6, col = k & 63, c = tc * 64 + r, d = td * 64 + col;
-        t[r][col] = (c < n && d < n) ? WLA[base + (size_t)c * n + d] : 0;
+        t[r][col] = (c < n && d < n) ? (fw[(size_t)i * C + (size_t)g * n + c] ? WLA[base + (size_t)c * n + d]
+                                                                               : kWlatNotFamous) : 0;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < 64 * 64; k += 256) {
@@ -833,7 +836,6 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
     if (!elig[(size_t)g * R + i]) return;
     __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
     const int lane = lane_id();
-    const size_t base = (size_t)i * C + (size_t)g * n;
     const size_t row = ((size_t)i * C + gd) * n;
     uint32_t v[CPL];   // int32 order as u32: sign bit flipped
     bool ok[CPL];
@@ -841,8 +843,8 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int c = lane + 64 * q;
-        ok[q] = c < n && fw[base + c];
-        const int32_t x = ok[q] ? WLAT[row + c] : 0;
+        const int32_t x = c < n ? WLAT[row + c] : kWlatNotFamous;
+        ok[q] = x != kWlatNotFamous;
         v[q] = (uint32_t)x ^ 0x80000000u;
         m += __popcll(__ballot(ok[q]));
     }
@@ -951,13 +953,12 @@ __global__ void __launch_bounds__(256) k_cts_small(const int32_t* __restrict__ f
     const int j = c_base[gc] + fu[gc] + e;
     const int i = p_rr[p];
     const size_t row = ((size_t)i * C + gc) * n;
-    const size_t fb = (size_t)i * C + (size_t)g * n;
     int64_t v[NP];
     uint32_t ok = 0;
 #pragma unroll
     for (int c = 0; c < NP; c++) {
         v[c] = 0;
-        if (c < n && fw[fb + c] && WLAT[row + c] >= j) {
+        if (c < n && WLAT[row + c] >= j) {
             const int ch = g * n + c;
             v[c] = p_ts[c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)c * Pcap + p])];
             ok |= 1u << c;
@@ -1061,10 +1062,9 @@ __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu
                 const bool in = i >= 0 && c < n;
                 const int cc = in ? c : 0;
                 const int ch = g * n + cc;
-                const uint8_t f = fw[fb + cc];
                 const int32_t w = WLAT[wrow + cc];
                 const int32_t k = c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)cc * Pcap + (in ? p : 0)]);
-                idx[u] = (in & (f != 0) & (w >= j)) ? k : -1;
+                idx[u] = (in & (w >= j)) ? k : -1;
             }
             int64_t x[U];
 #pragma unroll
@@ -1722,7 +1722,7 @@ void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n,
 void launch_wla_transpose(hipStream_t s, const DevArrays& a, int r0, int R, int G, int C, int n) {
     if (R <= r0) return;
     const int nt = (n + 63) / 64;
-    hipLaunchKernelGGL(k_wla_transpose, dim3(nt * nt, (R - r0) * G), dim3(256), 0, s, R, r0, G, C, n, a.elig, a.WLA,
+    hipLaunchKernelGGL(k_wla_transpose, dim3(nt * nt, (R - r0) * G), dim3(256), 0, s, R, r0, G, C, n, a.elig, a.fw, a.WLA,
                        a.WLAT);
 }
 

@@ -163,8 +163,12 @@ class Hashgraph:
     # ------------------------------------------------------------------ the consensus calls
     def _call(self, fn):
         err = hgx_error()
+        self._cb_error = None
         rc = fn(self.ctx, C.byref(err))
         _lib.check(rc, err)
+        cb_err, self._cb_error = getattr(self, "_cb_error", None), None
+        if cb_err is not None:   # a commit callback raised inside the call: re-raised here
+            raise cb_err
 
     def DivideRounds(self):
         self._call(self.L.hgx_divide_rounds)
@@ -191,13 +195,19 @@ class Hashgraph:
 
     def set_commit_callback(self, fn):
         """commitCh (hashgraph.go:848-854): fn(graph, block, rr, first, n_events, n_tx) for every new
-        block with transactions, from inside FindOrder; None removes it."""
+        block with transactions, at the end of FindOrder (after the counters are updated); None
+        removes it. An exception raised by fn is kept (later blocks are still delivered) and
+        re-raised when the FindOrder / RunConsensus call returns."""
         if fn is None:
             self._commit_cb = None
             rc = self.L.hgx_set_commit_callback(self.ctx, None, None)
         else:
             def tramp(_user, g, b, rr, first, nev, ntx):
-                fn(int(g), int(b), int(rr), int(first), int(nev), int(ntx))
+                try:
+                    fn(int(g), int(b), int(rr), int(first), int(nev), int(ntx))
+                except BaseException as ex:   # ctypes would print and drop it
+                    if getattr(self, "_cb_error", None) is None:
+                        self._cb_error = ex
             self._commit_cb = _lib.COMMIT_FN(tramp)   # kept alive while registered
             rc = self.L.hgx_set_commit_callback(self.ctx, C.cast(self._commit_cb, C.c_void_p), None)
         if rc:
@@ -206,14 +216,18 @@ class Hashgraph:
     # ------------------------------------------------------------------ Reset / GetFrame
     ROOT_Y, ROOT_OTHER = -3, -4   # other-parent codes after a Reset (hgx.h)
 
-    def Reset(self, root_index, root_round, root_y_is_event):
+    def Reset(self, root_index, root_round, root_y_is_event, others=None):
         """Hashgraph.Reset(roots) (hashgraph.go:877-895): per participant Root.Index, Root.Round and
-        whether Root.Y names an event. Then insert with self-parent -1 = Root.X and other-parent
+        whether Root.Y names an event; `others` = the 32-byte ids of the events the roots' Others
+        maps hold (hgx_set_root_others). Then insert with self-parent -1 = Root.X and other-parent
         ROOT_Y / ROOT_OTHER for parents outside the store."""
         a = [np.ascontiguousarray(x, np.int32) for x in (root_index, root_round, root_y_is_event)]
         err = hgx_error()
         rc = self.L.hgx_reset(self.ctx, *[ptr(x) for x in a], C.byref(err))
         _lib.check(rc, err)
+        if others is not None and len(others):
+            k = np.ascontiguousarray(others, np.uint8).reshape(-1, 32)
+            self._call(lambda ctx, e: self.L.hgx_set_root_others(ctx, ptr(k), k.shape[0], e))
 
     def GetFrame(self):
         """Hashgraph.GetFrame (hashgraph.go:897-995): roots (x, y, index, round per participant),
@@ -493,6 +507,13 @@ class Hashgraph:
         m = {"auto": 0, "persistent": 0, "block": 1, "candidate": 2}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
+
+    def set_cts_kernel(self, mode):
+        """FindOrder consensus timestamps: "auto" (default: pipelined resident blocks where they
+        apply) or "tile" (one tile of 8 positions per block)."""
+        m = {"auto": 0, "pipe": 0, "tile": 1}[mode] if isinstance(mode, str) else int(mode)
+        if self.L.hgx_set_cts_kernel(self.ctx, m) != 0:
+            raise ValueError(f"invalid timestamp kernel {mode}")
 
     def set_incremental(self, on: bool):
         """DivideRounds schedule: incremental (default) or full recompute on every call."""

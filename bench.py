@@ -355,6 +355,82 @@ def p256_leg(count, steps, warmup, device):
             "check": "bit-exact vs libcrypto 3.0.2 (ECDSA_do_verify)"}
 
 
+def _valid_signature_pool():
+    """libcrypto's valid (key, digest, r, s) rows of tests/golden/p256_vectors.txt, by key."""
+    pool = {}
+    with open(os.path.join(ROOT, "tests", "golden", "p256_vectors.txt")) as f:
+        for line in f:
+            pub, dg, r, s, exp, kok, _ = line.split()
+            if int(exp) == 1 and int(kok):
+                pool.setdefault(pub, []).append((dg, r, s))
+    return [(k, pool[k]) for k in sorted(pool)]
+
+
+def insert_verify_leg(h, tr, steps, ref, sha_ms, device):
+    """InsertEvent with Event.Verify (hashgraph.go:356-363, event.go:142-152) over the whole
+    headline trace: clear -> hgx_insert_events_verified_device (batched P-256 verify of every
+    event merged with the parent/index checks' first-failure rule) -> DivideRounds -> DecideFame
+    -> FindOrder, columns HBM-resident. Participant c signs with libcrypto fixture key c % K and
+    event (c, Index) carries that key's valid fixture signature number Index % len (the S column
+    is the signature's S, so the consensus tie-break runs on these S). Checked: every event is
+    accepted, and rounds / round received / timestamps equal the headline run's (they do not
+    depend on S). `ref` = (rr, cts) of the headline run."""
+    from babble_amd.hashgraph import DeviceBuffer, DeviceTrace
+    from babble_amd import trace as gtrace
+    pool = _valid_signature_pool()
+    nk = len(pool)
+    keys = np.stack([np.frombuffer(bytes.fromhex(pool[c % nk][0]), np.uint8) for c in range(h.n)])
+    per_key = [np.stack([np.stack([np.frombuffer(bytes.fromhex(x), np.uint8) for x in row]) for row in rows])
+               for _, rows in pool]                  # [K][rows][3][32]: digest, r, s
+    kk = (tr.creator % h.n) % nk
+    dig = np.empty((tr.E, 32), np.uint8)
+    sr = np.empty((tr.E, 32), np.uint8)
+    ss = np.empty((tr.E, 32), np.uint8)
+    for k in range(nk):
+        sel = np.nonzero(kk == k)[0]
+        if len(sel) == 0:
+            continue
+        rows = per_key[k]
+        pick = rows[tr.index[sel] % len(rows)]
+        dig[sel], sr[sel], ss[sel] = pick[:, 0], pick[:, 1], pick[:, 2]
+    t2 = gtrace.GossipTrace(**{**tr.__dict__, "s": ss})
+    dtr, dd, dr = DeviceTrace(t2, device=device), DeviceBuffer(dig, device), DeviceBuffer(sr, device)
+    del dig, sr, ss
+    h.set_participant_keys(np.stack([keys[p % h.n] for p in range(h.n * h.G)]))
+
+    def step():
+        h.clear()
+        ins = h.insert_verified_device(dtr, dd.addr, dr.addr)
+        h.DivideRounds()
+        h.DecideFame()
+        h.FindOrder()
+        return ins
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ins = step()
+    el = (time.perf_counter() - t0) / steps
+    rr, cts = h.received()
+    ok = ins == tr.E and np.array_equal(rr, ref[0]) and np.array_equal(cts, ref[1])
+    ordered = int(h.L.hgx_consensus_events_count(h.ctx, 0))
+    dtr.close(), dd.close(), dr.close()
+    if not ok:
+        raise SystemExit(f"INSERT-VERIFY CHECK FAILURE: accepted {ins} of {tr.E}, rr/cts equal to the headline: "
+                         f"{np.array_equal(rr, ref[0])}/{np.array_equal(cts, ref[1])}")
+    res = {"value": ordered / el, "unit": "consensus-ordered events/s", "ms_per_step": el * 1e3,
+           "signatures_verified_per_step": int(tr.E), "keys": nk,
+           "step": "clear + InsertEvent with Event.Verify (batched P-256 verify + parent/index checks, device) + "
+                   "DivideRounds + DecideFame + FindOrder, columns HBM-resident",
+           "check": "every event accepted; rounds received and consensus timestamps equal the headline run's",
+           "signatures": "libcrypto 3.0.2 fixture signatures (tests/golden/p256_vectors.txt), cycled per key"}
+    if sha_ms:
+        res["with_event_ids_ms"] = el * 1e3 + sha_ms
+        res["with_event_ids_value"] = ordered / (el + sha_ms * 1e-3)
+        res["with_event_ids_note"] = "plus one k_sha256_batch launch over the trace's event bodies (ingest_sha256)"
+    return res
+
+
 def device_of(local_rank):
     """The rank's GPU; ranks beyond the visible devices share them (gloo rehearsals on one GPU)."""
     try:
@@ -590,6 +666,16 @@ def main():
                 result["ingest_p256_verify"] = p256_leg(1 << 20, args.steps, args.warmup, dev)
             except Exception as e:  # reported, never fatal
                 result["ingest_p256_verify"] = {"error": str(e)}
+        if G == 1 and not args.no_ingest:
+            try:
+                sha = result.get("ingest_sha256", {}).get("ms_per_launch")
+                tv = time.time()
+                result["insert_verify"] = insert_verify_leg(h, tr, args.steps, h.received(), sha, dev)
+                log(f"[rank {rank}] insert+verify leg in {time.time() - tv:.1f}s")
+            except SystemExit:
+                raise
+            except Exception as e:  # reported, never fatal
+                result["insert_verify"] = {"error": str(e)}
         if G == 1 and not args.no_chunked:
             tcl = time.time()
             result["chunked_sync"] = chunked_leg(h, tr, args.sync_limit, not args.no_check)

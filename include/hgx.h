@@ -59,7 +59,8 @@ enum {
 /* After hgx_reset, other-parents outside the store that CheckOtherParent accepts through the
  * creator's Root (hashgraph.go:430-440): */
 #define HGX_ROOT_Y (-3)       /* Root.Y (the creator's first event, self-parent = Root.X = -1) */
-#define HGX_ROOT_OTHER (-4)   /* Root.Others[event] (the caller checked the entry) */
+#define HGX_ROOT_OTHER (-4)   /* Root.Others[event]: the event's hash must be a key registered with
+                                 hgx_set_root_others (the caller checked the entry's value) */
 
 typedef struct {
     int32_t code;
@@ -204,6 +205,14 @@ int32_t hgx_bootstrap(hgx_ctx* ctx, const char* path, hgx_error* err);
  * HGX_ROOT_Y / HGX_ROOT_OTHER. Single-graph contexts. */
 int32_t hgx_reset(hgx_ctx* ctx, const int32_t* root_index, const int32_t* root_round, const int32_t* root_y_is_event,
                   hgx_error* err);
+/* The keys of the roots' Others maps (root.go: Others[event hex] = other-parent hex,
+ * hashgraph.go:437-440): the 32-byte ids of the events allowed to name HGX_ROOT_OTHER. After
+ * hgx_reset the set is empty; an event inserted with HGX_ROOT_OTHER whose hash (hgx_events.hash)
+ * is not a key fails with "CheckOtherParent: Other-parent not known", as in the reference. The
+ * value (which other-parent the entry names) stays the shim's check, since the other-parent is
+ * outside the store. hgx_bootstrap accepts the HGX_ROOT_OTHER events of a rooted checkpoint
+ * (they passed this check when first inserted; the file carries no event ids). */
+int32_t hgx_set_root_others(hgx_ctx* ctx, const uint8_t* event_hash32, int64_t count, hgx_error* err);
 /* Hashgraph.GetFrame: per participant root_x / root_y (gid; -1 = the current Root.X / ""; 
  * HGX_ROOT_Y / HGX_ROOT_OTHER as inserted), root_index, root_round; the frame's events (gids,
  * topological order) and Root.Others pairs (event, other-parent). Counts are returned in full;
@@ -380,6 +389,10 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
  * (hgx_round_k.hip; candidates in chunks of 128 above n = 256). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
+/* FindOrder consensus timestamps: 0 = default: resident blocks with three tiles' gathers in
+ * flight (hgx_cts.hip) where it applies (32 < n <= 512, at most 4096 chains), otherwise mode 1;
+ * 1 = one tile of 8 positions per block (k_cts_small / k_cts_tile, hgx_kernels.hip). Same results. */
+int32_t hgx_set_cts_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds schedule: 1 = incremental (default: a call after more InsertEvents extends
  * lastAncestors/firstDescendants for the new events only and resumes the round steps at the
  * lowest round that can change; FindOrder works on the events not yet received), 0 = every

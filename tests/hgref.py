@@ -580,6 +580,14 @@ def frame_root_arrays(frame):
     return idx, rnd, yev
 
 
+def frame_others_keys(t, frame):
+    """The ids (32-byte hashes) of the events the frame's Root.Others maps hold (source gids of
+    trace t), for hgx_set_root_others."""
+    keys = sorted(frame["others"])
+    return np.asarray(t.hash, np.uint8).reshape(-1, 32)[np.asarray(keys, np.int64)] if keys else \
+        np.zeros((0, 32), np.uint8)
+
+
 def remap_after_reset(t, order, frame, new=None):
     """The source events `order` (source gids, topological) as a trace to insert into a
     hashgraph reset with `frame`'s roots, parents resolved like InsertEvent does

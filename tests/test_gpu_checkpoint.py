@@ -111,7 +111,7 @@ def test_rooted_context_round_trip(tmp_path):
     h.RunConsensus()
     f = h.GetFrame()
     roots = hgref.frame_root_arrays(f)
-    h.Reset(*roots)
+    h.Reset(*roots, others=hgref.frame_others_keys(t, f))
     sub, _ = hgref.remap_after_reset(t, f["events"], f)
     h.insert_trace(sub)
     h.RunConsensus()

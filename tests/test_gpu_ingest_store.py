@@ -378,6 +378,33 @@ def test_commit_callback_like_commit_ch():
     h.set_commit_callback(None)
 
 
+def test_commit_callback_sees_final_state_and_raises():
+    """The callback runs after FindOrder has updated the graph state (ConsensusTransactions,
+    PendingLoadedEvents read inside it equal the values after the call), and an exception it
+    raises surfaces from the RunConsensus call instead of being dropped by ctypes."""
+    t = gtrace.gossip(8, 3000, 92, stale_prob=0.1, stale_depth=2)
+    h = _hg(8, cap=t.E)
+    seen = []
+    h.set_commit_callback(lambda *a: seen.append((h.ConsensusTransactions(), h.PendingLoadedEvents())))
+    h.insert_trace(t)
+    h.RunConsensus()
+    assert seen and all(s == (h.ConsensusTransactions(), h.PendingLoadedEvents()) for s in seen)
+
+    class Boom(Exception):
+        pass
+
+    def bad(*a):
+        raise Boom("consumer failed")
+
+    h2 = _hg(8, cap=t.E)
+    h2.set_commit_callback(bad)
+    h2.insert_trace(t)
+    with pytest.raises(Boom):
+        h2.RunConsensus()
+    assert len(h2.ConsensusEvents()) > 0   # the call itself completed
+    h2.set_commit_callback(None)
+
+
 def test_core_playbooks_through_wire_events(plays):
     """node/core_test.go's playbooks with Core.Sync fed as the network delivers it: the sender's
     WireEvents (hgx_wire_info = SetWireInfo) inserted by the receiver with hgx_insert_wire_events

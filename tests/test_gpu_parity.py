@@ -17,12 +17,14 @@ def _hg(n, cap=1 << 14, graphs=1):
     return Hashgraph(n, capacity=cap, n_graphs=graphs)
 
 
-def run_gpu(t, chunk=None, cap=None, coord32=False, fame=None, round_kernel=None):
+def run_gpu(t, chunk=None, cap=None, coord32=False, fame=None, round_kernel=None, cts_kernel=None):
     h = _hg(t.n, cap or max(64, t.E))
     if coord32:
         h.set_coord_storage(1)
     if round_kernel:
         h.set_round_kernel(round_kernel)
+    if cts_kernel:
+        h.set_cts_kernel(cts_kernel)
     if fame:
         h.set_fame_tally(fame)
     if chunk is None:
@@ -126,6 +128,16 @@ def test_gossip_block_search_round_kernel(n, E, seed, silent, stale):
     above n = 256) against the oracle."""
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
     compare(run_gpu(t, round_kernel="block"), hgref.oracle_run(t), t, hashes=False)
+
+
+@pytest.mark.parametrize("n,E,seed,silent,stale,chunk", [(64, 12000, 10, 21, 0.2, None), (100, 15000, 11, 0, 0.0, None),
+                                                         (256, 30000, 16, 0, 0.0, None), (512, 24000, 18, 100, 0.2, None),
+                                                         (128, 20000, 12, 0, 0.0, 1000), (1000, 30000, 20, 330, 0.3, None)])
+def test_gossip_tile_cts_kernel(n, E, seed, silent, stale, chunk):
+    """The one-tile-per-block consensus timestamp kernel (hgx_set_cts_kernel(ctx, 1),
+    k_cts_tile) against the oracle; the default pipelined kernel runs in every other test."""
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
+    compare(run_gpu(t, chunk=chunk, cts_kernel="tile"), hgref.oracle_run(t, chunk=chunk), t, hashes=False)
 
 
 def _expect_compact(t):

@@ -26,7 +26,7 @@ def test_fixture_frame_and_reset_from_frame():
     h.RunConsensus()
     f = h.GetFrame()
     assert f == o.get_frame()
-    h.Reset(*hgref.frame_root_arrays(f))
+    h.Reset(*hgref.frame_root_arrays(f), others=hgref.frame_others_keys(t, f))
     o.reset(*hgref.frame_root_arrays(f))
     sub, _ = hgref.remap_after_reset(t, f["events"], f)
     h.insert_trace(sub)
@@ -46,7 +46,7 @@ def test_fixture_reset_with_explicit_roots():
     h.RunConsensus()
     frame = {"roots": [(idx["f02b"], idx["g1"], 4, 2), (idx["f10"], idx["f02b"], 4, 2), (idx["f21"], idx["g1"], 4, 2)],
              "others": {idx["o02"]: idx["f21"]}}
-    h.Reset(*hgref.frame_root_arrays(frame))
+    h.Reset(*hgref.frame_root_arrays(frame), others=hgref.frame_others_keys(t, frame))
     sub, _ = hgref.remap_after_reset(t, [idx[e] for e in ("g1", "g0", "g2", "g10", "g21", "o02", "g02", "h1", "h0",
                                                             "h2")], frame)
     h.insert_trace(sub)
@@ -69,6 +69,35 @@ def test_reset_errors():
     assert ei.value.msg == "CheckOtherParent: Other-parent not known"
 
 
+def test_root_other_needs_an_others_key():
+    """HGX_ROOT_OTHER is accepted only for an event whose id is a key of the roots' Others maps
+    (hashgraph.go:437-440): the same insert fails at o02 without the key, and at a later event
+    that claims a Root.Others parent it does not have."""
+    from babble_amd._lib import HgxError
+    t = hgref.fixture_trace("consensus_hashgraph")
+    idx = {nm: i for i, nm in enumerate(t.names)}
+    frame = {"roots": [(idx["f02b"], idx["g1"], 4, 2), (idx["f10"], idx["f02b"], 4, 2), (idx["f21"], idx["g1"], 4, 2)],
+             "others": {idx["o02"]: idx["f21"]}}
+    order = [idx[e] for e in ("g1", "g0", "g2", "g10", "g21", "o02", "g02", "h1", "h0", "h2")]
+    sub, _ = hgref.remap_after_reset(t, order, frame)
+    k_o02 = order.index(idx["o02"])
+    assert sub.op[k_o02] == hgref.ROOT_OTHER
+    h = _hg(t.n, 256)
+    h.Reset(*hgref.frame_root_arrays(frame))          # no Others keys
+    with pytest.raises(HgxError) as ei:
+        h.insert_trace(sub)
+    assert ei.value.msg == "CheckOtherParent: Other-parent not known" and h.num_events() == k_o02
+    # a bogus claim: g02 (whose other-parent is in the store) sent with ROOT_OTHER
+    k_g02 = order.index(idx["g02"])
+    sub.op = sub.op.copy()
+    sub.op[k_g02] = hgref.ROOT_OTHER
+    h2 = _hg(t.n, 256)
+    h2.Reset(*hgref.frame_root_arrays(frame), others=hgref.frame_others_keys(t, frame))
+    with pytest.raises(HgxError) as ei:
+        h2.insert_trace(sub)
+    assert ei.value.msg == "CheckOtherParent: Other-parent not known" and h2.num_events() == k_g02
+
+
 @pytest.mark.parametrize("n,E,seed,chunks", [(4, 1500, 71, 3), (16, 6000, 72, 4), (64, 20000, 73, 2),
                                              (256, 40000, 74, 2), (512, 40000, 75, 2)])
 def test_gossip_fast_forward_from_frame(n, E, seed, chunks):
@@ -85,7 +114,7 @@ def test_gossip_fast_forward_from_frame(n, E, seed, chunks):
     f = o.get_frame()
     assert h.GetFrame() == f
     o.reset(*hgref.frame_root_arrays(f))
-    h.Reset(*hgref.frame_root_arrays(f))
+    h.Reset(*hgref.frame_root_arrays(f), others=hgref.frame_others_keys(t, f))
     sub, new = hgref.remap_after_reset(t, f["events"], f)
     o.insert_trace(sub)
     h.insert_trace(sub)
