@@ -58,12 +58,30 @@ def _sig(L, name, res, args):
     f.argtypes = args
 
 
+def _one_hip_runtime():
+    """One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64 + libhsa-runtime64;
+    its libraries name the runtime "libamdhip64.so", libhgx names "libamdhip64.so.7" (the SONAME
+    both copies carry). If libhgx is loaded first and torch after, the process maps TWO HIP and
+    HSA runtimes, and libhgx's stops working once torch's initialises (measured: occupancy
+    queries fail, HIP events become invalid handles). If torch is loaded first, libhgx's NEEDED
+    entry resolves to torch's copy by SONAME and there is one runtime. So torch, when it is
+    installed, is imported before libhgx is opened (HGX_NO_TORCH=1 skips this, for processes
+    that never import torch). Loading libhgx by other means and torch later is unsupported."""
+    if os.environ.get("HGX_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401  (loads torch's HIP runtime; no device is touched)
+    except ImportError:
+        pass
+
+
 def lib():
     global _L
     if _L is not None:
         return _L
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    _one_hip_runtime()
     L = C.CDLL(LIB_PATH)
     i32, i64, u64, p, d = C.c_int32, C.c_int64, C.c_uint64, C.c_void_p, C.c_double
     E = C.POINTER(hgx_error)

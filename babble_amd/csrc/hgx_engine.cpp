@@ -816,7 +816,11 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(hipStreamSynchronize(stream));
             round_p_runs++;
             round_p_ovf += h_small[59];
-            if (h_small[56] != 0) return hipErrorLaunchTimeOut;   // a workgroup gave up waiting
+            if (h_small[56] != 0) {   // a workgroup gave up waiting: st[0] = 1 + its chain, st[3] its round
+                round_p_fail_chain = h_small[56] - 1;
+                round_p_fail_round = h_small[59];
+                return hipErrorLaunchTimeOut;
+            }
             last = std::max(last, h_small[57]);
             finished += h_small[58];
             if (finished >= G) {

@@ -185,7 +185,8 @@ class Engine {
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
     int cts_kernel = 0;       // hgx_set_cts_kernel: 0 pipelined resident blocks where they apply (hgx_cts.hip), 1 per-tile
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
-    int64_t round_p_ovf = 0;   // candidate rows the persistent launches counted exactly (over 8 bits)
+    int64_t round_p_ovf = 0;
+    int32_t round_p_fail_round = -1, round_p_fail_chain = -1;   // the last give-up: round and chain   // candidate rows the persistent launches counted exactly (over 8 bits)
     int dev = 0;
 
    private:

@@ -526,7 +526,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     rp_vm_drain();   // no LDS-DMA outlives the workgroup
     RP_PROF_END();
     if (failed) {
-        if (t == 0) __hip_atomic_store((gu32*)P.st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the first workgroup to give up records its chain and round (st[3] then holds the
+        // round, not the exact-row count: the launch is redone anyway)
+        if (t == 0 && atomicCAS((int32_t*)P.st, 0, gc + 1) == 0) atomicExch(&P.st[3], s);
         return;
     }
     if (t == 0) {

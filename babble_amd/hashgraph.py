@@ -480,13 +480,14 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(16, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 16)
+        out = np.zeros(18, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 18)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
                     la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
                     la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]),
-                    round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]))
+                    round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]),
+                    round_p_fail_round=int(out[16]), round_p_fail_chain=int(out[17]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""

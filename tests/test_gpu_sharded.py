@@ -54,3 +54,66 @@ def test_row_sharded_world2_bit_exact(tmp_path, n, E, chunk):
         for k in ("rr", "cts", "round"):
             assert np.array_equal(z[k], np.asarray(ref[k])), (r, k)
     assert len(ref["order"]) > 0
+
+
+@pytest.mark.parametrize("n,E,chunk", [(64, 12000, 4000), (256, 30000, 30000)])
+def test_shard_exchange_through_torch_device_tensors(n, E, chunk):
+    """The RCCL path of bench.py --sharded hands torch-allocated device buffers to
+    hgx_shard_export / hgx_shard_import (dst_on_device = 1). torch bundles its own HIP and HSA
+    runtimes, libhgx uses /opt/rocm's: both live in this process's single GPU address space, and
+    the exchange touches the buffers from a kernel only (k_cts_shard_copy, no hipMemcpy on a
+    foreign pointer). Two ranks' contexts in one process exchange through torch tensors on the
+    GPU; every rank's export read back by torch equals its host-pointer export, and both ranks'
+    results are bit-exact with the unsharded context."""
+    import ctypes as C
+    import torch
+    from babble_amd.hashgraph import Hashgraph
+    world = 2
+    t = gtrace.gossip(n, E, 77, stale_prob=0.1, stale_depth=2)
+    hs = []
+    for r in range(world):
+        h = Hashgraph(n, capacity=E)
+        h.set_shard(r, world)
+        hs.append(h)
+    ref = Hashgraph(n, capacity=E)
+    dev = torch.device("cuda", 0)
+    for lo in range(0, E, chunk):
+        hi = min(E, lo + chunk)
+        ref.insert_trace(t, lo, hi)
+        ref.RunConsensus()
+        err = C.create_string_buffer(256)
+        for h in hs:
+            h.insert_trace(t, lo, hi)
+            h.DivideRounds()
+            h.DecideFame()
+            assert h.L.hgx_find_order_begin(h.ctx, err) == 0
+        counts = [int(hs[0].L.hgx_shard_values(hs[0].ctx, r)) for r in range(world)]
+        assert counts == [int(hs[1].L.hgx_shard_values(hs[1].ctx, r)) for r in range(world)]
+        bufs = []
+        for r, h in enumerate(hs):
+            d = torch.full((max(1, counts[r]),), -7, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            if counts[r]:
+                assert h.L.hgx_shard_export(h.ctx, C.c_void_p(d.data_ptr()), 1) == 0
+                host = np.zeros(counts[r], np.int64)
+                assert h.L.hgx_shard_export(h.ctx, host.ctypes.data_as(C.c_void_p), 0) == 0
+                assert np.array_equal(d[:counts[r]].cpu().numpy(), host), r
+            bufs.append(d)
+        for r, h in enumerate(hs):
+            for q in range(world):
+                if q != r and counts[q]:
+                    src = bufs[q].clone()   # a fresh torch allocation, read by libhgx's kernel
+                    torch.cuda.synchronize()
+                    assert h.L.hgx_shard_import(h.ctx, q, C.c_void_p(src.data_ptr()), 1) == 0
+            assert h.L.hgx_find_order_end(h.ctx, err) == 0
+    want = ref.results()
+    assert len(want["order"]) > 0
+    for r, h in enumerate(hs):
+        got = h.results()
+        assert list(got["order"]) == list(want["order"]), r
+        for k in ("rr", "cts", "round"):
+            assert np.array_equal(np.asarray(got[k]), np.asarray(want[k])), (r, k)
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    libs = sorted({ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln})
+    print("HIP runtimes mapped:", libs)
+    assert any("/opt/rocm" in x for x in libs)
