@@ -1624,8 +1624,8 @@ int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
 }
 
 int32_t hgx_set_cts_kernel(hgx_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
-    c->eng.cts_kernel = mode;
+    if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
+    c->eng.cts_kernel = mode == 0 ? 1 : mode;
     return HGX_OK;
 }
 

@@ -10,9 +10,9 @@
 // three dependent global levels per tile (the tile's rr/ts -> the famous flag, WLAT and FD
 // of every witness chain -> the FD event's timestamp) with only one tile's loads in flight.
 // Here a block is resident (grid = what fits the device) and loops over its tiles with the
-// three levels of three consecutive tiles in flight at once:
-//    iteration k: gathers of tile k | famous/WLAT/FD loads of tile k+1 | rr/ts of tile k+2
-// so one tile costs about one global latency instead of three, plus the LDS radix select.
+// three levels of three consecutive tiles in flight at once, behind the selects of a fourth:
+//    gathers of tile k+1 | WLAT/FD loads of tile k+2 | rr/ts of tile k+3 | selects of tile k
+// so one tile costs about one global latency or one tile's selects, whichever is longer.
 // The per-chain terms that k_cts_tile loaded per lane (c_off - c_base of every chain, the
 // tile geometry fu / rcnt / c_off of the launched chains) are read once per block into LDS.
 #include <hip/hip_runtime.h>
@@ -143,7 +143,8 @@ __global__ void __launch_bounds__(256) k_cts_pipe(const int32_t* __restrict__ fu
         }
     };
 
-    // prologue: tiles 0 and 1's level 1, tile 0's level 2
+    // prologue: tiles 0 and 1's level 1, tile 0's level 2, then tile 0's gathers, tile 1's level
+    // 2 and tile 2's level 1 go out
     int u0 = next_tile(blockIdx.x);
     if (u0 >= total) return;
     int u1 = next_tile(u0 + gstep);
@@ -156,21 +157,22 @@ __global__ void __launch_bounds__(256) k_cts_pipe(const int32_t* __restrict__ fu
     l2_issue(0);
     l2_finish(0);
     const int lane = lane_id(), wave = t >> 6;
+    int64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = p_ts[max(idx[u], 0)];
+    cp_order();
+    l2_issue(1);
+    cp_order();
+    l1_issue(u2);
+    cp_order();
 
+    // iteration k: (A) tile k's gathers land -> offsets and membership into LDS buffer k & 1;
+    // (B) tile k+1's gather indices, tile k+2's level 1 into the ring; barrier; (C) tile k+1's
+    // gathers, tile k+2's level 2 and tile k+3's level 1 go out; (D) tile k's selects run while
+    // they are in flight
     for (int k = 0; u0 < total; k++) {
         const int s0 = k & (kCpRing - 1), s1 = (k + 1) & (kCpRing - 1), s2 = (k + 2) & (kCpRing - 1);
-        // (1) timestamp gathers of tile k
-        int64_t x[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) x[u] = p_ts[max(idx[u], 0)];
-        cp_order();
-        // (2) level 2 of tile k+1, (3) level 1 of tile k+2 (in flight behind the gathers)
-        l2_issue(s1);
-        cp_order();
-        l1_issue(u2);
-        cp_order();
-        // (4) tile k's offsets and membership into LDS buffer k & 1
-        {
+        {   // (A)
             uint32_t* v = vals + (k & 1) * NPAD * LD;
             uint8_t* mb = memb + (k & 1) * NPAD * LD;
             const int64_t base = ring[s0].ts[e];
@@ -184,11 +186,20 @@ __global__ void __launch_bounds__(256) k_cts_pipe(const int32_t* __restrict__ fu
                 mb[c * LD + e] = (uint8_t)((ok ? 1 : 0) | (ov ? 2 : 0));
             }
         }
-        // (5) tile k+1's gather indices, (6) tile k+2's level 1 into the ring
+        // (B)
         l2_finish(s1);
         l1_store(u2, s2);
         cp_lds_barrier();
-        // (7) one wave per event: radix select of element floor(m/2)
+        // (C)
+        const int u3 = next_tile(u2 + gstep);
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = p_ts[max(idx[u], 0)];
+        cp_order();
+        l2_issue(s2);
+        cp_order();
+        l1_issue(u3);
+        cp_order();
+        // (D) one wave per event: radix select of element floor(m/2)
         {
             const uint32_t* v = vals + (k & 1) * NPAD * LD;
             const uint8_t* mb = memb + (k & 1) * NPAD * LD;
@@ -218,7 +229,7 @@ __global__ void __launch_bounds__(256) k_cts_pipe(const int32_t* __restrict__ fu
         }
         u0 = u1;
         u1 = u2;
-        u2 = next_tile(u2 + gstep);
+        u2 = u3;
     }
 }
 

@@ -146,7 +146,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(p_gid.alloc(PP)); HGX_TRY(p_chain.alloc(PP)); HGX_TRY(p_op.alloc(PP)); HGX_TRY(p_opu.alloc(PP));
     HGX_TRY(p_opk.alloc(PP));
     HGX_TRY(p_round.alloc(PP)); HGX_TRY(p_rr.alloc(PP)); HGX_TRY(p_ts.alloc(PP)); HGX_TRY(p_cts.alloc(PP));
-    fd_ld = (Ppos + 1) & ~(int64_t)1;
+    fd_ld = (Ppos + 31) & ~(int64_t)31;   // firstDescendants columns: 64-byte aligned 32-position segments
     HGX_TRY(LA.alloc(PP * n));
     HGX_TRY(FDT.alloc((size_t)fd_ld * n + 128));   // slack: compact window staging reads past a column
     HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8 + 4 * kLaRing)); HGX_TRY(order_gid.alloc(P));
@@ -580,7 +580,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // slack shared evenly by the chains
         const int64_t slack = (Ppos - En) / C;
         h_off.assign(C + 1, 0);
-        for (int c = 0; c < C; c++) h_off[c + 1] = h_off[c] + chain_len[c] + (int32_t)slack;
+        // slots of multiples of 32 positions (slack >= 256 > 31): every chain starts 64-byte
+        // aligned in the firstDescendants columns (the persistent round kernel's staging)
+        for (int c = 0; c < C; c++) h_off[c + 1] = h_off[c] + ((chain_len[c] + (int32_t)slack) & ~31);
         HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
         h_len_div.assign(C, 0);
         last_rebuild = true;
@@ -795,7 +797,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     int32_t r_done = -1;
     auto run_persistent = [&]() -> hipError_t {
         const int ndw = round_k_ndw(n);
-        if (FD8p.n < (size_t)2 * C * ndw) HGX_TRY(FD8p.alloc((size_t)2 * C * ndw));
+        if (FD8p.n < (size_t)kRoundPBufs * C * ndw) HGX_TRY(FD8p.alloc((size_t)kRoundPBufs * C * ndw));
         if (rp_gran.n < (size_t)4 * C) HGX_TRY(rp_gran.alloc((size_t)4 * C));
         if (rp_st.n < (size_t)4 + G) HGX_TRY(rp_st.alloc((size_t)4 + G));
         int32_t* fin = rp_st.p + 4;
@@ -1076,7 +1078,7 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
         return collect_kernel_times();
     }
     kbeg(K_CTS);
-    if (cts_kernel != 0 || !launch_cts_pipe(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt))
+    if (cts_kernel != 2 || !launch_cts_pipe(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt))
         launch_cts(stream, a, shard_lo, shard_hi - shard_lo, C, n, fd_ld, max_cnt);
     int64_t own = 0;
     for (int c = shard_lo; c < shard_hi; c++) own += fo_cnt[c];

@@ -183,7 +183,7 @@ class Engine {
     int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
     int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence where it applies (hgx_round_p.hip),
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
-    int cts_kernel = 0;       // hgx_set_cts_kernel: 0 pipelined resident blocks where they apply (hgx_cts.hip), 1 per-tile
+    int cts_kernel = 1;       // hgx_set_cts_kernel: 1 per-tile blocks (default: measured faster), 2 pipelined (hgx_cts.hip)
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
     int64_t round_p_ovf = 0;
     int32_t round_p_fail_round = -1, round_p_fail_chain = -1;   // the last give-up: round and chain   // candidate rows the persistent launches counted exactly (over 8 bits)
@@ -257,7 +257,7 @@ class Engine {
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
     DBuf<uint32_t> FD8;   // [2][C][ndw] rebased candidate rows (k_round_k)
-    DBuf<uint32_t> FD8p;  // [2][C][ndw] the same, row-major (k_round_p)
+    DBuf<uint32_t> FD8p;  // [kRoundPBufs][C][ndw] the same, row-major, self-validating (k_round_p)
     DBuf<uint64_t> rp_gran;   // [4][C] k_round_p hand-off granules
     DBuf<int32_t> rp_st;      // k_round_p status: abort, rounds done, finished
     DBuf<int32_t> la_lmap;          // k_la_wave lanes -> chains with events (one graph, n > 896)

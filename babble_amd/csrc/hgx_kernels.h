@@ -170,6 +170,7 @@ int round_k_ndw(int n);
 // -1 per DivideRounds, a finished graph's workgroups leave at once in a later launch).
 // launch_round_p_tail writes the empty rows of rounds (fin[g], r_last] of every graph.
 bool round_p_ok(int n, int C, int num_cus);
+constexpr int kRoundPBufs = 4;   // candidate-row buffers of the persistent recurrence (round s: s % 4)
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
                           int32_t* fin, int r0, int r_end, int init, int num_cus);
 void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, int r_last);

@@ -11,13 +11,18 @@
 //    staged by LDS-DMA right after the boundary is known, while the other chains finish;
 //  * the only data a round needs from other workgroups is W'_s: for each chain its boundary
 //    and its candidate's rebased firstDescendants row. The producer (the workgroup that found
-//    the candidate) stores the row write-through (sc1), drains it, then stores an 8-byte
-//    granule {tag = s + 1, boundary | flags} write-through; a consumer wave polls the granules
-//    of ITS candidates (sc1 loads), then loads their rows (sc1 loads) and searches at once: a
-//    wave whose candidates arrived early searches while the last producers still run. This is
-//    the first row of the hand-off table in MI355X_MICROARCH.md (§Workgroup dispatch): one
-//    signalling lane per storing workgroup after its wave's vmcnt(0), an sc1 poll, sc1 stores
-//    and loads of every handed-off byte, one workgroup per CU, hipMalloc memory;
+//    the candidate) stores the row and an 8-byte granule {tag = s + 1, boundary | flags}, both
+//    write-through (sc1), without a drain in between: both are self-validating. The granule
+//    carries its round tag; the row's bytes are rebased values in [1, 127], so bit 7 of every
+//    byte is free and carries a validity bit v(s) = (s >> 2) & 1, with the rows of round s in
+//    buffer s % 4: the previous contents of that buffer are round s - 4's rows, whose v is the
+//    opposite. A consumer wave loads the granules and the rows of ITS candidates together (sc1
+//    loads, one hop), and reloads until every granule carries tag s + 1 and every row of a
+//    candidate that exists has every bit 7 equal to v(s) (4-byte stores are single-copy atomic,
+//    so a dword is old or new as a whole); a wave whose candidates arrived early searches while
+//    the last producers still run. These are MI355X_MICROARCH.md's data-tagged granules
+//    (handoff-1to1): no producer drain, no separate flag hop; one workgroup per CU, hipMalloc
+//    memory, sc1 stores and loads of every handed-off byte;
 //  * no grid barrier and no kernel boundary per round; every wait is bounded (s_memrealtime),
 //    a workgroup that gives up raises the abort word, every workgroup then leaves, and the
 //    host reruns the rounds with the per-launch step (k_round_k).
@@ -44,35 +49,46 @@ constexpr uint32_t kRpEx = 1u << 31, kRpOv = 1u << 30, kRpBm = (1u << 30) - 1;
 // Optional phase clocks (-DHGX_STEP_PROF, build variant "prof"): thread 0 of each workgroup adds
 // s_memtime deltas per phase of every round, flushed once at the end of the launch.
 #ifdef HGX_STEP_PROF
-__device__ unsigned long long hgx_rp_prof[8];
-#define RP_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+// slots: 0 rebase, 1 poll, 2 rows, 3 search, 4 boundary, 5 granule, 6 outputs, 7 staging wait,
+// 8 staging issue, 9 row build + stores; 15 = block-rounds
+__device__ unsigned long long hgx_rp_prof[16];
+#define RP_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[16] = {}
 #define RP_PROF(i)                                                \
     do {                                                          \
         if (threadIdx.x == 0) {                                   \
             const long long _t = clock64();                       \
             _pa[i] += (unsigned long long)(_t - _pt);             \
             _pt = _t;                                             \
-            if ((i) == 6) _pa[7] += 1;                            \
+            if ((i) == 6) _pa[15] += 1;                           \
         }                                                         \
+    } while (0)
+#define RP_PROF_COUNT(i)                                          \
+    do {                                                          \
+        if (threadIdx.x == 0) _pa[i] += 1;                        \
     } while (0)
 #define RP_PROF_END()                                                              \
     do {                                                                           \
         if (threadIdx.x == 0)                                                      \
-            for (int _i = 0; _i < 8; _i++)                                         \
+            for (int _i = 0; _i < 16; _i++)                                        \
                 if (_pa[_i]) atomicAdd(&hgx_rp_prof[_i], _pa[_i]);                 \
     } while (0)
 void round_p_prof_dump() {
-    unsigned long long h[8];
+    unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
-    fprintf(stderr, "[hgx] k_round_p phases (clk sums, thread 0): window+rebase %llu poll %llu rows %llu search %llu "
-            "boundary %llu publish %llu outputs %llu | block-rounds %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const double r = h[15] ? (double)h[15] : 1.0;
+    fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): staging-wait %.0f barrier %.0f rebase %.0f poll %.0f "
+            "rows %.0f search %.0f boundary %.0f staging-issue %.0f row-build %.0f granule %.0f outputs %.0f | "
+            "block-rounds %llu, synchronous stagings %llu, later windows %llu\n",
+            h[7] / r, h[12] / r, h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[6] / r,
+            h[15], h[10], h[11]);
+    unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
 }
 #else
 #define RP_PROF_BEGIN() (void)0
 #define RP_PROF(i) (void)0
 #define RP_PROF_END() (void)0
+#define RP_PROF_COUNT(i) (void)0
 void round_p_prof_dump() {}
 #endif
 
@@ -162,35 +178,38 @@ struct RpCfg {
     static constexpr int NW = T / 64;
     static constexpr int WS = NDW + 4;                         // 8-bit window row stride (dwords, == 4 mod 16)
     static constexpr int CSZ = (int)sizeof(CT);
-    static constexpr int RAW_DW = kRpP * NC * CSZ / 4;          // raw window rows (dwords) at n = NC
-    static constexpr int KR16 = (RAW_DW + NW * 256 - 1) / (NW * 256);   // 16-byte DMA per lane
-    static constexpr int KR4 = (RAW_DW + NW * 64 - 1) / (NW * 64);      // 4-byte DMA per lane
-    static constexpr int RAW_LDS = (KR16 * NW * 256 > KR4 * NW * 64 ? KR16 * NW * 256 : KR4 * NW * 64);   // dwords
-    static constexpr int CW = (CSZ == 2) ? 16 : 32;             // dwords per staged FD column (32 positions)
-    static constexpr int CPI = 64 / CW;                          // FD columns per DMA instruction
-    static constexpr int KF = (NC + NW * CPI - 1) / (NW * CPI);
-    static constexpr int FDC_LDS = KF * NW * 65;                 // dwords: groups of 64 + 1 pad
+    // staging ring: NSEG segments of SEG positions (64 bytes of one firstDescendants column) of
+    // the chain's rows; segment m (positions [SEG m, SEG m + SEG) from the chain's start) sits in
+    // slot m % NSEG
+    static constexpr int SEG = 64 / CSZ, NSEG = 4, RR = SEG * NSEG;
+    static constexpr int SEG_RAW = SEG * NC * CSZ;               // bytes: raw lastAncestors rows of a segment
+    static constexpr int KR16 = (SEG_RAW / 16 + T - 1) / T;      // 16-byte DMA per lane per segment
+    static constexpr int CW = 16;                                // dwords per staged FD column (SEG positions)
+    static constexpr int CPI = 4;                                // FD columns per DMA instruction (a group)
+    static constexpr int KF = (NDW + NW - 1) / NW;               // groups per wave per segment
+    static constexpr int SEG_FD = NDW * 65 * 4;                  // bytes: groups of 64 dwords + 1 pad
     // LDS carve (bytes, 16-aligned)
     static constexpr int O_WIN = 0;
-    static constexpr int O_RAW0 = O_WIN + ((kRpP * WS * 4 + 15) & ~15);
-    static constexpr int O_RAW1 = O_RAW0 + RAW_LDS * 4;
-    static constexpr int O_FDC0 = O_RAW1 + RAW_LDS * 4;
-    static constexpr int O_FDC1 = O_FDC0 + ((FDC_LDS * 4 + 15) & ~15);
-    static constexpr int O_CB = O_FDC1 + ((FDC_LDS * 4 + 15) & ~15);   // c_base[NC]
+    static constexpr int O_RAW = O_WIN + ((kRpP * WS * 4 + 15) & ~15);   // [RR][n] raw rows
+    static constexpr int O_FD = O_RAW + NSEG * SEG_RAW;                   // [NSEG][NDW groups][65]
+    static constexpr int O_CB = O_FD + NSEG * SEG_FD;                     // c_base[NC]
     static constexpr int O_CO = O_CB + NC * 4;                           // c_off[NC]
     static constexpr int O_BM0 = O_CO + NC * 4;                          // Bm of the candidates, by round parity
     static constexpr int O_BM1 = O_BM0 + NC * 4;
     static constexpr int O_HIST = O_BM1 + NC * 4;                        // 32 bins
-    static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits (NC / 32 words)
-    static constexpr int O_MISC = O_SB + ((NC / 32 + 4) * 4 + 15 & ~15); // [0] B, [1] tot, [2] any, [3] fail
+    static constexpr int SBW = (NC / 32 + 4 + 3) & ~3;                   // S row words per buffer
+    static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits [2][SBW], by round parity
+    static constexpr int O_MISC = O_SB + 2 * SBW * 4;                    // [0] B, [1] tot, [2] any, [3] fail
     static constexpr int USED = O_MISC + 64;
     // at least 82 KB: one workgroup per CU (the hand-off rule's geometry), whatever fits
     static constexpr int LDS = USED > 84 * 1024 ? USED : 84 * 1024;
+    static_assert(USED <= 160 * 1024, "k_round_p: LDS carve exceeds a CU's 160 KB");
 };
 
 struct RoundPArgs {
     RoundArgs A;
-    uint32_t* FD8p;     // [2][C][ndw] rebased candidate rows, row-major (parity = round & 1)
+    uint32_t* FD8p;     // [4][C][ndw] rebased candidate rows, row-major (round s: buffer s % 4, bit 7 of
+                        // every byte = v(s) = (s >> 2) & 1)
     uint64_t* gran;     // [kRpSlots][C]
     int32_t* st;        // [0] abort, [1] max over graphs of the round each stopped at, [2] graphs that
                         // finished (W'_s empty) in this launch, [3] rows counted exactly (over 8 bits)
@@ -202,7 +221,7 @@ struct RoundPArgs {
 template <typename CT, int NDW, int Q>
 __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round_p(RoundPArgs P) {
     typedef RpCfg<CT, NDW, Q> K;
-    constexpr int HD = K::HD, T = K::T, WS = K::WS, CW = K::CW, CPI = K::CPI;
+    constexpr int HD = K::HD, T = K::T, WS = K::WS;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const RoundArgs& A = P.A;
     const int n = A.n, C = A.C, sm = A.sm;
@@ -214,7 +233,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     int32_t* cbase = (int32_t*)(lds + K::O_CB);
     int32_t* coff = (int32_t*)(lds + K::O_CO);
     int32_t* hist = (int32_t*)(lds + K::O_HIST);
-    uint32_t* sbits = (uint32_t*)(lds + K::O_SB);
+    uint32_t* sbits_all = (uint32_t*)(lds + K::O_SB);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
 
     if (P.fin[g] >= 0) return;   // the graph finished in an earlier launch of this DivideRounds
@@ -227,66 +246,53 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     }
     int b = A.Bm[(size_t)P.r0 * C + gc];
 
-    // ---- staging of a window [kb, kb + 31) into buffer `buf` (LDS-DMA, fixed counts per wave)
-    int fsh_buf[2] = {0, 0};
-    auto stage = [&](int kb, int buf) {
-        const int nraw = min(kRpP, len - kb);
-        uint32_t* raw_w = (uint32_t*)(lds + (buf ? K::O_RAW1 : K::O_RAW0));
-        const int nel = (int)((size_t)nraw * n * K::CSZ / 4);   // dwords
-        const uint32_t* __restrict__ src = (const uint32_t*)A.LA + (size_t)(off + kb) * n * K::CSZ / 4;
-        if (((n * K::CSZ) & 15) == 0) {
+    // ---- staging ring (LDS-DMA, fixed instruction counts per wave): segment m = the raw
+    // lastAncestors rows and firstDescendants columns at positions [SEG m, SEG m + SEG) of the
+    // chain; chain offsets are multiples of 32 (hgx_engine.cpp layout), so every segment is
+    // 64-byte aligned in both arrays. Rows past the chain's end lie in its slot's slack (read,
+    // never used).
+    constexpr int SEG = K::SEG, NSEG = K::NSEG, RR = K::RR;
+    const int last_seg = len > 0 ? (len - 1) / SEG : -1;
+    int seg_hi = -1;   // highest segment staged (uniform); [seg_hi - NSEG + 1, seg_hi] are resident
+    auto stage_seg = [&](int m) {
+        const int slot = m % NSEG;
+        const uint32_t* __restrict__ src = (const uint32_t*)((const uint8_t*)A.LA + ((size_t)off + (size_t)m * SEG) * n * K::CSZ);
+        uint32_t* raw_w = (uint32_t*)(lds + K::O_RAW + slot * SEG * n * K::CSZ);   // rows (p % RR) * n
+        const int nch = SEG * n * K::CSZ / 16;   // 16-byte chunks
 #pragma unroll
-            for (int k = 0; k < K::KR16; k++) {
-                const int c0 = wave * 256 + k * K::NW * 256;
-                __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane * 4, nel - 4)),
-                                                 (lds_ptr_t)(raw_w + c0), 16, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < K::KR4; k++) {
-                const int c0 = wave * 64 + k * K::NW * 64;
-                __builtin_amdgcn_global_load_lds((const void*)(src + min(c0 + lane, nel - 1)),
-                                                 (lds_ptr_t)(raw_w + c0), 4, 0, 0);
-            }
+        for (int k = 0; k < K::KR16; k++) {
+            const int c0 = wave * 64 + k * T;    // this wave instruction's first chunk
+            if (c0 + lane < nch)
+                __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c0 + lane)), (lds_ptr_t)(raw_w + 4 * c0), 16, 0, 0);
         }
-        // firstDescendants columns at positions [off + kb, off + kb + 32) (uint16: from the even
-        // position below), 65-dword groups of CPI columns
-        uint32_t* fd_w = (uint32_t*)(lds + (buf ? K::O_FDC1 : K::O_FDC0));
-        const int pcol = lane % CW, icol = lane / CW;
-        const int64_t Pc = A.Pcap;
-        const uint32_t* __restrict__ fsrc;
-        size_t cstride, lim;
-        if constexpr (K::CSZ == 4) {
-            fsrc = (const uint32_t*)A.FDT + off + kb + pcol;
-            cstride = (size_t)Pc;
-            lim = (size_t)n * Pc - 1 - (size_t)(off + kb + pcol);
-        } else {
-            const int64_t p0 = (off + kb) & ~1;
-            fsh_buf[buf] = (off + kb) & 1;
-            fsrc = (const uint32_t*)((const CT*)A.FDT + p0) + pcol;
-            cstride = (size_t)(Pc / 2);
-            lim = (size_t)n * (Pc / 2) - 1 - (size_t)(p0 / 2 + pcol);
-        }
+        // columns: lane = (column % 4, dword); one instruction = one group of 4 columns
+        const int icol = lane >> 4, pcol = lane & 15;
+        const uint32_t* __restrict__ fsrc = (const uint32_t*)((const uint8_t*)A.FDT + ((size_t)off + (size_t)m * SEG) * K::CSZ) + pcol;
+        const size_t cstride = (size_t)A.Pcap * K::CSZ / 4;   // dwords between columns
+        uint32_t* fd_w = (uint32_t*)(lds + K::O_FD + slot * K::SEG_FD);
 #pragma unroll
         for (int k = 0; k < K::KF; k++) {
-            const int i0 = wave * CPI + k * K::NW * CPI;
-            const int i = min(i0 + icol, n - 1);
-            const size_t o = min((size_t)i * cstride, lim);
-            __builtin_amdgcn_global_load_lds((const void*)(fsrc + o), (lds_ptr_t)(fd_w + (size_t)(i0 / CPI) * 65), 4, 0, 0);
+            const int grp = min(wave + k * K::NW, NDW - 1);
+            const int i = min(grp * 4 + icol, n - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride), (lds_ptr_t)(fd_w + grp * 65), 4, 0, 0);
         }
     };
-    auto fd_at = [&](int buf, int i, int pk) -> CT {   // staged FD of coordinate i at window probe pk
-        const uint32_t* fd_w = (const uint32_t*)(lds + (buf ? K::O_FDC1 : K::O_FDC0));
-        const int col = (i / CPI) * 65 + (i % CPI) * CW;
-        if constexpr (K::CSZ == 2) return ((const CT*)fd_w)[2 * col + fsh_buf[buf] + pk];
-        else return (CT)fd_w[col + pk];
+    // segments [max(seg_hi + 1, lo), hi] (hi <= lo + NSEG - 1: a slot is reused only when its
+    // segment is below lo)
+    auto stage_range = [&](int lo, int hi) {
+        for (int m = max(seg_hi + 1, lo); m <= hi; m++) stage_seg(m);
+        seg_hi = max(seg_hi, hi);
     };
-    auto raw_at = [&](int buf, int p, int i) -> CT {
-        return ((const CT*)(lds + (buf ? K::O_RAW1 : K::O_RAW0)))[p * n + i];
+    auto fd_at = [&](int i, int p) -> CT {   // staged FD of coordinate i at chain offset p
+        const uint8_t* fd_w = lds + K::O_FD + ((p / SEG) % NSEG) * K::SEG_FD;
+        return *(const CT*)(fd_w + ((i >> 2) * 65 + (i & 3) * 16) * 4 + (p % SEG) * K::CSZ);
     };
-    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the staged rows [0, np)
+    auto raw_at = [&](int p, int i) -> CT {   // staged lastAncestors row of chain offset p
+        return ((const CT*)(lds + K::O_RAW))[(p % RR) * n + i];
+    };
+    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the window [kb, kb + np)
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    auto rebase = [&](int buf, int np, const int32_t* bmp) {
+    auto rebase = [&](int kb, int np, const int32_t* bmp) {
         constexpr int RS = T / NDW > 0 ? T / NDW : 1;   // rows per pass
         for (int d = t % NDW; d < NDW; d += T) {
             const int i0 = 4 * d;
@@ -296,7 +302,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             for (int p = t / NDW; p < np; p += RS) {
                 uint32_t w;
                 if constexpr (K::CSZ == 2) {
-                    const uint32_t* rp = (const uint32_t*)(lds + (buf ? K::O_RAW1 : K::O_RAW0)) + (p * n + i0) / 2;
+                    const uint32_t* rp = (const uint32_t*)(lds + K::O_RAW) + (((kb + p) % RR) * n + i0) / 2;
                     const uint32_t r01 = i0 < n ? rp[0] : 0u, r23 = i0 + 2 < n ? rp[1] : 0u;
                     const u16x2 b01 = {(unsigned short)bq[0], (unsigned short)bq[1]};
                     const u16x2 b23 = {(unsigned short)bq[2], (unsigned short)bq[3]};
@@ -310,7 +316,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         if (i0 + u < n) {
-                            const int32_t x = Coord<CT>::la(raw_at(buf, p, i0 + u)) - bq[u] + 1;
+                            const int32_t x = Coord<CT>::la(raw_at(kb + p, i0 + u)) - bq[u] + 1;
                             w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
                         }
                     }
@@ -320,15 +326,34 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
     };
 
-    // vector-memory instructions stage() issues per wave (explicit waits leave them in flight)
-    const bool dma16 = ((n * K::CSZ) & 15) == 0;
-    auto wait_all_but_dma = [&]() {   // every earlier memory operation of this wave but the staging
-        if (dma16) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K::KR16 + K::KF < 63 ? K::KR16 + K::KF : 63) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K::KR4 + K::KF < 63 ? K::KR4 + K::KF : 63) : "memory");
+    // round r's outputs (the per-launch step writes the same): rounds of the chain's events
+    // [o_b, o_kstar), wstat / wflag / Bm, the new candidate's WLA / WFD rows (its segment stays
+    // staged: o_kstar is the next window's start) and its S row (sbits buffer r & 1)
+    int o_b = 0, o_kstar = 0;
+    auto outputs = [&](int r) {
+        const bool o_have = o_b < len, o_nx = o_kstar < len;
+        for (int k = o_b + t; k < o_kstar; k += T) A.p_round[off + k] = r;
+        if (t == 0) {
+            A.wstat[(size_t)r * C + gc] = o_have ? ((o_kstar > o_b) ? 2 : 1) : 0;
+            A.wflag[(size_t)(r + 1) * C + gc] = o_nx ? 1 : 0;
+            A.Bm[(size_t)(r + 1) * C + gc] = o_kstar;
+            if (o_nx) A.active[r] = 1;
+        }
+        if (o_nx) {
+            const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
+            for (int i = t; i < n; i += T) {
+                A.WLA[nrow + i] = Coord<CT>::la(raw_at(o_kstar, i));
+                const CT f = fd_at(i, o_kstar);
+                if constexpr (K::CSZ == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
+                else A.WFD[nrow + i] = f;
+            }
+            const uint32_t* sb = sbits_all + (r & 1) * K::SBW;
+            const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
+            for (int wd = t; wd < A.nw; wd += T)
+                A.Smat[srow + wd] = (uint64_t)sb[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sb[2 * wd + 1] : 0) << 32);
+        }
     };
     RP_PROF_BEGIN();
-    int cur = 0;
-    if (b < len) stage(b, 0);
     int s = P.r0;
     bool failed = false;
     for (;; s++) {
@@ -337,34 +362,61 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         int32_t* bm_cur = (int32_t*)(lds + ((s & 1) ? K::O_BM1 : K::O_BM0));
         const bool have = b < len;   // block-uniform
         int kb = b, np = have ? min(kRpP, len - b) : 0;
-        // (a) the first poll of this lane's candidate granule (W'_s, tag s + 1) goes out first and
-        // is in flight while this round's window (staged at the end of the previous round, before
-        // the poll) lands and is rebased to base(s). Every lane issues it (a clamped address for
-        // the lanes past n), so the vmcnt below covers exactly the staging.
+        // (a) the first load of this lane's candidate granule and row part (W'_s) goes out first
+        // and is in flight while this round's window (staged at the end of the previous round,
+        // before these loads) lands and is rebased to base(s). Every lane issues them (a clamped
+        // address for the lanes past n), so the vmcnt below covers exactly the staging.
         const uint64_t* gp = P.gran + (size_t)(s % kRpSlots) * C + g0 + (jv ? j : 0);
+        const uint32_t* rowp = P.FD8p + ((size_t)(s & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD;
+        const uint32_t vbit = ((s >> 2) & 1) ? 0x80808080u : 0u;
         uint64_t gv = rp_ld_gran(gp);
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // this wave's staging has landed
+        uint32_t fd[HD];
+        rp_ld_row<HD>(rowp, fd);
+        // No wait here: the window's segments were staged two rounds ago or earlier, and every
+        // wave's poll drain of the previous round waited for them (the end-of-round barrier then
+        // covers every wave). Waiting here would also wait for the previous round's stores.
+        uint32_t* sbits = sbits_all + (s & 1) * K::SBW;
+        if (have && min((b + kRpP - 1) / SEG, last_seg) > seg_hi) {
+            // the window is not staged yet (the first round of a launch, or a chain that advanced
+            // by more than the ring's lookahead): stage it now and wait for it
+            stage_range(b / SEG, min(b / SEG + NSEG - 1, last_seg));
+            rp_vm_drain();
+            RP_PROF_COUNT(10);
+        }
+        RP_PROF(7);
         if (t < 32) hist[t] = 0;
         if (t == 0) { misc[2] = 0; misc[3] = 0; }
         if (t < K::NC / 32 + 1) sbits[t] = 0;
         rp_lds_barrier();
-        if (have) rebase(cur, np, bm_prev);
+        RP_PROF(12);
+        if (have) rebase(b, np, bm_prev);
         rp_lds_barrier();
         RP_PROF(0);
 
-        // (b) poll until every candidate of this wave is published, then load their rows
+        // (b) until every candidate of this wave is published: its granule carries tag s + 1 and,
+        // when the candidate exists, every byte of its row part carries v(s); reload otherwise
         bool wfail = false;
         {
             const long long tw = __builtin_amdgcn_s_memrealtime();
             for (int spins = 0;; spins++) {
-                if (!jv) gv = (uint64_t)(uint32_t)(s + 1) << 32;
-                if (__all((uint32_t)(gv >> 32) == (uint32_t)(s + 1))) break;
+                rp_vm_drain();
+#pragma unroll
+                for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+                uint32_t bad = 0;
+#pragma unroll
+                for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
+                const bool tag_ok = (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
+                const bool ok = !jv || (tag_ok && (!((uint32_t)gv & kRpEx) || bad == 0));
+                if (__all(ok)) break;
                 if ((spins & 31) == 31) {
                     const long long now = __builtin_amdgcn_s_memrealtime();
                     if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);
-                gv = rp_ld_gran(gp);
+                if (!ok) {
+                    gv = rp_ld_gran(gp);
+                    rp_ld_row<HD>(rowp, fd);
+                }
             }
         }
         RP_PROF(1);
@@ -373,18 +425,19 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         const bool ov = cand && (gval & kRpOv);
         const int bmj = (int)(gval & kRpBm);
         if (jv && q == 0 && !wfail) bm_cur[j] = bmj;
-        uint32_t fd[HD];
         if (cand && have) {
-            rp_ld_row<HD>(P.FD8p + ((size_t)(s & 1) * C + g0 + j) * NDW + q * HD, fd);
+#pragma unroll
+            for (int d = 0; d < HD; d++) fd[d] &= 0x7F7F7F7Fu;   // the validity bits off: rebased values
         } else {
 #pragma unroll
             for (int d = 0; d < HD; d++) fd[d] = 0x7F7F7F7Fu;   // never seen
         }
         if (wfail && lane == 0) misc[3] = 1;
         if (cand && q == 0) misc[2] = 1;   // (same value from every writer)
-        rp_vm_drain();
-#pragma unroll
-        for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+        // the ring ahead: segments up to b / SEG + NSEG - 1, landing behind the search, the
+        // publish and the outputs (the next round's first wait covers them; a window after a
+        // first-window boundary lies below b / SEG + 3)
+        if (have) stage_range(b / SEG, min(b / SEG + NSEG - 1, last_seg));
         RP_PROF(2);
 
         // (c) search, window after window until the boundary is found (a later window is rare)
@@ -409,7 +462,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                         const size_t pos = (size_t)coff[j] + bmj;
                         for (int i = i_lo; i < i_hi; i++) {
                             const int32_t fdv = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + pos]);
-                            const int32_t lav = min(Coord<CT>::la(raw_at(cur, mid, i)), kMaxI32 - 1);
+                            const int32_t lav = min(Coord<CT>::la(raw_at(kb + mid, i)), kMaxI32 - 1);
                             cnt += lav >= fdv ? 1u : 0u;
                         }
                     }
@@ -437,17 +490,17 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 break;
             }
             // no boundary in this window: the next one (synchronous staging)
+            RP_PROF_COUNT(11);
             carried = misc[1];
             if (cand && Kw < np) done = true;
             kb += np;
             if (kb >= len) break;
             np = min(kRpP, len - kb);
             if (t < 32) hist[t] = 0;
-            rp_lds_barrier();
-            stage(kb, cur);
+            if (min((kb + kRpP - 1) / SEG, last_seg) > seg_hi) stage_range(kb / SEG, min(kb / SEG + NSEG - 1, last_seg));
             rp_vm_drain();
             __syncthreads();
-            rebase(cur, np, bm_prev);
+            rebase(kb, np, bm_prev);
             rp_lds_barrier();
         }
         if (!have) rp_lds_barrier();   // the pollers' any / fail words
@@ -455,15 +508,15 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         if (misc[3] != 0) { failed = true; break; }
         if (misc[2] == 0) break;       // W'_s is empty: no round s (every workgroup of the graph agrees)
 
-        // (d) publish W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s]), written
-        // through by wave 0; every wave then stages the next window (buffer cur ^ 1: the outputs
-        // below still read buffer cur); wave 0 drains its row stores, not the staging, and stores
-        // the granule
+        // (d) wave 0 publishes W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s],
+        // bit 7 of every byte = v(s + 1)) and its granule, written through with no drain in between
+        // (both self-validating)
         const bool nx = kstar < len;
-        const int pk = kstar - kb;
+        RP_PROF(8);
         bool of = false;
         if (wave == 0 && nx) {
-            uint32_t* dst = P.FD8p + ((size_t)((s + 1) & 1) * C + gc) * NDW;
+            const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
+            uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
             for (int d = lane; d < NDW; d += 64) {
                 uint32_t w = 0;
 #pragma unroll
@@ -471,7 +524,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     const int i = 4 * d + u;
                     uint32_t v = 127u;
                     if (i < n) {
-                        const int32_t f = Coord<CT>::fd(fd_at(cur, i, pk));
+                        const int32_t f = Coord<CT>::fd(fd_at(i, kstar));
                         if (f != kMaxI32) {
                             const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
                             if (x > 126) of = true;
@@ -480,49 +533,29 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     }
                     w |= v << (8 * u);
                 }
-                rp_st_sc1(dst + d, w);
+                rp_st_sc1(dst + d, w | vb1);
             }
         }
-        if (nx) stage(kstar, cur ^ 1);
+        RP_PROF(9);
         if (wave == 0) {
             of = __any(of);
-            if (nx) wait_all_but_dma();   // the row stores are done (the staging went out after them)
-            else rp_vm_drain();
             if (lane == 0)
                 rp_st_gran(P.gran + (size_t)((s + 1) % kRpSlots) * C + gc,
                            ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u));
             if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
         RP_PROF(5);
-        // (e) the round's other outputs (read by later launches: plain stores)
-        if (have) {
-            for (int k = b + t; k < kstar; k += T) A.p_round[off + k] = s;
-            if (nx && cand && q == 0 && (done || K_last <= B)) atomicOr(&sbits[j >> 5], 1u << (j & 31));
-        }
-        if (t == 0) {
-            A.wstat[(size_t)s * C + gc] = have ? ((kstar > b) ? 2 : 1) : 0;
-            A.wflag[(size_t)(s + 1) * C + gc] = nx ? 1 : 0;
-            A.Bm[(size_t)(s + 1) * C + gc] = kstar;
-            if (nx) A.active[s] = 1;
-        }
-        if (nx) {
-            const size_t nrow = ((size_t)(s + 1) * C + gc) * n;
-            for (int i = t; i < n; i += T) {
-                A.WLA[nrow + i] = Coord<CT>::la(raw_at(cur, pk, i));
-                const CT f = fd_at(cur, i, pk);
-                if constexpr (K::CSZ == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
-                else A.WFD[nrow + i] = f;
-            }
-            rp_lds_barrier();
-            const size_t srow = ((size_t)(s + 1) * C + gc) * A.nw;
-            for (int wd = t; wd < A.nw; wd += T)
-                A.Smat[srow + wd] = (uint64_t)sbits[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sbits[2 * wd + 1] : 0) << 32);
-        }
+        // (e) the S row of the new candidate (the outputs are written next round, outputs())
+        if (have && nx && cand && q == 0 && (done || K_last <= B)) atomicOr(&sbits[j >> 5], 1u << (j & 31));
+        o_b = b;
+        o_kstar = kstar;
+        rp_lds_barrier();   // the S row bits are complete
+        outputs(s);
         b = kstar;
-        cur ^= 1;
         rp_lds_barrier();   // every read of this round's LDS is done
         RP_PROF(6);
     }
+
     rp_vm_drain();   // no LDS-DMA outlives the workgroup
     RP_PROF_END();
     if (failed) {
@@ -545,8 +578,10 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     }
 }
 
-// W'_{r} rows (row-major, rebased to base(r)) and their granules before the first launch of
-// a DivideRounds, from the WFD rows k_round_gather wrote. One workgroup per chain.
+// W'_{r} rows (row-major, rebased to base(r), bit 7 = v(r)) and their granules before the first
+// launch of a DivideRounds, from the WFD rows k_round_gather wrote; the chain's rows in the three
+// other buffers get the invalid bit for the rounds r + 1 .. r + 3 that will use them (they may
+// hold an earlier call's rows of those very rounds). One workgroup per chain.
 template <typename CT>
 __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
     const RoundArgs& A = P.A;
@@ -571,7 +606,10 @@ __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
             }
             w |= v << (8 * u);
         }
-        P.FD8p[((size_t)(r & 1) * C + gc) * ndw + d] = w;
+        P.FD8p[((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d] = w | ((((r >> 2) & 1) ? 0x80808080u : 0u));
+        for (int k = 1; k < kRoundPBufs; k++)
+            P.FD8p[((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d] =
+                (((r + k) >> 2) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu;   // bit 7 = !v(r + k)
     }
     of = __any(of);
     if (threadIdx.x == 0)

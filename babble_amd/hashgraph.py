@@ -510,9 +510,9 @@ class Hashgraph:
             raise ValueError(f"invalid round kernel {mode}")
 
     def set_cts_kernel(self, mode):
-        """FindOrder consensus timestamps: "auto" (default: pipelined resident blocks where they
-        apply) or "tile" (one tile of 8 positions per block)."""
-        m = {"auto": 0, "pipe": 0, "tile": 1}[mode] if isinstance(mode, str) else int(mode)
+        """FindOrder consensus timestamps: "auto" = "tile" (default: one tile of 8 positions per
+        block) or "pipe" (resident blocks with several tiles' loads in flight, hgx_cts.hip)."""
+        m = {"auto": 0, "tile": 1, "pipe": 2}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_cts_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid timestamp kernel {mode}")
 

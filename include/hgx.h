@@ -389,9 +389,10 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
  * (hgx_round_k.hip; candidates in chunks of 128 above n = 256). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
-/* FindOrder consensus timestamps: 0 = default: resident blocks with three tiles' gathers in
- * flight (hgx_cts.hip) where it applies (32 < n <= 512, at most 4096 chains), otherwise mode 1;
- * 1 = one tile of 8 positions per block (k_cts_small / k_cts_tile, hgx_kernels.hip). Same results. */
+/* FindOrder consensus timestamps: 0 = default = 1: one tile of 8 positions per block (k_cts_small /
+ * k_cts_tile, hgx_kernels.hip); 2 = resident blocks with three tiles' loads in flight behind the
+ * selects of a fourth (hgx_cts.hip) where it applies (32 < n <= 512, at most 4096 chains),
+ * otherwise mode 1 (measured slower at c3: 12.6 against 8.9 ms). Same results. */
 int32_t hgx_set_cts_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds schedule: 1 = incremental (default: a call after more InsertEvents extends
  * lastAncestors/firstDescendants for the new events only and resumes the round steps at the

@@ -133,11 +133,11 @@ def test_gossip_block_search_round_kernel(n, E, seed, silent, stale):
 @pytest.mark.parametrize("n,E,seed,silent,stale,chunk", [(64, 12000, 10, 21, 0.2, None), (100, 15000, 11, 0, 0.0, None),
                                                          (256, 30000, 16, 0, 0.0, None), (512, 24000, 18, 100, 0.2, None),
                                                          (128, 20000, 12, 0, 0.0, 1000), (1000, 30000, 20, 330, 0.3, None)])
-def test_gossip_tile_cts_kernel(n, E, seed, silent, stale, chunk):
-    """The one-tile-per-block consensus timestamp kernel (hgx_set_cts_kernel(ctx, 1),
-    k_cts_tile) against the oracle; the default pipelined kernel runs in every other test."""
+def test_gossip_pipelined_cts_kernel(n, E, seed, silent, stale, chunk):
+    """The pipelined consensus timestamp kernel (hgx_set_cts_kernel(ctx, 2), k_cts_pipe +
+    k_cts_redo) against the oracle; the default per-tile kernel runs in every other test."""
     t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
-    compare(run_gpu(t, chunk=chunk, cts_kernel="tile"), hgref.oracle_run(t, chunk=chunk), t, hashes=False)
+    compare(run_gpu(t, chunk=chunk, cts_kernel="pipe"), hgref.oracle_run(t, chunk=chunk), t, hashes=False)
 
 
 def _expect_compact(t):

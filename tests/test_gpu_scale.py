@@ -16,9 +16,11 @@ from babble_amd import trace as gtrace
 pytestmark = pytest.mark.gpu
 
 
-def _run(t, cap=None):
+def _run(t, cap=None, cts=None):
     from babble_amd.hashgraph import Hashgraph
     h = Hashgraph(t.n, capacity=cap or t.E)
+    if cts:
+        h.set_cts_kernel(cts)
     h.insert_trace(t)
     h.RunConsensus()
     return h
@@ -105,3 +107,10 @@ def test_wide_timestamps(n, E, seed, step, every):
     assert len(b["order"]) > 0
     if every == 1:
         assert span.bit_length() + int(rr.max()).bit_length() > 64 or span.bit_length() > 56
+
+
+@pytest.mark.parametrize("n,E,seed,step,every", [(64, 12000, 201, 46, 1), (256, 20000, 204, 44, 3)])
+def test_wide_timestamps_pipelined_cts(n, E, seed, step, every):
+    """The pipelined timestamp kernel's 64-bit redo pass (k_cts_redo) on offsets beyond 32 bits."""
+    t = _wide(gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3), step, every)
+    _compare(_run(t, cts="pipe"), hgref.oracle_run(t))
