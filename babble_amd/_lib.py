@@ -93,6 +93,7 @@ def lib():
     _sig(L, "hgx_destroy", None, [p])
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_insert_events_device", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
+    _sig(L, "hgx_insert_and_run", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_set_participant_keys", i32, [p, p, E])
     for nm in ("hgx_insert_events_verified", "hgx_insert_events_verified_device"):
         _sig(L, nm, i32, [p, C.POINTER(hgx_events), p, p, i64, C.POINTER(C.c_int64), E])

@@ -341,6 +341,58 @@ int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64
     return finish_insert(c, out, n_inserted, err);
 }
 
+// Bootstrap / Core.Sync + RunConsensus in one call (hashgraph.go:1008-1037, node/core.go:190-303):
+// InsertEvent for the batch, then DivideRounds, DecideFame and FindOrder. The insert is split
+// (Engine::insert_split_begin): the structure columns are validated and committed first, and
+// the payload columns (timestamps, hash, S, transactions: 80 of the 108 bytes per event) are
+// copied to HBM while DivideRounds runs, committed before DecideFame reads the coins.
+int32_t hgx_insert_and_run(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || !ev || count < 0 ||
+        (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
+                       !ev->hash || !ev->sig_s || !ev->ntx || !ev->tx_nil))) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_and_run: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (count < 65536 || c->rooted || c->shard_world > 1) {   // small batches gain nothing from the overlap
+        int32_t rc = hgx_insert_events(c, ev, count, n_inserted, err);
+        if (rc) return rc;
+        return hgx_run_consensus(c, err);
+    }
+    DeviceGuard dg(c);
+    const int64_t E0 = c->eng.E;
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert_split_begin(ev->creator, ev->index, ev->self_parent, ev->other_parent, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run");
+    e = c->eng.payload_begin(ev->timestamp_ns, ev->hash, ev->sig_s, ev->ntx, ev->tx_nil, out.accepted);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run");
+    // the per-creator mirrors and UndeterminedEvents now; PendingLoadedEvents once the payload
+    // (IsLoaded) is committed
+    hgx::InsertOut head = out;
+    head.graph_loaded.assign(c->g_loaded.begin(), c->g_loaded.end());
+    hgx_error ins_err{};
+    const int32_t ins_rc = finish_insert(c, head, n_inserted, &ins_err);
+    int32_t rc = ins_rc ? ins_rc : hgx_divide_rounds(c, err);
+    const bool laid_out = ins_rc == 0 && rc == 0;
+    std::vector<uint64_t> loaded;
+    e = c->eng.payload_end(E0, out.accepted, laid_out, c->rh.r_lo, loaded);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run");
+    for (int g = 0; g < c->G; g++) {
+        const int64_t l = (int64_t)loaded[g];
+        c->gs[g].pending_loaded += l - c->g_loaded[g];
+        c->g_loaded[g] = l;
+    }
+    c->mirror_ok = false;
+    if (ins_rc) {   // the accepted prefix is inserted; consensus does not run (as hgx_bootstrap)
+        if (err) *err = ins_err;
+        return ins_rc;
+    }
+    if (rc) return rc;
+    rc = hgx_decide_fame(c, err);
+    if (rc) return rc;
+    return hgx_find_order(c, err);
+}
+
 int32_t hgx_set_participant_keys(hgx_ctx* c, const uint8_t* keys65, hgx_error* err) {
     if (!c || !keys65) {
         set_err(err, HGX_ERR_INVALID, "hgx_set_participant_keys: bad arguments");
@@ -1618,7 +1670,7 @@ int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t cou
 }
 
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
+    if (!c || mode < 0 || mode > 3) return HGX_ERR_INVALID;
     c->eng.round_kernel = mode;
     return HGX_OK;
 }

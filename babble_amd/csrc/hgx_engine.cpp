@@ -63,6 +63,10 @@ static int bitlen(uint64_t v) {
 }
 
 Engine::~Engine() {
+    if (pay_thread.joinable()) pay_thread.join();
+    if (stream2) (void)hipStreamSynchronize(stream2);
+    if (ev_pay) (void)hipEventDestroy(ev_pay);
+    if (stream2) (void)hipStreamDestroy(stream2);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto e : kev) (void)hipEventDestroy(e);
     if (ph0) (void)hipEventDestroy(ph0);
@@ -397,7 +401,70 @@ hipError_t Engine::insert(const InsertIn& in, int64_t count, InsertOut& out) {
     return insert_impl(in, count, out, nullptr);
 }
 
-hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig) {
+hipError_t Engine::insert_split_begin(const int32_t* creator, const int64_t* index, const int64_t* sp,
+                                      const int64_t* op, int64_t count, InsertOut& out) {
+    const size_t c = (size_t)count;
+    HGX_TRY(stage_col(st_creator, creator, c, 1, stream));
+    HGX_TRY(stage_col(st_index, index, c, 1, stream));
+    HGX_TRY(stage_col(st_sp, sp, c, 1, stream));
+    HGX_TRY(stage_col(st_op, op, c, 1, stream));
+    InsertIn in{};
+    in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p;   // no payload yet
+    return insert_impl(in, count, out, nullptr, kCommitStructure);
+}
+
+hipError_t Engine::payload_begin(const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
+                                 const int32_t* nil, int64_t m_ok) {
+    if (!stream2) {
+        HGX_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        HGX_TRY(hipEventCreateWithFlags(&ev_pay, hipEventDisableTiming));
+    }
+    const size_t c = (size_t)m_ok;   // the accepted prefix only
+    if (st_ts.n < c) HGX_TRY(st_ts.alloc(c));
+    if (st_hash.n < 32 * c) HGX_TRY(st_hash.alloc(32 * c));
+    if (st_S.n < 32 * c) HGX_TRY(st_S.alloc(32 * c));
+    if (st_ntx.n < c) HGX_TRY(st_ntx.alloc(c));
+    if (st_nil.n < c) HGX_TRY(st_nil.alloc(c));
+    pay_err = hipSuccess;
+    // pageable host memory: each copy returns once its source has been consumed, so the copies
+    // run on their own host thread (and stream) beside the DivideRounds launches
+    pay_thread = std::thread([=]() {
+        hipError_t e = hipSetDevice(dev);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_ts.p, ts, c * 8, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_hash.p, hash, c * 32, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_S.p, S, c * 32, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_ntx.p, ntx, c * 4, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_nil.p, nil, c * 4, hipMemcpyHostToDevice, stream2);
+        if (e == hipSuccess) e = hipEventRecord(ev_pay, stream2);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream2);   // the caller's buffers are read completely
+        pay_err = e;
+    });
+    return hipSuccess;
+}
+
+hipError_t Engine::payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int32_t wcoin_r0,
+                               std::vector<uint64_t>& loaded) {
+    if (pay_thread.joinable()) pay_thread.join();
+    HGX_TRY(pay_err);
+    HGX_TRY(hipStreamWaitEvent(stream, ev_pay, 0));
+    InsertIn in{};
+    in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p;
+    in.ts = st_ts.p; in.hash = st_hash.p; in.S = st_S.p; in.ntx = st_ntx.p; in.nil = st_nil.p;
+    launch_insert_commit(stream, m_ok, E0, n, in, insert_state(), kCommitPayload);
+    if (laid_out_new) {   // the layout ran before the timestamps and coins were committed
+        launch_ts_to_pos(stream, E0, m_ok, g_pos.p, g_ts.p, p_ts.p);
+        if (R > wcoin_r0) launch_wcoin(stream, arrays(), wcoin_r0, R, C);
+    }
+    HGX_TRY(hipGetLastError());
+    HGX_TRY(hipMemcpyAsync(h_ins, ins_blk.p, ins_blk.n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    HGX_TRY(hipStreamSynchronize(stream));
+    loaded.resize(G);
+    std::memcpy(loaded.data(), h_ins + ins_gl_off, (size_t)G * 8);
+    return hipSuccess;
+}
+
+hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig,
+                               int commit_mode) {
     out = InsertOut();
     const int64_t E0 = E;
     InsertState st = insert_state();
@@ -416,7 +483,7 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
         const int64_t m_ok = (fail == ~0ull) ? count : (int64_t)(fail >> 8);
         out.accepted = m_ok;
         out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
-        launch_insert_commit(stream, m_ok, E0, n, in, st);
+        launch_insert_commit(stream, m_ok, E0, n, in, st, commit_mode);
         launch_insert_unclaim(stream, count, m_ok, E0, cap, C, in, st);
         if (out.code) {
             HGX_TRY(hipMemcpyAsync(&out.fail_creator, in.creator + m_ok, 4, hipMemcpyDeviceToHost, stream));
@@ -835,7 +902,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             s = h_small[57];   // the round tables' capacity: continue from there
         }
     };
-    if (!rooted && round_kernel == 0 && round_p_ok(n, C, num_cus)) {
+    // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
+    // workgroups) that a call resuming for a few rounds does not recover: those use the steps
+    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)

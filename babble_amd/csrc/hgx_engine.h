@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hgx_kernels.h"
@@ -108,6 +109,17 @@ class Engine {
     hipError_t stage_host(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
                           const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                           const int32_t* nil, int64_t count, InsertIn& in);
+    // hgx_insert_and_run's split insert of host columns: the structure columns (creator, index,
+    // parents) are staged, validated and committed now (out.graph_loaded is not final); a worker
+    // thread copies the payload columns (timestamps, hash, S, transactions) of the accepted
+    // prefix on a second stream while the caller runs DivideRounds; payload_end joins it, commits
+    // the payload, rewrites the layout's timestamps and the candidates' coins, and returns the
+    // graphs' loaded counts. Not for rooted contexts (Root.Others needs the hash at validation).
+    hipError_t insert_split_begin(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
+                                  int64_t count, InsertOut& out);
+    hipError_t payload_begin(const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
+                             const int32_t* nil, int64_t m_ok);
+    hipError_t payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int32_t wcoin_r0, std::vector<uint64_t>& loaded);
     // forget every event (a fresh NewHashgraph); allocations are kept
     hipError_t clear();
     // per-event columns (gid order) for the host-side getters
@@ -181,7 +193,7 @@ class Engine {
     KernelStat kstat[K_NUM];
     uint32_t time_mask = 0;   // kernels (bit = KernelId) timed with HIP events
     int fame_tally = 0;       // launch_fame tally (hgx_set_fame_tally)
-    int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence where it applies (hgx_round_p.hip),
+    int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence on rebuilds where it applies (3: every call),
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
     int cts_kernel = 1;       // hgx_set_cts_kernel: 1 per-tile blocks (default: measured faster), 2 pipelined (hgx_cts.hip)
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
@@ -191,7 +203,12 @@ class Engine {
 
    private:
     hipError_t ensure_round_cap(int32_t need);
-    hipError_t insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig);
+    hipError_t insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig,
+                           int commit_mode = kCommitAll);
+    hipStream_t stream2 = nullptr;   // payload copies of insert_split (created on first use)
+    hipEvent_t ev_pay = nullptr;
+    std::thread pay_thread;
+    hipError_t pay_err = hipSuccess;
     InsertState insert_state();
     void kbeg(int k, bool sample = true, int64_t count = 1);
     void kend(int k, double bytes);

@@ -121,7 +121,11 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
 // grid-stride: the loaded-event count of each graph is kept per wave while the wave's events
 // share a graph and added once when it changes (one word per graph: an atomic per wave of
 // events saturated it, 1.9 ms for 10 M events of one graph)
-__global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0, int n, InsertIn in, InsertState st) {
+// mode: kCommitAll, or the split of hgx_insert_and_run: kCommitStructure (the columns validation
+// and DivideRounds read) now, kCommitPayload (timestamps, S, coin, transactions, IsLoaded and the
+// graphs' loaded counts) once the payload columns have landed
+__global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0, int n, InsertIn in, InsertState st,
+                                                       int mode) {
     int acc_g = -1;                 // wave-uniform: the graph whose loaded count is pending
     unsigned long long acc = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -132,31 +136,36 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0,
         if (k < m_ok) {
             const int64_t gid = E0 + k;
             const int cr = in.creator[k];
-            const int64_t idx = in.index[k], sp = in.sp[k];
-            const int nt = in.ntx[k];
-            const int nil = in.nil[k] ? 1 : 0;
-            st.g_creator[gid] = cr;
-            st.g_index[gid] = (int32_t)idx;
-            st.g_sp[gid] = (int32_t)sp;
-            st.g_op[gid] = (int32_t)in.op[k];
-            st.g_ts[gid] = in.ts[k];
-            const uint4* s4 = (const uint4*)(in.S + 32 * k);
-            uint4* d4 = (uint4*)(st.g_S + 32 * gid);
-            d4[0] = s4[0];
-            d4[1] = s4[1];
-            st.g_coin[gid] = in.hash[32 * k + 16] != 0 ? 1 : 0;   // middleBit (hashgraph.go:1039-1048)
-            st.g_ntx[gid] = nt;
-            st.g_txnil[gid] = (uint8_t)nil;
-            ld = idx == 0 || (!nil && nt > 0);   // IsLoaded (event.go:119-126)
-            st.g_loaded[gid] = ld ? 1 : 0;
-            st.g_rr[gid] = -1;                   // roundReceived = nil
-            st.g_cts[gid] = 0;
-            if (sp == -1) st.chain_base[cr] = (int32_t)idx;
-            if (st.succ[gid] >= (uint32_t)(E0 + m_ok)) {   // no accepted event follows it on its chain
-                st.last_gid[cr] = (int32_t)gid;
-                st.last_index[cr] = (int32_t)idx;
+            const int64_t idx = in.index[k];
+            if (mode != kCommitPayload) {
+                const int64_t sp = in.sp[k];
+                st.g_creator[gid] = cr;
+                st.g_index[gid] = (int32_t)idx;
+                st.g_sp[gid] = (int32_t)sp;
+                st.g_op[gid] = (int32_t)in.op[k];
+                st.g_rr[gid] = -1;                   // roundReceived = nil
+                st.g_cts[gid] = 0;
+                if (sp == -1) st.chain_base[cr] = (int32_t)idx;
+                if (st.succ[gid] >= (uint32_t)(E0 + m_ok)) {   // no accepted event follows it on its chain
+                    st.last_gid[cr] = (int32_t)gid;
+                    st.last_index[cr] = (int32_t)idx;
+                }
             }
-            g = cr / n;
+            if (mode != kCommitStructure) {
+                const int nt = in.ntx[k];
+                const int nil = in.nil[k] ? 1 : 0;
+                st.g_ts[gid] = in.ts[k];
+                const uint4* s4 = (const uint4*)(in.S + 32 * k);
+                uint4* d4 = (uint4*)(st.g_S + 32 * gid);
+                d4[0] = s4[0];
+                d4[1] = s4[1];
+                st.g_coin[gid] = in.hash[32 * k + 16] != 0 ? 1 : 0;   // middleBit (hashgraph.go:1039-1048)
+                st.g_ntx[gid] = nt;
+                st.g_txnil[gid] = (uint8_t)nil;
+                ld = idx == 0 || (!nil && nt > 0);   // IsLoaded (event.go:119-126)
+                st.g_loaded[gid] = ld ? 1 : 0;
+                g = cr / n;
+            }
         }
         const int g0 = __builtin_amdgcn_readfirstlane(g);
         const uint64_t lm = __ballot(ld);
@@ -174,6 +183,18 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0,
         }
     }
     if (acc_g >= 0 && acc && lane_id() == 0) atomicAdd(&st.graph_loaded[acc_g], acc);
+}
+
+// p_ts of the events [E0, E0 + m) from their gid-order timestamps (the layout copied them
+// before the payload of hgx_insert_and_run had landed)
+__global__ void k_ts_to_pos(int64_t E0, int64_t m, const int32_t* __restrict__ g_pos, const int64_t* __restrict__ g_ts,
+                            int64_t* __restrict__ p_ts) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) p_ts[g_pos[E0 + k]] = g_ts[E0 + k];
+}
+
+void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos, const int64_t* g_ts, int64_t* p_ts) {
+    if (m > 0) hipLaunchKernelGGL(k_ts_to_pos, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, E0, m, g_pos, g_ts, p_ts);
 }
 
 // withdraw the claims of the discarded events [m_ok, m)
@@ -203,9 +224,10 @@ void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int 
     if (m > 0) hipLaunchKernelGGL(k_insert_check, dim3(nblocks(m)), dim3(256), 0, s, m, E0, cap, C, n, in, st);
 }
 
-void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st) {
+void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st,
+                          int mode) {
     const unsigned grid = nblocks(m_ok) < 4096u ? nblocks(m_ok) : 4096u;   // grid-stride beyond 1 M events
-    if (m_ok > 0) hipLaunchKernelGGL(k_insert_commit, dim3(grid), dim3(256), 0, s, m_ok, E0, n, in, st);
+    if (m_ok > 0) hipLaunchKernelGGL(k_insert_commit, dim3(grid), dim3(256), 0, s, m_ok, E0, n, in, st, mode);
 }
 
 // Event.Verify's place in InsertEvent (hashgraph.go:356-363): the smallest event of the batch

@@ -226,7 +226,10 @@ void launch_insert_claim(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int 
                          const InsertState& st);
 void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, int n, const InsertIn& in,
                          const InsertState& st);
-void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st);
+constexpr int kCommitAll = 0, kCommitStructure = 1, kCommitPayload = 2;
+void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st,
+                          int mode = kCommitAll);
+void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos, const int64_t* g_ts, int64_t* p_ts);
 void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
                            const InsertState& st);
 // verify results vout[k] (1 valid, 0 invalid, 2 key not a point) -> *fail = min (k << 8 | code)

@@ -200,7 +200,9 @@ struct RpCfg {
     static constexpr int SBW = (NC / 32 + 4 + 3) & ~3;                   // S row words per buffer
     static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits [2][SBW], by round parity
     static constexpr int O_MISC = O_SB + 2 * SBW * 4;                    // [0] B, [1] tot, [2] any, [3] fail
-    static constexpr int USED = O_MISC + 64;
+    static constexpr int O_FW8 = O_MISC + 64;                            // [kRpP][NDW] next-round rows of the probes
+    static constexpr int O_FWOV = O_FW8 + kRpP * NDW * 4;                // [32] a probe's row does not fit 8 bits
+    static constexpr int USED = O_FWOV + 32 * 4;
     // at least 82 KB: one workgroup per CU (the hand-off rule's geometry), whatever fits
     static constexpr int LDS = USED > 84 * 1024 ? USED : 84 * 1024;
     static_assert(USED <= 160 * 1024, "k_round_p: LDS carve exceeds a CU's 160 KB");
@@ -235,6 +237,8 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     int32_t* hist = (int32_t*)(lds + K::O_HIST);
     uint32_t* sbits_all = (uint32_t*)(lds + K::O_SB);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
+    uint32_t* fw8 = (uint32_t*)(lds + K::O_FW8);
+    int32_t* fwov = (int32_t*)(lds + K::O_FWOV);
 
     if (P.fin[g] >= 0) return;   // the graph finished in an earlier launch of this DivideRounds
     const int len = A.c_len[gc], off = A.c_off[gc];
@@ -473,8 +477,33 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             }
             const int Kw = lo;
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
+            if (t < 32) fwov[t] = 0;
             rp_lds_barrier();
             RP_PROF(3);
+            // while wave 0 scans for the boundary, every wave rebases the probes' firstDescendants
+            // rows to base(s + 1) = c_base + Bm[s] (bm_cur, complete since the poll): the row of
+            // whichever probe becomes W'_{s+1}'s candidate is then ready to publish
+            for (int it = t; it < np * NDW; it += T) {
+                const int pp = it / NDW, d = it % NDW;
+                uint32_t w = 0;
+                bool ofp = false;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int i = 4 * d + u;
+                    uint32_t v = 127u;
+                    if (i < n) {
+                        const int32_t f = Coord<CT>::fd(fd_at(i, kb + pp));
+                        if (f != kMaxI32) {
+                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
+                            if (x > 126) ofp = true;
+                            else v = (uint32_t)x;
+                        }
+                    }
+                    w |= v << (8 * u);
+                }
+                fw8[pp * NDW + d] = w;
+                if (ofp) fwov[pp] = 1;
+            }
             if (wave == 0) {   // boundary: first probe where #{K <= p} (+ seen in earlier windows) >= SM
                 const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
                 const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
@@ -517,24 +546,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         if (wave == 0 && nx) {
             const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
             uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
-            for (int d = lane; d < NDW; d += 64) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int i = 4 * d + u;
-                    uint32_t v = 127u;
-                    if (i < n) {
-                        const int32_t f = Coord<CT>::fd(fd_at(i, kstar));
-                        if (f != kMaxI32) {
-                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
-                            if (x > 126) of = true;
-                            else v = (uint32_t)x;
-                        }
-                    }
-                    w |= v << (8 * u);
-                }
-                rp_st_sc1(dst + d, w | vb1);
-            }
+            const int pk = kstar - kb;   // the boundary probe of the last window searched
+            for (int d = lane; d < NDW; d += 64) rp_st_sc1(dst + d, fw8[pk * NDW + d] | vb1);
+            of = fwov[pk] != 0;
         }
         RP_PROF(9);
         if (wave == 0) {

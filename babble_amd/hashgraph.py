@@ -152,6 +152,32 @@ class Hashgraph:
         return self.insert_arrays(t.creator[sl], t.index[sl], t.sp[sl], t.op[sl], t.ts[sl], t.hash[sl], t.s[sl],
                                   t.ntx[sl], t.txnil[sl])
 
+    def insert_and_run(self, t, lo: int = 0, hi: Optional[int] = None) -> int:
+        """Bootstrap / Core.Sync + RunConsensus in one call (hgx_insert_and_run): events [lo, hi) of a
+        trace inserted, then DivideRounds / DecideFame / FindOrder, the payload columns copied to HBM
+        while DivideRounds runs. Raises HgxError like insert_trace (.inserted = the accepted prefix)."""
+        hi = t.E if hi is None else hi
+        sl = slice(lo, hi)
+        a = dict(creator=np.ascontiguousarray(t.creator[sl], np.int32), index=np.ascontiguousarray(t.index[sl], np.int64),
+                 sp=np.ascontiguousarray(t.sp[sl], np.int64), op=np.ascontiguousarray(t.op[sl], np.int64),
+                 ts=np.ascontiguousarray(t.ts[sl], np.int64), h=np.ascontiguousarray(t.hash[sl], np.uint8),
+                 s=np.ascontiguousarray(t.s[sl], np.uint8), ntx=np.ascontiguousarray(t.ntx[sl], np.int32),
+                 nil=np.ascontiguousarray(t.txnil[sl], np.int32))
+        ev = hgx_events(ptr(a["creator"]), ptr(a["index"]), ptr(a["sp"]), ptr(a["op"]), ptr(a["ts"]),
+                        ptr(a["h"]), ptr(a["s"]), ptr(a["ntx"]), ptr(a["nil"]))
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        self._cb_error = None
+        rc = self.L.hgx_insert_and_run(self.ctx, C.byref(ev), hi - lo, C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        cb_err, self._cb_error = getattr(self, "_cb_error", None), None
+        if cb_err is not None:
+            raise cb_err
+        return n_ins.value
+
     def InsertEvent(self, creator: int, index: int, self_parent: int, other_parent: int, timestamp_ns: int,
                     hash32: bytes, s32: bytes, transactions: Optional[Sequence[bytes]]):
         """InsertEvent(event, true) (hashgraph.go:356-401): raises HgxError with the Go error string."""
@@ -502,10 +528,11 @@ class Hashgraph:
             raise ValueError(f"invalid lastAncestors kernel {mode}")
 
     def set_round_kernel(self, mode):
-        """DivideRounds rounds: "auto" (default: the persistent recurrence where it applies, else
-        per-round "candidate" launches), "block" (block binary search per round) or "candidate"
-        (one launch per round, one lane per candidate)."""
-        m = {"auto": 0, "persistent": 0, "block": 1, "candidate": 2}[mode] if isinstance(mode, str) else int(mode)
+        """DivideRounds rounds: "auto" (default: the persistent recurrence on calls that lay the DAG
+        out anew, where it applies, else per-round "candidate" launches), "persistent" (the
+        persistent recurrence on every call where it applies), "block" (block binary search per
+        round) or "candidate" (one launch per round, one lane per candidate)."""
+        m = {"auto": 0, "block": 1, "candidate": 2, "persistent": 3}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
 

@@ -7,9 +7,10 @@ per rank (weak scaling: independent 256-peer simulations, no data-path collectiv
 DESIGN.md §6). The trace is in host RAM when the clock starts. A step is one whole pass of
 the hot path, from the first event append to the order in host memory:
 
-    hgx_clear -> hgx_insert_events (the event columns copied to HBM, InsertEvent for every
-    event: parent/index validation + append, on the GPU) -> DivideRounds -> DecideFame
-    -> FindOrder
+    hgx_clear -> hgx_insert_and_run: InsertEvent for every event (the event columns copied to
+    HBM, parent/index validation + append on the GPU) -> DivideRounds -> DecideFame -> FindOrder,
+    in one call (Bootstrap, hashgraph.go:1008-1037); the payload columns (timestamps, hash, S,
+    transactions) are copied while DivideRounds runs
 
 Side legs on the same line: the step with the columns already in HBM (hbm_resident), the
 SyncLimit-chunked schedule (chunked_sync), event ids (ingest_sha256), signature checks
@@ -522,12 +523,10 @@ def main():
 
     def step():
         """from the first event append (the trace in host RAM, as the caller holds
-        it: the H2D copy of every event column is inside the step) to the order in host memory."""
+        it: the H2D copy of every event column is inside the step) to the order in host memory.
+        One hgx_insert_and_run = hgx_insert_events + DivideRounds + DecideFame + FindOrder."""
         h.clear()
-        h.insert_trace(tr)
-        h.DivideRounds()
-        h.DecideFame()
-        h.FindOrder()
+        h.insert_and_run(tr)
         return sum(int(h.L.hgx_consensus_events_count(h.ctx, g)) for g in range(G))
 
     h.set_kernel_timing(False)
@@ -636,8 +635,9 @@ def main():
             "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
                        "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
                        "ordered_events_per_step_per_gpu": int(m_pass),
-                       "step": "clear + InsertEvent (H2D of the event columns + device validation) + DivideRounds "
-                               "+ DecideFame + FindOrder, order in host memory",
+                       "step": "clear + hgx_insert_and_run: InsertEvent (H2D of the event columns + device "
+                               "validation) + DivideRounds + DecideFame + FindOrder, the payload columns' H2D "
+                               "beside DivideRounds; order in host memory",
                        "parallelism": f"replicas x{world} (seed-sharded)",
                        "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
                        "dominant_kernel": dom},

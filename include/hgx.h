@@ -165,6 +165,14 @@ int32_t hgx_set_shard(hgx_ctx* ctx, int32_t rank, int32_t world);
 int64_t hgx_shard_values(hgx_ctx* ctx, int32_t rank);
 int32_t hgx_shard_export(hgx_ctx* ctx, void* dst, int32_t dst_on_device);
 int32_t hgx_shard_import(hgx_ctx* ctx, int32_t src_rank, const void* src, int32_t src_on_device);
+/* Bootstrap from host columns / Core.Sync followed by Core.RunConsensus (hashgraph.go:1008-1037,
+ * node/core.go:190-303): hgx_insert_events for the batch, then hgx_run_consensus, in one call.
+ * For batches of 65 536 events and more (single-graph or batched contexts without roots, not
+ * row-sharded) the timestamps, hashes, S and transaction columns are copied to HBM while
+ * DivideRounds runs (they are read from FindOrder on); the result, the errors and the
+ * counters equal the two calls'. On an insert error the accepted prefix stays inserted and
+ * consensus does not run (the error is returned). The host buffers are read before it returns. */
+int32_t hgx_insert_and_run(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err);
 /* Core.RunConsensus (node/core.go:277-303): the three calls in sequence */
 int32_t hgx_run_consensus(hgx_ctx* ctx, hgx_error* err);
 /* Forget every consensus result but keep the inserted events resident in HBM:
@@ -384,7 +392,10 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds rounds: 0 = default: the persistent recurrence (hgx_round_p.hip, one resident
  * workgroup per chain runs every round in one launch) where it applies (n <= 256, at most one
- * chain per compute unit, no roots), otherwise one launch per round of mode 2;
+ * chain per compute unit, no roots) on a call that lays the DAG out anew (a call resuming after
+ * a few inserts runs a few rounds: one launch per round of mode 2 there, and wherever the
+ * persistent launch does not apply); 3 = the persistent recurrence on every call where it
+ * applies;
  * 1 = block binary search per round (hgx_rounds.hip; per-candidate search over streamed rows
  * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
  * (hgx_round_k.hip; candidates in chunks of 128 above n = 256). Same results. */

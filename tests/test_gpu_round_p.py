@@ -15,7 +15,7 @@ from babble_amd.trace import GossipTrace
 pytestmark = pytest.mark.gpu
 
 
-def _run(t, mode="auto", chunk=None, coord32=False, graphs=1, reserve=None):
+def _run(t, mode="persistent", chunk=None, coord32=False, graphs=1, reserve=None):
     from babble_amd.hashgraph import Hashgraph
     h = Hashgraph(t.n // graphs if graphs > 1 else t.n, capacity=max(64, t.E), n_graphs=graphs)
     if coord32:
@@ -96,6 +96,16 @@ def test_persistent_chunked_schedule(n, E, seed, chunk):
     ph = _check_persistent(h)
     assert ph["round_p_runs"] >= (E + chunk - 1) // chunk
     _compare(h, hgref.oracle_run(t, chunk))
+
+
+def test_auto_schedule_persistent_on_rebuild_only():
+    """The default: the persistent launch on the call that lays the DAG out, per-round steps on
+    the calls that resume after a sync's inserts; bit-exact either way."""
+    t = gtrace.gossip(64, 12000, 44, stale_prob=0.1, stale_depth=2)
+    h = _run(t, mode="auto", chunk=3000)
+    ph = h.phase_times()
+    assert ph["round_p_runs"] == 1 and ph["round_p_fallbacks"] == 0
+    _compare(h, hgref.oracle_run(t, 3000))
 
 
 @pytest.mark.parametrize("n,E,seed", [(8, 6000, 51), (16, 20000, 52)])
