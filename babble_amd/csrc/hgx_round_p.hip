@@ -77,10 +77,10 @@ void round_p_prof_dump() {
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
     const double r = h[15] ? (double)h[15] : 1.0;
     fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): staging-wait %.0f barrier %.0f rebase %.0f poll %.0f "
-            "rows %.0f search %.0f boundary %.0f staging-issue %.0f row-build %.0f granule %.0f outputs %.0f | "
-            "block-rounds %llu, synchronous stagings %llu, later windows %llu\n",
-            h[7] / r, h[12] / r, h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[6] / r,
-            h[15], h[10], h[11]);
+            "rows %.0f search-levels %.0f search-barrier %.0f boundary %.0f staging-issue %.0f row-build %.0f granule %.0f "
+            "outputs %.0f | block-rounds %llu, synchronous stagings %llu, later windows %llu\n",
+            h[7] / r, h[12] / r, h[0] / r, h[1] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r,
+            h[6] / r, h[15], h[10], h[11]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
 }
@@ -168,6 +168,12 @@ __device__ __forceinline__ uint32_t rp_combine(uint32_t x) {
     return x;
 }
 
+constexpr int rp_part_stride(int hd) {   // smallest stride >= hd that is 8 or 24 (mod 32)
+    int ps = hd;
+    while (ps % 32 != 8 && ps % 32 != 24) ps++;
+    return ps;
+}
+
 // geometry of one instantiation: n <= 4 NDW chains per graph; candidate j's row is split over
 // Q adjacent lanes (HD dwords each); T threads
 template <typename CT, int NDW, int Q>
@@ -176,7 +182,11 @@ struct RpCfg {
     static constexpr int HD = NDW / Q;
     static constexpr int T = (NC * Q < 64) ? 64 : NC * Q;
     static constexpr int NW = T / 64;
-    static constexpr int WS = NDW + 4;                         // 8-bit window row stride (dwords, == 4 mod 16)
+    // 8-bit window rows: part q of a row (HD dwords, what one lane of a candidate compares) at
+    // q * PS with PS = 8 or 24 (mod 32), so the Q lanes of a candidate read disjoint bank groups,
+    // and rows RS = Q * PS + 4 dwords apart (consecutive rows shifted by 4 banks)
+    static constexpr int PS = rp_part_stride(HD);
+    static constexpr int WS = Q * PS + 4;                      // row stride (dwords)
     static constexpr int CSZ = (int)sizeof(CT);
     // staging ring: NSEG segments of SEG positions (64 bytes of one firstDescendants column) of
     // the chain's rows; segment m (positions [SEG m, SEG m + SEG) from the chain's start) sits in
@@ -200,9 +210,7 @@ struct RpCfg {
     static constexpr int SBW = (NC / 32 + 4 + 3) & ~3;                   // S row words per buffer
     static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits [2][SBW], by round parity
     static constexpr int O_MISC = O_SB + 2 * SBW * 4;                    // [0] B, [1] tot, [2] any, [3] fail
-    static constexpr int O_FW8 = O_MISC + 64;                            // [kRpP][NDW] next-round rows of the probes
-    static constexpr int O_FWOV = O_FW8 + kRpP * NDW * 4;                // [32] a probe's row does not fit 8 bits
-    static constexpr int USED = O_FWOV + 32 * 4;
+    static constexpr int USED = O_MISC + 64;
     // at least 82 KB: one workgroup per CU (the hand-off rule's geometry), whatever fits
     static constexpr int LDS = USED > 84 * 1024 ? USED : 84 * 1024;
     static_assert(USED <= 160 * 1024, "k_round_p: LDS carve exceeds a CU's 160 KB");
@@ -237,8 +245,6 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     int32_t* hist = (int32_t*)(lds + K::O_HIST);
     uint32_t* sbits_all = (uint32_t*)(lds + K::O_SB);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
-    uint32_t* fw8 = (uint32_t*)(lds + K::O_FW8);
-    int32_t* fwov = (int32_t*)(lds + K::O_FWOV);
 
     if (P.fin[g] >= 0) return;   // the graph finished in an earlier launch of this DivideRounds
     const int len = A.c_len[gc], off = A.c_off[gc];
@@ -325,7 +331,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                         }
                     }
                 }
-                win[p * WS + d] = w;
+                win[p * WS + (d / HD) * K::PS + d % HD] = w;
             }
         }
     };
@@ -334,10 +340,10 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     // [o_b, o_kstar), wstat / wflag / Bm, the new candidate's WLA / WFD rows (its segment stays
     // staged: o_kstar is the next window's start) and its S row (sbits buffer r & 1)
     int o_b = 0, o_kstar = 0;
-    auto outputs = [&](int r) {
+    auto outputs = [&](int r, int tid, int nthr) {   // by threads [0, nthr) (tid = this thread's)
         const bool o_have = o_b < len, o_nx = o_kstar < len;
-        for (int k = o_b + t; k < o_kstar; k += T) A.p_round[off + k] = r;
-        if (t == 0) {
+        for (int k = o_b + tid; k < o_kstar; k += nthr) A.p_round[off + k] = r;
+        if (tid == 0) {
             A.wstat[(size_t)r * C + gc] = o_have ? ((o_kstar > o_b) ? 2 : 1) : 0;
             A.wflag[(size_t)(r + 1) * C + gc] = o_nx ? 1 : 0;
             A.Bm[(size_t)(r + 1) * C + gc] = o_kstar;
@@ -345,7 +351,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
         if (o_nx) {
             const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
-            for (int i = t; i < n; i += T) {
+            for (int i = tid; i < n; i += nthr) {
                 A.WLA[nrow + i] = Coord<CT>::la(raw_at(o_kstar, i));
                 const CT f = fd_at(i, o_kstar);
                 if constexpr (K::CSZ == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
@@ -353,7 +359,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             }
             const uint32_t* sb = sbits_all + (r & 1) * K::SBW;
             const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
-            for (int wd = t; wd < A.nw; wd += T)
+            for (int wd = tid; wd < A.nw; wd += nthr)
                 A.Smat[srow + wd] = (uint64_t)sb[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sb[2 * wd + 1] : 0) << 32);
         }
     };
@@ -457,7 +463,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     uint32_t cnt = 0;
                     if (!ov) {
                         uint32_t v[HD];
-                        rp_lds_row<HD>(win + mid * WS + q * HD, v);
+                        rp_lds_row<HD>(win + mid * WS + q * K::PS, v);
 #pragma unroll
                         for (int d = 0; d < HD; d++) cnt += __builtin_popcount((v[d] - fd[d]) & 0x80808080u);
                     } else if (!done && mid < np) {
@@ -476,34 +482,10 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 }
             }
             const int Kw = lo;
+            RP_PROF(13);
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
-            if (t < 32) fwov[t] = 0;
             rp_lds_barrier();
             RP_PROF(3);
-            // while wave 0 scans for the boundary, every wave rebases the probes' firstDescendants
-            // rows to base(s + 1) = c_base + Bm[s] (bm_cur, complete since the poll): the row of
-            // whichever probe becomes W'_{s+1}'s candidate is then ready to publish
-            for (int it = t; it < np * NDW; it += T) {
-                const int pp = it / NDW, d = it % NDW;
-                uint32_t w = 0;
-                bool ofp = false;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int i = 4 * d + u;
-                    uint32_t v = 127u;
-                    if (i < n) {
-                        const int32_t f = Coord<CT>::fd(fd_at(i, kb + pp));
-                        if (f != kMaxI32) {
-                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
-                            if (x > 126) ofp = true;
-                            else v = (uint32_t)x;
-                        }
-                    }
-                    w |= v << (8 * u);
-                }
-                fw8[pp * NDW + d] = w;
-                if (ofp) fwov[pp] = 1;
-            }
             if (wave == 0) {   // boundary: first probe where #{K <= p} (+ seen in earlier windows) >= SM
                 const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
                 const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
@@ -546,9 +528,24 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         if (wave == 0 && nx) {
             const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
             uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
-            const int pk = kstar - kb;   // the boundary probe of the last window searched
-            for (int d = lane; d < NDW; d += 64) rp_st_sc1(dst + d, fw8[pk * NDW + d] | vb1);
-            of = fwov[pk] != 0;
+            for (int d = lane; d < NDW; d += 64) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int i = 4 * d + u;
+                    uint32_t v = 127u;
+                    if (i < n) {
+                        const int32_t f = Coord<CT>::fd(fd_at(i, kstar));
+                        if (f != kMaxI32) {
+                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
+                            if (x > 126) of = true;
+                            else v = (uint32_t)x;
+                        }
+                    }
+                    w |= v << (8 * u);
+                }
+                rp_st_sc1(dst + d, w | vb1);
+            }
         }
         RP_PROF(9);
         if (wave == 0) {
@@ -559,12 +556,12 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
         RP_PROF(5);
-        // (e) the S row of the new candidate (the outputs are written next round, outputs())
+        // (e) the S row of the new candidate, then the round's outputs
         if (have && nx && cand && q == 0 && (done || K_last <= B)) atomicOr(&sbits[j >> 5], 1u << (j & 31));
         o_b = b;
         o_kstar = kstar;
         rp_lds_barrier();   // the S row bits are complete
-        outputs(s);
+        outputs(s, t, T);
         b = kstar;
         rp_lds_barrier();   // every read of this round's LDS is done
         RP_PROF(6);
