@@ -95,6 +95,12 @@ struct hgx_ctx {
     int64_t E = 0, E_div = 0;
     bool divided = false;
     hgx::RoundsHost rh;
+    std::vector<int8_t> fame_dev;                  // DecideFame's device fame rows (rows from the first undecided)
+    // the first undecided round of every graph at the last FindOrder that ran on the device:
+    // while it stays the same the eligible rounds only shrink (see hgx_find_order_begin)
+    std::vector<int32_t> fo_prev_u0;
+    bool fo_prev_valid = false;
+    std::vector<uint8_t> fo_elig, fo_fw;           // FindOrder's eligible rounds / famous witnesses
     std::vector<GraphState> gs;
     OrderArena arena;                        // consensus orders (gids) of all graphs
     std::vector<GraphOrder> order;           // [G] segments of each graph's order in the arena
@@ -570,6 +576,7 @@ int32_t hgx_clear(hgx_ctx* c) {
     c->arena.used = 0;
     c->E = c->E_div = 0;
     c->divided = false;
+    c->fo_prev_valid = false;
     c->mirror_ok = c->chains_ok = false;
     c->rounds_cached = c->recv_cached = false;
     if (c->rooted) {   // a fresh NewHashgraph has genesis roots
@@ -810,6 +817,7 @@ int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_rou
     c->arena.used = 0;
     c->E = c->E_div = 0;
     c->divided = false;
+    c->fo_prev_valid = false;
     c->mirror_ok = c->chains_ok = false;
     c->rounds_cached = c->recv_cached = false;
     return ok(err);
@@ -894,8 +902,11 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     if (c->divided && c->E_div == c->E) return ok(err);   // nothing new: AddEvent is idempotent
     DeviceGuard dg(c);
+    const bool fo_valid = c->fo_prev_valid;
+    c->fo_prev_valid = false;   // (until the call completes; a rebuild starts over)
     hipError_t e = c->eng.divide_rounds(c->E, c->chain_len, c->chain_base, c->rh);
     if (e != hipSuccess) return dev_err(err, e, "hgx_divide_rounds");
+    const bool keep_fo = fo_valid && !c->eng.last_rebuild;
     c->divided = true;
     c->E_div = c->E;
     c->rounds_cached = false;
@@ -938,6 +949,7 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
         }
         s.queued_upto = std::max(s.queued_upto, LR);
     }
+    c->fo_prev_valid = keep_fo;
     return ok(err);
 }
 
@@ -958,7 +970,7 @@ static bool witnesses_decided(const hgx_ctx* c, int g, int32_t r) {
 int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     DeviceGuard dg(c);
-    std::vector<int8_t> dev;
+    std::vector<int8_t>& dev = c->fame_dev;   // kept between calls (rows below the first undecided one unused)
     if (c->divided) {
         // decided fame is never revisited: only rounds from the first undecided one
         int32_t f0 = c->rh.R;
@@ -1019,10 +1031,30 @@ int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
     DeviceGuard dg(c);
     const int n = c->n, C = c->C, G = c->G;
     const int32_t R = c->rh.R;
+    // Nothing new can be received while every graph's UndecidedRounds[0] is what it was at the
+    // last FindOrder: the eligible rounds (decided, below it) are the same or fewer, their famous
+    // witnesses are the same events, and an event inserted since is an ancestor of none of them
+    // (hashgraph.go:753-799). The call then costs no device work (most calls of the chunked
+    // schedule). Not after a Reset (rounds queue out of order) or with an empty queue (the
+    // reference's UndecidedRounds[0] panics there), nor when sharded.
+    {
+        bool same = c->fo_prev_valid && !c->rooted && c->shard_world <= 1 && (int)c->fo_prev_u0.size() == G;
+        for (int g = 0; g < G && same; g++)
+            same = !c->gs[g].undecided.empty() && c->gs[g].undecided[0] == c->fo_prev_u0[(size_t)g];
+        if (same) return ok(err);
+    }
     // rounds below r0 cannot be the roundReceived of an event not received yet
     int max_unrecv = 0;
     const int32_t r0 = c->eng.recv_round_lo(c->rh, max_unrecv);
-    std::vector<uint8_t> elig((size_t)G * std::max(R, 1), 0), fw((size_t)std::max(R, 1) * C, 0), ure(G, 0);
+    // the famous flags and eligible rounds: rows below r0 are neither read nor sent (the buffers
+    // persist between calls and only rows [r0, R) are cleared: no O(R C) work per call)
+    std::vector<uint8_t>& elig = c->fo_elig;
+    std::vector<uint8_t>& fw = c->fo_fw;
+    std::vector<uint8_t> ure(G, 0);
+    elig.assign((size_t)G * std::max(R, 1), 0);
+    if (fw.size() < (size_t)std::max(R, 1) * C) fw.resize((size_t)std::max(R, 1) * C, 0);
+    if (R > std::max(r0, 0))
+        std::memset(fw.data() + (size_t)std::max(r0, 0) * C, 0, (size_t)(R - std::max(r0, 0)) * C);
     for (int g = 0; g < G; g++) {
         const GraphState& s = c->gs[g];
         ure[g] = s.undecided.empty() ? 1 : 0;
@@ -1046,8 +1078,15 @@ int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
     hipError_t e = c->eng.find_order_begin(elig, fw, ure, r0, max_unrecv, oh);
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     if (oh.panic) {
+        c->fo_prev_valid = false;
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
         return HGX_ERR_PANIC;
+    }
+    c->fo_prev_u0.assign(G, -1);
+    c->fo_prev_valid = true;
+    for (int g = 0; g < G; g++) {
+        if (c->gs[g].undecided.empty()) c->fo_prev_valid = false;
+        else c->fo_prev_u0[(size_t)g] = c->gs[g].undecided[0];
     }
     c->fo_open = true;
     return ok(err);
@@ -1062,7 +1101,17 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
     (void)n;
     const int32_t R = c->rh.R;
     hgx::OrderHost& oh = c->fo;
-    hipError_t e = c->eng.find_order_end(oh);
+    // the m received events' order lands in the arena with the block tables (one round trip)
+    const size_t base_off = c->arena.used;
+    int32_t* pre = nullptr;
+    if (oh.m > 0) {
+        if (!c->arena.reserve(base_off + (size_t)oh.m)) {
+            set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
+            return HGX_ERR_CAPACITY;
+        }
+        pre = c->arena.p + base_off;
+    }
+    hipError_t e = c->eng.find_order_end(oh, pre);
     if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
     c->recv_cached = false;
     // the device order is graph-major: one D2H copy appends it to the arena and every
@@ -1076,8 +1125,7 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
         seg_len[g] = mg;
         total += mg;
     }
-    const size_t base_off = c->arena.used;
-    if (total > 0) {
+    if (total > 0 && !(pre && total == (int64_t)oh.m)) {   // (every received event is in a block: total == m)
         if (!c->arena.reserve(base_off + (size_t)total)) {
             set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
             return HGX_ERR_CAPACITY;
@@ -1086,8 +1134,8 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
         if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
         e = c->eng.sync();
         if (e != hipSuccess) return dev_err(err, e, "hgx_find_order");
-        c->arena.used = base_off + (size_t)total;
     }
+    c->arena.used = base_off + (size_t)total;
     // committed blocks (graph, block index): commitCh receives them once the graph state
     // (counters, pending, undetermined) is final for this call
     std::vector<std::pair<int, int64_t>> commits;
@@ -1198,6 +1246,7 @@ int32_t hgx_reset_consensus(hgx_ctx* c) {
     }
     c->arena.used = 0;
     c->divided = false;
+    c->fo_prev_valid = false;
     c->E_div = 0;
     c->rounds_cached = c->recv_cached = false;
     return c->eng.reset_received() == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;

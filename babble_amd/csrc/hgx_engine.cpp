@@ -71,7 +71,9 @@ Engine::~Engine() {
     for (auto e : kev) (void)hipEventDestroy(e);
     if (ph0) (void)hipEventDestroy(ph0);
     if (ph1) (void)hipEventDestroy(ph1);
+    if (ph2) (void)hipEventDestroy(ph2);
     if (h_small) (void)hipHostFree(h_small);
+    if (h_pack) (void)hipHostFree(h_pack);
     if (h_stage) (void)hipHostFree(h_stage);
     if (h_ins) (void)hipHostFree(h_ins);
     if (h_cpar) (void)hipHostFree(h_cpar);
@@ -107,6 +109,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HGX_TRY(hipEventCreate(&ph0));
     HGX_TRY(hipEventCreate(&ph1));
+    HGX_TRY(hipEventCreate(&ph2));
     G = n_graphs;
     n = n_part;
     C = G * n;
@@ -276,25 +279,71 @@ hipError_t Engine::stage_reserve(size_t bytes) {
     }
     h_stage = q;
     stage_cap = cap;
-    return hipSuccess;
+    return hipHostGetDevicePointer((void**)&d_stage, h_stage, 0);
 }
 
 hipError_t Engine::stage_h2d(void* dev, const void* host, size_t bytes) {
     if (bytes == 0) return hipSuccess;
     HGX_TRY(stage_reserve(bytes));
-    uint8_t* h = h_stage + stage_used;
-    std::memcpy(h, host, bytes);
+    std::memcpy(h_stage + stage_used, host, bytes);
+    pend.push_back({0, stage_used, dev, nullptr, nullptr, bytes});
     stage_used += (bytes + 63) & ~(size_t)63;
-    return hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, stream);
+    return hipSuccess;
 }
 
 hipError_t Engine::stage_d2h(void* host, const void* dev, size_t bytes) {
     if (bytes == 0) return hipSuccess;
     HGX_TRY(stage_reserve(bytes));
     stage_out.push_back({host, stage_used, bytes});
-    uint8_t* h = h_stage + stage_used;
+    pend.push_back({1, stage_used, dev, nullptr, nullptr, bytes});
     stage_used += (bytes + 63) & ~(size_t)63;
-    return hipMemcpyAsync(h, dev, bytes, hipMemcpyDeviceToHost, stream);
+    return hipSuccess;
+}
+
+hipError_t Engine::copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    void* d = nullptr;
+    HGX_TRY(hipHostGetDevicePointer(&d, pinned_dst, 0));
+    pend.push_back({2, 0, dev, pinned_dst, d, bytes});
+    return hipSuccess;
+}
+
+hipError_t Engine::copy_from_pinned(void* dev, const void* pinned_src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    void* d = nullptr;
+    HGX_TRY(hipHostGetDevicePointer(&d, const_cast<void*>(pinned_src), 0));
+    PendCopy p{3, 0, dev, nullptr, nullptr, bytes};
+    p.host_src = pinned_src;
+    p.dev_src = d;
+    pend.push_back(p);
+    return hipSuccess;
+}
+
+hipError_t Engine::stage_issue() {
+    if (pend.empty()) return hipSuccess;
+    size_t total = 0;
+    for (const PendCopy& p : pend) total += p.bytes;
+    if (pend.size() <= (size_t)kCopyMax && total <= kCopyKernelMax) {
+        CopyRange r[kCopyMax];
+        int k = 0;
+        for (const PendCopy& p : pend) {
+            if (p.kind == 0) r[k++] = {d_stage + p.off, const_cast<void*>(p.dev), (uint32_t)p.bytes};
+            else if (p.kind == 1) r[k++] = {p.dev, d_stage + p.off, (uint32_t)p.bytes};
+            else if (p.kind == 2) r[k++] = {p.dev, p.dev_dst, (uint32_t)p.bytes};
+            else r[k++] = {p.dev_src, const_cast<void*>(p.dev), (uint32_t)p.bytes};
+        }
+        launch_copy_many(stream, r, k);
+        pend.clear();
+        return hipGetLastError();
+    }
+    for (const PendCopy& p : pend) {
+        if (p.kind == 0) HGX_TRY(hipMemcpyAsync(const_cast<void*>(p.dev), h_stage + p.off, p.bytes, hipMemcpyHostToDevice, stream));
+        else if (p.kind == 1) HGX_TRY(hipMemcpyAsync(h_stage + p.off, p.dev, p.bytes, hipMemcpyDeviceToHost, stream));
+        else if (p.kind == 2) HGX_TRY(hipMemcpyAsync(p.host_dst, p.dev, p.bytes, hipMemcpyDeviceToHost, stream));
+        else HGX_TRY(hipMemcpyAsync(const_cast<void*>(p.dev), p.host_src, p.bytes, hipMemcpyHostToDevice, stream));
+    }
+    pend.clear();
+    return hipSuccess;
 }
 
 void Engine::stage_flush() {
@@ -342,6 +391,32 @@ hipError_t Engine::stage_host(const int32_t* creator, const int64_t* index, cons
                               const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                               const int32_t* nil, int64_t count, InsertIn& in) {
     const size_t c = (size_t)count;
+    if (count <= kPackEvents) {
+        // a sync-sized batch: the nine columns packed into pinned memory and sent as one copy
+        // (nine pageable copies cost a staged, blocking transfer each)
+        const void* src[9] = {creator, index, sp, op, ts, hash, S, ntx, nil};
+        const size_t bytes[9] = {4 * c, 8 * c, 8 * c, 8 * c, 8 * c, 32 * c, 32 * c, 4 * c, 4 * c};
+        size_t off[9], total = 0;
+        for (int i = 0; i < 9; i++) {
+            off[i] = total;
+            total += (bytes[i] + 255) & ~(size_t)255;
+        }
+        if (st_pack.n < total) HGX_TRY(st_pack.alloc(std::max(total, (size_t)2 * st_pack.n)));
+        if (h_pack_cap < total) {   // (every insert synchronized before returning: the buffer is free)
+            if (h_pack) (void)hipHostFree(h_pack);
+            h_pack = nullptr;
+            h_pack_cap = 0;
+            HGX_TRY(hipHostMalloc((void**)&h_pack, std::max(total, (size_t)2 * st_pack.n), hipHostMallocDefault));
+            h_pack_cap = std::max(total, (size_t)2 * st_pack.n);
+        }
+        for (int i = 0; i < 9; i++) std::memcpy(h_pack + off[i], src[i], bytes[i]);
+        HGX_TRY(hipMemcpyAsync(st_pack.p, h_pack, total, hipMemcpyHostToDevice, stream));
+        uint8_t* d = st_pack.p;
+        in.creator = (const int32_t*)(d + off[0]); in.index = (const int64_t*)(d + off[1]);
+        in.sp = (const int64_t*)(d + off[2]); in.op = (const int64_t*)(d + off[3]); in.ts = (const int64_t*)(d + off[4]);
+        in.hash = d + off[5]; in.S = d + off[6]; in.ntx = (const int32_t*)(d + off[7]); in.nil = (const int32_t*)(d + off[8]);
+        return hipSuccess;
+    }
     HGX_TRY(stage_col(st_creator, creator, c, 1, stream));
     HGX_TRY(stage_col(st_index, index, c, 1, stream));
     HGX_TRY(stage_col(st_sp, sp, c, 1, stream));
@@ -450,7 +525,7 @@ hipError_t Engine::payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int3
     InsertIn in{};
     in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p;
     in.ts = st_ts.p; in.hash = st_hash.p; in.S = st_S.p; in.ntx = st_ntx.p; in.nil = st_nil.p;
-    launch_insert_commit(stream, m_ok, E0, n, in, insert_state(), kCommitPayload);
+    launch_insert_commit(stream, m_ok, nullptr, nullptr, E0, n, in, insert_state(), kCommitPayload);
     if (laid_out_new) {   // the layout ran before the timestamps and coins were committed
         launch_ts_to_pos(stream, E0, m_ok, g_pos.p, g_ts.p, p_ts.p);
         if (R > wcoin_r0) launch_wcoin(stream, arrays(), wcoin_r0, R, C);
@@ -469,35 +544,43 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
     const int64_t E0 = E;
     InsertState st = insert_state();
     if (count > 0) {
+        // checks, then the commit of the accepted prefix and the withdrawal of the rest's claims:
+        // the kernels take the prefix from the first-failure words, so the batch costs one host
+        // round trip (the chunked schedule inserts 1 000 events per call)
         HGX_TRY(hipMemsetAsync(ins_fail.p, 0xFF, 8, stream));
         launch_insert_claim(stream, count, E0, cap, C, in, st);
         launch_insert_check(stream, count, E0, cap, C, n, in, st);
-        unsigned long long fail = 0, fsig = ~0ull;
-        HGX_TRY(hipMemcpyAsync(h_small, ins_fail.p, 8, hipMemcpyDeviceToHost, stream));
-        if (fail_sig) HGX_TRY(hipMemcpyAsync(h_small + 2, fail_sig, 8, hipMemcpyDeviceToHost, stream));
-        HGX_TRY(hipStreamSynchronize(stream));
-        std::memcpy(&fail, h_small, 8);
-        if (fail_sig) std::memcpy(&fsig, h_small + 2, 8);
-        // Verify comes first in InsertEvent: at the same event the signature's failure wins
-        if ((fsig >> 8) <= (fail >> 8) && fsig != ~0ull) fail = fsig;
-        const int64_t m_ok = (fail == ~0ull) ? count : (int64_t)(fail >> 8);
-        out.accepted = m_ok;
-        out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
-        launch_insert_commit(stream, m_ok, E0, n, in, st, commit_mode);
-        launch_insert_unclaim(stream, count, m_ok, E0, cap, C, in, st);
-        if (out.code) {
-            HGX_TRY(hipMemcpyAsync(&out.fail_creator, in.creator + m_ok, 4, hipMemcpyDeviceToHost, stream));
-            HGX_TRY(hipMemcpyAsync(&out.fail_index, in.index + m_ok, 8, hipMemcpyDeviceToHost, stream));
-        }
-        E = E0 + m_ok;
+        launch_insert_commit(stream, count, ins_fail.p, fail_sig, E0, n, in, st, commit_mode);
+        launch_insert_unclaim(stream, count, ins_fail.p, fail_sig, E0, cap, C, in, st);
+        HGX_TRY(copy_to_pinned(h_small, ins_fail.p, 8));
+        if (fail_sig) HGX_TRY(copy_to_pinned(h_small + 2, fail_sig, 8));
     }
     out.last_gid.resize(C);
     out.last_index.resize(C);
     out.chain_base.resize(C);
     out.graph_loaded.resize(G);
-    // one copy of the whole block into pinned memory, then the host mirrors
-    HGX_TRY(hipMemcpyAsync(h_ins, ins_blk.p, ins_blk.n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    // the first-failure words and the whole state block into pinned memory (one launch), then
+    // the host mirrors
+    HGX_TRY(copy_to_pinned(h_ins, ins_blk.p, ins_blk.n * sizeof(int32_t)));
+    HGX_TRY(stage_issue());
     HGX_TRY(hipStreamSynchronize(stream));
+    if (count > 0) {
+        unsigned long long fail = 0, fsig = ~0ull;
+        std::memcpy(&fail, h_small, 8);
+        if (fail_sig) std::memcpy(&fsig, h_small + 2, 8);
+        // Verify comes first in InsertEvent: at the same event the signature's failure wins
+        // (the kernels' accepted_prefix)
+        if ((fsig >> 8) <= (fail >> 8) && fsig != ~0ull) fail = fsig;
+        const int64_t m_ok = (fail == ~0ull) ? count : (int64_t)(fail >> 8);
+        out.accepted = m_ok;
+        out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
+        if (out.code) {   // the failing event's creator and Index for the error string
+            HGX_TRY(hipMemcpyAsync(&out.fail_creator, in.creator + m_ok, 4, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipMemcpyAsync(&out.fail_index, in.index + m_ok, 8, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+        }
+        E = E0 + m_ok;
+    }
     std::memcpy(out.last_gid.data(), h_ins, (size_t)C * 4);
     std::memcpy(out.last_index.data(), h_ins + C, (size_t)C * 4);
     std::memcpy(out.chain_base.data(), h_ins + 2 * C, (size_t)C * 4);
@@ -624,6 +707,7 @@ hipError_t Engine::reserve_rounds(int32_t rounds) {
 hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_len,
                                  const std::vector<int32_t>& chain_base, RoundsHost& out) {
     stage_out.clear();   // every earlier call synchronized: the staging is free
+    pend.clear();
     stage_used = 0;
     int32_t max_index = -1;
     int new_max_len = 0;
@@ -661,7 +745,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     std::memcpy(h_cpar, chain_len.data(), (size_t)C * 4);
     std::memcpy(h_cpar + C, chain_base.data(), (size_t)C * 4);
     std::memcpy(h_cpar + 2 * C, h_len_div.data(), (size_t)C * 4);
-    HGX_TRY(hipMemcpyAsync(cpar_blk.p, h_cpar, (size_t)3 * C * 4, hipMemcpyHostToDevice, stream));
+    HGX_TRY(copy_from_pinned(cpar_blk.p, h_cpar, (size_t)3 * C * 4));
+    HGX_TRY(stage_issue());
     // first round whose step can change: the lowest round of the last old event of a chain
     // that got new events (every boundary below it is among old events)
     int32_t r_lo = 0;
@@ -778,7 +863,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6, la_map, la_na));
         const double rows = (double)(En - E0);
         kend(K_LA_SWEEP, rows * (3.0 * csz * n + 16));
-        HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
+        if (rebuild) HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
         if (la_wave_segs > 1) HGX_TRY(run_sweeps(2));   // verify sweep + dirty sweeps (counted there)
         la_sweeps++;
         la_rows += (int64_t)rows;
@@ -803,30 +888,37 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         h_fu.assign(C, 0);
         HGX_TRY(hipMemcpyAsync(h_fu.data(), fu.p, (size_t)C * 4, hipMemcpyDeviceToHost, stream));
     }
-    HGX_TRY(hipEventRecord(ph1, stream));
-    HGX_TRY(hipEventSynchronize(ph1));
-    if (la_wave_used && h_small[48] != 0) {
-        // a wavefront lane gave up waiting (bounded spins): redo lastAncestors and the
-        // firstDescendants built from them with the sweeps
-        la_wave_used = false;
-        la_wave_fallbacks++;
-        if (rebuild) HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
-        else launch_init_new(stream, a, E0, En - E0, n, fd_ld);
-        HGX_TRY(run_sweeps(1));
-        launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
-        if (rooted) launch_root_floor(stream, a, root_round_d.p, gfl.p, gB.p, root_gmax, C, n, max_len);
+    // a call resuming the state (not a rebuild) makes one host round trip: the wavefront's
+    // error flag is read with the rounds' results, and a lane that gave up (never seen in
+    // practice) redoes the call as a rebuild with the sweeps
+    const bool one_trip = !rebuild;
+    if (one_trip) {
+        HGX_TRY(hipEventRecord(ph2, stream));
+    } else {
         HGX_TRY(hipEventRecord(ph1, stream));
         HGX_TRY(hipEventSynchronize(ph1));
+        if (la_wave_used && h_small[48] != 0) {
+            // a wavefront lane gave up waiting (bounded spins): redo lastAncestors and the
+            // firstDescendants built from them with the sweeps
+            la_wave_used = false;
+            la_wave_fallbacks++;
+            HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
+            HGX_TRY(run_sweeps(1));
+            launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
+            if (rooted) launch_root_floor(stream, a, root_round_d.p, gfl.p, gB.p, root_gmax, C, n, max_len);
+            HGX_TRY(hipEventRecord(ph1, stream));
+            HGX_TRY(hipEventSynchronize(ph1));
+        }
+        float ms = 0;
+        HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+        phase_ms[0] = ms;
     }
-    float ms = 0;
-    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
-    phase_ms[0] = ms;
     h_len_div = chain_len;
     E_div = En;
     laid_out = true;
 
     // rounds, step by step from r_lo
-    HGX_TRY(hipEventRecord(ph0, stream));
+    if (!one_trip) HGX_TRY(hipEventRecord(ph0, stream));
     HGX_TRY(ensure_round_cap(r_lo + 2 * kStepBatch + 2));
     a = arrays();
     {   // one launch for the round tables' resets
@@ -854,6 +946,28 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         A.gB = rooted ? gB.p : c_len.p;   // (any int array without roots: read, never used)
         A.gmax = rooted ? root_gmax : -1;
         return A;
+    };
+    // the tail of the call: every graph's last round over the rounds stepped so far, and the rows
+    // [r_lo, r_hi] of the boundaries / [r_lo, r_hi) of the witness flags for the host copies
+    // (rows beyond the last round are copied and dropped), then ph1
+    const int r_scan = rebuild ? 0 : r_lo;
+    const std::vector<int32_t> prev_last = out.last_round;
+    bool tail_ready = false;
+    auto enqueue_tail = [&](int32_t r_hi) -> hipError_t {
+        stage_out.clear();   // (a tail queued before more steps were needed is superseded)
+        pend.clear();
+        stage_used = 0;
+        launch_last_round(stream, r_scan, r_hi, G, C, n, wstat.p, lr.p);
+        h_lr.assign(G, -1);
+        HGX_TRY(stage_d2h(h_lr.data(), lr.p, (size_t)G * 4));
+        const size_t b0 = (size_t)r_lo * C;
+        if (out.bm.size() < (size_t)(r_hi + 1) * C) out.bm.resize((size_t)(r_hi + 1) * C);
+        if (out.wflag.size() < (size_t)r_hi * C) out.wflag.resize((size_t)r_hi * C);
+        HGX_TRY(stage_d2h(out.bm.data() + b0, Bm.p + b0, ((size_t)(r_hi + 1) * C - b0) * 4));
+        if (r_hi > r_lo) HGX_TRY(stage_d2h(out.wflag.data() + b0, wstat.p + b0, (size_t)r_hi * C - b0));
+        if (one_trip && la_wave_used) HGX_TRY(copy_to_pinned(h_small + 48, counters.p + 6, 4));
+        HGX_TRY(stage_issue());
+        return hipEventRecord(ph1, stream);
     };
     kbeg(K_ROUND_GATHER);
     launch_round_gather(stream, a, r_lo, C, n, fd_ld);   // W'_{r_lo}: round 0 = first event of every chain
@@ -1003,7 +1117,20 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // batch, so it waits for that batch's flag before queueing another
         HGX_TRY(launch_batch());
         if (rebuild) HGX_TRY(launch_batch());
-        for (;;) {
+        if (one_trip) {
+            // the tail queued right behind the first batch: when that batch ends the rounds (the
+            // usual resumed call), the call has made its only host round trip here
+            HGX_TRY(enqueue_tail(r_lo + launched * nb));
+            HGX_TRY(hipEventSynchronize(ph1));
+            const int more = __atomic_load_n(&h_flag[0], __ATOMIC_ACQUIRE);
+            checked = 1;
+            if (!more) tail_ready = true;
+            else {
+                if (launched == checked) HGX_TRY(launch_batch());
+                HGX_TRY(launch_batch());
+            }
+        }
+        while (!tail_ready) {
             HGX_TRY(hipEventSynchronize(flag_ev[checked & 1]));
             const int more = __atomic_load_n(&h_flag[checked & 1], __ATOMIC_ACQUIRE);
             checked++;
@@ -1012,36 +1139,49 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(launch_batch());
         }
     }
+    if (!tail_ready) {
+        HGX_TRY(enqueue_tail(r_done >= 0 ? r_done : r_lo + launched * nb));
+        HGX_TRY(hipEventSynchronize(ph1));
+    }
+    if (one_trip && la_wave_used && h_small[48] != 0) {
+        // a wavefront lane gave up waiting (bounded spins): the call again as a rebuild, with
+        // the sweeps for lastAncestors
+        la_wave_fallbacks++;
+        laid_out = false;
+        stage_out.clear();
+        const int keep = la_kernel;
+        la_kernel = 1;
+        const hipError_t re = divide_rounds(En, chain_len, chain_base, out);
+        la_kernel = keep;
+        return re;
+    }
+    stage_flush();
     // rounds below r_lo are unchanged and every round up to a graph's last one has witnesses,
     // so only [r_lo, R) is scanned: last = max(that, min(previous last, r_lo - 1))
-    const int r_scan = rebuild ? 0 : r_lo;
-    const std::vector<int32_t> prev_last = out.last_round;
-    launch_last_round(stream, r_scan, r_done >= 0 ? r_done : r_lo + launched * nb, G, C, n, wstat.p, lr.p);
-    out.last_round.assign(G, -1);
-    HGX_TRY(hipMemcpyAsync(out.last_round.data(), lr.p, (size_t)G * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipStreamSynchronize(stream));
     if (r_scan > 0)
         for (int g = 0; g < G; g++) {
             const int32_t pl = g < (int)prev_last.size() ? prev_last[g] : -1;
-            out.last_round[g] = std::max(out.last_round[g], std::min(pl, r_scan - 1));
+            h_lr[g] = std::max(h_lr[g], std::min(pl, r_scan - 1));
         }
+    out.last_round.assign(h_lr.begin(), h_lr.end());
     int32_t mx = -1;
     for (int g = 0; g < G; g++) mx = std::max(mx, out.last_round[g]);
     R = mx + 1;
     out.R = R;
     out.r_lo = std::min(r_lo, R);
-    launch_wcoin(stream, a, out.r_lo, R, C);
-    HGX_TRY(hipGetLastError());
-    // the host copies keep the rows below r_lo
+    // the host copies keep the rows below r_lo (rows the tail copied beyond R are dropped)
     out.bm.resize((size_t)(R + 1) * C);
     out.wflag.resize((size_t)R * C);
-    const size_t b0 = (size_t)out.r_lo * C;
-    HGX_TRY(stage_d2h(out.bm.data() + b0, Bm.p + b0, out.bm.size() * 4 - b0 * 4));
-    if (R > out.r_lo) HGX_TRY(stage_d2h(out.wflag.data() + b0, wstat.p + b0, out.wflag.size() - b0));
-    HGX_TRY(hipEventRecord(ph1, stream));
-    HGX_TRY(hipEventSynchronize(ph1));
-    stage_flush();
-    HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    launch_wcoin(stream, a, out.r_lo, R, C);   // (DecideFame reads the coins on this stream)
+    HGX_TRY(hipGetLastError());
+    float ms = 0;
+    if (one_trip) {
+        HGX_TRY(hipEventElapsedTime(&ms, ph0, ph2));
+        phase_ms[0] = ms;
+        HGX_TRY(hipEventElapsedTime(&ms, ph2, ph1));
+    } else {
+        HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
+    }
     phase_ms[1] = ms;
     step_prof_dump();   // -DHGX_STEP_PROF builds only
     return collect_kernel_times();
@@ -1071,8 +1211,11 @@ int32_t Engine::recv_round_lo(const RoundsHost& rh, int& max_unrecv) const {
 // ---- DecideFame -----------------------------------------------------------------
 hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
     stage_out.clear();   // every earlier call synchronized: the staging is free
+    pend.clear();
     stage_used = 0;
-    fame_out.assign((size_t)R * C, 0);
+    // rows [r0, R) are copied back below; the caller reads no row below r0, so the buffer only
+    // grows (no O(R C) clear per call: the chunked schedule calls this thousands of times)
+    if (fame_out.size() < (size_t)R * C) fame_out.resize((size_t)R * C, 0);
     r0 = std::max(r0, 0);
     if (R <= r0) return hipSuccess;
     DevArrays a = arrays();
@@ -1084,6 +1227,7 @@ hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
     HGX_TRY(hipGetLastError());
     const size_t o = (size_t)r0 * C;
     HGX_TRY(stage_d2h(fame_out.data() + o, fame.p + o, fame_out.size() - o));
+    HGX_TRY(stage_issue());
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
     stage_flush();
@@ -1097,13 +1241,14 @@ hipError_t Engine::decide_fame(int32_t r0, std::vector<int8_t>& fame_out) {
 hipError_t Engine::find_order(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
                               const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
     HGX_TRY(find_order_begin(el, famous, ure, r0, max_unrecv, out));
-    return find_order_end(out);
+    return find_order_end(out, nullptr);
 }
 
 // threshold and roundReceived (every chain), consensus timestamps of the shard's chains
 hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::vector<uint8_t>& famous,
                                     const std::vector<uint8_t>& ure, int32_t r0, int max_unrecv, OrderHost& out) {
     stage_out.clear();   // every earlier call synchronized: the staging is free
+    pend.clear();
     stage_used = 0;
     out = OrderHost();
     fo_m = 0;
@@ -1115,6 +1260,7 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     HGX_TRY(stage_h2d(elig.p, el.data(), (size_t)G * R));
     HGX_TRY(stage_h2d(fw.p + o, famous.data() + o, (size_t)R * C - o));
     HGX_TRY(stage_h2d(ur_empty.p, ure.data(), (size_t)G));
+    HGX_TRY(stage_issue());
     if (WLAT.n < (size_t)R * C * n) {   // grown geometrically: R grows by a round or two per call
         HGX_TRY(WLAT.alloc(std::max((size_t)R * C * n + (size_t)C * n, 2 * WLAT.n)));
         a = arrays();
@@ -1131,8 +1277,9 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     kbeg(K_ROUND_RECEIVED);
     launch_round_received(stream, a, R, C, n, max_unrecv);
     kend(K_ROUND_RECEIVED, 0);
-    HGX_TRY(hipMemcpyAsync(h_small, counters.p, 8, hipMemcpyDeviceToHost, stream));
+    HGX_TRY(copy_to_pinned(h_small, counters.p, 8));
     HGX_TRY(stage_d2h(fo_cnt.data(), rcnt.p, (size_t)C * 4));
+    HGX_TRY(stage_issue());
     HGX_TRY(hipStreamSynchronize(stream));
     stage_flush();
     fo_m = h_small[0];
@@ -1182,7 +1329,9 @@ hipError_t Engine::shard_copy(int lo, int hi, void* buf, bool on_device, bool to
 }
 
 // sort by (graph, rr, cts, S), blocks
-hipError_t Engine::find_order_end(OrderHost& out) {
+// order_dst (pinned, room for the m received events): the order is copied there with the block
+// tables, in the same host round trip
+hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
     out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
     out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
     out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);
@@ -1192,7 +1341,17 @@ hipError_t Engine::find_order_end(OrderHost& out) {
     fo_m = 0;
     DevArrays a = arrays();
     uint32_t* vals = nullptr;
-    if (sort_small_ok(m)) {
+    const bool small = sort_small_ok(m);
+    {   // one launch for the per-(graph, rr) block tables (and the small sort's ranks)
+        FillRange fr[5] = {{blk_cnt.p, (uint32_t)((size_t)G * R * 4), 0},
+                           {blk_loaded.p, (uint32_t)((size_t)G * R * 4), 0},
+                           {blk_ntx.p, (uint32_t)((size_t)G * R * 8), 0},
+                           {blk_nil.p, (uint32_t)((size_t)G * R), 0},
+                           {val_b.p, (uint32_t)((size_t)m * 4), 0}};
+        launch_fill_many(stream, fr, small ? 5 : 4);
+        HGX_TRY(hipGetLastError());
+    }
+    if (small) {
         kbeg(K_SORT);
         launch_sort_small(stream, a, m, n, &vals);
         kend(K_SORT, (double)m * 24.0);
@@ -1215,23 +1374,21 @@ hipError_t Engine::find_order_end(OrderHost& out) {
                          (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
                                                     : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
     }
-    {   // one launch for the per-(graph, rr) block tables
-        FillRange fr[4] = {{blk_cnt.p, (uint32_t)((size_t)G * R * 4), 0},
-                           {blk_loaded.p, (uint32_t)((size_t)G * R * 4), 0},
-                           {blk_ntx.p, (uint32_t)((size_t)G * R * 8), 0},
-                           {blk_nil.p, (uint32_t)((size_t)G * R), 0}};
-        launch_fill_many(stream, fr, 4);
-        HGX_TRY(hipGetLastError());
-    }
     launch_finish_order(stream, a, m, vals, R, n);
     launch_fu_advance(stream, a, C);
     for (int c = 0; c < C; c++) h_fu[c] += fo_cnt[c];
-    HGX_TRY(hipMemcpyAsync(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4, hipMemcpyDeviceToHost, stream));
-    HGX_TRY(hipMemcpyAsync(out.blk_nil.data(), blk_nil.p, (size_t)G * R, hipMemcpyDeviceToHost, stream));
+    stage_out.clear();
+    pend.clear();
+    stage_used = 0;
+    HGX_TRY(stage_d2h(out.blk_cnt.data(), blk_cnt.p, (size_t)G * R * 4));
+    HGX_TRY(stage_d2h(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8));
+    HGX_TRY(stage_d2h(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4));
+    HGX_TRY(stage_d2h(out.blk_nil.data(), blk_nil.p, (size_t)G * R));
+    if (order_dst) HGX_TRY(copy_to_pinned(order_dst, order_gid.p, (size_t)m * 4));
+    HGX_TRY(stage_issue());
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
+    stage_flush();
     float ms = 0;
     HGX_TRY(hipEventElapsedTime(&ms, ph0, ph1));
     phase_ms[3] = ms;

@@ -143,7 +143,7 @@ class Engine {
     // end = sort and blocks
     hipError_t find_order_begin(const std::vector<uint8_t>& elig, const std::vector<uint8_t>& famous,
                                 const std::vector<uint8_t>& ur_empty, int32_t r0, int max_unrecv, OrderHost& out);
-    hipError_t find_order_end(OrderHost& out);
+    hipError_t find_order_end(OrderHost& out, int32_t* order_dst = nullptr);
     int64_t shard_values(int lo, int hi) const;   // newly received events of chains [lo, hi)
     // their consensus timestamps to (to_buf) or from buf, a device or host pointer
     hipError_t shard_copy(int lo, int hi, void* buf, bool on_device, bool to_buf);
@@ -248,6 +248,12 @@ class Engine {
     DBuf<int32_t> st_creator, st_ntx, st_nil;
     DBuf<int64_t> st_index, st_sp, st_op, st_ts;
     DBuf<uint8_t> st_hash, st_S, st_dig, st_r;
+    // batches of at most kPackEvents from host memory: the columns packed in one pinned buffer,
+    // one H2D copy into st_pack
+    static constexpr int64_t kPackEvents = 65536;
+    DBuf<uint8_t> st_pack;
+    uint8_t* h_pack = nullptr;
+    size_t h_pack_cap = 0;
     // signatures (Event.Verify): keys, window tables, per-event results, first failure
     DBuf<uint8_t> pk_keys, pk_valid, pk_out;
     DBuf<uint32_t> pk_tab;
@@ -289,20 +295,41 @@ class Engine {
     DBuf<uint32_t> val_a, val_b, hist;
     DBuf<int64_t> minmax, blk_ntx;
     int32_t* h_small = nullptr;   // pinned scratch (flags)
-    // pinned staging of the per-call host tables (DMA instead of pageable copies): a cursor per
-    // phase; D2H copies land here and are handed out by stage_flush() after the phase's sync
+    // pinned staging of the per-call host tables (instead of pageable copies): a cursor per
+    // phase; D2H copies land here and are handed out by stage_flush() after the phase's sync.
+    // The copies are queued and stage_issue() sends them: up to kCopyMax small ones (together
+    // at most kCopyKernelMax bytes) as ONE k_copy_many launch, otherwise one DMA copy each
     uint8_t* h_stage = nullptr;
+    uint8_t* d_stage = nullptr;   // its device address
     size_t stage_cap = 0, stage_used = 0;
     struct StagedD2H { void* dst; size_t off, bytes; };
     std::vector<StagedD2H> stage_out;
+    // kind 0: stage -> dev (H2D), 1: dev -> stage (D2H), 2: dev -> pinned host (host_dst, its
+    // device address dev_dst), 3: pinned host (host_src, its device address dev_src) -> dev
+    struct PendCopy {
+        int kind;
+        size_t off;
+        const void* dev;
+        void* host_dst;
+        void* dev_dst;
+        size_t bytes;
+        const void* host_src = nullptr;
+        const void* dev_src = nullptr;
+    };
+    std::vector<PendCopy> pend;
+    static constexpr size_t kCopyKernelMax = 256 << 10;
     hipError_t stage_reserve(size_t bytes);
     hipError_t stage_h2d(void* dev, const void* host, size_t bytes);
     hipError_t stage_d2h(void* host, const void* dev, size_t bytes);
+    hipError_t copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes);   // queued like the stagings
+    hipError_t copy_from_pinned(void* dev, const void* pinned_src, size_t bytes);
+    hipError_t stage_issue();
     void stage_flush();   // after the stream synchronized: copy the D2H tables out, reset the cursor
     int32_t* h_flag = nullptr;    // host-mapped, coherent: the round-step batches' "candidates left" flags
     int32_t* d_flag = nullptr;    // its device address
     // timing
-    hipEvent_t ph0 = nullptr, ph1 = nullptr;
+    hipEvent_t ph0 = nullptr, ph1 = nullptr, ph2 = nullptr;
+    std::vector<int32_t> h_lr;   // DivideRounds: every graph's last round (staged copy)
     std::vector<hipEvent_t> kev;
     struct Open { int k; size_t e0; double bytes; int64_t count; };
     std::vector<Open> kopen;

@@ -116,6 +116,20 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
     if (code != INS_OK) atomicMin(st.fail, ((unsigned long long)k << 8) | (unsigned long long)code);
 }
 
+// the accepted prefix of a batch of m from the first-failure words (no host round trip between
+// the checks and the commit): Verify comes first in InsertEvent, so at the same event the
+// signature's failure wins; fail == nullptr: all m
+__device__ __forceinline__ int64_t accepted_prefix(int64_t m, const unsigned long long* fail,
+                                                   const unsigned long long* fail_sig) {
+    if (!fail) return m;
+    unsigned long long f = *fail;
+    if (fail_sig) {
+        const unsigned long long s = *fail_sig;
+        if (s != ~0ull && (s >> 8) <= (f >> 8)) f = s;
+    }
+    return f == ~0ull ? m : (int64_t)(f >> 8);
+}
+
 // Append the accepted events [0, m_ok) to the context's arrays (gid order) and move the
 // per-creator state (last event, last Index, first Index) forward.
 // grid-stride: the loaded-event count of each graph is kept per wave while the wave's events
@@ -124,8 +138,10 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
 // mode: kCommitAll, or the split of hgx_insert_and_run: kCommitStructure (the columns validation
 // and DivideRounds read) now, kCommitPayload (timestamps, S, coin, transactions, IsLoaded and the
 // graphs' loaded counts) once the payload columns have landed
-__global__ void __launch_bounds__(256) k_insert_commit(int64_t m_ok, int64_t E0, int n, InsertIn in, InsertState st,
-                                                       int mode) {
+__global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned long long* fail,
+                                                       const unsigned long long* fail_sig, int64_t E0, int n,
+                                                       InsertIn in, InsertState st, int mode) {
+    const int64_t m_ok = accepted_prefix(m, fail, fail_sig);
     int acc_g = -1;                 // wave-uniform: the graph whose loaded count is pending
     unsigned long long acc = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -198,10 +214,11 @@ void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos
 }
 
 // withdraw the claims of the discarded events [m_ok, m)
-__global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C,
-                                                        InsertIn in, InsertState st) {
-    const int64_t k = m_ok + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
+__global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, const unsigned long long* fail,
+                                                        const unsigned long long* fail_sig, int64_t E0, int64_t cap,
+                                                        int C, InsertIn in, InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m || k < accepted_prefix(m, fail, fail_sig)) return;
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
     const int64_t sp = in.sp[k];
@@ -224,10 +241,11 @@ void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int 
     if (m > 0) hipLaunchKernelGGL(k_insert_check, dim3(nblocks(m)), dim3(256), 0, s, m, E0, cap, C, n, in, st);
 }
 
-void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st,
-                          int mode) {
-    const unsigned grid = nblocks(m_ok) < 4096u ? nblocks(m_ok) : 4096u;   // grid-stride beyond 1 M events
-    if (m_ok > 0) hipLaunchKernelGGL(k_insert_commit, dim3(grid), dim3(256), 0, s, m_ok, E0, n, in, st, mode);
+void launch_insert_commit(hipStream_t s, int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
+                          int64_t E0, int n, const InsertIn& in, const InsertState& st, int mode) {
+    const unsigned grid = nblocks(m) < 4096u ? nblocks(m) : 4096u;   // grid-stride beyond 1 M events
+    if (m > 0)
+        hipLaunchKernelGGL(k_insert_commit, dim3(grid), dim3(256), 0, s, m, fail, fail_sig, E0, n, in, st, mode);
 }
 
 // Event.Verify's place in InsertEvent (hashgraph.go:356-363): the smallest event of the batch
@@ -253,10 +271,10 @@ void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* cre
     if (m > 0) hipLaunchKernelGGL(k_insert_sig_first, dim3(nblocks(m)), dim3(256), 0, s, m, C, creator, vout, fail);
 }
 
-void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
-                           const InsertState& st) {
-    if (m > m_ok)
-        hipLaunchKernelGGL(k_insert_unclaim, dim3(nblocks(m - m_ok)), dim3(256), 0, s, m, m_ok, E0, cap, C, in, st);
+void launch_insert_unclaim(hipStream_t s, int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
+                           int64_t E0, int64_t cap, int C, const InsertIn& in, const InsertState& st) {
+    if (m > 0)
+        hipLaunchKernelGGL(k_insert_unclaim, dim3(nblocks(m)), dim3(256), 0, s, m, fail, fail_sig, E0, cap, C, in, st);
 }
 
 }  // namespace hgx

@@ -120,6 +120,15 @@ struct FillRange {
 };
 constexpr int kFillMax = 8;
 void launch_fill_many(hipStream_t s, const FillRange* r, int count);
+// several small copies between HBM and pinned host memory (device-visible pointers) in one
+// launch: the small read-backs and uploads of a call cost one kernel instead of a blit each
+struct CopyRange {
+    const void* src;
+    void* dst;
+    uint32_t bytes;
+};
+constexpr int kCopyMax = 8;
+void launch_copy_many(hipStream_t s, const CopyRange* r, int count);
 
 int fd_tile_rows(int n, int compact);
 // gid order -> chain-major positions; p_opu = lastAncestors unit of the op row (SEG rows),
@@ -227,11 +236,12 @@ void launch_insert_claim(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int 
 void launch_insert_check(hipStream_t s, int64_t m, int64_t E0, int64_t cap, int C, int n, const InsertIn& in,
                          const InsertState& st);
 constexpr int kCommitAll = 0, kCommitStructure = 1, kCommitPayload = 2;
-void launch_insert_commit(hipStream_t s, int64_t m_ok, int64_t E0, int n, const InsertIn& in, const InsertState& st,
-                          int mode = kCommitAll);
+// m_ok = the accepted prefix of m from the first-failure words (all m when fail is null)
+void launch_insert_commit(hipStream_t s, int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
+                          int64_t E0, int n, const InsertIn& in, const InsertState& st, int mode);
 void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos, const int64_t* g_ts, int64_t* p_ts);
-void launch_insert_unclaim(hipStream_t s, int64_t m, int64_t m_ok, int64_t E0, int64_t cap, int C, const InsertIn& in,
-                           const InsertState& st);
+void launch_insert_unclaim(hipStream_t s, int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
+                           int64_t E0, int64_t cap, int C, const InsertIn& in, const InsertState& st);
 // verify results vout[k] (1 valid, 0 invalid, 2 key not a point) -> *fail = min (k << 8 | code)
 void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* creator, const uint8_t* vout,
                              unsigned long long* fail);

@@ -59,6 +59,27 @@ __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __
     p_cts[p] = g_cts[gid];
 }
 
+// a few thousand new events (the incremental schedule): one thread per event, direct scatter
+// (a 4 096-event block of k_layout would run the whole batch on one CU)
+__global__ void __launch_bounds__(256) k_layout_direct(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
+                                                       const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                                       const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
+                                                       const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
+                                                       const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
+                                                       int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
+                                                       int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu,
+                                                       int32_t* __restrict__ p_opk, int64_t* __restrict__ p_ts,
+                                                       int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C,
+                                                       int n, int seg) {
+    const int64_t gid = E0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= E) return;
+    const int c = g_creator[gid];
+    const int p = c_off[c] + g_index[gid] - c_base[c];
+    g_pos[gid] = p;
+    layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu, p_opk,
+               p_ts, p_rr, p_cts, C, n, seg);
+}
+
 __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
                                                 const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
                                                 const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
@@ -1504,67 +1525,73 @@ __global__ void k_root_bound(const int32_t* __restrict__ c_off, const int32_t* _
 
 // ---------------------------------------------------------------------------------
 // order of a small received set (m <= kSortSmallMax, the incremental schedule's usual
-// case): one block bitonic-sorts (graph, rr, cts, S) in LDS, S compared from HBM only on
-// equal (graph, rr, cts) (consensus_sorter.go:36-51). Replaces the radix passes' ~40
-// launches and the cts range read-back.
+// case) by ranks: an event's place is the number of events before it in (graph, rr, cts, S)
+// order (consensus_sorter.go:36-51), S compared from HBM only when the first 8 bytes tie.
+// A (256 events) x (256 events) tile per workgroup, the column tile's keys broadcast from
+// LDS, partial counts added to rank[]; then one scatter. 16 x 16 workgroups at m = 4096
+// instead of one workgroup's 78 bitonic stages (LDS-bandwidth bound, 145 us per call).
 constexpr int kSortSmallMax = 4096;
+constexpr int kRankTile = 256;
 
-__global__ void __launch_bounds__(1024) k_sort_small(int32_t m, const int32_t* __restrict__ list,
-                                                     const int64_t* __restrict__ p_cts,
-                                                     const int32_t* __restrict__ p_chain,
-                                                     const int32_t* __restrict__ p_rr, const int32_t* __restrict__ p_gid,
-                                                     const uint8_t* __restrict__ g_S, int n,
-                                                     uint32_t* __restrict__ out) {
-    __shared__ uint64_t khi[kSortSmallMax], klo[kSortSmallMax];
-    __shared__ uint64_t ks[kSortSmallMax];   // S's first 8 bytes, big-endian: the tie-break, almost always
-    __shared__ int32_t kv[kSortSmallMax];
-    int NP = 1;
-    while (NP < m) NP <<= 1;
-    for (int i = threadIdx.x; i < NP; i += blockDim.x) {
-        if (i < m) {
-            const int p = list[i];
-            khi[i] = ((uint64_t)(uint32_t)(p_chain[p] / n) << 32) | (uint64_t)(uint32_t)p_rr[p];
-            klo[i] = (uint64_t)p_cts[p] ^ 0x8000000000000000ull;
-            const uint8_t* sp = g_S + (size_t)p_gid[p] * 32;
-            uint64_t h = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) h = (h << 8) | sp[k];
-            ks[i] = h;
-            kv[i] = p;
-        } else {   // padding sorts last
-            khi[i] = ~0ull;
-            klo[i] = ~0ull;
-            ks[i] = ~0ull;
-            kv[i] = -1;
-        }
+struct SortKey {
+    uint64_t hi, lo, s8;   // (graph << 32 | rr), cts with the sign flipped, S's first 8 bytes
+    int32_t p;             // position
+};
+
+__device__ __forceinline__ SortKey sort_key(int p, const int64_t* __restrict__ p_cts, const int32_t* __restrict__ p_chain,
+                                            const int32_t* __restrict__ p_rr, const int32_t* __restrict__ p_gid,
+                                            const uint8_t* __restrict__ g_S, int n) {
+    SortKey k;
+    k.hi = ((uint64_t)(uint32_t)(p_chain[p] / n) << 32) | (uint64_t)(uint32_t)p_rr[p];
+    k.lo = (uint64_t)p_cts[p] ^ 0x8000000000000000ull;
+    const uint2 w = *(const uint2*)(g_S + (size_t)p_gid[p] * 32);
+    k.s8 = ((uint64_t)__builtin_bswap32(w.x) << 32) | (uint64_t)__builtin_bswap32(w.y);
+    k.p = p;
+    return k;
+}
+
+__global__ void __launch_bounds__(256) k_sort_rank(int32_t m, const int32_t* __restrict__ list,
+                                                    const int64_t* __restrict__ p_cts,
+                                                    const int32_t* __restrict__ p_chain,
+                                                    const int32_t* __restrict__ p_rr, const int32_t* __restrict__ p_gid,
+                                                    const uint8_t* __restrict__ g_S, int n,
+                                                    uint32_t* __restrict__ rank) {
+    __shared__ uint64_t jhi[kRankTile], jlo[kRankTile], js8[kRankTile];
+    __shared__ int32_t jp[kRankTile];
+    const int i = blockIdx.x * kRankTile + threadIdx.x;
+    const int j0 = blockIdx.y * kRankTile;
+    const int jn = min(kRankTile, m - j0);
+    if ((int)threadIdx.x < jn) {
+        const SortKey k = sort_key(list[j0 + threadIdx.x], p_cts, p_chain, p_rr, p_gid, g_S, n);
+        jhi[threadIdx.x] = k.hi;
+        jlo[threadIdx.x] = k.lo;
+        js8[threadIdx.x] = k.s8;
+        jp[threadIdx.x] = k.p;
     }
     __syncthreads();
-    // equal (graph, rr, timestamp) runs are ordered by S (256-bit big-endian): the prefix in LDS
-    // decides unless two signatures share 8 bytes (then the rows are read from HBM)
-    auto less = [&](int a, int b) -> bool {   // element a before element b
-        if (khi[a] != khi[b]) return khi[a] < khi[b];
-        if (klo[a] != klo[b]) return klo[a] < klo[b];
-        if (kv[a] < 0 || kv[b] < 0) return kv[b] < 0 && kv[a] >= 0;
-        if (ks[a] != ks[b]) return ks[a] < ks[b];
-        return cmp_s(g_S + (size_t)p_gid[kv[a]] * 32, g_S + (size_t)p_gid[kv[b]] * 32) < 0;
-    };
-    for (int k = 2; k <= NP; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = threadIdx.x; t < NP / 2; t += blockDim.x) {
-                const int i = 2 * t - (t & (j - 1));   // lower index of the pair (bit j clear)
-                const int l = i + j;
-                const bool up = (i & k) == 0;
-                if (up ? less(l, i) : less(i, l)) {
-                    const uint64_t h = khi[i], o = klo[i], q = ks[i];
-                    const int32_t v = kv[i];
-                    khi[i] = khi[l]; klo[i] = klo[l]; ks[i] = ks[l]; kv[i] = kv[l];
-                    khi[l] = h; klo[l] = o; ks[l] = q; kv[l] = v;
-                }
-            }
-            __syncthreads();
+    if (i >= m) return;
+    const SortKey me = sort_key(list[i], p_cts, p_chain, p_rr, p_gid, g_S, n);
+    uint32_t cnt = 0;
+    for (int jj = 0; jj < jn; jj++) {
+        const uint64_t h = jhi[jj], l = jlo[jj], q = js8[jj];
+        bool before;
+        if (h != me.hi) before = h < me.hi;
+        else if (l != me.lo) before = l < me.lo;
+        else if (q != me.s8) before = q < me.s8;
+        else if (j0 + jj == i) before = false;   // itself (without this, every diagonal step reads S from HBM)
+        else {   // 8 equal bytes of S: the whole S, then the list order
+            const int c = cmp_s(g_S + (size_t)p_gid[jp[jj]] * 32, g_S + (size_t)p_gid[me.p] * 32);
+            before = c < 0 || (c == 0 && j0 + jj < i);
         }
+        cnt += before ? 1u : 0u;
     }
-    for (int i = threadIdx.x; i < m; i += blockDim.x) out[i] = (uint32_t)kv[i];
+    if (cnt) atomicAdd(&rank[i], cnt);
+}
+
+__global__ void __launch_bounds__(256) k_sort_place(int32_t m, const int32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ rank, uint32_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[rank[i]] = (uint32_t)list[i];
 }
 
 // ---------------------------------------------------------------------------------
@@ -1610,8 +1637,52 @@ void launch_fill_many(hipStream_t s, const FillRange* r, int count) {
     hipLaunchKernelGGL(k_fill_many, dim3(bx, f.count), dim3(256), 0, s, f);
 }
 
+struct CopyArgs {
+    CopyRange r[kCopyMax];
+};
+__global__ void __launch_bounds__(256) k_copy_many(CopyArgs f) {
+    const CopyRange r = f.r[blockIdx.y];
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x, st = gridDim.x * blockDim.x;
+    const uintptr_t al = (uintptr_t)r.src | (uintptr_t)r.dst;
+    uint32_t done = 0;
+    if ((al & 15u) == 0) {
+        const uint4* s4 = (const uint4*)r.src;
+        uint4* d4 = (uint4*)r.dst;
+        const uint32_t nq = r.bytes / 16;
+        for (uint32_t t = t0; t < nq; t += st) d4[t] = s4[t];
+        done = nq * 16;
+    } else if ((al & 3u) == 0) {
+        const uint32_t* s1 = (const uint32_t*)r.src;
+        uint32_t* d1 = (uint32_t*)r.dst;
+        const uint32_t nw = r.bytes / 4;
+        for (uint32_t t = t0; t < nw; t += st) d1[t] = s1[t];
+        done = nw * 4;
+    }
+    const uint8_t* sb = (const uint8_t*)r.src;
+    uint8_t* db = (uint8_t*)r.dst;
+    for (uint32_t t = done + t0; t < r.bytes; t += st) db[t] = sb[t];
+}
+
+void launch_copy_many(hipStream_t s, const CopyRange* r, int count) {
+    if (count <= 0) return;
+    CopyArgs f{};
+    uint32_t mx = 0;
+    for (int i = 0; i < count && i < kCopyMax; i++) {
+        f.r[i] = r[i];
+        mx = std::max(mx, r[i].bytes);
+    }
+    const unsigned bx = std::max(1u, std::min(64u, (mx / 16 + 255) / 256));
+    hipLaunchKernelGGL(k_copy_many, dim3(bx, std::min(count, kCopyMax)), dim3(256), 0, s, f);
+}
+
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
     if (E <= E0) return;
+    if (E - E0 <= 8 * kLayoutB) {
+        hipLaunchKernelGGL(k_layout_direct, dim3(nblk(E - E0, 256)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index,
+                           a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
+                           a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
+        return;
+    }
     hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
                        a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_opk,
                        a.p_ts, a.p_rr, a.p_cts, C, n, seg);
@@ -1926,8 +1997,11 @@ void launch_round_first_gid(hipStream_t s, const DevArrays& a, int r0, int R, in
 bool sort_small_ok(int32_t m) { return m <= kSortSmallMax; }
 
 void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals) {
-    hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr, a.p_gid,
-                       a.g_S, n, a.val_a);
+    // (rank[] = val_b[0, m) zeroed by the caller)
+    const unsigned t = (unsigned)((m + kRankTile - 1) / kRankTile);
+    hipLaunchKernelGGL(k_sort_rank, dim3(t, t), dim3(kRankTile), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr,
+                       a.p_gid, a.g_S, n, a.val_b);
+    hipLaunchKernelGGL(k_sort_place, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.val_b, a.val_a);
     *final_vals = a.val_a;
 }
 
