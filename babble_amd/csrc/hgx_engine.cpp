@@ -135,6 +135,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     chain_base_d.view(ins_blk.p + 2 * C, C);
     graph_loaded_d.view((unsigned long long*)(ins_blk.p + ins_gl_off), G);
     HGX_TRY(ins_fail.alloc(1));
+    HGX_TRY(hipMemsetAsync(ins_fail.p, 0xFF, 8, stream));   // re-armed after every read
     HGX_TRY(hipHostMalloc((void**)&h_ins, ins_blk.n * sizeof(int32_t), hipHostMallocDefault));
     HGX_TRY(cpar_blk.alloc((size_t)3 * C));
     HGX_TRY(hipHostMalloc((void**)&h_cpar, (size_t)3 * C * sizeof(int32_t), hipHostMallocDefault));
@@ -156,7 +157,8 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     fd_ld = (Ppos + 31) & ~(int64_t)31;   // firstDescendants columns: 64-byte aligned 32-position segments
     HGX_TRY(LA.alloc(PP * n));
     HGX_TRY(FDT.alloc((size_t)fd_ld * n + 128));   // slack: compact window staging reads past a column
-    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8 + 4 * kLaRing)); HGX_TRY(order_gid.alloc(P));
+    HGX_TRY(recv_list.alloc(P)); HGX_TRY(counters.alloc(8 + 4 * kLaRing));
+    HGX_TRY(hipMemsetAsync(counters.p, 0, (8 + 4 * kLaRing) * 4, stream)); HGX_TRY(order_gid.alloc(P));
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
@@ -300,11 +302,13 @@ hipError_t Engine::stage_d2h(void* host, const void* dev, size_t bytes) {
     return hipSuccess;
 }
 
-hipError_t Engine::copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes) {
+hipError_t Engine::copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes, int reset) {
     if (bytes == 0) return hipSuccess;
     void* d = nullptr;
     HGX_TRY(hipHostGetDevicePointer(&d, pinned_dst, 0));
-    pend.push_back({2, 0, dev, pinned_dst, d, bytes});
+    PendCopy p{2, 0, dev, pinned_dst, d, bytes};
+    p.reset = reset;
+    pend.push_back(p);
     return hipSuccess;
 }
 
@@ -329,7 +333,7 @@ hipError_t Engine::stage_issue() {
         for (const PendCopy& p : pend) {
             if (p.kind == 0) r[k++] = {d_stage + p.off, const_cast<void*>(p.dev), (uint32_t)p.bytes};
             else if (p.kind == 1) r[k++] = {p.dev, d_stage + p.off, (uint32_t)p.bytes};
-            else if (p.kind == 2) r[k++] = {p.dev, p.dev_dst, (uint32_t)p.bytes};
+            else if (p.kind == 2) r[k++] = {p.dev, p.dev_dst, (uint32_t)p.bytes, p.reset};
             else r[k++] = {p.dev_src, const_cast<void*>(p.dev), (uint32_t)p.bytes};
         }
         launch_copy_many(stream, r, k);
@@ -339,7 +343,10 @@ hipError_t Engine::stage_issue() {
     for (const PendCopy& p : pend) {
         if (p.kind == 0) HGX_TRY(hipMemcpyAsync(const_cast<void*>(p.dev), h_stage + p.off, p.bytes, hipMemcpyHostToDevice, stream));
         else if (p.kind == 1) HGX_TRY(hipMemcpyAsync(h_stage + p.off, p.dev, p.bytes, hipMemcpyDeviceToHost, stream));
-        else if (p.kind == 2) HGX_TRY(hipMemcpyAsync(p.host_dst, p.dev, p.bytes, hipMemcpyDeviceToHost, stream));
+        else if (p.kind == 2) {
+            HGX_TRY(hipMemcpyAsync(p.host_dst, p.dev, p.bytes, hipMemcpyDeviceToHost, stream));
+            if (p.reset >= 0) HGX_TRY(hipMemsetAsync(const_cast<void*>(p.dev), p.reset, p.bytes, stream));
+        }
         else HGX_TRY(hipMemcpyAsync(const_cast<void*>(p.dev), p.host_src, p.bytes, hipMemcpyHostToDevice, stream));
     }
     pend.clear();
@@ -547,12 +554,12 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
         // checks, then the commit of the accepted prefix and the withdrawal of the rest's claims:
         // the kernels take the prefix from the first-failure words, so the batch costs one host
         // round trip (the chunked schedule inserts 1 000 events per call)
-        HGX_TRY(hipMemsetAsync(ins_fail.p, 0xFF, 8, stream));
+        // (ins_fail is ~0 here: set at creation, re-armed by the read-back below)
         launch_insert_claim(stream, count, E0, cap, C, in, st);
         launch_insert_check(stream, count, E0, cap, C, n, in, st);
         launch_insert_commit(stream, count, ins_fail.p, fail_sig, E0, n, in, st, commit_mode);
         launch_insert_unclaim(stream, count, ins_fail.p, fail_sig, E0, cap, C, in, st);
-        HGX_TRY(copy_to_pinned(h_small, ins_fail.p, 8));
+        HGX_TRY(copy_to_pinned(h_small, ins_fail.p, 8, 0xFF));
         if (fail_sig) HGX_TRY(copy_to_pinned(h_small + 2, fail_sig, 8));
     }
     out.last_gid.resize(C);
@@ -856,14 +863,17 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     };
     if (la_wave_used) {
         // one dataflow pass (k_la_wave); its error flag is read with the phase clock below
-        HGX_TRY(hipMemsetAsync(counters.p + 6, 0, 4, stream));
+        // the error flag is 0 here: zeroed at creation, re-armed by every read
         kbeg(K_LA_SWEEP);
         HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na));
         if (la_wave_segs > 1)
             HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6, la_map, la_na));
         const double rows = (double)(En - E0);
         kend(K_LA_SWEEP, rows * (3.0 * csz * n + 16));
-        if (rebuild) HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
+        if (rebuild) {
+            HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipMemsetAsync(counters.p + 6, 0, 4, stream));
+        }
         if (la_wave_segs > 1) HGX_TRY(run_sweeps(2));   // verify sweep + dirty sweeps (counted there)
         la_sweeps++;
         la_rows += (int64_t)rows;
@@ -952,7 +962,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // (rows beyond the last round are copied and dropped), then ph1
     const int r_scan = rebuild ? 0 : r_lo;
     const std::vector<int32_t> prev_last = out.last_round;
-    bool tail_ready = false;
+    bool tail_ready = false, la_flag_read = false;
     auto enqueue_tail = [&](int32_t r_hi) -> hipError_t {
         stage_out.clear();   // (a tail queued before more steps were needed is superseded)
         pend.clear();
@@ -965,7 +975,10 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         if (out.wflag.size() < (size_t)r_hi * C) out.wflag.resize((size_t)r_hi * C);
         HGX_TRY(stage_d2h(out.bm.data() + b0, Bm.p + b0, ((size_t)(r_hi + 1) * C - b0) * 4));
         if (r_hi > r_lo) HGX_TRY(stage_d2h(out.wflag.data() + b0, wstat.p + b0, (size_t)r_hi * C - b0));
-        if (one_trip && la_wave_used) HGX_TRY(copy_to_pinned(h_small + 48, counters.p + 6, 4));
+        if (one_trip && la_wave_used && !la_flag_read) {   // (read and re-armed once)
+            HGX_TRY(copy_to_pinned(h_small + 48, counters.p + 6, 4, 0));
+            la_flag_read = true;
+        }
         HGX_TRY(stage_issue());
         return hipEventRecord(ph1, stream);
     };
@@ -1029,9 +1042,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         }
     }
     if (r_done < 0) launch_round_k_gather(stream, round_args(), r_lo);   // W'_{r_lo} rebased for k_round_k
-    // a rebuild replays kStepBatch steps per hipGraph; a resumed call (a few rounds) kStepBatchSmall
-    StepGraph& sgr = step_g[rebuild ? 0 : 1];
-    const int nb = rebuild ? kStepBatch : kStepBatchSmall;
+    // a rebuild replays kStepBatch steps per hipGraph; a resumed call (a few rounds) 2 or 4: a
+    // round holds ~10-14 events per chain, so fewer than 6 new events per chain rarely take
+    // more than two steps (a second batch costs another host round trip)
+    const bool few = (En - E0) < 6 * (int64_t)C;
+    StepGraph& sgr = step_g[rebuild ? 0 : few ? 1 : 2];
+    const int nb = rebuild ? kStepBatch : few ? kStepBatchSmall : 2 * kStepBatchSmall;
     if (r_done < 0) {   // n <= 1024 (hgx_create's limit)
         // nb step nodes replayed as one hipGraph; before each replay the nodes' round
         // arguments are rewritten (hipGraphExecKernelNodeSetParams), so a step knows its

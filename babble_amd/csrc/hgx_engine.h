@@ -15,7 +15,7 @@ namespace hgx {
 
 
 constexpr int kStepBatch = 16;        // round steps per hipGraph replay (a full DivideRounds)
-constexpr int kStepBatchSmall = 4;    // ... when resuming at the lowest changed round
+constexpr int kStepBatchSmall = 2;    // ... when resuming at the lowest changed round
 
 // kStepBatch round steps captured as one hipGraph, replayed with rewritten round arguments
 struct StepGraph {
@@ -275,7 +275,7 @@ class Engine {
     hipEvent_t flag_ev[2] = {nullptr, nullptr};
     static constexpr int kLaRing = 8, kLaAhead = 3;   // lastAncestors sweeps queued ahead of the check
     hipEvent_t la_ev[kLaRing] = {};
-    StepGraph step_g[2];   // [0] full DivideRounds, [1] resumed (incremental) calls
+    StepGraph step_g[3];   // [0] full DivideRounds, [1] / [2] resumed (incremental) calls of 2 / 4 steps
     void drop_step_graph();
     DBuf<uint8_t> wflag, wstat, wcoin, elig, fw, ur_empty;
     DBuf<uint64_t> Smat, Vbuf;
@@ -315,13 +315,14 @@ class Engine {
         size_t bytes;
         const void* host_src = nullptr;
         const void* dev_src = nullptr;
+        int reset = -1;   // kind 2: the device bytes are set to this value once copied
     };
     std::vector<PendCopy> pend;
     static constexpr size_t kCopyKernelMax = 256 << 10;
     hipError_t stage_reserve(size_t bytes);
     hipError_t stage_h2d(void* dev, const void* host, size_t bytes);
     hipError_t stage_d2h(void* host, const void* dev, size_t bytes);
-    hipError_t copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes);   // queued like the stagings
+    hipError_t copy_to_pinned(void* pinned_dst, const void* dev, size_t bytes, int reset = -1);   // queued like the stagings
     hipError_t copy_from_pinned(void* dev, const void* pinned_src, size_t bytes);
     hipError_t stage_issue();
     void stage_flush();   // after the stream synchronized: copy the D2H tables out, reset the cursor

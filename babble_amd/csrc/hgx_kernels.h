@@ -126,6 +126,7 @@ struct CopyRange {
     const void* src;
     void* dst;
     uint32_t bytes;
+    int reset = -1;   // >= 0: the source bytes are set to this value once copied (a flag re-armed)
 };
 constexpr int kCopyMax = 8;
 void launch_copy_many(hipStream_t s, const CopyRange* r, int count);

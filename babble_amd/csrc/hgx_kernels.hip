@@ -628,6 +628,7 @@ __global__ void __launch_bounds__(256) k_fame_vote(int R, int r0, int nw, const 
 typedef int int4v __attribute__((ext_vector_type(4)));
 constexpr int kFameTile = 64;     // witnesses x per block
 constexpr int kFameMaxW = 16;     // words per bit row (n <= 1024)
+constexpr int kFameSW = 4096;     // S words of a voter round staged in LDS (n <= 512)
 
 // 16 bits -> 16 bytes of 0/1 (bit q of b -> byte q): nibble * 0x00204081 puts bits
 // 0..3 at 0, 8, 16, 24 with no overlapping partial products.
@@ -640,22 +641,42 @@ __device__ __forceinline__ int4v expand16(uint32_t b) {
     return r;
 }
 
-// wave 0 compacts { c < n : st[c] == 2 } into out (ascending; count to *cnt) and/or
-// writes it as a bit mask (word k = chains [64k, 64k+64))
+// the block compacts { c < n : st[c] == 2 } into out (ascending; count to *cnt) and/or writes it
+// as a bit mask (word k = chains [64k, 64k+64)): wave w takes the words w, w+4, ... (a resumed
+// call's DecideFame is a chain of these per voter round: one wave walking every word serially
+// was a load latency per word). All threads call it; it synchronizes once inside, the caller
+// after. wcnt: LDS scratch of kFameMaxW ints.
 __device__ __forceinline__ void compact_witnesses(const uint8_t* __restrict__ st, int n, int32_t* out, int* cnt,
-                                                  uint64_t* mask) {
-    if (threadIdx.x >= 64) return;
-    const int lane = lane_id();
-    int base = 0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int c = c0 + lane;
-        const bool w = c < n && st[c] == 2;
-        const uint64_t m = __ballot(w);
-        if (out && w) out[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
-        if (mask && lane == 0) mask[c0 >> 6] = m;
-        base += __popcll(m);
+                                                  uint64_t* mask, int* wcnt) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int nwd = (n + 63) >> 6;
+    uint64_t m[kFameMaxW / 4];
+#pragma unroll
+    for (int q = 0; q < kFameMaxW / 4; q++) {
+        const int k = wave + 4 * q;
+        m[q] = 0;
+        if (k < nwd) {
+            const int c = 64 * k + lane;
+            m[q] = __ballot(c < n && st[c] == 2);
+            if (lane == 0) {
+                wcnt[k] = __popcll(m[q]);
+                if (mask) mask[k] = m[q];
+            }
+        }
     }
-    if (cnt && lane == 0) *cnt = base;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int k = 0; k < nwd; k++) tot += wcnt[k];
+#pragma unroll
+    for (int q = 0; q < kFameMaxW / 4; q++) {
+        const int k = wave + 4 * q;
+        if (k < nwd && out) {
+            base = 0;
+            for (int k2 = 0; k2 < k; k2++) base += wcnt[k2];
+            if ((m[q] >> lane) & 1ull) out[base + __popcll(m[q] & ((1ull << lane) - 1ull))] = 64 * k + lane;
+        }
+    }
+    if (cnt && threadIdx.x == 0) *cnt = tot;
 }
 
 template <bool kMfma>
@@ -663,13 +684,15 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
                             const uint8_t* __restrict__ wstat, const uint8_t* __restrict__ wcoin,
                             const int32_t* __restrict__ Bm, const int32_t* __restrict__ c_base,
                             const int32_t* __restrict__ WLA, const uint64_t* __restrict__ Smat,
-                            int8_t* __restrict__ fame, int C, int n, int nw, int sm) {
+                            int8_t* __restrict__ fame, int C, int n, int nw, int sm, int sw) {
     extern __shared__ __align__(16) unsigned char fsm[];   // kMfma: int8 vote image [64][nw*64+16]
-    __shared__ int32_t xs[kFameTile], dec[kFameTile];
+    __shared__ int32_t xs[kFameTile], dec[kFameTile], xidx[kFameTile];
     __shared__ int32_t ys[1024], ytot[1024];
-    __shared__ int32_t s_ny, s_und;
+    __shared__ int32_t s_ny, s_und, wcnt[kFameMaxW];
     __shared__ uint64_t wmask[2][kFameMaxW];   // witness masks of rounds j-1 / j (by parity)
     __shared__ uint64_t Vb[2][kFameTile][kFameMaxW];   // vote bit rows V[x][w] (current / next)
+    // !kMfma: the dynamic LDS holds S_j[y] & wm of the round's voters (sw words; 0 = none)
+    uint64_t* sS = reinterpret_cast<uint64_t*>(fsm);
     const int RR = R - r0;   // rounds [r0, R): the undecided ones and later
     const int xt = blockIdx.x % XT;
     const int i = r0 + (blockIdx.x / XT) % RR;
@@ -679,7 +702,7 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
     const size_t gi = (size_t)g * n;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     // witnesses of round i, this block's slice
-    compact_witnesses(wstat + (size_t)i * C + gi, n, ys, &s_ny, nullptr);
+    compact_witnesses(wstat + (size_t)i * C + gi, n, ys, &s_ny, nullptr, wcnt);
     __syncthreads();
     const int nxt = min(kFameTile, s_ny - xt * kFameTile);
     if (nxt <= 0) return;
@@ -692,26 +715,40 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
         if ((int)threadIdx.x < nxt) fame[(size_t)i * C + gi + xs[threadIdx.x]] = 0;
         return;
     }
-    // j = i+1: vote(y, x) = See(y, x) = LA[y][cr(x)] >= Index(x)
-    {
-        const size_t jr = (size_t)(i + 1) * C + gi;
-        for (int t = threadIdx.x; t < kFameTile * nw; t += blockDim.x) {
-            const int x = t % kFameTile, wd = t / kFameTile;
-            uint64_t bits = 0;
-            if (x < nxt) {
-                const int xc = xs[x];
-                const int32_t xidx = c_base[gi + xc] + Bm[(size_t)i * C + gi + xc];
-                for (int bb = 0; bb < 64; bb++) {
-                    const int y = wd * 64 + bb;
-                    if (y >= n) break;
-                    if (wstat[jr + y] != 2) continue;
-                    if (WLA[(jr + y) * n + xc] >= xidx) bits |= 1ull << bb;
-                }
-            }
-            Vb[0][x][wd] = bits;
-        }
+    // j = i+1: vote(y, x) = See(y, x) = LA[y][cr(x)] >= Index(x), one (witness y of round i+1,
+    // x) pair per lane: independent loads (a lane walking 64 y with a dependent witness test
+    // each was most of a resumed call's DecideFame)
+    compact_witnesses(wstat + (size_t)(i + 1) * C + gi, n, ys, &s_ny, wmask[(i + 1) & 1], wcnt);
+    for (int t = threadIdx.x; t < kFameTile * nw; t += blockDim.x) Vb[0][t / nw][t % nw] = 0;
+    if ((int)threadIdx.x < nxt) {
+        const int xc = xs[threadIdx.x];
+        xidx[threadIdx.x] = c_base[gi + xc] + Bm[(size_t)i * C + gi + xc];
     }
-    compact_witnesses(wstat + (size_t)(i + 1) * C + gi, n, nullptr, nullptr, wmask[(i + 1) & 1]);
+    __syncthreads();
+    {
+        // lane = x, wave w takes the voters w, w+4, ...: the bits gather in registers, one LDS
+        // OR per word at the end
+        const size_t jr = (size_t)(i + 1) * C + gi;
+        const int ny1 = s_ny;
+        const int x = lane;
+        const int xc = x < nxt ? xs[x] : 0;
+        const int32_t xi = x < nxt ? xidx[x] : 0x7FFFFFFF;
+        uint64_t acc[kFameMaxW];
+#pragma unroll
+        for (int k = 0; k < kFameMaxW; k++) acc[k] = 0;
+        for (int yi = wave; yi < ny1; yi += 4) {
+            const int y = ys[yi];
+            const uint64_t b = WLA[(jr + y) * n + xc] >= xi ? 1ull << (y & 63) : 0ull;
+#pragma unroll
+            for (int k = 0; k < kFameMaxW; k++)
+                if (k == (y >> 6)) acc[k] |= b;
+        }
+        if (x < nxt)
+#pragma unroll
+            for (int k = 0; k < kFameMaxW; k++)
+                if (k < nw && acc[k]) atomicOr((unsigned long long*)&Vb[0][x][k], acc[k]);
+    }
+    __syncthreads();
     const int KB = nw * 64 + 16;   // int8 image row stride (16-B pad: 16 lanes of one x-group hit distinct banks)
     int cur = 0;
     for (int j = i + 2; j <= LR; j++) {
@@ -719,14 +756,28 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
         const size_t jr = (size_t)j * C + gi;
         const uint64_t* wm = wmask[(j - 1) & 1];   // witnesses of round j-1 (S rows may cover jumped candidates)
         for (int t = threadIdx.x; t < kFameTile * nw; t += blockDim.x) Vb[cur ^ 1][t / nw][t % nw] = 0;
-        compact_witnesses(wstat + jr, n, ys, &s_ny, wmask[j & 1]);
+        compact_witnesses(wstat + jr, n, ys, &s_ny, wmask[j & 1], wcnt);
         __syncthreads();
         const int ny = s_ny;
+        // the voters' S rows (masked to the witnesses of j-1) staged in LDS by all lanes at once:
+        // the tally then reads them as broadcasts instead of one dependent HBM row per voter
+        const bool s_lds = !kMfma && ny * nw <= sw;
+        if (s_lds) {
+            for (int t = threadIdx.x; t < ny * nw; t += blockDim.x) {
+                const int y = t / nw, k = t - y * nw;
+                sS[t] = Smat[(jr + ys[y]) * nw + k] & wm[k];
+            }
+            __syncthreads();
+        }
         // tot[y] = #{w witness of j-1 : S_j[y][w]}
         for (int t = threadIdx.x; t < ny; t += blockDim.x) {
-            const uint64_t* srow = Smat + (jr + ys[t]) * nw;
             int tot = 0;
-            for (int k = 0; k < nw; k++) tot += __popcll(srow[k] & wm[k]);
+            if (s_lds) {
+                for (int k = 0; k < nw; k++) tot += __popcll(sS[t * nw + k]);
+            } else {
+                const uint64_t* srow = Smat + (jr + ys[t]) * nw;
+                for (int k = 0; k < nw; k++) tot += __popcll(srow[k] & wm[k]);
+            }
             ytot[t] = tot;
         }
         if constexpr (kMfma) {
@@ -796,11 +847,18 @@ __global__ void __launch_bounds__(256) k_fame_tile(int R, int r0, int XT, const 
 #pragma unroll
             for (int k = 0; k < kFameMaxW; k++) vx[k] = k < nw ? Vb[cur][x][k] : 0ull;
             for (int yi = wave; yi < ny; yi += 4) {
-                const uint64_t* srow = Smat + (jr + ys[yi]) * nw;
                 int yays = 0;
+                if (s_lds) {
+                    const uint64_t* srow = sS + yi * nw;
 #pragma unroll
-                for (int k = 0; k < kFameMaxW; k++)
-                    if (k < nw) yays += __popcll(srow[k] & wm[k] & vx[k]);
+                    for (int k = 0; k < kFameMaxW; k++)
+                        if (k < nw) yays += __popcll(srow[k] & vx[k]);
+                } else {
+                    const uint64_t* srow = Smat + (jr + ys[yi]) * nw;
+#pragma unroll
+                    for (int k = 0; k < kFameMaxW; k++)
+                        if (k < nw) yays += __popcll(srow[k] & wm[k] & vx[k]);
+                }
                 if (x < nxt) vote(yi, x, yays);
             }
         }
@@ -940,15 +998,23 @@ __global__ void k_fu_count(int64_t E, const int32_t* __restrict__ g_creator, con
 // new rows of an incremental DivideRounds start as none: LA rows (read before they are
 // computed by the sweeps) and FD entries (no chain has seen the new events yet)
 template <typename CT>
-__global__ void k_init_new(int64_t E0, int64_t m, const int32_t* __restrict__ g_pos, CT* __restrict__ LA,
-                           CT* __restrict__ FDT, int n, int64_t P) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m * n) return;
-    const int64_t k = t / n;
-    const int i = (int)(t % n);
-    const int p = g_pos[E0 + k];
-    LA[(size_t)p * n + i] = Coord<CT>::enc_la(-1);
-    FDT[(size_t)i * P + p] = Coord<CT>::enc_fd(kMaxI32);
+__global__ void __launch_bounds__(256) k_init_new(int64_t E0, int64_t m, const int32_t* __restrict__ g_pos,
+                                                  CT* __restrict__ LA, CT* __restrict__ FDT, int n, int64_t P) {
+    // a tile of 16 new events x 64 observers per workgroup: the lastAncestors rows with the
+    // observer fastest, the firstDescendants entries with the event fastest (a chain's new
+    // positions are adjacent)
+    __shared__ int32_t s_pos[16];
+    const int64_t k0 = (int64_t)blockIdx.x * 16;
+    const int kn = (int)min<int64_t>(16, m - k0);
+    const int i0 = blockIdx.y * 64;
+    if ((int)threadIdx.x < kn) s_pos[threadIdx.x] = g_pos[E0 + k0 + threadIdx.x];
+    __syncthreads();
+    for (int t = threadIdx.x; t < 16 * 64; t += blockDim.x) {
+        const int k = t >> 6, i = i0 + (t & 63);
+        if (k < kn && i < n) LA[(size_t)s_pos[k] * n + i] = Coord<CT>::enc_la(-1);
+        const int k2 = t & 15, i2 = i0 + (t >> 4);
+        if (k2 < kn && i2 < n) FDT[(size_t)i2 * P + s_pos[k2]] = Coord<CT>::enc_fd(kMaxI32);
+    }
 }
 
 // consensus timestamp: upper median (ByTimestamp, index floor(|s|/2), event.go:227-237)
@@ -1645,22 +1711,33 @@ __global__ void __launch_bounds__(256) k_copy_many(CopyArgs f) {
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x, st = gridDim.x * blockDim.x;
     const uintptr_t al = (uintptr_t)r.src | (uintptr_t)r.dst;
     uint32_t done = 0;
+    const bool rs = r.reset >= 0;
+    const uint32_t f4 = 0x01010101u * (uint32_t)(r.reset & 0xFF);
     if ((al & 15u) == 0) {
-        const uint4* s4 = (const uint4*)r.src;
+        uint4* s4 = (uint4*)r.src;
         uint4* d4 = (uint4*)r.dst;
         const uint32_t nq = r.bytes / 16;
-        for (uint32_t t = t0; t < nq; t += st) d4[t] = s4[t];
+        for (uint32_t t = t0; t < nq; t += st) {
+            d4[t] = s4[t];
+            if (rs) s4[t] = make_uint4(f4, f4, f4, f4);
+        }
         done = nq * 16;
     } else if ((al & 3u) == 0) {
-        const uint32_t* s1 = (const uint32_t*)r.src;
+        uint32_t* s1 = (uint32_t*)r.src;
         uint32_t* d1 = (uint32_t*)r.dst;
         const uint32_t nw = r.bytes / 4;
-        for (uint32_t t = t0; t < nw; t += st) d1[t] = s1[t];
+        for (uint32_t t = t0; t < nw; t += st) {
+            d1[t] = s1[t];
+            if (rs) s1[t] = f4;
+        }
         done = nw * 4;
     }
-    const uint8_t* sb = (const uint8_t*)r.src;
+    uint8_t* sb = (uint8_t*)r.src;
     uint8_t* db = (uint8_t*)r.dst;
-    for (uint32_t t = done + t0; t < r.bytes; t += st) db[t] = sb[t];
+    for (uint32_t t = done + t0; t < r.bytes; t += st) {
+        db[t] = sb[t];
+        if (rs) sb[t] = (uint8_t)r.reset;
+    }
 }
 
 void launch_copy_many(hipStream_t s, const CopyRange* r, int count) {
@@ -1779,10 +1856,12 @@ void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n,
                 attr = true;
             }
             hipLaunchKernelGGL(k_fame_tile<true>, grid, dim3(256), shm, s, R, r0, XT, a.lr, a.wstat, a.wcoin, a.Bm,
-                               a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
+                               a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm, 0);
         } else {
-            hipLaunchKernelGGL(k_fame_tile<false>, grid, dim3(256), 0, s, R, r0, XT, a.lr, a.wstat, a.wcoin, a.Bm,
-                               a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm);
+            // the voters' S rows in LDS up to 512 chains (n x nw words <= 32 KB)
+            const int sw = (size_t)n * nw * 8 <= kFameSW * 8 ? n * nw : 0;
+            hipLaunchKernelGGL(k_fame_tile<false>, grid, dim3(256), (size_t)sw * 8, s, R, r0, XT, a.lr, a.wstat, a.wcoin,
+                               a.Bm, a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm, sw);
         }
         return;
     }
@@ -1827,10 +1906,10 @@ void launch_fu_count(hipStream_t s, const DevArrays& a, int64_t E) {
 void launch_init_new(hipStream_t s, const DevArrays& a, int64_t E0, int64_t m, int n, int64_t P) {
     if (m <= 0) return;
     if (a.compact)
-        hipLaunchKernelGGL(k_init_new<uint16_t>, dim3(nblk(m * n, 256)), dim3(256), 0, s, E0, m, a.g_pos,
+        hipLaunchKernelGGL(k_init_new<uint16_t>, dim3(nblk(m, 16), (n + 63) / 64), dim3(256), 0, s, E0, m, a.g_pos,
                            (uint16_t*)a.LA, (uint16_t*)a.FDT, n, P);
     else
-        hipLaunchKernelGGL(k_init_new<int32_t>, dim3(nblk(m * n, 256)), dim3(256), 0, s, E0, m, a.g_pos,
+        hipLaunchKernelGGL(k_init_new<int32_t>, dim3(nblk(m, 16), (n + 63) / 64), dim3(256), 0, s, E0, m, a.g_pos,
                            (int32_t*)a.LA, (int32_t*)a.FDT, n, P);
 }
 

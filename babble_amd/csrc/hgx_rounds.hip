@@ -762,10 +762,11 @@ __global__ void __launch_bounds__(256) k_last_round(int rs, int R, int C, int n,
     __shared__ int32_t s_max[4];
     const int g = blockIdx.x;
     const int r0 = rs + blockIdx.y * 64;
+    const int nr = min(64, R - r0);   // (a resumed call scans a few rounds)
     int m = -1;
-    for (int t = threadIdx.x; t < 64 * n; t += blockDim.x) {
-        const int r = r0 + t / n, i = t % n;
-        if (r < R && wstat[(size_t)r * C + (size_t)g * n + i] == 2) m = max(m, r);
+    for (int t = threadIdx.x; t < nr * n; t += blockDim.x) {
+        const int r = r0 + t / n, i = t - (t / n) * n;
+        if (wstat[(size_t)r * C + (size_t)g * n + i] == 2) m = max(m, r);
     }
     for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
