@@ -865,7 +865,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // one dataflow pass (k_la_wave); its error flag is read with the phase clock below
         // the error flag is 0 here: zeroed at creation, re-armed by every read
         kbeg(K_LA_SWEEP);
-        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na));
+        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na,
+                               !rebuild && (En - E0) <= 8 * (int64_t)C));
         if (la_wave_segs > 1)
             HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6, la_map, la_na));
         const double rows = (double)(En - E0);

@@ -145,11 +145,13 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
 // a verify sweep confirms or completes the rows.
 // lmap (one graph, n > 896): the chains that have events, one compute lane each (na of them);
 // null: lane i = chain i of every graph
+// narrow (a resumed call with a few new rows per chain): one-dword column blocks, 4x the workgroups
 bool la_wave_ok(int n, int max_len, int n_active);
 int la_wave_blocks(int n, int compact);   // column blocks of the time-segment passes (workgroups per segment)
 int la_wave_segments(int n, int compact, int num_cus, int max_segs);   // time segments that fill the device
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                          int head, int32_t* err, const int32_t* lmap = nullptr, int na = 0);
+                          int head, int32_t* err, const int32_t* lmap = nullptr, int na = 0,
+                          bool narrow = false);
 // one Gauss-Seidel sweep over the dirty units (all when `first`) from unit u0: a unit is dirty
 // when its carry unit or an op unit has chg == stamp - 1, and gets chg = stamp when its values
 // change (usum = per-unit sums); out[0] += rows recomputed, out[1] += units changed; out_next

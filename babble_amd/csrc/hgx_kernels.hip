@@ -422,8 +422,11 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     // read while the current one is written: no dependent LDS round trip per chain.
     int32_t* slot = (int32_t*)(tw + (FT + 1) * ldw) + 64 * wave;
     const int ownv = base_c + k0;
-    for (int d0 = wave; d0 < n; d0 += nwaves * 64) {
-        const int dq = d0 + nwaves * lane;
+    // gridDim.z > 1 (a resumed call: a few new rows per chain): the target chains are split over
+    // z blocks, so a block's serial per-target loop is z times shorter
+    const int S = nwaves * (int)gridDim.z;   // target stride
+    for (int d0 = wave + nwaves * (int)blockIdx.z; d0 < n; d0 += S * 64) {
+        const int dq = d0 + S * lane;
         int q_len = 0, q_base = 0, q_off = 0, q_lo = 0, q_hv = 0;
         if (dq < n) {
             q_len = m_len[dq];
@@ -432,11 +435,11 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
             q_lo = (k0 > 0) ? K::la(tile[dq]) : q_base - 1;
             if (rows > 0) q_hv = K::la(tile[rows * ld + dq]);
         }
-        const int nq = min(64, (n - d0 + nwaves - 1) / nwaves);
+        const int nq = min(64, (n - d0 + S - 1) / S);
         int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0]) : 0;
         for (int q = 0; q < nq; q++) {
             const int vraw = vnext;
-            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + nwaves * (q + 1)]);
+            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + S * (q + 1)]);
             const int len_d = __builtin_amdgcn_readlane(q_len, q);
             if (len_d == 0) continue;
             const int base_d = __builtin_amdgcn_readlane(q_base, q);
@@ -1811,11 +1814,13 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     const int nwd = a.compact ? n / 2 : n;
     // + 8 waves x 64 owner slots
     const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n + 8 * 64) * sizeof(int32_t);
+    // a resumed call with a few new rows per chain: target chains split over up to 8 blocks
+    const int z = (c_old && max_new <= ft) ? max(1, min(8, n / 64)) : 1;
     if (a.compact)
-        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
+        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
                            (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
     else
-        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles), dim3(512), lds, s, (const uint32_t*)a.LA,
+        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
                            (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
 }
 

@@ -392,7 +392,7 @@ inline SegCfg seg_cfg(int n, int nwd) {
 // LDS: NP * (R * DW + R + Q) + 5 n words <= 160 KB (NP = n rounded up to a power of two); DW divides the row's words
 template <typename CT>
 hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                            int head, int32_t* err, const int32_t* lmap, int na) {
+                            int head, int32_t* err, const int32_t* lmap, int na, bool narrow) {
     const int nwd = a.compact ? n / 2 : n;
     if (nts > 1) {   // time segments: wider blocks, smaller rings (seg_cfg)
         const SegCfg g = seg_cfg(n, nwd);
@@ -414,11 +414,12 @@ hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, con
 #undef SEG
     }
     if (n <= 128) {
-        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err, lmap, na);
+        if (nwd % 4 == 0 && !(narrow && c_old)) return la_wave_launch<CT, 4, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err, lmap, na);
         return la_wave_launch<CT, 1, 32, 64, 1, 2, 16>(s, a, G, n, c_old, E, err, lmap, na);
     }
     if (n <= 256) {
-        if (nwd % 4 == 0) return la_wave_launch<CT, 4, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err, lmap, na);
+        if (nwd % 4 == 0 && !(narrow && c_old))
+            return la_wave_launch<CT, 4, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err, lmap, na);
         return la_wave_launch<CT, 1, 16, 64, 1, 4, 16>(s, a, G, n, c_old, E, err, lmap, na);
     }
     if (n <= 512) return la_wave_launch<CT, 1, 16, 32, 1, 8, 8>(s, a, G, n, c_old, E, err, lmap, na);
@@ -451,10 +452,10 @@ bool la_wave_ok(int n, int max_len, int n_active) {
 }
 
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
-                          int head, int32_t* err, const int32_t* lmap, int na) {
+                          int head, int32_t* err, const int32_t* lmap, int na, bool narrow) {
     if (nts > 1 && (G != 1 || c_old)) return hipErrorInvalidValue;
-    return a.compact ? la_wave_dispatch<uint16_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na)
-                     : la_wave_dispatch<int32_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na);
+    return a.compact ? la_wave_dispatch<uint16_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na, narrow)
+                     : la_wave_dispatch<int32_t>(s, a, G, n, c_old, E, nts, head, err, lmap, na, narrow);
 }
 
 }  // namespace hgx
