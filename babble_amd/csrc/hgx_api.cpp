@@ -241,6 +241,9 @@ hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capa
     c->order = std::vector<GraphOrder>(n_graphs);
     c->g_events.assign(n_graphs, 0);
     c->g_loaded.assign(n_graphs, 0);
+    // the order arena sized for the capacity up front (at most 64 MB pinned): growing it copies
+    // the whole order so far, a multi-millisecond outlier inside one FindOrder of the chunked schedule
+    (void)c->arena.reserve((size_t)std::min<int64_t>(capacity_events, (int64_t)1 << 24));
     ok(err);
     return c;
 }

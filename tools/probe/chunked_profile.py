@@ -44,3 +44,6 @@ for k, v in acc.items():
           f"  first-quarter {np.mean(v[:q]):.3f}  last-quarter {np.mean(v[-q:]):.3f}")
 for k, v in ph_acc.items():
     print(f"  device {k:10s} mean {np.mean(v):.3f} ms")
+tot = np.asarray(acc["total"])
+for w in np.argsort(-tot)[:5]:
+    print(f"  worst call {w + calls // 10}: " + " ".join(f"{k} {acc[k][w]:.3f}" for k in acc))
