@@ -1128,7 +1128,11 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
         seg_len[g] = mg;
         total += mg;
     }
-    if (total > 0 && !(pre && total == (int64_t)oh.m)) {   // (every received event is in a block: total == m)
+    if (pre && total != (int64_t)oh.m) {   // every received event is in exactly one block
+        set_err(err, HGX_ERR_INVALID, "hgx_find_order: block counts differ from the received events");
+        return HGX_ERR_INVALID;
+    }
+    if (total > 0 && !pre) {
         if (!c->arena.reserve(base_off + (size_t)total)) {
             set_err(err, HGX_ERR_CAPACITY, "hgx_find_order: out of pinned host memory");
             return HGX_ERR_CAPACITY;

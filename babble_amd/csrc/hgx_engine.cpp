@@ -1391,6 +1391,17 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
                          (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
                                                     : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
     }
+    // a large order (a full pass: 40 MB at c3) is written by k_finish_order straight into the
+    // pinned host arena (coalesced writes over the host link while the kernel runs) instead of a
+    // D2H copy after it; a small one comes back with the block tables in the copy launch
+    bool direct = false;
+    if (order_dst && (size_t)m * 4 > kCopyKernelMax) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, order_dst, 0) == hipSuccess && d) {
+            a.order_gid = (int32_t*)d;
+            direct = true;
+        }
+    }
     launch_finish_order(stream, a, m, vals, R, n);
     launch_fu_advance(stream, a, C);
     for (int c = 0; c < C; c++) h_fu[c] += fo_cnt[c];
@@ -1401,7 +1412,7 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
     HGX_TRY(stage_d2h(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8));
     HGX_TRY(stage_d2h(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4));
     HGX_TRY(stage_d2h(out.blk_nil.data(), blk_nil.p, (size_t)G * R));
-    if (order_dst) HGX_TRY(copy_to_pinned(order_dst, order_gid.p, (size_t)m * 4));
+    if (order_dst && !direct) HGX_TRY(copy_to_pinned(order_dst, order_gid.p, (size_t)m * 4));
     HGX_TRY(stage_issue());
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));
