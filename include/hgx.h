@@ -85,7 +85,9 @@ typedef struct {
 /* ---- lifecycle ------------------------------------------------------------ */
 int32_t hgx_abi_version(void);
 /* NewHashgraph(participants, store, ...) (hashgraph.go:39-66) with an InmemStore of
- * cacheSize >= capacity_events (no eviction). device = HIP device ordinal. */
+ * cacheSize >= capacity_events (no eviction). device = HIP device ordinal. The context pins
+ * 4 bytes of host memory per event of capacity (at most 64 MB up front, grown on demand) for
+ * the consensus order, which FindOrder writes there directly. */
 hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t device, hgx_error* err);
 /* n_graphs independent hashgraphs of n_participants each (seed-sharded simulations) */
 hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capacity_events,
