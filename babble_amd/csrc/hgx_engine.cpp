@@ -1032,7 +1032,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     };
     // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
-    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
+    // (nor does a rebuild of a DAG with fewer than 16 events per chain: the first sync of a run)
+    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild && En >= 16 * (int64_t)C)) &&
+        round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)
@@ -1279,7 +1281,12 @@ hipError_t Engine::find_order_begin(const std::vector<uint8_t>& el, const std::v
     HGX_TRY(stage_h2d(ur_empty.p, ure.data(), (size_t)G));
     HGX_TRY(stage_issue());
     if (WLAT.n < (size_t)R * C * n) {   // grown geometrically: R grows by a round or two per call
-        HGX_TRY(WLAT.alloc(std::max((size_t)R * C * n + (size_t)C * n, 2 * WLAT.n)));
+        // the first allocation covers the round tables' capacity (at most 256 M entries): each
+        // later doubling was a synchronous free + allocation inside one FindOrder of the chunked
+        // schedule (0.6-0.9 ms outliers)
+        const size_t want = (size_t)R * C * n + (size_t)C * n;
+        const size_t first = WLAT.n ? 0 : std::min((size_t)r_cap * C * n, (size_t)1 << 28);
+        HGX_TRY(WLAT.alloc(std::max(want, std::max(2 * WLAT.n, first))));
         a = arrays();
     }
     kbeg(K_THRESHOLD);

@@ -1,7 +1,7 @@
 """Probe: the SyncLimit-chunked schedule (Core.Sync + RunConsensus per 1 000 events) at a config's
 shape: host wall time per API call (insert, DivideRounds, DecideFame, FindOrder) and the device
 phase times, averaged over calls after a warm-up; optional kernel timing per call.
-Usage: python tools/probe/chunked_profile.py [cfg] [calls] [sync_limit]"""
+Usage: python tools/probe/chunked_profile.py [cfg] [calls] [sync_limit] [warm-up calls]"""
 import os
 import sys
 import time
@@ -15,6 +15,7 @@ from babble_amd.hashgraph import Hashgraph  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 calls = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
 sl = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+warm = int(sys.argv[4]) if len(sys.argv) > 4 else calls // 10
 n, E, G, *_ = bench.CONFIGS[cfg]
 tr, G = bench.make_trace(cfg, 0)
 h = Hashgraph(n, capacity=tr.E, device=0, n_graphs=G)
@@ -29,7 +30,7 @@ for c in range(calls):
     ph = h.phase_times()
     h.DecideFame(); t3 = time.perf_counter()
     h.FindOrder(); t4 = time.perf_counter()
-    if c >= calls // 10:
+    if c >= warm:
         for k, v in (("insert", t1 - t0), ("divide", t2 - t1), ("fame", t3 - t2), ("order", t4 - t3), ("total", t4 - t0)):
             acc[k].append(v * 1e3)
         for k in ("coords_ms", "rounds_ms"):
@@ -37,7 +38,7 @@ for c in range(calls):
         ph2 = h.phase_times()
         for k in ("fame_ms", "order_ms"):
             ph_acc.setdefault(k, []).append(ph2[k])
-print(f"{cfg}: {len(acc['total'])} calls of {sl} events (after {calls // 10} warm-up calls)")
+print(f"{cfg}: {len(acc['total'])} calls of {sl} events (after {warm} warm-up calls)")
 for k, v in acc.items():
     q = len(v) // 4
     print(f"  host {k:7s} mean {np.mean(v):.3f} ms  p50 {np.median(v):.3f}  max {np.max(v):.3f}"
@@ -46,4 +47,4 @@ for k, v in ph_acc.items():
     print(f"  device {k:10s} mean {np.mean(v):.3f} ms")
 tot = np.asarray(acc["total"])
 for w in np.argsort(-tot)[:5]:
-    print(f"  worst call {w + calls // 10}: " + " ".join(f"{k} {acc[k][w]:.3f}" for k in acc))
+    print(f"  worst call {w + warm}: " + " ".join(f"{k} {acc[k][w]:.3f}" for k in acc))
