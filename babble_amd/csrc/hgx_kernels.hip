@@ -1076,7 +1076,7 @@ __global__ void __launch_bounds__(256) k_cts_small(const int32_t* __restrict__ f
 // kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
 // do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
 // per event: radix select of element floor(m/2) in registers.
-constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8
+constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8 (round 2); 4: 13.4 vs 8.2 (round 3)
 template <int NPAD, typename CT>
 __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu, const int32_t* __restrict__ rcnt,
                                                   const int32_t* __restrict__ p_rr,
