@@ -1032,9 +1032,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     };
     // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
-    // (nor does a rebuild of a DAG with fewer than 16 events per chain: the first sync of a run)
-    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild && En >= 16 * (int64_t)C)) &&
-        round_p_ok(n, C, num_cus)) {
+    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)

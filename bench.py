@@ -351,9 +351,24 @@ def p256_leg(count, steps, warmup, device):
     res = p256_verify_bench(kb, kid, *cols, warmup=max(1, warmup), iters=steps, device=device)
     assert np.array_equal(res["out"], exp), "P-256 verify differs from libcrypto"
     ms = res["ms_per_launch"]
-    return {"kernel": "k_p256_verify", "signatures": count, "keys": len(keys), "ms_per_launch": ms,
-            "verifies_per_s": count / (ms * 1e-3), "valid_fraction": float((exp == 1).mean()),
-            "check": "bit-exact vs libcrypto 3.0.2 (ECDSA_do_verify)"}
+    out = {"kernel": "k_p256_verify", "signatures": count, "keys": len(keys), "ms_per_launch": ms,
+           "verifies_per_s": count / (ms * 1e-3), "valid_fraction": float((exp == 1).mean()),
+           "check": "bit-exact vs libcrypto 3.0.2 (ECDSA_do_verify)"}
+    # VALU issue roofline from the PMC pass of this leg (tools/gpurun/pmc_p256.sh: SQ_INSTS_VALU
+    # over the same 1 M-signature launch): wave instructions x 64 lanes per launch / this line's ms
+    vf = os.path.join(ROOT, "profiles", "valu_p256.json")
+    try:
+        vj = json.load(open(vf)).get("p256_verify") or {}
+        if vj.get("valu_insts_per_pass") and vj.get("dispatches") and count == (1 << 20):
+            per = vj["valu_insts_per_pass"] / vj["dispatches"]
+            ach = 64.0 * per / (ms * 1e-3) / 1e12
+            out["roofline"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                               "frac": ach / VALU_PEAK_TOPS, "valu_insts_per_launch": per,
+                               "lane_ops_per_verify": 64.0 * per / count,
+                               "source": "profiles/valu_p256.json (rocprofv3 --pmc SQ_INSTS_VALU, this leg's launch)"}
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def _valid_signature_pool():

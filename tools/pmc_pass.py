@@ -27,7 +27,10 @@ ROLES = {
     "threshold": r"k_threshold|k_wla_transpose",
     "round_received": r"k_round_received",
     "cts_median": r"k_cts",
-    "order_sort": r"k_radix|k_sort_small|k_tie|k_keys|k_scan|k_minmax|k_finish_order",
+    "order_sort": r"k_radix|k_sort_small|k_sort_rank|k_sort_place|k_tie|k_keys|k_scan|k_minmax|k_finish_order",
+    # ingest legs (bench.py p256_leg / ingest_leg; not in a consensus pass)
+    "p256_verify": r"k_p256_verify",
+    "sha256": r"k_sha256",
 }
 
 
