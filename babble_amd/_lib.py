@@ -73,6 +73,10 @@ def _one_hip_runtime():
         import torch  # noqa: F401  (loads torch's HIP runtime; no device is touched)
     except ImportError:
         pass
+    except Exception as e:  # installed but broken (e.g. an OSError from its ROCm libraries)
+        import warnings
+        warnings.warn(f"libhgx: importing torch failed ({type(e).__name__}: {e}); libhgx is loaded with its own "
+                      "HIP runtime, so a later torch import in this process is unsupported", RuntimeWarning)
 
 
 def lib():

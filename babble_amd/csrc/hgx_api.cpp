@@ -100,6 +100,8 @@ struct hgx_ctx {
     // while it stays the same the eligible rounds only shrink (see hgx_find_order_begin)
     std::vector<int32_t> fo_prev_u0;
     bool fo_prev_valid = false;
+    std::vector<int32_t> fo_pend_u0;   // set by hgx_find_order_begin, committed by _end
+    bool fo_pend_valid = false;
     std::vector<uint8_t> fo_elig, fo_fw;           // FindOrder's eligible rounds / famous witnesses
     std::vector<GraphState> gs;
     OrderArena arena;                        // consensus orders (gids) of all graphs
@@ -1085,11 +1087,14 @@ int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
         set_err(err, HGX_ERR_PANIC, "runtime error: index out of range [0] with length 0");
         return HGX_ERR_PANIC;
     }
-    c->fo_prev_u0.assign(G, -1);
-    c->fo_prev_valid = true;
+    // the skip rule's UndecidedRounds[0] of this FindOrder: pending until _end commits the
+    // order (an _end that fails leaves the skip rule off, so the next FindOrder redoes the work)
+    c->fo_prev_valid = false;
+    c->fo_pend_u0.assign(G, -1);
+    c->fo_pend_valid = true;
     for (int g = 0; g < G; g++) {
-        if (c->gs[g].undecided.empty()) c->fo_prev_valid = false;
-        else c->fo_prev_u0[(size_t)g] = c->gs[g].undecided[0];
+        if (c->gs[g].undecided.empty()) c->fo_pend_valid = false;
+        else c->fo_pend_u0[(size_t)g] = c->gs[g].undecided[0];
     }
     c->fo_open = true;
     return ok(err);
@@ -1176,6 +1181,9 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
         }
         s.undetermined -= mg;
     }
+    c->fo_prev_u0.swap(c->fo_pend_u0);   // the order is committed: the skip rule may use it
+    c->fo_prev_valid = c->fo_pend_valid;
+    c->fo_pend_valid = false;
     for (const auto& gb : commits) {   // commitCh <- block, in SetBlock order
         const Block& b = c->gs[gb.first].blocks[(size_t)gb.second];
         c->commit_fn(c->commit_user, gb.first, gb.second, b.rr, b.first, b.nev, b.ntx);

@@ -1025,6 +1025,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 // graphs that finished earlier: empty rows up to the last round (k_last_round,
                 // fame and the host copies read every graph's rows of every round)
                 launch_round_p_tail(stream, round_args(), fin, last);
+                kbeg(K_ROUND_GATHER);
+                launch_round_p_post(stream, round_args(), r_lo, last);
+                kend(K_ROUND_GATHER, (double)(last - r_lo + 1) * C * n * (sizeof(int32_t) + (compact ? 2 : 4)));
                 return hipGetLastError();
             }
             s = h_small[57];   // the round tables' capacity: continue from there

@@ -186,6 +186,9 @@ constexpr int kRoundPBufs = 4;   // candidate-row buffers of the persistent recu
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
                           int32_t* fin, int r0, int r_end, int init, int num_cus);
 void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, int r_last);
+// after the persistent launches: rounds of the events, wstat / wflag / active and the candidates'
+// WLA rows of rounds [r_lo, r_hi], from Bm (the persistent loop writes only Bm and the S rows)
+void launch_round_p_post(hipStream_t s, const RoundArgs& A, int r_lo, int r_hi);
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,

@@ -32,6 +32,9 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
@@ -49,9 +52,31 @@ constexpr uint32_t kRpEx = 1u << 31, kRpOv = 1u << 30, kRpBm = (1u << 30) - 1;
 // Optional phase clocks (-DHGX_STEP_PROF, build variant "prof"): thread 0 of each workgroup adds
 // s_memtime deltas per phase of every round, flushed once at the end of the launch.
 #ifdef HGX_STEP_PROF
-// slots: 0 rebase, 1 poll, 2 rows, 3 search, 4 boundary, 5 granule, 6 outputs, 7 staging wait,
-// 8 staging issue, 9 row build + stores; 15 = block-rounds
+// slots: 1 poll, 2 post-poll barrier + S row of the previous round, 13 search levels, 3 vm drain +
+// histogram barrier, 4 scan + later windows, 5 publish / next-window rebase / outputs / staging /
+// next poll issue;
+// 10 synchronous stagings, 11 later windows; 15 = block-rounds
 __device__ unsigned long long hgx_rp_prof[16];
+// per (round, chain) s_memrealtime stamps (100 MHz, low 32 bits) of wave 0 (thread 0) and of
+// wave 1 (thread 64): poll done, boundary known, publish issued (wave 0) / next window rebased
+// (wave 1), end of round; rounds < 4096, chains < 256
+constexpr int kRpTrR = 4096, kRpTrC = 256, kRpTrW = 8;
+__device__ uint32_t hgx_rp_trace[kRpTrR * kRpTrC * kRpTrW];
+// every wave's poll-done and end-of-round stamps for rounds [100, 164): [64][256][16][2]
+__device__ uint32_t hgx_rp_trace2[64 * 256 * 16 * 2];
+#define RP_TRACE_W(r, k)                                                                           \
+    do {                                                                                           \
+        if (lane == 0 && (r) >= 100 && (r) < 164 && gc < 256 && wave < 16)                        \
+            hgx_rp_trace2[((((r) - 100) * 256 + gc) * 16 + wave) * 2 + (k)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define RP_TRACE(k) const uint32_t _tr##k = (uint32_t)__builtin_amdgcn_s_memrealtime()
+#define RP_TRACE_STORE(r)                                                                        \
+    do {                                                                                         \
+        if ((threadIdx.x == 0 || threadIdx.x == 64) && (r) < kRpTrR && gc < kRpTrC) {            \
+            uint32_t* _p = hgx_rp_trace + ((size_t)(r) * kRpTrC + gc) * kRpTrW + (threadIdx.x ? 4 : 0); \
+            _p[0] = _tr0; _p[1] = _tr1; _p[2] = _tr2; _p[3] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+        }                                                                                        \
+    } while (0)
 #define RP_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[16] = {}
 #define RP_PROF(i)                                                \
     do {                                                          \
@@ -59,7 +84,7 @@ __device__ unsigned long long hgx_rp_prof[16];
             const long long _t = clock64();                       \
             _pa[i] += (unsigned long long)(_t - _pt);             \
             _pt = _t;                                             \
-            if ((i) == 6) _pa[15] += 1;                           \
+            if ((i) == 5) _pa[15] += 1;                           \
         }                                                         \
     } while (0)
 #define RP_PROF_COUNT(i)                                          \
@@ -76,16 +101,33 @@ void round_p_prof_dump() {
     unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
     const double r = h[15] ? (double)h[15] : 1.0;
-    fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): staging-wait %.0f barrier %.0f rebase %.0f poll %.0f "
-            "rows %.0f search-levels %.0f search-barrier %.0f boundary %.0f staging-issue %.0f row-build %.0f granule %.0f "
-            "outputs %.0f | block-rounds %llu, synchronous stagings %llu, later windows %llu\n",
-            h[7] / r, h[12] / r, h[0] / r, h[1] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r,
-            h[6] / r, h[15], h[10], h[11]);
+    fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): poll %.0f barrier %.0f search-levels %.0f "
+            "drain+barrier %.0f scan %.0f publish..poll-issue %.0f | block-rounds %llu, synchronous stagings %llu, "
+            "later windows %llu\n",
+            h[1] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[5] / r, h[15], h[10], h[11]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
+    if (const char* path = getenv("HGX_RP_TRACE_FILE")) {
+        std::vector<uint32_t> tr((size_t)kRpTrR * kRpTrC * kRpTrW);
+        if (hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(hgx_rp_trace), tr.size() * 4) == hipSuccess) {
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(tr.data(), 4, tr.size(), f);
+                fclose(f);
+            }
+            std::vector<uint32_t> t2((size_t)64 * 256 * 16 * 2);
+            if (hipMemcpyFromSymbol(t2.data(), HIP_SYMBOL(hgx_rp_trace2), t2.size() * 4) == hipSuccess)
+                if (FILE* f = fopen((std::string(path) + ".waves").c_str(), "wb")) {
+                    fwrite(t2.data(), 4, t2.size(), f);
+                    fclose(f);
+                }
+        }
+    }
 }
 #else
 #define RP_PROF_BEGIN() (void)0
+#define RP_TRACE(k) (void)0
+#define RP_TRACE_STORE(r) (void)0
+#define RP_TRACE_W(r, k) (void)0
 #define RP_PROF(i) (void)0
 #define RP_PROF_END() (void)0
 #define RP_PROF_COUNT(i) (void)0
@@ -108,53 +150,133 @@ __device__ __forceinline__ uint32_t rp_ld_abort(const int32_t* p) {
 __device__ __forceinline__ void rp_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void rp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// HD dwords of this lane's part of a candidate row, sc1 loads (every load of handed-off bytes)
+// A candidate's granule and this lane's HD dwords of its row, sc1 loads (every load of handed-off
+// bytes), issued AND waited for in ONE asm statement: an asm load's destination registers are
+// written when the data returns, so a load left in flight across compiler-visible code lets the
+// register allocator copy (or reuse) them before the data lands.
 template <int HD>
-__device__ __forceinline__ void rp_ld_row(const uint32_t* p, uint32_t (&v)[HD]) {
-    if constexpr (HD >= 4) {
+__device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p, uint64_t& gv, uint32_t (&v)[HD]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (HD == 16) {
+        u32x4 a, b, c, d;
+#ifdef HGX_EXP_DBLPOLL
+        u32x4 e2, f2, g2, h2;   // experiment: every row load issued twice (twice the hand-off traffic)
+        asm volatile(
+            "global_load_dwordx4 %0, %4, off sc1\n\t"
+            "global_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
+            "global_load_dwordx4 %2, %4, off offset:32 sc1\n\t"
+            "global_load_dwordx4 %3, %4, off offset:48 sc1\n\t"
+            : "=&v"(e2), "=&v"(f2), "=&v"(g2), "=&v"(h2) : "v"(p) : "memory");
+#endif
+        asm volatile(
+            "global_load_dwordx2 %0, %5, off sc1\n\t"
+            "global_load_dwordx4 %1, %6, off sc1\n\t"
+            "global_load_dwordx4 %2, %6, off offset:16 sc1\n\t"
+            "global_load_dwordx4 %3, %6, off offset:32 sc1\n\t"
+            "global_load_dwordx4 %4, %6, off offset:48 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(p) : "memory");
+        const u32x4 q4[4] = {a, b, c, d};
 #pragma unroll
-        for (int k = 0; k < HD / 4; k++) {
-            uint4 x;
-            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(x) : "v"(p + 4 * k) : "memory");
-            v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
-        }
-    } else if constexpr (HD == 2) {
-        uint2 x;
-        asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(x) : "v"(p) : "memory");
-        v[0] = x.x; v[1] = x.y;
+        for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
+#ifdef HGX_EXP_DBLPOLL
+        asm volatile("" :: "v"(e2), "v"(f2), "v"(g2), "v"(h2));   // (landed: the asm above waited)
+#endif
+    } else if constexpr (HD == 8) {
+        u32x4 a, b;
+        asm volatile(
+            "global_load_dwordx2 %0, %3, off sc1\n\t"
+            "global_load_dwordx4 %1, %4, off sc1\n\t"
+            "global_load_dwordx4 %2, %4, off offset:16 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(gv), "=&v"(a), "=&v"(b) : "v"(gp), "v"(p) : "memory");
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else if constexpr (HD == 4) {
+        u32x4 a;
+        asm volatile(
+            "global_load_dwordx2 %0, %2, off sc1\n\t"
+            "global_load_dwordx4 %1, %3, off sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(gv), "=&v"(a) : "v"(gp), "v"(p) : "memory");
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     } else {
+        static_assert(HD == 1, "rp_ld_cand: HD in {1, 4, 8, 16}");
         uint32_t x;
-        asm volatile("global_load_dword %0, %1, off sc1" : "=v"(x) : "v"(p) : "memory");
+        asm volatile(
+            "global_load_dwordx2 %0, %2, off sc1\n\t"
+            "global_load_dword %1, %3, off sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(gv), "=&v"(x) : "v"(gp), "v"(p) : "memory");
         v[0] = x;
     }
 }
 
-// HD dwords of an LDS row, all reads in flight before one wait (16-byte reads when HD % 4 == 0)
+// the granule alone / the row part alone (each load and its wait in one asm statement)
+__device__ __forceinline__ uint64_t rp_ld_gran_w(const uint64_t* gp) {
+    uint64_t gv;
+    asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(gv) : "v"(gp) : "memory");
+    return gv;
+}
+template <int HD>
+__device__ __forceinline__ void rp_ld_row_w(const uint32_t* p, uint32_t (&v)[HD]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (HD == 16) {
+        u32x4 a, b, c, d;
+        asm volatile(
+            "global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
+            "global_load_dwordx4 %2, %4, off offset:32 sc1\n\tglobal_load_dwordx4 %3, %4, off offset:48 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(p) : "memory");
+        const u32x4 q4[4] = {a, b, c, d};
+#pragma unroll
+        for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
+    } else if constexpr (HD == 8) {
+        u32x4 a, b;
+        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:16 sc1\n\ts_waitcnt vmcnt(0)"
+                     : "=&v"(a), "=&v"(b) : "v"(p) : "memory");
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else if constexpr (HD == 4) {
+        u32x4 a;
+        asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(a) : "v"(p) : "memory");
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else {
+        uint32_t x;
+        asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(x) : "v"(p) : "memory");
+        v[0] = x;
+    }
+}
+
+// HD dwords of an LDS row: every read and its wait in one asm statement (16-byte reads when
+// HD % 4 == 0)
 template <int HD>
 __device__ __forceinline__ void rp_lds_row(const uint32_t* p, uint32_t (&v)[HD]) {
     const uint32_t a = (uint32_t)(uintptr_t)p;
-    if constexpr (HD % 4 == 0) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        u32x4 r[HD / 4];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (HD == 16) {
+        u32x4 r0, r1, r2, r3;
+        asm volatile(
+            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\t"
+            "ds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(a) : "memory");
+        const u32x4 q4[4] = {r0, r1, r2, r3};
 #pragma unroll
-        for (int k = 0; k < HD / 4; k++) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[k]) : "v"(a), "i"(16 * k));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int k = 0; k < HD / 4; k++) {
-            asm volatile("" : "+v"(r[k]));
-            v[4 * k] = r[k].x; v[4 * k + 1] = r[k].y; v[4 * k + 2] = r[k].z; v[4 * k + 3] = r[k].w;
-        }
+        for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
+    } else if constexpr (HD == 8) {
+        u32x4 r0, r1;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(r0), "=&v"(r1) : "v"(a) : "memory");
+        v[0] = r0.x; v[1] = r0.y; v[2] = r0.z; v[3] = r0.w; v[4] = r1.x; v[5] = r1.y; v[6] = r1.z; v[7] = r1.w;
+    } else if constexpr (HD == 4) {
+        u32x4 r0;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r0) : "v"(a) : "memory");
+        v[0] = r0.x; v[1] = r0.y; v[2] = r0.z; v[3] = r0.w;
     } else if constexpr (HD == 2) {
         uint64_t r;
-        asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(a));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(r));
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r) : "v"(a) : "memory");
         v[0] = (uint32_t)r; v[1] = (uint32_t)(r >> 32);
     } else {
         uint32_t r;
-        asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(a));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(r));
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r) : "v"(a) : "memory");
         v[0] = r;
     }
 }
@@ -194,22 +316,24 @@ struct RpCfg {
     static constexpr int SEG = 64 / CSZ, NSEG = 4, RR = SEG * NSEG;
     static constexpr int SEG_RAW = SEG * NC * CSZ;               // bytes: raw lastAncestors rows of a segment
     static constexpr int KR16 = (SEG_RAW / 16 + T - 1) / T;      // 16-byte DMA per lane per segment
-    static constexpr int CW = 16;                                // dwords per staged FD column (SEG positions)
-    static constexpr int CPI = 4;                                // FD columns per DMA instruction (a group)
-    static constexpr int KF = (NDW + NW - 1) / NW;               // groups per wave per segment
-    static constexpr int SEG_FD = NDW * 65 * 4;                  // bytes: groups of 64 dwords + 1 pad
+    // firstDescendants columns: one 16-byte DMA instruction = 16 columns x 64 bytes (lane k:
+    // column k / 4, 16-byte chunk k % 4), groups FDG = 1040 bytes apart (16-byte pad: the 16
+    // groups start on different banks)
+    static constexpr int FDG = 1040;
+    static constexpr int NG = (NC + 15) / 16;                    // column groups of a segment
+    static constexpr int KF = (NG + NW - 1) / NW;                // groups per wave per segment
+    static constexpr int SEG_FD = NG * FDG;                      // bytes
     // LDS carve (bytes, 16-aligned)
     static constexpr int O_WIN = 0;
     static constexpr int O_RAW = O_WIN + ((kRpP * WS * 4 + 15) & ~15);   // [RR][n] raw rows
-    static constexpr int O_FD = O_RAW + NSEG * SEG_RAW;                   // [NSEG][NDW groups][65]
+    static constexpr int O_FD = O_RAW + NSEG * SEG_RAW;                   // [NSEG][NG groups][FDG]
     static constexpr int O_CB = O_FD + NSEG * SEG_FD;                     // c_base[NC]
     static constexpr int O_CO = O_CB + NC * 4;                           // c_off[NC]
-    static constexpr int O_BM0 = O_CO + NC * 4;                          // Bm of the candidates, by round parity
-    static constexpr int O_BM1 = O_BM0 + NC * 4;
-    static constexpr int O_HIST = O_BM1 + NC * 4;                        // 32 bins
-    static constexpr int SBW = (NC / 32 + 4 + 3) & ~3;                   // S row words per buffer
-    static constexpr int O_SB = O_HIST + 32 * 4;                         // S row bits [2][SBW], by round parity
-    static constexpr int O_MISC = O_SB + 2 * SBW * 4;                    // [0] B, [1] tot, [2] any, [3] fail
+    static constexpr int O_BS0 = O_CO + NC * 4;                          // bases c_base + Bm[r], by round parity
+    static constexpr int O_BS1 = O_BS0 + NC * 4;
+    static constexpr int O_HIST = O_BS1 + NC * 4;                        // [2][32] bins, by round parity
+    static constexpr int O_SL = O_HIST + 2 * 32 * 4;                     // S row slices [2][NW] u64, by round parity
+    static constexpr int O_MISC = O_SL + 2 * NW * 8;                     // [2][8] by parity: [2] any, [3] fail
     static constexpr int USED = O_MISC + 64;
     // at least 82 KB: one workgroup per CU (the hand-off rule's geometry), whatever fits
     static constexpr int LDS = USED > 84 * 1024 ? USED : 84 * 1024;
@@ -228,10 +352,20 @@ struct RoundPArgs {
     long long tmo;      // one wait's budget in s_memrealtime ticks (100 MHz)
 };
 
+// One round s of chain c, in the order of its critical path:
+//  (a) poll: every lane waits for its candidate's granule and row part (W'_s, published by the
+//      other chains in round s - 1), writes base(s+1)[j] = c_base[j] + Bm[s][j];
+//  (b) the outputs of round s - 1 (plain stores) and the staging ring ahead (LDS-DMA) are issued
+//      behind the poll: they land during the search, nothing waits for them until (d);
+//  (c) search of the window [b, b + 31), rebased to base(s) in round s - 1;
+//  (d) K(w) histogram, one barrier, every wave scans it (the boundary B, no second barrier);
+//  (e) wave 0 publishes W'_{s+1} of chain c (row rebased to base(s+1), granule) at once, while the
+//      other waves rebase the next window [kstar, kstar + 31) to base(s+1); one barrier; the poll
+//      loads of round s + 1 go out.
 template <typename CT, int NDW, int Q>
 __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round_p(RoundPArgs P) {
     typedef RpCfg<CT, NDW, Q> K;
-    constexpr int HD = K::HD, T = K::T, WS = K::WS;
+    constexpr int HD = K::HD, T = K::T, WS = K::WS, NW = K::NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const RoundArgs& A = P.A;
     const int n = A.n, C = A.C, sm = A.sm;
@@ -242,18 +376,21 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     uint32_t* win = (uint32_t*)(lds + K::O_WIN);
     int32_t* cbase = (int32_t*)(lds + K::O_CB);
     int32_t* coff = (int32_t*)(lds + K::O_CO);
-    int32_t* hist = (int32_t*)(lds + K::O_HIST);
-    uint32_t* sbits_all = (uint32_t*)(lds + K::O_SB);
-    int32_t* misc = (int32_t*)(lds + K::O_MISC);
+    auto bases = [&](int r) { return (int32_t*)(lds + ((r & 1) ? K::O_BS1 : K::O_BS0)); };   // c_base + Bm[r]
+    auto hist_of = [&](int r) { return (int32_t*)(lds + K::O_HIST) + (r & 1) * 32; };
+    auto misc_of = [&](int r) { return (int32_t*)(lds + K::O_MISC) + (r & 1) * 8; };
 
     if (P.fin[g] >= 0) return;   // the graph finished in an earlier launch of this DivideRounds
     const int len = A.c_len[gc], off = A.c_off[gc];
     for (int i = t; i < n; i += T) {
-        cbase[i] = A.c_base[g0 + i];
+        const int32_t cb = A.c_base[g0 + i];
+        cbase[i] = cb;
         coff[i] = A.c_off[g0 + i];
-        // Bm of round r0 - 1 (bases of round r0's window), written by earlier launches
-        ((int32_t*)(lds + (((P.r0 - 1) & 1) ? K::O_BM1 : K::O_BM0)))[i] = P.r0 > 0 ? A.Bm[(size_t)(P.r0 - 1) * C + g0 + i] : 0;
+        // bases of round r0's window: c_base + Bm[r0 - 1], written by earlier launches
+        bases(P.r0 - 1)[i] = cb + (P.r0 > 0 ? A.Bm[(size_t)(P.r0 - 1) * C + g0 + i] : 0);
     }
+    if (t < 64) hist_of(0)[t] = 0;
+    if (t < 16) misc_of(t >> 3)[t & 7] = 0;
     int b = A.Bm[(size_t)P.r0 * C + gc];
 
     // ---- staging ring (LDS-DMA, fixed instruction counts per wave): segment m = the raw
@@ -267,24 +404,27 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     auto stage_seg = [&](int m) {
         const int slot = m % NSEG;
         const uint32_t* __restrict__ src = (const uint32_t*)((const uint8_t*)A.LA + ((size_t)off + (size_t)m * SEG) * n * K::CSZ);
-        uint32_t* raw_w = (uint32_t*)(lds + K::O_RAW + slot * SEG * n * K::CSZ);   // rows (p % RR) * n
+        const int raw_w = K::O_RAW + slot * SEG * n * K::CSZ;   // rows (p % RR) * n
         const int nch = SEG * n * K::CSZ / 16;   // 16-byte chunks
 #pragma unroll
         for (int k = 0; k < K::KR16; k++) {
             const int c0 = wave * 64 + k * T;    // this wave instruction's first chunk
             if (c0 + lane < nch)
-                __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c0 + lane)), (lds_ptr_t)(raw_w + 4 * c0), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c0 + lane)), (lds_ptr_t)(lds + raw_w + 16 * c0), 16, 0, 0);
         }
-        // columns: lane = (column % 4, dword); one instruction = one group of 4 columns
-        const int icol = lane >> 4, pcol = lane & 15;
-        const uint32_t* __restrict__ fsrc = (const uint32_t*)((const uint8_t*)A.FDT + ((size_t)off + (size_t)m * SEG) * K::CSZ) + pcol;
-        const size_t cstride = (size_t)A.Pcap * K::CSZ / 4;   // dwords between columns
-        uint32_t* fd_w = (uint32_t*)(lds + K::O_FD + slot * K::SEG_FD);
+        // columns: lane = (column % 16 via lane / 4, 16-byte chunk lane % 4); one instruction =
+        // one group of 16 columns
+        const int icol = lane >> 2, pch = lane & 3;
+        const uint8_t* __restrict__ fsrc = (const uint8_t*)A.FDT + ((size_t)off + (size_t)m * SEG) * K::CSZ + pch * 16;
+        const size_t cstride = (size_t)A.Pcap * K::CSZ;   // bytes between columns
+        const int fd_w = K::O_FD + slot * K::SEG_FD;
 #pragma unroll
         for (int k = 0; k < K::KF; k++) {
-            const int grp = min(wave + k * K::NW, NDW - 1);
-            const int i = min(grp * 4 + icol, n - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride), (lds_ptr_t)(fd_w + grp * 65), 4, 0, 0);
+            const int grp = wave + k * NW;
+            if (grp < K::NG) {
+                const int i = min(grp * 16 + icol, n - 1);
+                __builtin_amdgcn_global_load_lds((const void*)(fsrc + (size_t)i * cstride), (lds_ptr_t)(lds + fd_w + grp * K::FDG), 16, 0, 0);
+            }
         }
     };
     // segments [max(seg_hi + 1, lo), hi] (hi <= lo + NSEG - 1: a slot is reused only when its
@@ -295,21 +435,22 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     };
     auto fd_at = [&](int i, int p) -> CT {   // staged FD of coordinate i at chain offset p
         const uint8_t* fd_w = lds + K::O_FD + ((p / SEG) % NSEG) * K::SEG_FD;
-        return *(const CT*)(fd_w + ((i >> 2) * 65 + (i & 3) * 16) * 4 + (p % SEG) * K::CSZ);
+        return *(const CT*)(fd_w + (i >> 4) * K::FDG + (i & 15) * 64 + (p % SEG) * K::CSZ);
     };
     auto raw_at = [&](int p, int i) -> CT {   // staged lastAncestors row of chain offset p
         return ((const CT*)(lds + K::O_RAW))[(p % RR) * n + i];
     };
-    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the window [kb, kb + np)
+    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the window [kb, kb + np),
+    // by threads [0, nthr) (tid = this thread's), bases bq = c_base + Bm of the previous round
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    auto rebase = [&](int kb, int np, const int32_t* bmp) {
-        constexpr int RS = T / NDW > 0 ? T / NDW : 1;   // rows per pass
-        for (int d = t % NDW; d < NDW; d += T) {
+    auto rebase = [&](int kb, int np, const int32_t* bsp, int tid, int nthr) {
+        const int RS = nthr / NDW > 0 ? nthr / NDW : 1;   // rows per pass
+        for (int d = tid % NDW; d < NDW && tid < RS * NDW; d += nthr) {
             const int i0 = 4 * d;
             int32_t bq[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) bq[u] = (i0 + u < n) ? cbase[i0 + u] + bmp[i0 + u] : 0;
-            for (int p = t / NDW; p < np; p += RS) {
+            for (int u = 0; u < 4; u++) bq[u] = (i0 + u < n) ? bsp[i0 + u] : 0;
+            for (int p = tid / NDW; p < np; p += RS) {
                 uint32_t w;
                 if constexpr (K::CSZ == 2) {
                     const uint32_t* rp = (const uint32_t*)(lds + K::O_RAW) + (((kb + p) % RR) * n + i0) / 2;
@@ -336,105 +477,103 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
     };
 
-    // round r's outputs (the per-launch step writes the same): rounds of the chain's events
-    // [o_b, o_kstar), wstat / wflag / Bm, the new candidate's WLA / WFD rows (its segment stays
-    // staged: o_kstar is the next window's start) and its S row (sbits buffer r & 1)
-    int o_b = 0, o_kstar = 0;
-    auto outputs = [&](int r, int tid, int nthr) {   // by threads [0, nthr) (tid = this thread's)
-        const bool o_have = o_b < len, o_nx = o_kstar < len;
-        for (int k = o_b + tid; k < o_kstar; k += nthr) A.p_round[off + k] = r;
-        if (tid == 0) {
-            A.wstat[(size_t)r * C + gc] = o_have ? ((o_kstar > o_b) ? 2 : 1) : 0;
-            A.wflag[(size_t)(r + 1) * C + gc] = o_nx ? 1 : 0;
-            A.Bm[(size_t)(r + 1) * C + gc] = o_kstar;
-            if (o_nx) A.active[r] = 1;
-        }
-        if (o_nx) {
-            const size_t nrow = ((size_t)(r + 1) * C + gc) * n;
-            for (int i = tid; i < n; i += nthr) {
-                A.WLA[nrow + i] = Coord<CT>::la(raw_at(o_kstar, i));
-                const CT f = fd_at(i, o_kstar);
-                if constexpr (K::CSZ == 2) ((uint16_t*)A.WFD)[nrow + i] = f;
-                else A.WFD[nrow + i] = f;
-            }
-            const uint32_t* sb = sbits_all + (r & 1) * K::SBW;
-            const size_t srow = ((size_t)(r + 1) * C + gc) * A.nw;
-            for (int wd = tid; wd < A.nw; wd += nthr)
-                A.Smat[srow + wd] = (uint64_t)sb[2 * wd] | ((2 * wd + 1 < K::NC / 32 + 1 ? (uint64_t)sb[2 * wd + 1] : 0) << 32);
+    // Round r's outputs: only Bm[r + 1] (the chain's next boundary) and the new candidate's S row
+    // are written in the loop, by wave 0 behind round r + 1's poll (a wave's vm counter is in
+    // order: stores before a poll hold its loads back). The rest (rounds of the chain's events,
+    // wstat / wflag / active, the candidates' WLA rows) follows from Bm alone and is written after
+    // the launch by k_round_p_post, coalesced.
+    // round r's S row from the waves' slices (LDS buffer r & 1) and its Bm, by wave 0 after the
+    // barrier that follows them
+    constexpr int CPW = 64 / Q;   // candidates per wave
+    auto s_row = [&](int r, int kst) {
+        if (lane == 0) A.Bm[(size_t)(r + 1) * C + gc] = kst;
+        if (kst >= len) return;   // no new candidate: no S row
+        const uint64_t* sl = (const uint64_t*)(lds + K::O_SL) + (r & 1) * NW;
+        constexpr int WPW = 64 / CPW;   // waves per 64-bit word
+        if (lane < A.nw) {
+            uint64_t w = 0;
+#pragma unroll
+            for (int k = 0; k < WPW; k++)
+                if (lane * WPW + k < NW) w |= sl[lane * WPW + k] << (k * CPW);
+            A.Smat[((size_t)(r + 1) * C + gc) * A.nw + lane] = w;
         }
     };
     RP_PROF_BEGIN();
+    // prologue: round r0's window staged and rebased to base(r0) = c_base + Bm[r0 - 1]
+    if (b < len) stage_range(b / SEG, min(b / SEG + NSEG - 1, last_seg));
+    rp_vm_drain();
+    rp_lds_barrier();
+    if (b < len) rebase(b, min(kRpP, len - b), bases(P.r0 - 1), t, T);
+    // the first poll's loads (each round issues the next round's)
+    auto gran_at = [&](int r) { return P.gran + (size_t)(r % kRpSlots) * C + g0 + (jv ? j : 0); };
+    auto row_at = [&](int r) { return P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD; };
     int s = P.r0;
     bool failed = false;
+    int s_r = -1, s_k = 0;   // the round whose Bm / S row is still to be written (by wave 0, after the next barrier)
     for (;; s++) {
         if (s >= P.r_end) break;   // capacity: the host continues from round s
-        const int32_t* bm_prev = (const int32_t*)(lds + (((s - 1) & 1) ? K::O_BM1 : K::O_BM0));
-        int32_t* bm_cur = (int32_t*)(lds + ((s & 1) ? K::O_BM1 : K::O_BM0));
+        int32_t* hist = hist_of(s);
+        int32_t* misc = misc_of(s);
         const bool have = b < len;   // block-uniform
         int kb = b, np = have ? min(kRpP, len - b) : 0;
-        // (a) the first load of this lane's candidate granule and row part (W'_s) goes out first
-        // and is in flight while this round's window (staged at the end of the previous round,
-        // before these loads) lands and is rebased to base(s). Every lane issues them (a clamped
-        // address for the lanes past n), so the vmcnt below covers exactly the staging.
-        const uint64_t* gp = P.gran + (size_t)(s % kRpSlots) * C + g0 + (jv ? j : 0);
-        const uint32_t* rowp = P.FD8p + ((size_t)(s & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD;
-        const uint32_t vbit = ((s >> 2) & 1) ? 0x80808080u : 0u;
-        uint64_t gv = rp_ld_gran(gp);
-        uint32_t fd[HD];
-        rp_ld_row<HD>(rowp, fd);
-        // No wait here: the window's segments were staged two rounds ago or earlier, and every
-        // wave's poll drain of the previous round waited for them (the end-of-round barrier then
-        // covers every wave). Waiting here would also wait for the previous round's stores.
-        uint32_t* sbits = sbits_all + (s & 1) * K::SBW;
-        if (have && min((b + kRpP - 1) / SEG, last_seg) > seg_hi) {
-            // the window is not staged yet (the first round of a launch, or a chain that advanced
-            // by more than the ring's lookahead): stage it now and wait for it
-            stage_range(b / SEG, min(b / SEG + NSEG - 1, last_seg));
-            rp_vm_drain();
-            RP_PROF_COUNT(10);
-        }
-        RP_PROF(7);
-        if (t < 32) hist[t] = 0;
-        if (t == 0) { misc[2] = 0; misc[3] = 0; }
-        if (t < K::NC / 32 + 1) sbits[t] = 0;
-        rp_lds_barrier();
-        RP_PROF(12);
-        if (have) rebase(b, np, bm_prev);
-        rp_lds_barrier();
-        RP_PROF(0);
 
-        // (b) until every candidate of this wave is published: its granule carries tag s + 1 and,
-        // when the candidate exists, every byte of its row part carries v(s); reload otherwise
+        // (a) this lane's candidate granule and row part (W'_s): reload until the granule carries
+        // tag s + 1 and, when the candidate exists, every byte of the row part carries v(s)
+        const uint32_t vbit = ((s >> 2) & 1) ? 0x80808080u : 0u;
         bool wfail = false;
+        uint64_t gv;
+        uint32_t fd[HD];
         {
+            const uint64_t* gp = gran_at(s);
+            const uint32_t* rowp = row_at(s);
             const long long tw = __builtin_amdgcn_s_memrealtime();
+#ifdef HGX_EXP_GPOLL
+            // granule first: a lane reloads only its granule until the tag matches, then its row part
+            // once (again only if a byte still lacks v(s)): stale rows are not fetched over and over
+            bool gok = false, rok = false;
             for (int spins = 0;; spins++) {
-                rp_vm_drain();
+                if (spins == 0) rp_ld_cand<HD>(gp, rowp, gv, fd);
+                else if (!gok) gv = rp_ld_gran_w(gp);
+                else if (!rok) rp_ld_row_w<HD>(rowp, fd);
+                uint32_t bad = 0;
 #pragma unroll
-                for (int d = 0; d < HD; d++) asm volatile("" : "+v"(fd[d]));
+                for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
+                gok = !jv || (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
+                rok = !jv || (gok && (!((uint32_t)gv & kRpEx) || bad == 0));
+                if (__all(gok && rok)) break;
+                if ((spins & 31) == 31) {
+                    const long long now = __builtin_amdgcn_s_memrealtime();
+                    if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+#else
+            bool ok = false;
+            for (int spins = 0;; spins++) {
+                if (!ok) rp_ld_cand<HD>(gp, rowp, gv, fd);   // (a lane whose candidate is complete keeps it)
                 uint32_t bad = 0;
 #pragma unroll
                 for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
                 const bool tag_ok = (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
-                const bool ok = !jv || (tag_ok && (!((uint32_t)gv & kRpEx) || bad == 0));
+                ok = !jv || (tag_ok && (!((uint32_t)gv & kRpEx) || bad == 0));
                 if (__all(ok)) break;
                 if ((spins & 31) == 31) {
                     const long long now = __builtin_amdgcn_s_memrealtime();
                     if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);
-                if (!ok) {
-                    gv = rp_ld_gran(gp);
-                    rp_ld_row<HD>(rowp, fd);
-                }
             }
         }
+#endif
         RP_PROF(1);
+        RP_TRACE(0);
+        RP_TRACE_W(s, 0);
         const uint32_t gval = (uint32_t)gv;
         const bool cand = jv && !wfail && (gval & kRpEx);
         const bool ov = cand && (gval & kRpOv);
         const int bmj = (int)(gval & kRpBm);
-        if (jv && q == 0 && !wfail) bm_cur[j] = bmj;
+        if (jv && q == 0 && !wfail) bases(s)[j] = cbase[j] + bmj;   // base(s + 1)[j]
         if (cand && have) {
 #pragma unroll
             for (int d = 0; d < HD; d++) fd[d] &= 0x7F7F7F7Fu;   // the validity bits off: rebased values
@@ -444,17 +583,29 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
         if (wfail && lane == 0) misc[3] = 1;
         if (cand && q == 0) misc[2] = 1;   // (same value from every writer)
-        // the ring ahead: segments up to b / SEG + NSEG - 1, landing behind the search, the
-        // publish and the outputs (the next round's first wait covers them; a window after a
-        // first-window boundary lies below b / SEG + 3)
+        rp_lds_barrier();   // this window's rebase (round s - 1's other waves) is complete
+        // round s + 1's histogram and flags start empty: their buffers were last read in round
+        // s - 1 (before this barrier) and are next written in round s + 1's poll (after round s's
+        // histogram barrier)
+        if (t >= T - 32) hist_of(s + 1)[t - (T - 32)] = 0;
+        if (t < 8) misc_of(s + 1)[t] = 0;
+        if (s_r >= 0) {   // round s - 1's S row: every wave set its slice before this barrier
+            if (wave == 0) s_row(s_r, s_k);
+            s_r = -1;
+        }
+        // the ring ahead (segments up to b / SEG + NSEG - 1), behind the poll (a wave's loads return
+        // in order: staging issued before the poll would hold it back) and behind the LDS writes
+        // above (the compiler waits for an LDS-DMA before the next LDS access it cannot tell
+        // apart); it lands during the search, and the histogram wait covers it before the next
+        // window's rebase reads it
         if (have) stage_range(b / SEG, min(b / SEG + NSEG - 1, last_seg));
         RP_PROF(2);
 
         // (c) search, window after window until the boundary is found (a later window is rare)
         int kstar = len, B = -1, K_last = kRpP, carried = 0;
-        bool done = false;
+        bool done = false, any = false;
         const bool wave_cand = __any(cand) && have;
-        for (; have;) {
+        for (;;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
 #pragma unroll 1
@@ -484,90 +635,119 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             const int Kw = lo;
             RP_PROF(13);
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
+            // (d) the histogram is complete (and the staging issued in round s - 1 has landed: the
+            // next window's rebase reads it); every wave scans it (the boundary: first probe where
+            // #{K <= p} (+ seen in earlier windows) >= SM)
+            rp_vm_drain();
             rp_lds_barrier();
             RP_PROF(3);
-            if (wave == 0) {   // boundary: first probe where #{K <= p} (+ seen in earlier windows) >= SM
+            int tot;
+            {
                 const uint32_t v = lane < np ? (uint32_t)hist[lane] : 0u;
                 const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried;
                 const uint64_t m = __ballot(lane < np && (int)inc >= sm);
-                const int tot = __builtin_amdgcn_readlane((int)inc, 63);
-                if (lane == 0) { misc[0] = m ? (int)__builtin_ctzll(m) : -1; misc[1] = tot; }
+                tot = __builtin_amdgcn_readlane((int)inc, 63);
+                B = m ? (int)__builtin_ctzll(m) : -1;
             }
-            rp_lds_barrier();
-            B = misc[0];
+            any = misc[2] != 0;
             K_last = Kw;
-            if (B >= 0 || misc[2] == 0 || misc[3] != 0) {
+            if (B >= 0 || !any || misc[3] != 0 || !have) {
                 if (B >= 0) kstar = kb + B;
                 break;
             }
             // no boundary in this window: the next one (synchronous staging)
             RP_PROF_COUNT(11);
-            carried = misc[1];
+            carried = tot;
             if (cand && Kw < np) done = true;
             kb += np;
             if (kb >= len) break;
             np = min(kRpP, len - kb);
+            rp_lds_barrier();   // every wave has scanned the histogram
             if (t < 32) hist[t] = 0;
             if (min((kb + kRpP - 1) / SEG, last_seg) > seg_hi) stage_range(kb / SEG, min(kb / SEG + NSEG - 1, last_seg));
             rp_vm_drain();
-            __syncthreads();
-            rebase(kb, np, bm_prev);
+            rp_lds_barrier();
+            rebase(kb, np, bases(s - 1), t, T);
             rp_lds_barrier();
         }
-        if (!have) rp_lds_barrier();   // the pollers' any / fail words
         RP_PROF(4);
+        RP_TRACE(1);
         if (misc[3] != 0) { failed = true; break; }
-        if (misc[2] == 0) break;       // W'_s is empty: no round s (every workgroup of the graph agrees)
+        if (!any) break;       // W'_s is empty: no round s (every workgroup of the graph agrees)
 
-        // (d) wave 0 publishes W'_{s+1} of chain c: its rebased row (base(s+1) = c_base + Bm[s],
-        // bit 7 of every byte = v(s + 1)) and its granule, written through with no drain in between
-        // (both self-validating)
+        // (e) wave 0 publishes W'_{s+1} of chain c at once: its row rebased to base(s+1) =
+        // c_base + Bm[s] (bit 7 of every byte = v(s + 1)) and its granule, written through with no
+        // drain in between (both self-validating); the other waves rebase the next window to the
+        // same bases and write round s's outputs; then every wave stages the ring ahead and issues
+        // the next poll's loads
         const bool nx = kstar < len;
-        RP_PROF(8);
-        bool of = false;
-        if (wave == 0 && nx) {
-            const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
-            uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
-            for (int d = lane; d < NDW; d += 64) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int i = 4 * d + u;
-                    uint32_t v = 127u;
-                    if (i < n) {
-                        const int32_t f = Coord<CT>::fd(fd_at(i, kstar));
-                        if (f != kMaxI32) {
-                            const int32_t x = f - (cbase[i] + bm_cur[i]) + 1;
-                            if (x > 126) of = true;
-                            else v = (uint32_t)x;
-                        }
-                    }
-                    w |= v << (8 * u);
-                }
-                rp_st_sc1(dst + d, w | vb1);
-            }
+        if (nx && min((kstar + kRpP - 1) / SEG, last_seg) > seg_hi) {
+            // the next window is not staged (int32 coordinates, or a boundary past the first window)
+            stage_range(kstar / SEG, min(kstar / SEG + NSEG - 1, last_seg));
+            rp_vm_drain();
+            rp_lds_barrier();
+            RP_PROF_COUNT(10);
         }
-        RP_PROF(9);
+        const int32_t* bs1 = bases(s);
+        const int np1 = nx ? min(kRpP, len - kstar) : 0;
         if (wave == 0) {
+            bool of = false;
+            if (nx) {
+                const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
+                uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
+                for (int d = lane; d < NDW; d += 64) {
+                    // every LDS read first (4 firstDescendants, 4 bases), then the byte arithmetic
+                    CT f[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) f[u] = fd_at(min(4 * d + u, n - 1), kstar);
+                    const int4 bq = *(const int4*)(bs1 + 4 * d);
+                    const int32_t bqa[4] = {bq.x, bq.y, bq.z, bq.w};
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int32_t fv = Coord<CT>::fd(f[u]);
+                        const bool real = 4 * d + u < n && fv != kMaxI32;
+                        const int32_t x = fv - bqa[u] + 1;
+                        of |= real && x > 126;
+                        w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
+                    }
+                    rp_st_sc1(dst + d, w | vb1);
+                }
+            }
             of = __any(of);
             if (lane == 0)
                 rp_st_gran(P.gran + (size_t)((s + 1) % kRpSlots) * C + gc,
                            ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u));
             if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
-        RP_PROF(5);
-        // (e) the S row of the new candidate, then the round's outputs
-        if (have && nx && cand && q == 0 && (done || K_last <= B)) atomicOr(&sbits[j >> 5], 1u << (j & 31));
-        o_b = b;
-        o_kstar = kstar;
-        rp_lds_barrier();   // the S row bits are complete
-        outputs(s, t, T);
+        if (NW == 1) {
+            if (nx) rebase(kstar, np1, bs1, t, T);
+        } else if (wave > 0) {
+            if (nx) rebase(kstar, np1, bs1, t - 64, T - 64);
+        }
+        RP_TRACE(2);
+        {
+            // the new candidate's S row (DecideFame, hashgraph.go:688-705): bit j = it strongly sees
+            // candidate j of W'_s. The Q lanes of a candidate agree, so each wave's ballot holds its
+            // 64 / Q candidates' bits every Q-th lane; the wave parks its slice in LDS and wave 0
+            // writes the row (and Bm) after the next barrier
+            const uint64_t m = __ballot(have && nx && cand && (done || K_last <= B));
+            uint64_t x = 0;
+#pragma unroll
+            for (int k = 0; k < CPW; k++) x |= ((m >> (k * Q)) & 1ull) << k;
+            if (lane == 0) ((uint64_t*)(lds + K::O_SL))[(s & 1) * NW + wave] = x;
+            s_r = s;
+            s_k = kstar;
+        }
         b = kstar;
-        rp_lds_barrier();   // every read of this round's LDS is done
-        RP_PROF(6);
+        RP_PROF(5);
+        RP_TRACE_W(s, 1);
+        RP_TRACE_STORE(s);
     }
 
     rp_vm_drain();   // no LDS-DMA outlives the workgroup
+    rp_lds_barrier();
+    if (!failed && s_r >= 0 && wave == 0) s_row(s_r, s_k);   // the last round's Bm and S row
     RP_PROF_END();
     if (failed) {
         // the first workgroup to give up records its chain and round (st[3] then holds the
@@ -673,6 +853,39 @@ __global__ void k_round_p_tail(RoundArgs A, const int32_t* __restrict__ fin, int
         A.wflag[(size_t)(r + 1) * A.C + gc] = 0;
         A.Bm[(size_t)(r + 1) * A.C + gc] = len;
     }
+}
+
+// After the persistent launches of a DivideRounds: what the per-launch step writes besides Bm
+// and the S rows, for rounds [r_lo, r_hi] of every chain, from Bm alone: the rounds of the chain's
+// events [Bm[r], Bm[r+1]), wstat[r], wflag[r+1], active[r] and the new candidate's WLA row (the
+// lastAncestors row at Bm[r+1]). One block per (chain, kPostRB rounds); coalesced row copies.
+constexpr int kPostRB = 16;
+template <typename CT>
+__global__ void __launch_bounds__(256) k_round_p_post(RoundArgs A, int r_lo, int r_hi) {
+    const int gc = blockIdx.x, r_b = r_lo + (int)blockIdx.y * kPostRB;
+    const int n = A.n, C = A.C, len = A.c_len[gc], off = A.c_off[gc];
+    const CT* __restrict__ LA = (const CT*)A.LA;
+    for (int r = r_b; r < min(r_b + kPostRB, r_hi + 1); r++) {
+        const int b = A.Bm[(size_t)r * C + gc], k = A.Bm[(size_t)(r + 1) * C + gc];
+        for (int x = b + (int)threadIdx.x; x < k; x += 256) A.p_round[off + x] = r;
+        if (threadIdx.x == 0) {
+            A.wstat[(size_t)r * C + gc] = b < len ? ((k > b) ? 2 : 1) : 0;
+            A.wflag[(size_t)(r + 1) * C + gc] = k < len ? 1 : 0;
+            if (k < len) A.active[r] = 1;
+        }
+        if (k < len) {
+            const CT* row = LA + (size_t)(off + k) * n;
+            int32_t* dst = A.WLA + ((size_t)(r + 1) * C + gc) * n;
+            for (int i = threadIdx.x; i < n; i += 256) dst[i] = Coord<CT>::la(row[i]);
+        }
+    }
+}
+
+void launch_round_p_post(hipStream_t st, const RoundArgs& A, int r_lo, int r_hi) {
+    if (r_hi < r_lo) return;
+    const dim3 grid(A.C, (r_hi - r_lo + kPostRB) / kPostRB);
+    if (A.compact) hipLaunchKernelGGL(k_round_p_post<uint16_t>, grid, dim3(256), 0, st, A, r_lo, r_hi);
+    else hipLaunchKernelGGL(k_round_p_post<int32_t>, grid, dim3(256), 0, st, A, r_lo, r_hi);
 }
 
 void launch_round_p_tail(hipStream_t st, const RoundArgs& A, const int32_t* fin, int r_last) {

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HGX_ABI_VERSION 2
+#define HGX_ABI_VERSION 3   /* 3: HGX_ROOT_OTHER needs its key registered (hgx_set_root_others) */
 
 /* Error codes. 1..5 mirror common.StoreErrType + 1 (common/errors.go:7-13). */
 enum {
