@@ -35,6 +35,11 @@ class hgx_events(C.Structure):
                  "ntx", "tx_nil")]
 
 
+class hgx_events32(C.Structure):
+    _fields_ = [(nm, C.c_void_p) for nm in
+                ("creator", "index", "self_parent", "other_parent", "timestamp_ns", "coin", "sig_s", "ntx")]
+
+
 class hgx_wire_events(C.Structure):
     _fields_ = [(nm, C.c_void_p) for nm in
                 ("creator_id", "index", "self_parent_index", "other_parent_creator", "other_parent_index",
@@ -98,11 +103,16 @@ def lib():
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_insert_events_device", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_insert_and_run", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
+    for nm in ("hgx_insert_events32", "hgx_insert_and_run32"):
+        _sig(L, nm, i32, [p, C.POINTER(hgx_events32), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_set_participant_keys", i32, [p, p, E])
     for nm in ("hgx_insert_events_verified", "hgx_insert_events_verified_device"):
         _sig(L, nm, i32, [p, C.POINTER(hgx_events), p, p, i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_reset_consensus", i32, [p])
     _sig(L, "hgx_save", i32, [p, C.c_char_p, E])
+    _sig(L, "hgx_save_ex", i32, [p, C.c_char_p, p, p, E])
+    _sig(L, "hgx_get_event_id", i32, [p, i64, p, E])
+    _sig(L, "hgx_get_event_payload", i32, [p, i64, p, i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_checksum", u64, [p, i64])
     _sig(L, "hgx_bootstrap", i32, [p, C.c_char_p, E])
     _sig(L, "hgx_clear", i32, [p])

@@ -126,6 +126,18 @@ struct hgx_ctx {
     std::vector<int32_t> root_index, root_round;
     std::vector<uint8_t> root_y_ext;
     bool rooted = false;
+    // what Reset kept (LastConsensusRound, LastCommitedRoundEvents, ConsensusTransactions, the
+    // blocks), as it was when the roots were installed: a rooted checkpoint carries it
+    struct Kept {
+        bool has_lcr = false;
+        int32_t lcr = 0, lcre = 0;
+        int64_t consensus_tx = 0;
+        std::vector<Block> blocks;
+    };
+    std::vector<Kept> reset_kept;
+    std::vector<uint8_t> others_keys;            // Root.Others keys (hgx_set_root_others), 32 bytes each
+    std::vector<int64_t> pl_off;                 // per-event payloads restored by hgx_bootstrap ([E0, E0 + m))
+    std::vector<uint8_t> pl_blob;
     // commitCh (hashgraph.go:848-854): called for every new block with transactions
     hgx_commit_fn commit_fn = nullptr;
     void* commit_user = nullptr;
@@ -404,6 +416,80 @@ int32_t hgx_insert_and_run(hgx_ctx* c, const hgx_events* ev, int64_t count, int6
     return hgx_find_order(c, err);
 }
 
+static bool bad_events32(const hgx_events32* ev, int64_t count) {
+    return !ev || count < 0 ||
+           (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
+                          !ev->coin || !ev->sig_s || !ev->ntx));
+}
+
+int32_t hgx_insert_events32(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || bad_events32(ev, count)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events32: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (c->rooted) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events32: a reset context checks Root.Others by event id: use hgx_insert_events");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    hgx::InsertIn in{};
+    if (count > 0) {
+        hipError_t e = c->eng.stage_host32(ev->creator, ev->index, ev->self_parent, ev->other_parent, ev->timestamp_ns,
+                                           ev->coin, ev->sig_s, ev->ntx, count, in);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events32");
+    }
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert(in, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events32");
+    return finish_insert(c, out, n_inserted, err);
+}
+
+// hgx_insert_and_run with the compact columns: the structure columns (16 bytes per event) are
+// validated and committed first, the payload (45 bytes) copied beside DivideRounds
+int32_t hgx_insert_and_run32(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || bad_events32(ev, count)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_and_run32: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (count < 65536 || c->rooted || c->shard_world > 1) {
+        int32_t rc = hgx_insert_events32(c, ev, count, n_inserted, err);
+        if (rc) return rc;
+        return hgx_run_consensus(c, err);
+    }
+    DeviceGuard dg(c);
+    const int64_t E0 = c->eng.E;
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert_split_begin32(ev->creator, ev->index, ev->self_parent, ev->other_parent, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    e = c->eng.payload_begin32(ev->timestamp_ns, ev->coin, ev->sig_s, ev->ntx, out.accepted);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    hgx::InsertOut head = out;
+    head.graph_loaded.assign(c->g_loaded.begin(), c->g_loaded.end());
+    hgx_error ins_err{};
+    const int32_t ins_rc = finish_insert(c, head, n_inserted, &ins_err);
+    int32_t rc = ins_rc ? ins_rc : hgx_divide_rounds(c, err);
+    const bool laid_out = ins_rc == 0 && rc == 0;
+    std::vector<uint64_t> loaded;
+    e = c->eng.payload_end(E0, out.accepted, laid_out, c->rh.r_lo, loaded);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    for (int g = 0; g < c->G; g++) {
+        const int64_t l = (int64_t)loaded[g];
+        c->gs[g].pending_loaded += l - c->g_loaded[g];
+        c->g_loaded[g] = l;
+    }
+    c->mirror_ok = false;
+    if (ins_rc) {
+        if (err) *err = ins_err;
+        return ins_rc;
+    }
+    if (rc) return rc;
+    rc = hgx_decide_fame(c, err);
+    if (rc) return rc;
+    return hgx_find_order(c, err);
+}
+
 int32_t hgx_set_participant_keys(hgx_ctx* c, const uint8_t* keys65, hgx_error* err) {
     if (!c || !keys65) {
         set_err(err, HGX_ERR_INVALID, "hgx_set_participant_keys: bad arguments");
@@ -584,6 +670,10 @@ int32_t hgx_clear(hgx_ctx* c) {
     c->fo_prev_valid = false;
     c->mirror_ok = c->chains_ok = false;
     c->rounds_cached = c->recv_cached = false;
+    c->pl_off.clear();
+    c->pl_blob.clear();
+    c->reset_kept.clear();
+    c->others_keys.clear();
     if (c->rooted) {   // a fresh NewHashgraph has genesis roots
         std::fill(c->root_index.begin(), c->root_index.end(), -1);
         std::fill(c->root_round.begin(), c->root_round.end(), -1);
@@ -635,18 +725,42 @@ struct CkptReader {
 };
 }  // namespace
 
-int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
-    if (!c || !path) {
+enum : int32_t { kCkRooted = 1, kCkIds = 2, kCkKeys = 4, kCkPayloads = 8 };
+
+int32_t hgx_save_ex(hgx_ctx* c, const char* path, const int64_t* payload_off, const uint8_t* payload, hgx_error* err) {
+    if (!c || !path || (payload_off && !payload && c->E > 0)) {
         set_err(err, HGX_ERR_INVALID, "hgx_save: bad arguments");
         return HGX_ERR_INVALID;
     }
     DeviceGuard dg(c);
     std::vector<int32_t> creator, index, sp, op, ntx;
     std::vector<int64_t> ts;
-    std::vector<uint8_t> S, coin, nil;
+    std::vector<uint8_t> S, coin, nil, ids, keys;
     hipError_t e = c->eng.get_columns(creator, index, sp, op, ts, S, coin, ntx, nil);
     if (e != hipSuccess) return dev_err(err, e, "hgx_save");
     const int64_t E = (int64_t)creator.size();
+    const bool have_ids = c->eng.ids_known && E > 0;
+    if (have_ids) {
+        ids.resize((size_t)E * 32);
+        e = c->eng.get_ids(0, E, ids.data());
+        if (e != hipSuccess) return dev_err(err, e, "hgx_save");
+    }
+    if (c->eng.keys_set) {
+        keys.resize((size_t)c->C * 65);
+        e = c->eng.get_keys(keys.data());
+        if (e != hipSuccess) return dev_err(err, e, "hgx_save");
+    }
+    if (payload_off) {   // offsets must be non-decreasing from 0
+        if (payload_off[0] != 0) {
+            set_err(err, HGX_ERR_INVALID, "hgx_save: payload offsets must start at 0");
+            return HGX_ERR_INVALID;
+        }
+        for (int64_t i = 0; i < E; i++)
+            if (payload_off[i + 1] < payload_off[i]) {
+                set_err(err, HGX_ERR_INVALID, "hgx_save: payload offsets must not decrease");
+                return HGX_ERR_INVALID;
+            }
+    }
     const std::string tmp = std::string(path) + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) {
@@ -654,8 +768,9 @@ int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
         return HGX_ERR_INVALID;
     }
     CkptWriter w{f};
-    const uint32_t version = 1;
-    const int32_t flags = c->rooted ? 1 : 0;
+    const uint32_t version = 2;
+    const int32_t flags = (c->rooted ? kCkRooted : 0) | (have_ids ? kCkIds : 0) | (keys.empty() ? 0 : kCkKeys) |
+                          (payload_off ? kCkPayloads : 0);
     w.put(kCkptMagic, 8);
     w.put(&version, 4);
     w.put(&c->n, 4);
@@ -663,11 +778,30 @@ int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
     w.put(&flags, 4);
     w.put(&E, 8);
     if (c->rooted) {
+        // the roots, the Root.Others keys and what Reset kept (badger_store.go persists the roots
+        // and the blocks; LastConsensusRound & co. are Hashgraph fields Reset leaves in place)
         w.put(c->root_index.data(), (size_t)c->C * 4);
         w.put(c->root_round.data(), (size_t)c->C * 4);
         std::vector<uint8_t> y(c->root_y_ext.begin(), c->root_y_ext.end());
         y.resize(((size_t)c->C + 3) & ~(size_t)3, 0);
         w.put(y.data(), y.size());
+        const int64_t no = (int64_t)(c->others_keys.size() / 32);
+        w.put(&no, 8);
+        w.put(c->others_keys.data(), c->others_keys.size());
+        for (int g = 0; g < c->G; g++) {
+            const hgx_ctx::Kept k = g < (int)c->reset_kept.size() ? c->reset_kept[g] : hgx_ctx::Kept();
+            const int32_t hdr[4] = {k.has_lcr ? 1 : 0, k.lcr, k.lcre, 0};
+            const int64_t cnt[2] = {k.consensus_tx, (int64_t)k.blocks.size()};
+            w.put(hdr, 16);
+            w.put(cnt, 16);
+            for (const Block& b : k.blocks) {
+                const int32_t a0[2] = {b.rr, b.nev};
+                const int32_t a1[2] = {b.tx_nil, b.committed};
+                w.put(a0, 8);
+                w.put(&b.ntx, 8);
+                w.put(a1, 8);
+            }
+        }
     }
     std::vector<int64_t> wide((size_t)E);
     w.put(creator.data(), (size_t)E * 4);
@@ -680,6 +814,12 @@ int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
     w.put(coin.data(), (size_t)E);
     w.put(ntx.data(), (size_t)E * 4);
     w.put(nil.data(), (size_t)E);
+    if (have_ids) w.put(ids.data(), ids.size());
+    if (!keys.empty()) w.put(keys.data(), keys.size());
+    if (payload_off) {
+        w.put(payload_off, (size_t)(E + 1) * 8);
+        w.put(payload, (size_t)payload_off[E]);
+    }
     const uint64_t sum = w.h;
     w.put(&sum, 8);
     const bool ok_w = w.ok && std::fflush(f) == 0;
@@ -691,6 +831,8 @@ int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) {
     }
     return ok(err);
 }
+
+int32_t hgx_save(hgx_ctx* c, const char* path, hgx_error* err) { return hgx_save_ex(c, path, nullptr, nullptr, err); }
 
 int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
     if (!c || !path) {
@@ -715,6 +857,7 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
     uint64_t stored = 0;
     std::memcpy(&stored, r.buf.data() + r.buf.size() - 8, 8);
     if (fnv1a(14695981039346656037ull, r.buf.data(), r.buf.size() - 8) != stored) return bad("checksum mismatch");
+    r.buf.resize(r.buf.size() - 8);   // (reads past the body fail: truncated sections are caught)
     char magic[8];
     uint32_t version = 0;
     int32_t n = 0, G = 0, flags = 0;
@@ -726,49 +869,150 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
     r.get(&flags, 4);
     r.get(&E, 8);
     if (std::memcmp(magic, kCkptMagic, 8) != 0) return bad("not a checkpoint file");
-    if (version != 1) return bad("unsupported version " + std::to_string(version));
+    if (version != 1 && version != 2) return bad("unsupported version " + std::to_string(version));
+    if (version == 1 && (flags & ~kCkRooted)) return bad("unsupported flags");
     if (n != c->n || G != c->G)
         return bad("file has " + std::to_string(G) + " x " + std::to_string(n) + " participants, the context " +
                    std::to_string(c->G) + " x " + std::to_string(c->n));
-    const size_t Ez = (size_t)E, Cz = (size_t)c->C;
-    const size_t need = (flags & 1 ? Cz * 8 + ((Cz + 3) & ~(size_t)3) : 0) + Ez * (4 + 8 * 4 + 32 + 1 + 4 + 1) + 8;
-    if (E < 0 || r.buf.size() - r.pos != need) return bad("truncated file");
+    if (E < 0 || E > (int64_t)(r.buf.size() / 60)) return bad("truncated file");
     if (E > c->eng.cap) return bad("the file has " + std::to_string(E) + " events, the context's capacity is " +
                                    std::to_string(c->eng.cap));
-    if (flags & 1) {
+    const size_t Ez = (size_t)E, Cz = (size_t)c->C;
+    std::vector<uint8_t> others;
+    std::vector<hgx_ctx::Kept> kept;
+    if (flags & kCkRooted) {
         std::vector<int32_t> ri(Cz), rr(Cz), ry(Cz);
         std::vector<uint8_t> y((Cz + 3) & ~(size_t)3);
-        r.get(ri.data(), Cz * 4);
-        r.get(rr.data(), Cz * 4);
-        r.get(y.data(), y.size());
+        if (!r.get(ri.data(), Cz * 4) || !r.get(rr.data(), Cz * 4) || !r.get(y.data(), y.size())) return bad("truncated file");
         for (size_t p = 0; p < Cz; p++) ry[p] = y[p];
+        if (version >= 2) {
+            int64_t no = 0;
+            if (!r.get(&no, 8) || no < 0 || no > (int64_t)(r.buf.size() / 32)) return bad("truncated file");
+            others.resize((size_t)no * 32);
+            if (!r.get(others.data(), others.size())) return bad("truncated file");
+            kept.resize((size_t)G);
+            for (int g = 0; g < G; g++) {
+                int32_t hdr[4];
+                int64_t cnt[2];
+                if (!r.get(hdr, 16) || !r.get(cnt, 16) || cnt[1] < 0 || cnt[1] > (int64_t)(r.buf.size() / 24))
+                    return bad("truncated file");
+                hgx_ctx::Kept& k = kept[(size_t)g];
+                k.has_lcr = hdr[0] != 0;
+                k.lcr = hdr[1];
+                k.lcre = hdr[2];
+                k.consensus_tx = cnt[0];
+                k.blocks.resize((size_t)cnt[1]);
+                for (Block& b : k.blocks) {
+                    int32_t a0[2], a1[2];
+                    if (!r.get(a0, 8) || !r.get(&b.ntx, 8) || !r.get(a1, 8)) return bad("truncated file");
+                    b.rr = a0[0];
+                    b.nev = a0[1];
+                    b.tx_nil = a1[0];
+                    b.committed = a1[1];
+                    b.first = -1;
+                }
+            }
+        }
         const int32_t rc = hgx_reset(c, ri.data(), rr.data(), ry.data(), err);
         if (rc) return rc;
+        if (!others.empty()) {
+            const int32_t rc2 = hgx_set_root_others(c, others.data(), (int64_t)(others.size() / 32), err);
+            if (rc2) return rc2;
+        }
+        if (version >= 2) {   // what Reset kept at the saved context
+            for (int g = 0; g < G; g++) {
+                GraphState& s = c->gs[g];
+                const hgx_ctx::Kept& k = kept[(size_t)g];
+                s.has_lcr = k.has_lcr;
+                s.lcr = k.lcr;
+                s.lcre = k.lcre;
+                s.consensus_tx = k.consensus_tx;
+                s.blocks = k.blocks;
+            }
+            c->reset_kept = kept;
+        }
     }
     std::vector<int32_t> creator(Ez), ntx(Ez), nil(Ez);
     std::vector<int64_t> index(Ez), sp(Ez), op(Ez), ts(Ez);
     std::vector<uint8_t> S(Ez * 32), coin(Ez), nil8(Ez), hash(Ez * 32, 0);
-    r.get(creator.data(), Ez * 4);
-    r.get(index.data(), Ez * 8);
-    r.get(sp.data(), Ez * 8);
-    r.get(op.data(), Ez * 8);
-    r.get(ts.data(), Ez * 8);
-    r.get(S.data(), Ez * 32);
-    r.get(coin.data(), Ez);
-    r.get(ntx.data(), Ez * 4);
-    r.get(nil8.data(), Ez);
-    for (size_t i = 0; i < Ez; i++) {
-        hash[32 * i + 16] = coin[i] ? 1 : 0;   // the byte middleBit reads (hashgraph.go:1039-1048)
-        nil[i] = nil8[i];
+    if (!r.get(creator.data(), Ez * 4) || !r.get(index.data(), Ez * 8) || !r.get(sp.data(), Ez * 8) ||
+        !r.get(op.data(), Ez * 8) || !r.get(ts.data(), Ez * 8) || !r.get(S.data(), Ez * 32) ||
+        !r.get(coin.data(), Ez) || !r.get(ntx.data(), Ez * 4) || !r.get(nil8.data(), Ez))
+        return bad("truncated file");
+    const bool have_ids = (flags & kCkIds) != 0;
+    if (have_ids) {
+        if (!r.get(hash.data(), Ez * 32)) return bad("truncated file");
+        for (size_t i = 0; i < Ez; i++)
+            if ((hash[32 * i + 16] != 0) != (coin[i] != 0)) return bad("event id and coin disagree at event " + std::to_string(i));
+    } else {
+        for (size_t i = 0; i < Ez; i++) hash[32 * i + 16] = coin[i] ? 1 : 0;   // the byte middleBit reads (hashgraph.go:1039-1048)
+    }
+    for (size_t i = 0; i < Ez; i++) nil[i] = nil8[i];
+    std::vector<uint8_t> keys;
+    if (flags & kCkKeys) {
+        keys.resize(Cz * 65);
+        if (!r.get(keys.data(), keys.size())) return bad("truncated file");
+    }
+    std::vector<int64_t> poff;
+    std::vector<uint8_t> pblob;
+    if (flags & kCkPayloads) {
+        poff.resize(Ez + 1);
+        if (!r.get(poff.data(), (Ez + 1) * 8) || poff[0] != 0) return bad("truncated file");
+        for (size_t i = 0; i < Ez; i++)
+            if (poff[i + 1] < poff[i]) return bad("payload offsets decrease");
+        if (poff[Ez] < 0 || poff[Ez] > (int64_t)(r.buf.size() - r.pos)) return bad("truncated file");
+        pblob.resize((size_t)poff[Ez]);
+        if (!r.get(pblob.data(), pblob.size())) return bad("truncated file");
+    }
+    if (r.pos != r.buf.size()) return bad("size mismatch");
+    if (!keys.empty()) {
+        const int32_t rc = hgx_set_participant_keys(c, keys.data(), err);
+        if (rc) return rc;
     }
     hgx_events ev{creator.data(), index.data(), sp.data(), op.data(), ts.data(), hash.data(), S.data(), ntx.data(),
                   nil.data()};
     int64_t inserted = 0;
-    c->eng.others_trust = true;   // Root.Others codes were checked when the events were first inserted
+    // a version-1 file carries no ids: its Root.Others codes were checked when the events were
+    // first inserted; a version-2 rooted file brings the keys and the ids, so they are checked again
+    c->eng.others_trust = (flags & kCkRooted) && !have_ids;
     int32_t rc = hgx_insert_events(c, &ev, E, &inserted, err);
     c->eng.others_trust = false;
+    if (!have_ids) c->eng.ids_known = false;
+    c->pl_off = std::move(poff);
+    c->pl_blob = std::move(pblob);
     if (rc) return rc;
     return hgx_run_consensus(c, err);
+}
+
+int32_t hgx_get_event_id(hgx_ctx* c, int64_t gid, uint8_t* out32, hgx_error* err) {
+    if (!c || !out32 || gid < 0 || gid >= c->E) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(gid) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    if (!c->eng.ids_known) {
+        set_err(err, HGX_ERR_INVALID, "hgx_get_event_id: the events were inserted without their ids (hgx_events32)");
+        return HGX_ERR_INVALID;
+    }
+    DeviceGuard dg(c);
+    const hipError_t e = c->eng.get_ids(gid, 1, out32);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_get_event_id");
+    return ok(err);
+}
+
+int32_t hgx_get_event_payload(hgx_ctx* c, int64_t gid, uint8_t* out, int64_t cap, int64_t* len, hgx_error* err) {
+    if (len) *len = 0;
+    if (!c || gid < 0 || gid >= c->E) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(gid) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    if (c->pl_off.empty() || gid + 1 >= (int64_t)c->pl_off.size()) {
+        set_err(err, HGX_ERR_KEY_NOT_FOUND, std::to_string(gid) + ", Not Found");
+        return HGX_ERR_KEY_NOT_FOUND;
+    }
+    const int64_t a = c->pl_off[(size_t)gid], b = c->pl_off[(size_t)gid + 1];
+    if (len) *len = b - a;
+    if (out && cap > 0) std::memcpy(out, c->pl_blob.data() + a, (size_t)std::min<int64_t>(cap, b - a));
+    return ok(err);
 }
 
 // ---- Reset (hashgraph.go:877-895, inmem_store.go:184-192) ---------------------------------
@@ -801,6 +1045,20 @@ int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_rou
     c->root_round = rr;
     c->root_y_ext = ye;
     c->rooted = rooted;
+    c->others_keys.clear();
+    c->pl_off.clear();
+    c->pl_blob.clear();
+    c->reset_kept.assign(c->G, hgx_ctx::Kept());
+    for (int g = 0; g < c->G; g++) {
+        const GraphState& s = c->gs[g];
+        hgx_ctx::Kept& k = c->reset_kept[g];
+        k.has_lcr = s.has_lcr;
+        k.lcr = s.lcr;
+        k.lcre = s.lcre;
+        k.consensus_tx = s.consensus_tx;
+        k.blocks = s.blocks;
+        for (Block& b : k.blocks) b.first = -1;
+    }
     std::fill(c->chain_len.begin(), c->chain_len.end(), 0);
     std::fill(c->chain_base.begin(), c->chain_base.end(), 0);
     std::fill(c->last_gid.begin(), c->last_gid.end(), -1);
@@ -1730,6 +1988,7 @@ int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t cou
     DeviceGuard dg(c);
     const hipError_t e = c->eng.set_root_others(event_hash32, count);
     if (e != hipSuccess) return dev_err(err, e, "hgx_set_root_others");
+    c->others_keys.assign(event_hash32, event_hash32 + (size_t)count * 32);
     return ok(err);
 }
 

@@ -125,7 +125,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_sp.alloc(P)); HGX_TRY(g_op.alloc(P));
     HGX_TRY(g_ntx.alloc(P)); HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P));
     HGX_TRY(g_cts.alloc(P)); HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
-    HGX_TRY(g_txnil.alloc(P));
+    HGX_TRY(g_txnil.alloc(P)); HGX_TRY(g_id.alloc(P * 32));
     // insert state: no claims, no events per creator
     HGX_TRY(succ.alloc(P)); HGX_TRY(first_none.alloc(C));
     ins_gl_off = ((size_t)3 * C + 1) & ~(size_t)1;
@@ -379,7 +379,7 @@ InsertState Engine::insert_state() {
     InsertState st;
     st.g_creator = g_creator.p; st.g_index = g_index.p; st.g_sp = g_sp.p; st.g_op = g_op.p; st.g_ntx = g_ntx.p;
     st.g_rr = g_rr.p; st.g_ts = g_ts.p; st.g_cts = g_cts.p; st.g_S = g_S.p; st.g_coin = g_coin.p;
-    st.g_loaded = g_loaded.p; st.g_txnil = g_txnil.p;
+    st.g_loaded = g_loaded.p; st.g_txnil = g_txnil.p; st.g_id = g_id.p;
     st.succ = succ.p; st.first_none = first_none.p;
     st.last_gid = last_gid_d.p; st.last_index = last_index_d.p; st.chain_base = chain_base_d.p;
     st.fail = ins_fail.p; st.graph_loaded = graph_loaded_d.p;
@@ -438,6 +438,51 @@ hipError_t Engine::stage_host(const int32_t* creator, const int64_t* index, cons
     return hipSuccess;
 }
 
+hipError_t Engine::stage_host32(const int32_t* creator, const int32_t* index, const int32_t* sp, const int32_t* op,
+                                const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx,
+                                int64_t count, InsertIn& in) {
+    const size_t c = (size_t)count;
+    in = InsertIn{};
+    if (count <= kPackEvents) {   // one pinned packed copy (as stage_host)
+        const void* src[8] = {creator, index, sp, op, ts, coin, S, ntx};
+        const size_t bytes[8] = {4 * c, 4 * c, 4 * c, 4 * c, 8 * c, c, 32 * c, 4 * c};
+        size_t off[8], total = 0;
+        for (int i = 0; i < 8; i++) {
+            off[i] = total;
+            total += (bytes[i] + 255) & ~(size_t)255;
+        }
+        if (st_pack.n < total) HGX_TRY(st_pack.alloc(std::max(total, (size_t)2 * st_pack.n)));
+        if (h_pack_cap < total) {
+            if (h_pack) (void)hipHostFree(h_pack);
+            h_pack = nullptr;
+            h_pack_cap = 0;
+            HGX_TRY(hipHostMalloc((void**)&h_pack, std::max(total, (size_t)2 * st_pack.n), hipHostMallocDefault));
+            h_pack_cap = std::max(total, (size_t)2 * st_pack.n);
+        }
+        for (int i = 0; i < 8; i++) std::memcpy(h_pack + off[i], src[i], bytes[i]);
+        HGX_TRY(hipMemcpyAsync(st_pack.p, h_pack, total, hipMemcpyHostToDevice, stream));
+        uint8_t* d = st_pack.p;
+        in.creator = (const int32_t*)(d + off[0]); in.index32 = (const int32_t*)(d + off[1]);
+        in.sp32 = (const int32_t*)(d + off[2]); in.op32 = (const int32_t*)(d + off[3]);
+        in.ts = (const int64_t*)(d + off[4]); in.coin = d + off[5]; in.S = d + off[6];
+        in.ntx = (const int32_t*)(d + off[7]);
+        if (count > 0) ids_known = false;
+        return hipSuccess;
+    }
+    HGX_TRY(stage_col(st_creator, creator, c, 1, stream));
+    HGX_TRY(stage_col(st_index32, index, c, 1, stream));
+    HGX_TRY(stage_col(st_sp32, sp, c, 1, stream));
+    HGX_TRY(stage_col(st_op32, op, c, 1, stream));
+    HGX_TRY(stage_col(st_ts, ts, c, 1, stream));
+    HGX_TRY(stage_col(st_coin, coin, c, 1, stream));
+    HGX_TRY(stage_col(st_S, S, c, 32, stream));
+    HGX_TRY(stage_col(st_ntx, ntx, c, 1, stream));
+    in.creator = st_creator.p; in.index32 = st_index32.p; in.sp32 = st_sp32.p; in.op32 = st_op32.p;
+    in.ts = st_ts.p; in.coin = st_coin.p; in.S = st_S.p; in.ntx = st_ntx.p;
+    if (count > 0) ids_known = false;
+    return hipSuccess;
+}
+
 hipError_t Engine::set_keys(const uint8_t* keys65) {
     HGX_TRY(pk_keys.alloc((size_t)C * 65 + 1));
     HGX_TRY(pk_valid.alloc((size_t)C + 1));
@@ -492,7 +537,48 @@ hipError_t Engine::insert_split_begin(const int32_t* creator, const int64_t* ind
     HGX_TRY(stage_col(st_op, op, c, 1, stream));
     InsertIn in{};
     in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p;   // no payload yet
+    split32 = false;
     return insert_impl(in, count, out, nullptr, kCommitStructure);
+}
+
+hipError_t Engine::insert_split_begin32(const int32_t* creator, const int32_t* index, const int32_t* sp,
+                                        const int32_t* op, int64_t count, InsertOut& out) {
+    const size_t c = (size_t)count;
+    HGX_TRY(stage_col(st_creator, creator, c, 1, stream));
+    HGX_TRY(stage_col(st_index32, index, c, 1, stream));
+    HGX_TRY(stage_col(st_sp32, sp, c, 1, stream));
+    HGX_TRY(stage_col(st_op32, op, c, 1, stream));
+    InsertIn in{};
+    in.creator = st_creator.p; in.index32 = st_index32.p; in.sp32 = st_sp32.p; in.op32 = st_op32.p;
+    split32 = true;
+    return insert_impl(in, count, out, nullptr, kCommitStructure);
+}
+
+hipError_t Engine::payload_begin32(const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx,
+                                   int64_t m_ok) {
+    if (!stream2) {
+        HGX_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        HGX_TRY(hipEventCreateWithFlags(&ev_pay, hipEventDisableTiming));
+    }
+    const size_t c = (size_t)m_ok;
+    if (st_ts.n < c) HGX_TRY(st_ts.alloc(c));
+    if (st_coin.n < c) HGX_TRY(st_coin.alloc(c));
+    if (st_S.n < 32 * c) HGX_TRY(st_S.alloc(32 * c));
+    if (st_ntx.n < c) HGX_TRY(st_ntx.alloc(c));
+    pay_err = hipSuccess;
+    pay32 = true;
+    if (m_ok > 0) ids_known = false;
+    pay_thread = std::thread([=]() {
+        hipError_t e = hipSetDevice(dev);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_ts.p, ts, c * 8, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_coin.p, coin, c, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_S.p, S, c * 32, hipMemcpyHostToDevice, stream2);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(st_ntx.p, ntx, c * 4, hipMemcpyHostToDevice, stream2);
+        if (e == hipSuccess) e = hipEventRecord(ev_pay, stream2);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream2);
+        pay_err = e;
+    });
+    return hipSuccess;
 }
 
 hipError_t Engine::payload_begin(const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
@@ -508,6 +594,7 @@ hipError_t Engine::payload_begin(const int64_t* ts, const uint8_t* hash, const u
     if (st_ntx.n < c) HGX_TRY(st_ntx.alloc(c));
     if (st_nil.n < c) HGX_TRY(st_nil.alloc(c));
     pay_err = hipSuccess;
+    pay32 = false;
     // pageable host memory: each copy returns once its source has been consumed, so the copies
     // run on their own host thread (and stream) beside the DivideRounds launches
     pay_thread = std::thread([=]() {
@@ -530,8 +617,12 @@ hipError_t Engine::payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int3
     HGX_TRY(pay_err);
     HGX_TRY(hipStreamWaitEvent(stream, ev_pay, 0));
     InsertIn in{};
-    in.creator = st_creator.p; in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p;
-    in.ts = st_ts.p; in.hash = st_hash.p; in.S = st_S.p; in.ntx = st_ntx.p; in.nil = st_nil.p;
+    in.creator = st_creator.p; in.ts = st_ts.p; in.S = st_S.p; in.ntx = st_ntx.p;
+    if (split32) { in.index32 = st_index32.p; in.sp32 = st_sp32.p; in.op32 = st_op32.p; }
+    else { in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p; }
+    if (pay32) in.coin = st_coin.p;
+    else { in.hash = st_hash.p; in.nil = st_nil.p; }
+    split32 = false;
     launch_insert_commit(stream, m_ok, nullptr, nullptr, E0, n, in, insert_state(), kCommitPayload);
     if (laid_out_new) {   // the layout ran before the timestamps and coins were committed
         launch_ts_to_pos(stream, E0, m_ok, g_pos.p, g_ts.p, p_ts.p);
@@ -583,7 +674,14 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
         out.code = (fail == ~0ull) ? 0 : (int)(fail & 0xFF);
         if (out.code) {   // the failing event's creator and Index for the error string
             HGX_TRY(hipMemcpyAsync(&out.fail_creator, in.creator + m_ok, 4, hipMemcpyDeviceToHost, stream));
-            HGX_TRY(hipMemcpyAsync(&out.fail_index, in.index + m_ok, 8, hipMemcpyDeviceToHost, stream));
+            if (in.index32) {
+                int32_t fi = 0;
+                HGX_TRY(hipMemcpyAsync(&fi, in.index32 + m_ok, 4, hipMemcpyDeviceToHost, stream));
+                HGX_TRY(hipStreamSynchronize(stream));
+                out.fail_index = fi;
+            } else {
+                HGX_TRY(hipMemcpyAsync(&out.fail_index, in.index + m_ok, 8, hipMemcpyDeviceToHost, stream));
+            }
             HGX_TRY(hipStreamSynchronize(stream));
         }
         E = E0 + m_ok;
@@ -604,6 +702,20 @@ hipError_t Engine::clear() {
     E_div = 0;
     R = 0;
     laid_out = false;
+    ids_known = true;
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_ids(int64_t first, int64_t count, uint8_t* out32) {
+    if (!ids_known || first < 0 || first + count > E) return hipErrorInvalidValue;
+    if (count <= 0) return hipSuccess;
+    HGX_TRY(hipMemcpyAsync(out32, g_id.p + 32 * first, (size_t)count * 32, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t Engine::get_keys(uint8_t* out65) {
+    if (!keys_set) return hipErrorNotReady;
+    HGX_TRY(hipMemcpyAsync(out65, pk_keys.p, (size_t)C * 65, hipMemcpyDeviceToHost, stream));
     return hipStreamSynchronize(stream);
 }
 

@@ -120,12 +120,26 @@ class Engine {
     hipError_t payload_begin(const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                              const int32_t* nil, int64_t m_ok);
     hipError_t payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int32_t wcoin_r0, std::vector<uint64_t>& loaded);
+    // the same three for the compact columns of hgx_events32 (int32 Index and parents, the coin
+    // byte instead of the event id, len(Transactions) with -1 for nil): 61 instead of 108 bytes
+    // per event cross PCIe
+    hipError_t stage_host32(const int32_t* creator, const int32_t* index, const int32_t* sp, const int32_t* op,
+                            const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx, int64_t count,
+                            InsertIn& in);
+    hipError_t insert_split_begin32(const int32_t* creator, const int32_t* index, const int32_t* sp, const int32_t* op,
+                                    int64_t count, InsertOut& out);
+    hipError_t payload_begin32(const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx, int64_t m_ok);
     // forget every event (a fresh NewHashgraph); allocations are kept
     hipError_t clear();
     // per-event columns (gid order) for the host-side getters
     hipError_t get_events(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
                           std::vector<int32_t>& op);
     hipError_t get_event_fields(int64_t gid, int64_t* ts, int32_t* ntx, int32_t* tx_nil);
+    // event ids (Event.Hash) of events [first, first + count): only when every inserted event
+    // brought its id (hgx_events; an hgx_events32 insert brings the coin byte alone)
+    bool ids_known = true;
+    hipError_t get_ids(int64_t first, int64_t count, uint8_t* out32);
+    hipError_t get_keys(uint8_t* out65);   // the participants' keys (hgx_set_participant_keys)
     // every column of the inserted events (gid order) for a checkpoint (hgx_save)
     hipError_t get_columns(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
                            std::vector<int32_t>& op, std::vector<int64_t>& ts, std::vector<uint8_t>& S,
@@ -206,6 +220,8 @@ class Engine {
     hipError_t insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig,
                            int commit_mode = kCommitAll);
     hipStream_t stream2 = nullptr;   // payload copies of insert_split (created on first use)
+    bool pay32 = false;              // the payload in flight is hgx_events32's (coin byte, ntx -1 = nil)
+    bool split32 = false;            // the structure columns staged by insert_split_begin32
     hipEvent_t ev_pay = nullptr;
     std::thread pay_thread;
     hipError_t pay_err = hipSuccess;
@@ -232,7 +248,7 @@ class Engine {
     // gid order
     DBuf<int32_t> g_creator, g_index, g_sp, g_op, g_ntx, g_rr, g_pos;
     DBuf<int64_t> g_ts, g_cts;
-    DBuf<uint8_t> g_S, g_coin, g_loaded, g_txnil;
+    DBuf<uint8_t> g_S, g_coin, g_loaded, g_txnil, g_id;
     // insert state (hgx_insert.hip)
     DBuf<uint32_t> succ, first_none;
     // small per-call tables in one block each, so that one copy moves them (views below):
@@ -248,6 +264,8 @@ class Engine {
     DBuf<int32_t> st_creator, st_ntx, st_nil;
     DBuf<int64_t> st_index, st_sp, st_op, st_ts;
     DBuf<uint8_t> st_hash, st_S, st_dig, st_r;
+    DBuf<int32_t> st_index32, st_sp32, st_op32;   // hgx_events32 columns
+    DBuf<uint8_t> st_coin;
     // batches of at most kPackEvents from host memory: the columns packed in one pinned buffer,
     // one H2D copy into st_pack
     static constexpr int64_t kPackEvents = 65536;

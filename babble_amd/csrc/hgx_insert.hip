@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) k_insert_claim(int64_t m, int64_t E0, int
     if (k >= m) return;
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
-    const int64_t sp = in.sp[k];
+    const int64_t sp = in.sp_at(k);
     if (sp == -1) {
         if (cr >= 0 && cr < C) atomicMin(&st.first_none[cr], (uint32_t)gid);
     } else if (sp >= 0 && sp < gid && sp < cap) {
@@ -48,7 +48,7 @@ __device__ __forceinline__ int creator_of(int64_t x, int64_t E0, const InsertIn&
 }
 
 __device__ __forceinline__ int64_t index_of(int64_t x, int64_t E0, const InsertIn& in, const InsertState& st) {
-    return x < E0 ? (int64_t)st.g_index[x] : in.index[x - E0];
+    return x < E0 ? (int64_t)st.g_index[x] : in.idx_at(x - E0);
 }
 
 // Checks in the reference's order: creator known (LastFrom -> KeyNotFound), self-parent,
@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
     if (k >= m) return;
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
-    const int64_t sp = in.sp[k], op = in.op[k], idx = in.index[k];
+    const int64_t sp = in.sp_at(k), op = in.op_at(k), idx = in.idx_at(k);
     int code = INS_OK;
     if (cr < 0 || cr >= C) {
         code = INS_KEY_NOT_FOUND;
@@ -152,13 +152,13 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned
         if (k < m_ok) {
             const int64_t gid = E0 + k;
             const int cr = in.creator[k];
-            const int64_t idx = in.index[k];
+            const int64_t idx = in.idx_at(k);
             if (mode != kCommitPayload) {
-                const int64_t sp = in.sp[k];
+                const int64_t sp = in.sp_at(k);
                 st.g_creator[gid] = cr;
                 st.g_index[gid] = (int32_t)idx;
                 st.g_sp[gid] = (int32_t)sp;
-                st.g_op[gid] = (int32_t)in.op[k];
+                st.g_op[gid] = (int32_t)in.op_at(k);
                 st.g_rr[gid] = -1;                   // roundReceived = nil
                 st.g_cts[gid] = 0;
                 if (sp == -1) st.chain_base[cr] = (int32_t)idx;
@@ -168,14 +168,20 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned
                 }
             }
             if (mode != kCommitStructure) {
-                const int nt = in.ntx[k];
-                const int nil = in.nil[k] ? 1 : 0;
+                const int nt = in.ntx_at(k);
+                const int nil = in.nil_at(k);
                 st.g_ts[gid] = in.ts[k];
                 const uint4* s4 = (const uint4*)(in.S + 32 * k);
                 uint4* d4 = (uint4*)(st.g_S + 32 * gid);
                 d4[0] = s4[0];
                 d4[1] = s4[1];
-                st.g_coin[gid] = in.hash[32 * k + 16] != 0 ? 1 : 0;   // middleBit (hashgraph.go:1039-1048)
+                st.g_coin[gid] = (uint8_t)in.coin_at(k);   // middleBit (hashgraph.go:1039-1048)
+                if (in.hash) {   // the event id, for a checkpoint (a compact insert brings only the coin)
+                    const uint4* h4 = (const uint4*)(in.hash + 32 * k);
+                    uint4* i4 = (uint4*)(st.g_id + 32 * gid);
+                    i4[0] = h4[0];
+                    i4[1] = h4[1];
+                }
                 st.g_ntx[gid] = nt;
                 st.g_txnil[gid] = (uint8_t)nil;
                 ld = idx == 0 || (!nil && nt > 0);   // IsLoaded (event.go:119-126)
@@ -221,7 +227,7 @@ __global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, const unsigne
     if (k >= m || k < accepted_prefix(m, fail, fail_sig)) return;
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
-    const int64_t sp = in.sp[k];
+    const int64_t sp = in.sp_at(k);
     if (sp == -1) {
         if (cr >= 0 && cr < C && st.first_none[cr] == (uint32_t)gid) st.first_none[cr] = kNone32;
     } else if (sp >= 0 && sp < gid && sp < cap) {

@@ -54,12 +54,23 @@ struct DevArrays {
     uint8_t* blk_nil;   // [G x R] Transactions of the block's first event are nil
 };
 
-// One batch of events to insert, device pointers (the hgx_events columns, include/hgx.h)
+// One batch of events to insert, device pointers (the hgx_events columns, include/hgx.h), or
+// the compact columns of hgx_events32: Index and parents as int32, the coin byte instead of the
+// 32-byte id, len(Transactions) with -1 for nil (then nil == nullptr)
 struct InsertIn {
     const int32_t* creator;
     const int64_t *index, *sp, *op, *ts;
     const uint8_t *hash, *S;
     const int32_t *ntx, *nil;
+    const int32_t *index32 = nullptr, *sp32 = nullptr, *op32 = nullptr;
+    const uint8_t* coin = nullptr;
+    __host__ __device__ int64_t idx_at(int64_t k) const { return index32 ? (int64_t)index32[k] : index[k]; }
+    __host__ __device__ int64_t sp_at(int64_t k) const { return sp32 ? (int64_t)sp32[k] : sp[k]; }
+    __host__ __device__ int64_t op_at(int64_t k) const { return op32 ? (int64_t)op32[k] : op[k]; }
+    // middleBit (hashgraph.go:1039-1048): byte 16 of the event id is not 0
+    __host__ __device__ int coin_at(int64_t k) const { return coin ? (coin[k] != 0) : (hash[32 * k + 16] != 0); }
+    __host__ __device__ int ntx_at(int64_t k) const { return nil ? ntx[k] : (ntx[k] < 0 ? 0 : ntx[k]); }
+    __host__ __device__ int nil_at(int64_t k) const { return nil ? (nil[k] ? 1 : 0) : (ntx[k] < 0 ? 1 : 0); }
 };
 
 // Device state the insert path reads and writes (hgx_engine.h owns the buffers)
@@ -67,6 +78,7 @@ struct InsertState {
     int32_t *g_creator, *g_index, *g_sp, *g_op, *g_ntx, *g_rr;
     int64_t *g_ts, *g_cts;
     uint8_t *g_S, *g_coin, *g_loaded, *g_txnil;
+    uint8_t* g_id;          // [cap][32] event ids (Event.Hash) of events inserted with them (checkpoints)
     uint32_t* succ;         // [cap] smallest gid whose self-parent is this event (UINT32_MAX none)
     uint32_t* first_none;   // [C] smallest gid of the chain with self-parent "" (UINT32_MAX none)
     int32_t *last_gid, *last_index, *chain_base;   // [C] per-chain state before / after the batch

@@ -159,15 +159,6 @@ __device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     if constexpr (HD == 16) {
         u32x4 a, b, c, d;
-#ifdef HGX_EXP_DBLPOLL
-        u32x4 e2, f2, g2, h2;   // experiment: every row load issued twice (twice the hand-off traffic)
-        asm volatile(
-            "global_load_dwordx4 %0, %4, off sc1\n\t"
-            "global_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:32 sc1\n\t"
-            "global_load_dwordx4 %3, %4, off offset:48 sc1\n\t"
-            : "=&v"(e2), "=&v"(f2), "=&v"(g2), "=&v"(h2) : "v"(p) : "memory");
-#endif
         asm volatile(
             "global_load_dwordx2 %0, %5, off sc1\n\t"
             "global_load_dwordx4 %1, %6, off sc1\n\t"
@@ -179,9 +170,6 @@ __device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p
         const u32x4 q4[4] = {a, b, c, d};
 #pragma unroll
         for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
-#ifdef HGX_EXP_DBLPOLL
-        asm volatile("" :: "v"(e2), "v"(f2), "v"(g2), "v"(h2));   // (landed: the asm above waited)
-#endif
     } else if constexpr (HD == 8) {
         u32x4 a, b;
         asm volatile(
@@ -207,41 +195,6 @@ __device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p
             "global_load_dword %1, %3, off sc1\n\t"
             "s_waitcnt vmcnt(0)"
             : "=&v"(gv), "=&v"(x) : "v"(gp), "v"(p) : "memory");
-        v[0] = x;
-    }
-}
-
-// the granule alone / the row part alone (each load and its wait in one asm statement)
-__device__ __forceinline__ uint64_t rp_ld_gran_w(const uint64_t* gp) {
-    uint64_t gv;
-    asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(gv) : "v"(gp) : "memory");
-    return gv;
-}
-template <int HD>
-__device__ __forceinline__ void rp_ld_row_w(const uint32_t* p, uint32_t (&v)[HD]) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    if constexpr (HD == 16) {
-        u32x4 a, b, c, d;
-        asm volatile(
-            "global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %4, off offset:16 sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:32 sc1\n\tglobal_load_dwordx4 %3, %4, off offset:48 sc1\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(p) : "memory");
-        const u32x4 q4[4] = {a, b, c, d};
-#pragma unroll
-        for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
-    } else if constexpr (HD == 8) {
-        u32x4 a, b;
-        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:16 sc1\n\ts_waitcnt vmcnt(0)"
-                     : "=&v"(a), "=&v"(b) : "v"(p) : "memory");
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else if constexpr (HD == 4) {
-        u32x4 a;
-        asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(a) : "v"(p) : "memory");
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    } else {
-        uint32_t x;
-        asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(x) : "v"(p) : "memory");
         v[0] = x;
     }
 }
@@ -527,28 +480,6 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             const uint64_t* gp = gran_at(s);
             const uint32_t* rowp = row_at(s);
             const long long tw = __builtin_amdgcn_s_memrealtime();
-#ifdef HGX_EXP_GPOLL
-            // granule first: a lane reloads only its granule until the tag matches, then its row part
-            // once (again only if a byte still lacks v(s)): stale rows are not fetched over and over
-            bool gok = false, rok = false;
-            for (int spins = 0;; spins++) {
-                if (spins == 0) rp_ld_cand<HD>(gp, rowp, gv, fd);
-                else if (!gok) gv = rp_ld_gran_w(gp);
-                else if (!rok) rp_ld_row_w<HD>(rowp, fd);
-                uint32_t bad = 0;
-#pragma unroll
-                for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
-                gok = !jv || (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
-                rok = !jv || (gok && (!((uint32_t)gv & kRpEx) || bad == 0));
-                if (__all(gok && rok)) break;
-                if ((spins & 31) == 31) {
-                    const long long now = __builtin_amdgcn_s_memrealtime();
-                    if (now - tw > P.tmo || rp_ld_abort(P.st) != 0) { wfail = true; break; }
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-#else
             bool ok = false;
             for (int spins = 0;; spins++) {
                 if (!ok) rp_ld_cand<HD>(gp, rowp, gv, fd);   // (a lane whose candidate is complete keeps it)
@@ -565,7 +496,6 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-#endif
         RP_PROF(1);
         RP_TRACE(0);
         RP_TRACE_W(s, 0);
@@ -605,6 +535,12 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         int kstar = len, B = -1, K_last = kRpP, carried = 0;
         bool done = false, any = false;
         const bool wave_cand = __any(cand) && have;
+        // VALU and memory issue go to the older waves of a SIMD first, so with 4 waves per SIMD the
+        // youngest finished the search ~1.3 us after the oldest and everyone waited for it at the
+        // histogram barrier: the younger half searches at a higher priority (c3 rounds 22.9 ->
+        // 21.2 ms; graded priorities by age measured the same, priority kept through the publish
+        // and the poll 7x slower)
+        if (NW >= 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(2);
         for (;;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
@@ -633,6 +569,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 }
             }
             const int Kw = lo;
+            if (NW >= 8) __builtin_amdgcn_s_setprio(0);
             RP_PROF(13);
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
             // (d) the histogram is complete (and the staging issued in round s - 1 has landed: the

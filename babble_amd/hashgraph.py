@@ -22,6 +22,18 @@ from ._lib import HgxError, hgx_error, hgx_events, ptr
 UNKNOWN_PARENT = -2
 
 
+def compact_columns(t) -> dict:
+    """hgx_events32 columns of a trace (include/hgx.h): int32 Index and parents, the coin byte
+    (middleBit: byte 16 of the event id is not 0, hashgraph.go:1039-1048) instead of the id, and
+    len(Transactions) with -1 for nil. What a caller builds instead of the wide columns."""
+    ntx = np.where(np.asarray(t.txnil) != 0, -1, np.asarray(t.ntx)).astype(np.int32)
+    return dict(creator=np.ascontiguousarray(t.creator, np.int32), index=np.ascontiguousarray(t.index, np.int32),
+                sp=np.ascontiguousarray(t.sp, np.int32), op=np.ascontiguousarray(t.op, np.int32),
+                ts=np.ascontiguousarray(t.ts, np.int64),
+                coin=np.ascontiguousarray(np.asarray(t.hash)[:, 16] != 0, np.uint8),
+                s=np.ascontiguousarray(t.s, np.uint8), ntx=ntx)
+
+
 class Hashgraph:
     """One context = NewHashgraph(participants, NewInmemStore(participants, cap)) (hashgraph.go:39-66).
 
@@ -178,6 +190,40 @@ class Hashgraph:
             raise cb_err
         return n_ins.value
 
+    def _events32(self, cols: dict, lo: int, hi: int):
+        a = {k: v[lo:hi] for k, v in cols.items()}
+        return a, _lib.hgx_events32(*[ptr(a[k]) for k in ("creator", "index", "sp", "op", "ts", "coin", "s", "ntx")])
+
+    def insert_events32(self, cols: dict, lo: int = 0, hi: Optional[int] = None) -> int:
+        """InsertEvent from the compact columns of compact_columns() (hgx_insert_events32)."""
+        hi = len(cols["creator"]) if hi is None else hi
+        a, ev = self._events32(cols, lo, hi)
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        rc = self.L.hgx_insert_events32(self.ctx, C.byref(ev), hi - lo, C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        return n_ins.value
+
+    def insert_and_run32(self, cols: dict, lo: int = 0, hi: Optional[int] = None) -> int:
+        """insert_and_run from the compact columns (hgx_insert_and_run32: 61 bytes per event)."""
+        hi = len(cols["creator"]) if hi is None else hi
+        a, ev = self._events32(cols, lo, hi)
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        self._cb_error = None
+        rc = self.L.hgx_insert_and_run32(self.ctx, C.byref(ev), hi - lo, C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        cb_err, self._cb_error = getattr(self, "_cb_error", None), None
+        if cb_err is not None:
+            raise cb_err
+        return n_ins.value
+
     def InsertEvent(self, creator: int, index: int, self_parent: int, other_parent: int, timestamp_ns: int,
                     hash32: bytes, s32: bytes, transactions: Optional[Sequence[bytes]]):
         """InsertEvent(event, true) (hashgraph.go:356-401): raises HgxError with the Go error string."""
@@ -213,6 +259,27 @@ class Hashgraph:
         """Checkpoint of the resident events (hgx_save; the BadgerStore's topological event log,
         badger_store.go:309-343). Format: include/hgx.h, babble_amd/checkpoint.py."""
         self._call(lambda ctx, e: self.L.hgx_save(ctx, os.fsencode(path), e))
+
+    def save_with_payloads(self, path: str, payloads: Sequence[bytes]):
+        """Checkpoint with the caller's per-event bytes (hgx_save_ex), one entry per event."""
+        off = np.zeros(len(payloads) + 1, np.int64)
+        off[1:] = np.cumsum([len(b) for b in payloads]) if len(payloads) else []
+        blob = np.frombuffer(b"".join(payloads) or b"\0", np.uint8).copy()
+        self._call(lambda ctx, e: self.L.hgx_save_ex(ctx, os.fsencode(path), ptr(off), ptr(blob), e))
+
+    def event_id(self, gid: int) -> bytes:
+        """Event.Hash of an inserted event (hgx_get_event_id)."""
+        out = np.zeros(32, np.uint8)
+        self._call(lambda ctx, e: self.L.hgx_get_event_id(ctx, gid, ptr(out), e))
+        return out.tobytes()
+
+    def event_payload(self, gid: int) -> bytes:
+        """The payload a bootstrapped checkpoint stored for the event (hgx_get_event_payload)."""
+        ln = C.c_int64(0)
+        self._call(lambda ctx, e: self.L.hgx_get_event_payload(ctx, gid, None, 0, C.byref(ln), e))
+        out = np.zeros(max(1, ln.value), np.uint8)
+        self._call(lambda ctx, e: self.L.hgx_get_event_payload(ctx, gid, ptr(out), ln.value, C.byref(ln), e))
+        return out[:ln.value].tobytes()
 
     def Bootstrap(self, path: str):
         """Hashgraph.Bootstrap (hashgraph.go:1008-1037) from a checkpoint file: replay the events

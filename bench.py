@@ -40,6 +40,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# what each dominant-kernel candidate is bound by; achieved/peak/frac stay the
+# SURVEY 8(d) HBM figures and `valu` carries the issue-rate fraction beside them
+BOUND = {
+    "round_search": "latency: sequential round recurrence (per round an all-to-all of every chain's candidate "
+                    "row, 64 KB into each compute unit, then a 5-level dependent search); neither HBM nor VALU",
+    "cts_median": "latency: dependent firstDescendants -> timestamp gathers",
+    "fd_build": "VALU issue per (tile, target chain)",
+}
 
 CONFIGS = {
     # name: (n, events per graph, graphs per GPU, silent, stale_prob, stale_depth, description)
@@ -47,12 +55,12 @@ CONFIGS = {
     "c2": (64, 1 << 20, 1, 0, 0.0, 1, "64 peers, 1,048,576 gossip events, one hashgraph"),
     "c3": (256, 10_000_000, 1, 0, 0.0, 1, "256 peers, 10,000,000 gossip events, one hashgraph per GPU"),
     "c4": (16, 16384, 512, 0, 0.0, 1, "512 independent 16-peer sims x 16,384 events per GPU (4096 over 8 GPUs)"),
-    "c5": (1024, 1 << 20, 1, 300, 0.3, 4, "1024 peers (300 silent, 30% stale other-parents), 1,048,576 events"),
+    "c5": (1024, 1 << 20, 1, 341, 0.3, 4, "1024 peers (341 = 1/3 silent, 30% stale other-parents), 1,048,576 events"),
 }
 
 # oracle sample (events of graph 0's trace) for the prefix parity check and the CPU baseline:
 # about 10-30 s of single-threaded oracle work
-SAMPLE = {4: 1024, 16: 16384, 64: 100_000, 256: 100_000, 1024: 12_000}
+SAMPLE = {4: 1024, 16: 16384, 64: 100_000, 256: 100_000, 1024: 16_000}
 
 
 def log(*a):
@@ -84,10 +92,15 @@ def kernel_bytes(name, n, E, m, compact):
     }.get(name)
 
 
-def cpu_baseline(t, n, budget_note):
+def cpu_baseline(t, n, budget_note, ordered_frac=None):
     """The oracle (single-threaded C restatement of the reference loops, oracle/hg_oracle.c)
     on a bounded prefix of the same workload, timed on this host: InsertEvent (one C batch
-    call) + DivideRounds + DecideFame + FindOrder. Returns the baseline and the oracle."""
+    call) + DivideRounds + DecideFame + FindOrder. Returns the baseline and the oracle.
+    When the bounded sample decides no round (c5: 1/3 silent peers make a round span ~20 k
+    events, so ordering anything takes minutes of oracle time), the rate is a labelled
+    extrapolation: the oracle's events/s over the sample times the fraction of
+    the full trace a GPU pass orders (ordered_frac), i.e. assuming the CPU cost per event stays
+    what the sample measured."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import hgref
     o = hgref.Oracle(n)
@@ -101,8 +114,15 @@ def cpu_baseline(t, n, budget_note):
     if rc:
         raise RuntimeError(f"oracle consensus failed: {msg}")
     ordered = len(o.consensus_events())
-    note = "" if ordered else " (no round is decided within the sample: no rate is reported)"
-    base = dict(value=(ordered / dt) if ordered else None, unit="consensus-ordered events/s", cores=1, kind="port",
+    value, note = (ordered / dt) if ordered else None, ""
+    if not ordered and ordered_frac:
+        value = t.E / dt * ordered_frac
+        note = (f"; no round is decided within the sample, so the value is an EXTRAPOLATION: {t.E / dt:.0f} "
+                f"events/s through the oracle x {ordered_frac:.3f} (the fraction of the full trace one GPU pass "
+                f"orders)")
+    elif not ordered:
+        note = " (no round is decided within the sample: no rate is reported)"
+    base = dict(value=value, unit="consensus-ordered events/s", cores=1, kind="port",
                 sample=f"first {t.E} events of the {budget_note} trace (seed 1), oracle InsertEvent+DivideRounds+"
                        f"DecideFame+FindOrder single-threaded, {ordered} events ordered in {dt:.2f}s on "
                        f"{platform.processor() or platform.machine()}{note}")
@@ -514,6 +534,8 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the full-size property checks")
     ap.add_argument("--no-chunked", action="store_true", help="skip the SyncLimit-chunked schedule leg")
     ap.add_argument("--sync-limit", type=int, default=1000)
+    ap.add_argument("--wide", action="store_true", help="hand the events over as hgx_events (108 B/event) "
+                                                        "instead of hgx_events32 (61 B/event)")
     ap.add_argument("--sharded", action="store_true",
                     help="C3's mode: one graph row-sharded over the ranks (strong scaling) instead of replicas")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
@@ -528,20 +550,26 @@ def main():
             raise SystemExit("--sharded needs torch.distributed.run with >= 2 ranks")
         return run_sharded(args, red, world, rank, local_rank)
 
-    from babble_amd.hashgraph import DeviceTrace, Hashgraph
+    from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns
     n, E, G, *_ = CONFIGS[args.config]
     t0 = time.time()
     tr, G = make_trace(args.config, rank)
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
     dev = device_of(local_rank)   # one GPU per rank (ranks share a GPU only in gloo rehearsals)
     h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
+    # the columns as the caller hands them over, built before the clock: hgx_events32 (int32 Index
+    # and parents, the coin byte, ntx -1 = nil; 61 B per event) unless --wide (hgx_events, 108 B)
+    cols = None if args.wide else compact_columns(tr)
 
     def step():
         """from the first event append (the trace in host RAM, as the caller holds
         it: the H2D copy of every event column is inside the step) to the order in host memory.
         One hgx_insert_and_run = hgx_insert_events + DivideRounds + DecideFame + FindOrder."""
         h.clear()
-        h.insert_and_run(tr)
+        if cols is None:
+            h.insert_and_run(tr)
+        else:
+            h.insert_and_run32(cols)
         return sum(int(h.L.hgx_consensus_events_count(h.ctx, g)) for g in range(G))
 
     h.set_kernel_timing(False)
@@ -602,11 +630,22 @@ def main():
     if rank == 0:
         m_pass = total // max(1, args.steps)
         per_pass = {}
+        tj_all = {}
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(tf):
+            try:
+                tj_all = json.load(open(tf))
+            except Exception:
+                tj_all = {}
         for k, v in ks_w.items():
             ms = v["ms"] / nw
             b = kernel_bytes(k, n, tr.E, m_pass, phases["compact"])
+            pmc = tj_all.get(k, {}).get("bytes_per_pass") if isinstance(tj_all.get(k), dict) else None
             per_pass[k] = {"ms": round(ms, 4), "launches": v["launches"] // nw,
-                           "algorithmic_bytes": b, "GB_per_s": (b / (ms * 1e-3) / 1e9) if (b and ms > 0) else None}
+                           "algorithmic_bytes": b, "GB_per_s": (b / (ms * 1e-3) / 1e9) if (b and ms > 0) else None,
+                           # the PMC-measured bytes of the same kernel (profiles/traffic_<cfg>.json) over this
+                           # line's time: for gathers (cts_median) the model counts L2 hits as bytes, this does not
+                           "pmc_GB_per_s": (pmc / (ms * 1e-3) / 1e9) if (pmc and ms > 0) else None}
         r = ks.get(dom, {"ms": 0, "launches": 0})
         dom_ms = r["ms"] / max(1, args.steps)
         dom_bytes = kernel_bytes(dom, n, tr.E, m_pass, phases["compact"])
@@ -650,13 +689,16 @@ def main():
             "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
                        "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
                        "ordered_events_per_step_per_gpu": int(m_pass),
-                       "step": "clear + hgx_insert_and_run: InsertEvent (H2D of the event columns + device "
-                               "validation) + DivideRounds + DecideFame + FindOrder, the payload columns' H2D "
-                               "beside DivideRounds; order in host memory",
+                       "step": ("clear + hgx_insert_and_run" + ("" if args.wide else "32") +
+                                ": InsertEvent (H2D of the event columns + device validation) + DivideRounds + "
+                                "DecideFame + FindOrder, the payload columns' H2D beside DivideRounds; order in "
+                                "host memory"),
+                       "host_columns": "hgx_events (108 B/event)" if args.wide else
+                                       "hgx_events32 (int32 Index/parents, coin byte, ntx -1 = nil: 61 B/event)",
                        "parallelism": f"replicas x{world} (seed-sharded)",
                        "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
                        "dominant_kernel": dom},
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": dom, "bound": BOUND.get(dom, "hbm"), "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "ms_per_pass": dom_ms, "launches_per_pass": r["launches"] // max(1, args.steps),
                          "algorithmic_bytes_per_pass": dom_bytes, "valu": valu,
@@ -686,6 +728,9 @@ def main():
                 sha = result.get("ingest_sha256", {}).get("ms_per_launch")
                 tv = time.time()
                 result["insert_verify"] = insert_verify_leg(h, tr, args.steps, h.received(), sha, dev)
+                # next to `value`: the same step with Event.Verify inside InsertEvent (hashgraph.go:358-363),
+                # columns HBM-resident (the headline and its CPU baseline both leave Verify out)
+                result["value_with_verify"] = result["insert_verify"].get("value")
                 log(f"[rank {rank}] insert+verify leg in {time.time() - tv:.1f}s")
             except SystemExit:
                 raise
@@ -701,7 +746,7 @@ def main():
             _, _, _, silent, stale, depth, desc = CONFIGS[args.config]
             sample = min(E, SAMPLE.get(n, 20000))
             ts = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
-            base, o = cpu_baseline(ts, n, desc)
+            base, o = cpu_baseline(ts, n, desc, ordered_frac=m_pass / max(1, int(tr.E)))
             result["cpu_baseline"] = base
             checks["prefix_parity"] = prefix_parity(ts, o, dev)
             log(f"[rank {rank}] prefix parity ({sample} events) bit-exact")

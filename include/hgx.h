@@ -103,6 +103,25 @@ void hgx_destroy(hgx_ctx* ctx);
  * Event.Verify (the signature) stays with the caller. */
 int32_t hgx_insert_events(hgx_ctx* ctx, const hgx_events* ev, int64_t count, int64_t* n_inserted,
                           hgx_error* err);
+/* The compact form of the same batch (61 instead of 108 bytes per event cross PCIe): Index and
+ * parents as int32 (gids are < 2^31 by hgx_create's capacity), the one byte of the event id that
+ * consensus reads instead of the 32-byte id, and len(Body.Transactions) with -1 for nil. */
+typedef struct {
+    const int32_t* creator;       /* participant id (global id in a batched ctx) */
+    const int32_t* index;         /* Body.Index */
+    const int32_t* self_parent;   /* gid, -1 for "" */
+    const int32_t* other_parent;  /* gid, -1 for "", HGX_UNKNOWN_PARENT / HGX_ROOT_Y as in hgx_events */
+    const int64_t* timestamp_ns;  /* Body.Timestamp as Unix ns (UTC) */
+    const uint8_t* coin;          /* 1 byte per event: middleBit (hashgraph.go:1039-1048), i.e. byte 16 of
+                                     Event.Hash() is not 0 -- the coin of DecideFame's coin rounds */
+    const uint8_t* sig_s;         /* 32 bytes per event: signature S, big-endian, zero-padded */
+    const int32_t* ntx;           /* len(Body.Transactions); -1 if Body.Transactions == nil */
+} hgx_events32;
+/* hgx_insert_events / hgx_insert_and_run with hgx_events32 host columns. Same results, errors and
+ * counters. Not after hgx_reset (the Root.Others check reads the 32-byte id): HGX_ERR_INVALID. */
+int32_t hgx_insert_events32(hgx_ctx* ctx, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err);
+int32_t hgx_insert_and_run32(hgx_ctx* ctx, const hgx_events32* ev, int64_t count, int64_t* n_inserted,
+                             hgx_error* err);
 /* The same with every hgx_events column a DEVICE pointer on the context's device (events
  * decoded / hashed on the GPU, or a trace resident in HBM). hash and sig_s must be
  * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */
@@ -186,26 +205,47 @@ int32_t hgx_reset_consensus(hgx_ctx* ctx);
 int32_t hgx_clear(hgx_ctx* ctx);
 
 /* ---- persistence: checkpoint file + Bootstrap (hashgraph.go:1008-1037) ----- */
-/* The reference persists the DAG in its BadgerStore (events under topological-index keys,
- * badger_store.go:103-125, 309-343) and Hashgraph.Bootstrap replays them in topological order
- * through InsertEvent, then runs DivideRounds / DecideFame / FindOrder once
- * (dbTopologicalEvents, badger_store.go:345-386). The equivalent here is a binary SoA file of
- * the resident events in gid (= topological) order, little-endian:
- *   "HGXCKPT1" | u32 version 1 | i32 n | i32 graphs | i32 flags (1 = rooted) | i64 E
+/* The reference persists the DAG in its BadgerStore (events under topological-index keys with
+ * their bodies and signatures, the participants, the roots and the blocks; badger_store.go:103-125,
+ * 309-343, 540) and Hashgraph.Bootstrap replays the events in topological order through
+ * InsertEvent, then runs DivideRounds / DecideFame / FindOrder once (dbTopologicalEvents,
+ * badger_store.go:345-386). The equivalent here is a binary SoA file of the resident events in
+ * gid (= topological) order, little-endian (version 2; version-1 files are still read):
+ *   "HGXCKPT1" | u32 version 2 | i32 n | i32 graphs | i32 flags | i64 E
+ *     flags: 1 rooted, 2 event ids, 4 participant keys, 8 payloads
  *   | rooted: i32 root_index[C], i32 root_round[C], u8 root_y_is_event[C], zero pad to 4
+ *     | i64 n_others | u8 others[n_others][32] (the Root.Others keys, hgx_set_root_others)
+ *     | per graph, what Reset kept (hashgraph.go:877-895): i32 has_lcr, i32 LastConsensusRound,
+ *       i32 LastCommitedRoundEvents, i32 0, i64 ConsensusTransactions, i64 n_blocks, then per block
+ *       i32 RoundReceived, i32 events, i64 transactions, i32 nil, i32 committed
  *   | i32 creator[E] | i64 index[E] | i64 self_parent[E] | i64 other_parent[E]
  *   | i64 timestamp_ns[E] | u8 sig_s[E][32] | u8 coin[E] (Event.Hash byte 16 != 0)
- *   | i32 ntx[E] | u8 tx_nil[E] | u64 FNV-1a of every preceding byte
- * (C = graphs * n). It holds what consensus reads; bodies and signatures stay with the caller,
- * as in hgx_insert_events. hgx_save writes it (atomically: a temporary file renamed over
- * `path`). hgx_bootstrap = Bootstrap on a fresh context (no events inserted): checks the file
- * (magic, version, n, graphs, checksum: HGX_ERR_INVALID "<reason>"), installs the roots of a
- * rooted file (hgx_reset), inserts every event in order (hgx_insert_events; its Go error if one
- * is rejected) and runs the three consensus calls once (hgx_run_consensus). */
+ *   | i32 ntx[E] | u8 tx_nil[E]
+ *   | ids: u8 id[E][32] (Event.Hash), when every event was inserted with its id (hgx_events)
+ *   | keys: u8 key[C][65] (hgx_set_participant_keys)
+ *   | payloads: i64 off[E+1] | u8 bytes[off[E]] (the caller's per-event bytes, e.g. the body's
+ *     transactions as the shim serialises them; opaque to libhgx)
+ *   | u64 FNV-1a of every preceding byte
+ * (C = graphs * n). hgx_save writes it atomically (a temporary file renamed over `path`);
+ * hgx_save_ex also stores the caller's payloads (payload_off: E + 1 non-decreasing offsets from
+ * 0 into payload, or NULL). hgx_bootstrap = Bootstrap on a fresh context (no events inserted):
+ * checks the file (magic, version, n, graphs, sizes, checksum: HGX_ERR_INVALID "<reason>"),
+ * installs the roots, the Root.Others keys and the kept state of a rooted file, the participant
+ * keys, inserts every event in order (hgx_insert_events with the ids when the file has them:
+ * their Go error if one is rejected), keeps the payloads (hgx_get_event_payload) and runs the
+ * three consensus calls once (hgx_run_consensus). */
 int32_t hgx_save(hgx_ctx* ctx, const char* path, hgx_error* err);
+int32_t hgx_save_ex(hgx_ctx* ctx, const char* path, const int64_t* payload_off, const uint8_t* payload,
+                    hgx_error* err);
 /* the file's checksum: 64-bit FNV-1a of `bytes` bytes (host function, no device) */
 uint64_t hgx_checksum(const void* data, int64_t bytes);
 int32_t hgx_bootstrap(hgx_ctx* ctx, const char* path, hgx_error* err);
+/* The id (Event.Hash, 32 bytes) of an inserted event: known when every event was inserted with
+ * hgx_events (or bootstrapped from a file with ids); else HGX_ERR_INVALID. */
+int32_t hgx_get_event_id(hgx_ctx* ctx, int64_t gid, uint8_t* out32, hgx_error* err);
+/* The payload bytes of a bootstrapped event (hgx_save_ex): *len = its size, the first min(cap,
+ * len) bytes to out; HGX_ERR_KEY_NOT_FOUND "<gid>, Not Found" without one. */
+int32_t hgx_get_event_payload(hgx_ctx* ctx, int64_t gid, uint8_t* out, int64_t cap, int64_t* len, hgx_error* err);
 
 /* ---- persistence: Reset / GetFrame (hashgraph.go:877-995, root.go) -------- */
 /* Hashgraph.Reset(roots): forget the events and rounds (keeping LastConsensusRound,
@@ -220,8 +260,8 @@ int32_t hgx_reset(hgx_ctx* ctx, const int32_t* root_index, const int32_t* root_r
  * hgx_reset the set is empty; an event inserted with HGX_ROOT_OTHER whose hash (hgx_events.hash)
  * is not a key fails with "CheckOtherParent: Other-parent not known", as in the reference. The
  * value (which other-parent the entry names) stays the shim's check, since the other-parent is
- * outside the store. hgx_bootstrap accepts the HGX_ROOT_OTHER events of a rooted checkpoint
- * (they passed this check when first inserted; the file carries no event ids). */
+ * outside the store. hgx_bootstrap re-checks the HGX_ROOT_OTHER events of a rooted version-2
+ * checkpoint against its keys and ids (a version-1 file, without ids, is trusted). */
 int32_t hgx_set_root_others(hgx_ctx* ctx, const uint8_t* event_hash32, int64_t count, hgx_error* err);
 /* Hashgraph.GetFrame: per participant root_x / root_y (gid; -1 = the current Root.X / ""; 
  * HGX_ROOT_Y / HGX_ROOT_OTHER as inserted), root_index, root_round; the frame's events (gids,

@@ -27,10 +27,44 @@ def test_trace_round_trip(tmp_path):
     assert np.array_equal(r["other_parent"], t.op) and np.array_equal(r["timestamp_ns"], t.ts)
     assert np.array_equal(r["sig_s"], t.s) and np.array_equal(r["coin"], (t.hash[:, 16] != 0).astype(np.uint8))
     assert np.array_equal(r["ntx"], t.ntx) and np.array_equal(r["tx_nil"], t.txnil.astype(np.uint8))
-    # header layout: magic, version 1, n, graphs, flags, E (little-endian)
+    assert np.array_equal(r["ids"], t.hash) and r["keys"] is None and r["payloads"] is None
+    # header layout: magic, version 2, n, graphs, flags (2 = event ids), E (little-endian)
     raw = open(p, "rb").read()
-    assert raw[:8] == b"HGXCKPT1" and raw[8:12] == (1).to_bytes(4, "little")
-    assert len(raw) == 32 + t.E * (4 + 8 * 4 + 32 + 1 + 4 + 1) + 8
+    assert raw[:8] == b"HGXCKPT1" and raw[8:12] == (2).to_bytes(4, "little")
+    assert raw[20:24] == (2).to_bytes(4, "little")
+    assert len(raw) == 32 + t.E * (4 + 8 * 4 + 32 + 1 + 4 + 1 + 32) + 8
+
+
+def test_optional_sections_round_trip(tmp_path):
+    """Rooted state (roots, Root.Others keys, what Reset kept), keys and payloads."""
+    t = gtrace.gossip(4, 300, 9)
+    keys = np.arange(4 * 65, dtype=np.uint8).reshape(4, 65)
+    pay = [b"tx%d" % i * (i % 3) for i in range(t.E)]
+    others = np.arange(2 * 32, dtype=np.uint8).reshape(2, 32)
+    kept = [dict(has_lcr=True, lcr=7, lcre=12, consensus_tx=99, blocks=[(3, 10, 5, 0, 1), (4, 2, 0, 1, 0)])]
+    data = checkpoint.encode(4, 1, t.creator, t.index, t.sp, t.op, t.ts, t.s, t.hash[:, 16], t.ntx, t.txnil,
+                             roots=([3, -1, 7, 2], [1, -1, 2, 0], [1, 0, 1, 0]), others=others, kept=kept,
+                             ids=t.hash, keys=keys, payloads=pay)
+    p = tmp_path / "o.ckpt"
+    p.write_bytes(data)
+    r = checkpoint.read(str(p))
+    assert r["flags"] == 1 | 2 | 4 | 8
+    assert np.array_equal(r["others"], others) and r["kept"] == kept
+    assert np.array_equal(r["ids"], t.hash) and np.array_equal(r["keys"], keys) and r["payloads"] == pay
+
+
+def test_version1_file_still_reads(tmp_path):
+    t = gtrace.gossip(4, 100, 10)
+    body = b"".join([b"HGXCKPT1", (1).to_bytes(4, "little"), np.array([4, 1, 0], "<i4").tobytes(),
+                     np.array([t.E], "<i8").tobytes(), np.asarray(t.creator, "<i4").tobytes(),
+                     np.asarray(t.index, "<i8").tobytes(), np.asarray(t.sp, "<i8").tobytes(),
+                     np.asarray(t.op, "<i8").tobytes(), np.asarray(t.ts, "<i8").tobytes(), t.s.tobytes(),
+                     (t.hash[:, 16] != 0).astype(np.uint8).tobytes(), np.asarray(t.ntx, "<i4").tobytes(),
+                     t.txnil.astype(np.uint8).tobytes()])
+    p = tmp_path / "v1.ckpt"
+    p.write_bytes(body + np.array([checkpoint.fnv1a(body)], "<u8").tobytes())
+    r = checkpoint.read(str(p))
+    assert r["version"] == 1 and r["ids"] is None and np.array_equal(r["creator"], t.creator)
 
 
 def test_rooted_header(tmp_path):

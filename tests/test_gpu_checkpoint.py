@@ -133,6 +133,75 @@ def test_rooted_context_round_trip(tmp_path):
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
     assert list(a["order"]) == list(b["order"])
     assert a["last_round"] == b["last_round"] and a["undecided"] == b["undecided"]
+    # what Reset kept (LastConsensusRound, LastCommitedRoundEvents, ConsensusTransactions, the
+    # blocks) travels with the file: the bootstrapped node continues the saved one's state
+    assert r["kept"] is not None and r["others"] is not None and len(r["others"]) == len(hgref.frame_others_keys(t, f))
+    assert h2.LastConsensusRound() == h.LastConsensusRound()
+    assert h2.LastCommitedRoundEvents() == h.LastCommitedRoundEvents()
+    assert h2.ConsensusTransactions() == h.ConsensusTransactions()
+    assert h2.PendingLoadedEvents() == h.PendingLoadedEvents()
+    blk = lambda x: [(v["rr"], v["ntx"], v["tx_nil"], v["committed"]) for v in x.Blocks()]
+    assert blk(h2) == blk(h) and len(blk(h)) > 0
+    assert list(h2.Known()) == list(h.Known())
+    # the Root.Others keys came back: a re-save is the same file
+    p2 = str(tmp_path / "rooted2.ckpt")
+    h2.save(p2)
+    assert open(p2, "rb").read() == open(p, "rb").read()
+
+
+def test_bootstrap_restores_node_state(tmp_path):
+    """TestBootstrap (hashgraph_test.go:1351-1404): the bootstrapped Hashgraph has the same
+    consensus events, Known, LastConsensusRound, LastCommitedRoundEvents, ConsensusTransactions and
+    PendingLoadedEvents; the file also brings back what the BadgerStore keeps for a node to serve
+    its peers (badger_store.go:103-125, 309-343, 540): every event id, the participants' keys and
+    the caller's per-event payloads."""
+    n, E = 16, 6000
+    t = gtrace.gossip(n, E, 61, stale_prob=0.1, stale_depth=2)
+    keys = hgref.sign_batch(n, [0], np.zeros((1, 32), np.uint8))[0]
+    pay = [gtrace.payload(int(t.creator[i]), int(t.tx_seq[i])) if t.ntx[i] else b"" for i in range(E)]
+    h = _hg(n, E)
+    h.set_participant_keys(keys)
+    h.insert_trace(t)
+    h.RunConsensus()
+    p = str(tmp_path / "node.ckpt")
+    h.save_with_payloads(p, pay)
+    r = checkpoint.read(p)
+    assert np.array_equal(r["ids"], t.hash) and np.array_equal(r["keys"], keys) and r["payloads"] == pay
+    h2 = _hg(n, E)
+    h2.Bootstrap(p)
+    assert list(h2.ConsensusEvents()) == list(h.ConsensusEvents()) and len(h.ConsensusEvents()) > 0
+    assert list(h2.Known()) == list(h.Known())
+    assert h2.LastConsensusRound() == h.LastConsensusRound()
+    assert h2.LastCommitedRoundEvents() == h.LastCommitedRoundEvents()
+    assert h2.ConsensusTransactions() == h.ConsensusTransactions()
+    assert h2.PendingLoadedEvents() == h.PendingLoadedEvents()
+    for i in (0, 1, E // 2, E - 1):
+        assert h2.event_id(i) == t.hash[i].tobytes() == h.event_id(i)
+        assert h2.event_payload(i) == pay[i]
+    p2 = str(tmp_path / "node2.ckpt")
+    h2.save_with_payloads(p2, [h2.event_payload(i) for i in range(E)])
+    assert open(p2, "rb").read() == open(p, "rb").read()
+
+
+def test_compact_insert_has_no_ids(tmp_path):
+    """Events inserted from hgx_events32 columns bring only the coin byte: the checkpoint has no
+    id section, and the id getter says so."""
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns
+    n, E = 8, 2000
+    t = gtrace.gossip(n, E, 62)
+    h = _hg(n, E)
+    h.insert_events32(compact_columns(t))
+    h.RunConsensus()
+    p = str(tmp_path / "c.ckpt")
+    h.save(p)
+    r = checkpoint.read(p)
+    assert r["ids"] is None and np.array_equal(r["coin"], (t.hash[:, 16] != 0).astype(np.uint8))
+    with pytest.raises(HgxError, match="without their ids"):
+        h.event_id(0)
+    h2 = _hg(n, E)
+    h2.Bootstrap(p)
+    assert list(h2.ConsensusEvents()) == list(h.ConsensusEvents())
 
 
 def test_bootstrap_rejections(tmp_path):

@@ -89,3 +89,94 @@ def test_batched_graphs():
     b.insert_trace(t)
     b.RunConsensus()
     _same(a, b, graphs=G)
+
+
+# ---- the compact columns (hgx_events32: int32 Index / parents, the coin byte, ntx -1 = nil) ----
+
+def _with_nil(t, every=7):
+    """Some events with Body.Transactions == nil (the generator only makes empty non-nil ones)."""
+    nil = t.txnil.copy()
+    ntx = t.ntx.copy()
+    k = np.arange(0, t.E, every)
+    nil[k], ntx[k] = 1, 0
+    return gtrace.GossipTrace(**{**t.__dict__, "txnil": nil, "ntx": ntx})
+
+
+@pytest.mark.parametrize("n,E,seed", [(16, 70000, 11), (64, 120000, 12)])
+def test_compact_columns_equal_wide(n, E, seed):
+    from babble_amd.hashgraph import compact_columns
+    t = _with_nil(gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3))
+    a = _hg(n, E)
+    assert a.insert_and_run32(compact_columns(t)) == E
+    b = _hg(n, E)
+    assert b.insert_and_run(t) == E
+    _same(a, b)
+    if n <= 16:
+        compare(a, hgref.oracle_run(t), t, hashes=False)
+
+
+def test_compact_chunked_and_small_batches():
+    """Batches under 65 536 events (one packed pinned copy) through hgx_insert_events32, then
+    RunConsensus per sync, equal the wide columns' path."""
+    from babble_amd.hashgraph import compact_columns
+    n, E, chunk = 32, 30000, 1000
+    t = _with_nil(gtrace.gossip(n, E, 13, stale_prob=0.2, stale_depth=3), every=5)
+    cols = compact_columns(t)
+    a, b = _hg(n, E), _hg(n, E)
+    for lo in range(0, E, chunk):
+        hi = min(E, lo + chunk)
+        assert a.insert_events32(cols, lo, hi) == hi - lo
+        a.RunConsensus()
+        b.insert_trace(t, lo, hi)
+        b.RunConsensus()
+    _same(a, b)
+
+
+@pytest.mark.parametrize("kind", ["other_parent", "passed_index"])
+def test_compact_insert_error(kind):
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns
+    n, E, k0 = 32, 100000, 81234
+    t = gtrace.gossip(n, E, 14)
+    cols = compact_columns(t)
+    if kind == "other_parent":
+        cols["op"][k0] = -2
+        want = "CheckOtherParent: Other-parent not known"
+    else:
+        cols["index"][k0] = cols["index"][k0] - 1   # the self-parent's Index again
+        want = None
+    a = _hg(n, E)
+    with pytest.raises(HgxError) as ei:
+        a.insert_and_run32(cols)
+    assert ei.value.inserted == k0 and a.num_events() == k0
+    b = _hg(n, E)
+    bad = {k: v.copy() for k, v in cols.items()}
+    wide = gtrace.GossipTrace(**{**t.__dict__, "op": bad["op"].astype(np.int64), "index": bad["index"].astype(np.int64)})
+    with pytest.raises(HgxError) as ew:
+        b.insert_and_run(wide)
+    assert ei.value.msg == ew.value.msg and ei.value.code == ew.value.code
+    if want:
+        assert ei.value.msg == want
+
+
+def test_compact_batched_graphs():
+    from babble_amd.hashgraph import compact_columns
+    n, G, E1 = 16, 8, 12000
+    t = gtrace.concat_graphs([gtrace.gossip(n, E1, 70 + g, stale_prob=0.1, stale_depth=2) for g in range(G)])
+    a = _hg(n, t.E, graphs=G)
+    assert a.insert_and_run32(compact_columns(t)) == t.E
+    b = _hg(n, t.E, graphs=G)
+    b.insert_and_run(t)
+    _same(a, b, graphs=G)
+
+
+def test_compact_refused_after_reset():
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns
+    n = 4
+    t = gtrace.gossip(n, 100, 15)
+    a = _hg(n, 1000)
+    a.Reset([5] * n, [2] * n, [0] * n)
+    with pytest.raises(HgxError) as ei:
+        a.insert_events32(compact_columns(t))
+    assert "use hgx_insert_events" in ei.value.msg
