@@ -286,13 +286,9 @@ static bool cts_pipe_launch(hipStream_t s, const DevArrays& a, int c_lo, int c_c
     const size_t lds = (((size_t)4 * C + (size_t)8 * c_cnt + 15) & ~(size_t)15) + (size_t)2 * NPAD * LD * 5;
     const void* f = (const void*)k_cts_pipe<NPAD, CT>;
     static int dev_cus[64] = {0};
-    static size_t lds_set = 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    if (lds > lds_set) {
-        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
-        lds_set = lds;
-    }
+    if (ensure_lds_limit(f, lds) != hipSuccess) return false;
     if (dev_cus[dev] == 0) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -300,7 +296,7 @@ static bool cts_pipe_launch(hipStream_t s, const DevArrays& a, int c_lo, int c_c
         dev_cus[dev] = cus;
     }
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, lds) != hipSuccess || per_cu < 1) return false;
+    if (blocks_per_cu(f, 256, lds, &per_cu) != hipSuccess || per_cu < 1) return false;
     const int ntt = (max_cnt + kCpT - 1) / kCpT;
     const int64_t tiles = (int64_t)c_cnt * ntt;
     if (tiles <= 0) return true;

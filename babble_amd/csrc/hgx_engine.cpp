@@ -1145,9 +1145,46 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             s = h_small[57];   // the round tables' capacity: continue from there
         }
     };
+    // the whole-graph recurrence (hgx_round_g.hip, n <= 16): one workgroup per graph, every round
+    // in one launch, nothing shared between workgroups; relaunched from the round tables'
+    // capacity (its prologue rebuilds a round's state from Bm alone)
+    auto run_graph = [&]() -> hipError_t {
+        if (rp_st.n < (size_t)4 + G) HGX_TRY(rp_st.alloc((size_t)4 + G));
+        int32_t* fin = rp_st.p + 4;
+        HGX_TRY(hipMemsetAsync(fin, 0xFF, (size_t)G * 4, stream));
+        int32_t s = r_lo, last = -1;
+        int finished = 0;
+        for (;;) {
+            if (r_cap - 1 <= s + 1) {
+                HGX_TRY(ensure_round_cap(s + 64));
+                a = arrays();
+            }
+            HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
+            kbeg(K_ROUND_SEARCH);
+            HGX_TRY(launch_round_g(stream, round_args(), rp_st.p, fin, s, r_cap - 1));
+            kend(K_ROUND_SEARCH, 0);
+            HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+            round_g_runs++;
+            round_p_ovf += h_small[59];
+            last = std::max(last, h_small[57]);
+            finished += h_small[58];
+            if (finished >= G) {
+                r_done = last + 1;
+                launch_round_p_tail(stream, round_args(), fin, last);
+                kbeg(K_ROUND_GATHER);
+                launch_round_p_post(stream, round_args(), r_lo, last);
+                kend(K_ROUND_GATHER, (double)(last - r_lo + 1) * C * n * (sizeof(int32_t) + (compact ? 2 : 4)));
+                return hipGetLastError();
+            }
+            s = h_small[57];   // the round tables' capacity: continue from there
+        }
+    };
+    const bool graph_ok = !rooted && round_g_ok(n, nw) && (round_kernel == 0 || round_kernel == 4);
+    if (graph_ok) HGX_TRY(run_graph());
     // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
-    if (!rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
+    if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)

@@ -210,6 +210,7 @@ class Engine {
     int round_kernel = 0;     // hgx_set_round_kernel: 0 persistent recurrence on rebuilds where it applies (3: every call),
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
     int cts_kernel = 1;       // hgx_set_cts_kernel: 1 per-tile blocks (default: measured faster), 2 pipelined (hgx_cts.hip)
+    int64_t round_g_runs = 0;   // whole-graph recurrence launches (n <= 16)
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
     int64_t round_p_ovf = 0;
     int32_t round_p_fail_round = -1, round_p_fail_chain = -1;   // the last give-up: round and chain   // candidate rows the persistent launches counted exactly (over 8 bits)

@@ -124,6 +124,12 @@ struct RoundArgs {
     int32_t* hflag;
 };
 
+// A kernel's dynamic-LDS limit raised to at least `bytes` on the current device, once per
+// (device, kernel, size); thread-safe (hipFuncSetAttribute applies per device).
+hipError_t ensure_lds_limit(const void* f, size_t bytes);
+// blocks of T threads with `lds` bytes that fit one compute unit, cached per (device, kernel)
+hipError_t blocks_per_cu(const void* f, int T, size_t lds, int* out);
+
 // several small device ranges set to a byte value in one launch (instead of one memset each)
 struct FillRange {
     void* p;          // 4-byte aligned
@@ -194,6 +200,10 @@ int round_k_ndw(int n);
 // -1 per DivideRounds, a finished graph's workgroups leave at once in a later launch).
 // launch_round_p_tail writes the empty rows of rounds (fin[g], r_last] of every graph.
 bool round_p_ok(int n, int C, int num_cus);
+// whole-graph recurrence (hgx_round_g.hip): one workgroup per graph of n <= 16 chains, rounds
+// [r0, r_end) in one launch; status / fin as launch_round_p's
+bool round_g_ok(int n, int nw);
+hipError_t launch_round_g(hipStream_t s, const RoundArgs& A, int32_t* status, int32_t* fin, int r0, int r_end);
 constexpr int kRoundPBufs = 4;   // candidate-row buffers of the persistent recurrence (round s: s % 4)
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
                           int32_t* fin, int r0, int r_end, int init, int num_cus);
@@ -211,6 +221,7 @@ void launch_last_round(hipStream_t s, int rs, int R, int G, int C, int n, const 
 void step_prof_dump();     // -DHGX_STEP_PROF builds only
 void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
 void round_p_prof_dump();  // -DHGX_STEP_PROF builds only
+void round_g_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
 // rounds [r0, R) (r0 = the first undecided round)
 void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n, int nw, int sm, int G, int tally);

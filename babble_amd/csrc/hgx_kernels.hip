@@ -13,6 +13,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "hgx_device.h"
 #include "hgx_kernels.h"
@@ -1693,6 +1696,41 @@ __global__ void __launch_bounds__(256) k_fill_many(FillArgs f) {
     if (blockIdx.x == 0 && threadIdx.x < (r.bytes & 3u)) ((uint8_t*)r.p)[nw * 4 + threadIdx.x] = r.value;
 }
 
+namespace {
+std::mutex g_attr_mu;
+std::map<std::pair<int, const void*>, size_t> g_lds_set;
+std::map<std::tuple<int, const void*, int, size_t>, int> g_occ;
+}  // namespace
+
+hipError_t ensure_lds_limit(const void* f, size_t bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_attr_mu);
+    size_t& cur = g_lds_set[{dev, f}];
+    if (bytes <= cur) return hipSuccess;
+    e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) cur = bytes;
+    return e;
+}
+
+hipError_t blocks_per_cu(const void* f, int T, size_t lds, int* out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_attr_mu);
+    const auto key = std::make_tuple(dev, f, T, lds);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) {
+        *out = it->second;
+        return hipSuccess;
+    }
+    int v = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, f, T, lds);
+    if (e == hipSuccess) g_occ[key] = *out = v;
+    return e;
+}
+
 void launch_fill_many(hipStream_t s, const FillRange* r, int count) {
     if (count <= 0) return;
     FillArgs f{};
@@ -1854,12 +1892,7 @@ void launch_fame(hipStream_t s, const DevArrays& a, int r0, int R, int C, int n,
         const dim3 grid((unsigned)((int64_t)G * (R - r0) * XT));
         if (mode == 2) {
             const int shm = kFameTile * (nw * 64 + 16);
-            static bool attr = false;
-            if (!attr) {
-                (void)hipFuncSetAttribute((const void*)k_fame_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          kFameTile * (kFameMaxW * 64 + 16));
-                attr = true;
-            }
+            (void)ensure_lds_limit((const void*)k_fame_tile<true>, kFameTile * (kFameMaxW * 64 + 16));
             hipLaunchKernelGGL(k_fame_tile<true>, grid, dim3(256), shm, s, R, r0, XT, a.lr, a.wstat, a.wcoin, a.Bm,
                                a.c_base, a.WLA, a.Smat, a.fame, C, n, nw, sm, 0);
         } else {
@@ -1929,12 +1962,7 @@ template <int NPAD, typename CT>
 static void cts_tile_launch(hipStream_t s, const DevArrays& a, int c_lo, int c_cnt, int C, int n, int64_t P,
                             int max_cnt) {
     const size_t lds = (size_t)NPAD * (kCtsTile + 1) * sizeof(uint32_t);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_cts_tile<NPAD, CT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        attr = true;
-    }
+    (void)ensure_lds_limit((const void*)k_cts_tile<NPAD, CT>, lds);
     const unsigned grid = (unsigned)((int64_t)c_cnt * ((max_cnt + kCtsTile - 1) / kCtsTile));
     if (grid == 0) return;
     hipLaunchKernelGGL((k_cts_tile<NPAD, CT>), dim3(grid), dim3(256), lds, s, a.fu, a.rcnt, a.p_rr,

@@ -361,11 +361,9 @@ hipError_t la_wave_launch1(hipStream_t s, const DevArrays& a, int G, int n, cons
     const size_t np2 = (size_t)1 << lgnp;
     const size_t words = np2 * (R * DW + R + Q) + 5 * (size_t)n + 1;
     auto kern = k_la_wave<CT, DW, R, Q, NLW, J, CH, MODE>;
-    static bool attr_set = false;   // per instantiation
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    {
+        const hipError_t e = ensure_lds_limit((const void*)kern, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     const int threads = (((lmap ? na : n) + 63) & ~63) + 64 * NLW;
     if (threads > 1024 || (lmap && G != 1)) return hipErrorInvalidValue;

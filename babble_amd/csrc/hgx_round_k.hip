@@ -711,11 +711,9 @@ static hipError_t round_k_launch_v(hipStream_t st, const RoundArgs& A, int s) {
     const void* f = (const void*)k_round_k<CT, NDW, CG, H, GPB, STG, NCH>;
     const RoundKLds L = round_k_lds<NDW, CG * H, sizeof(CT) == 2 ? 2 : 4>(STG);
     const size_t lds = (size_t)L.total * GPB;
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        const hipError_t e = ensure_lds_limit(f, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
     hipLaunchKernelGGL((k_round_k<CT, NDW, CG, H, GPB, STG, NCH>), dim3(grid), dim3(64 * CG * H * GPB), lds, st, A, s);

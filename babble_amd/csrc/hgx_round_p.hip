@@ -749,15 +749,10 @@ template <typename CT, int NDW, int Q>
 static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus) {
     typedef RpCfg<CT, NDW, Q> K;
     const void* f = (const void*)k_round_p<CT, NDW, Q>;
-    static bool attr = false;
-    static int per_cu = 0;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
-        if (e != hipSuccess) return e;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, K::T, K::LDS);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    int per_cu = 0;
+    hipError_t e = ensure_lds_limit(f, K::LDS);
+    if (e == hipSuccess) e = blocks_per_cu(f, K::T, K::LDS, &per_cu);
+    if (e != hipSuccess) return e;
     // every workgroup must be resident at once (they wait for each other): one per CU
     if (per_cu < 1 || P.A.C > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
     hipLaunchKernelGGL((k_round_p<CT, NDW, Q>), dim3(P.A.C), dim3(K::T), K::LDS, st, P);

@@ -692,11 +692,9 @@ template <int CPL, int P, typename CT, bool VEC>
 static hipError_t step_big_launch_v(hipStream_t s, const RoundArgs& A, int kstep) {
     const void* f = (const void*)k_round_step_big<CPL, P, CT, VEC>;
     const size_t lds = (size_t)(P * A.n + 64 * CPL) * sizeof(CT);
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+    {
+        const hipError_t e = ensure_lds_limit(f, 160 * 1024 - 4096);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_round_step_big<CPL, P, CT, VEC>), dim3(A.C), dim3(kBigWaves * 64), lds, s, A, kstep);
     return hipGetLastError();
@@ -711,11 +709,9 @@ template <int CPL, int NWC, int OWN, int P, int GPB, typename CT, bool VEC>
 static hipError_t step_launch_v(hipStream_t s, const RoundArgs& A, int kstep) {
     const void* f = (const void*)k_round_step<CPL, NWC, OWN, P, GPB, CT, VEC>;
     const size_t lds = (size_t)GPB * StepLds<P, CT>::group_bytes(A.n, CPL);
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+    {
+        const hipError_t e = ensure_lds_limit(f, 160 * 1024 - 2048);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned grid = (unsigned)((A.C + GPB - 1) / GPB);
     hipLaunchKernelGGL((k_round_step<CPL, NWC, OWN, P, GPB, CT, VEC>), dim3(grid), dim3(GPB * NWC * 64), lds, s, A,
@@ -792,6 +788,7 @@ void step_prof_dump() {
     fprintf(stderr, "\n");
     round_k_prof_dump();
     round_p_prof_dump();
+    round_g_prof_dump();
 }
 #else
 void step_prof_dump() {}

@@ -573,14 +573,15 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(18, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 18)
+        out = np.zeros(19, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 19)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
                     la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
                     la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]),
                     round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]),
-                    round_p_fail_round=int(out[16]), round_p_fail_chain=int(out[17]))
+                    round_p_fail_round=int(out[16]), round_p_fail_chain=int(out[17]),
+                    round_g_runs=int(out[18]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
@@ -596,10 +597,12 @@ class Hashgraph:
 
     def set_round_kernel(self, mode):
         """DivideRounds rounds: "auto" (default: the persistent recurrence on calls that lay the DAG
-        out anew, where it applies, else per-round "candidate" launches), "persistent" (the
-        persistent recurrence on every call where it applies), "block" (block binary search per
-        round) or "candidate" (one launch per round, one lane per candidate)."""
-        m = {"auto": 0, "block": 1, "candidate": 2, "persistent": 3}[mode] if isinstance(mode, str) else int(mode)
+        out anew, where it applies, else per-round "candidate" launches; the whole-graph
+        recurrence on every call for n <= 16), "persistent" (the persistent recurrence on every
+        call where it applies), "graph" (one workgroup per graph of n <= 16 on every call),
+        "block" (block binary search per round) or "candidate" (one launch per round, one lane
+        per candidate)."""
+        m = {"auto": 0, "block": 1, "candidate": 2, "persistent": 3, "graph": 4}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
 

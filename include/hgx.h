@@ -410,7 +410,8 @@ int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_k
  * the number of dataflow passes that gave up and were redone by the sweeps, and the time
  * segments of the last dataflow pass; then the persistent round launches so far and the
  * DivideRounds calls whose persistent launch gave up and were redone per round, and the
- * candidate rows it counted with exact compares (over 8 bits) (up to 16 values) */
+ * candidate rows it counted with exact compares (over 8 bits), the round and chain of the last
+ * persistent launch that gave up, then the whole-graph round launches so far (up to 19 values) */
 int32_t hgx_phase_times(hgx_ctx* ctx, double* out, int32_t cap);
 /* dominant-kernel accounting for the roofline line of bench.py:
  * name of the kernel, summed device ms (the round steps time one hipGraph replay in four and
@@ -440,7 +441,9 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * applies;
  * 1 = block binary search per round (hgx_rounds.hip; per-candidate search over streamed rows
  * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
- * (hgx_round_k.hip; candidates in chunks of 128 above n = 256). Same results. */
+ * (hgx_round_k.hip; candidates in chunks of 128 above n = 256); 4 = the whole-graph recurrence
+ * (hgx_round_g.hip: one workgroup per graph runs every round in one launch, n <= 16), which mode 0
+ * also uses on every call where it applies. Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
 /* FindOrder consensus timestamps: 0 = default = 1: one tile of 8 positions per block (k_cts_small /
  * k_cts_tile, hgx_kernels.hip); 2 = resident blocks with three tiles' loads in flight behind the

@@ -127,6 +127,7 @@ def test_persistent_batched_graphs():
     t = gtrace.concat_graphs(traces)
     from babble_amd.hashgraph import Hashgraph
     h = Hashgraph(n, capacity=t.E, n_graphs=G)
+    h.set_round_kernel("persistent")   # (the default runs n <= 16 by the whole-graph kernel)
     h.insert_trace(t)
     h.RunConsensus()
     _check_persistent(h)
