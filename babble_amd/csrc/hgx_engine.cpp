@@ -62,7 +62,23 @@ static int bitlen(uint64_t v) {
     return b;
 }
 
+hipError_t Engine::ensure_shard_streams() {
+    if (round_shards < 1 || round_shards > kMaxRoundShards) return hipErrorInvalidValue;
+    for (int k = 0; k <= round_shards; k++)
+        if (!sh_ev[k]) HGX_TRY(hipEventCreateWithFlags(&sh_ev[k], hipEventDisableTiming));
+    for (int k = 0; k < round_shards; k++)
+        if (!sh_stream[k]) HGX_TRY(hipStreamCreateWithFlags(&sh_stream[k], hipStreamNonBlocking));
+    return hipSuccess;
+}
+
 Engine::~Engine() {
+    for (auto& q : sh_stream)
+        if (q) {
+            (void)hipStreamSynchronize(q);
+            (void)hipStreamDestroy(q);
+        }
+    for (auto e : sh_ev)
+        if (e) (void)hipEventDestroy(e);
     if (pay_thread.joinable()) pay_thread.join();
     if (stream2) (void)hipStreamSynchronize(stream2);
     if (ev_pay) (void)hipEventDestroy(ev_pay);
@@ -977,8 +993,19 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // one dataflow pass (k_la_wave); its error flag is read with the phase clock below
         // the error flag is 0 here: zeroed at creation, re-armed by every read
         kbeg(K_LA_SWEEP);
-        HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na,
-                               !rebuild && (En - E0) <= 8 * (int64_t)C));
+        // a small graph (c1) entirely in one workgroup's LDS
+        int64_t gpos = 0;   // the most events of a graph
+        for (int g = 0; g < G && la_wave_segs == 1 && !la_map; g++) {
+            int64_t e = 0;
+            for (int c = 0; c < n; c++) e += chain_len[(size_t)g * n + c];
+            gpos = std::max(gpos, e);
+        }
+        const size_t small_lds = (la_wave_segs == 1 && !la_map && la_small_override != 0) ? la_small_bytes(n, compact, gpos) : 0;
+        la_small_used = small_lds > 0;
+        if (la_small_used) HGX_TRY(launch_la_small(stream, a, G, n, cold, small_lds, counters.p + 6));
+        else
+            HGX_TRY(launch_la_wave(stream, a, G, n, cold, En, la_wave_segs, 0, counters.p + 6, la_map, la_na,
+                                   !rebuild && (En - E0) <= 8 * (int64_t)C));
         if (la_wave_segs > 1)
             HGX_TRY(launch_la_wave(stream, a, G, n, nullptr, En, la_wave_segs, kLaHeadRows, counters.p + 6, la_map, la_na));
         const double rows = (double)(En - E0);
@@ -994,7 +1021,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         HGX_TRY(run_sweeps(1));
     }
     kbeg(K_FD_BUILD);
-    launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
+    if (round_shards > 1) {   // the sharded rehearsal: each shard builds the rows of its own chains' events
+        for (int k = 0; k < round_shards; k++)
+            launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new, n * k / round_shards, n * (k + 1) / round_shards);
+    } else {
+        launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
+    }
     kend(K_FD_BUILD, (double)(En - E0) * 2.0 * csz * n);
     if (rooted) {   // root floors of every position (after a Reset)
         if (gfl.n < (size_t)Ppos) HGX_TRY(gfl.alloc((size_t)Ppos));
@@ -1119,7 +1151,25 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             }
             HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
             kbeg(K_ROUND_SEARCH);
-            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, init, num_cus));
+            if (round_shards > 1) {
+                // the one-GPU rehearsal of a chain-sharded recurrence: W launches over
+                // disjoint chain blocks on W streams, handing rows and granules over through the shared
+                // buffers that stand in for the peers' xGMI windows
+                HGX_TRY(ensure_shard_streams());
+                if (init) HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus));
+                HGX_TRY(hipEventRecord(sh_ev[0], stream));
+                for (int k = 0; k < round_shards; k++) {
+                    HGX_TRY(hipStreamWaitEvent(sh_stream[k], sh_ev[0], 0));
+                    const int lo = C * k / round_shards, hi = C * (k + 1) / round_shards;
+                    if (hi > lo)
+                        HGX_TRY(launch_round_p(sh_stream[k], round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 0,
+                                               num_cus, lo, hi));
+                    HGX_TRY(hipEventRecord(sh_ev[1 + k], sh_stream[k]));
+                    HGX_TRY(hipStreamWaitEvent(stream, sh_ev[1 + k], 0));
+                }
+            } else {
+                HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, init, num_cus));
+            }
             kend(K_ROUND_SEARCH, 0);
             HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipStreamSynchronize(stream));
@@ -1180,11 +1230,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             s = h_small[57];   // the round tables' capacity: continue from there
         }
     };
-    const bool graph_ok = !rooted && round_g_ok(n, nw) && (round_kernel == 0 || round_kernel == 4);
+    const bool graph_ok = !rooted && round_g_ok(n, nw) && (round_kernel == 0 || round_kernel == 4) && round_shards == 1;
     if (graph_ok) HGX_TRY(run_graph());
     // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
-    if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild)) && round_p_ok(n, C, num_cus)) {
+    if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild) || round_shards > 1) &&
+        round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)

@@ -16,6 +16,7 @@ namespace hgx {
 
 constexpr int kStepBatch = 16;        // round steps per hipGraph replay (a full DivideRounds)
 constexpr int kStepBatchSmall = 2;    // ... when resuming at the lowest changed round
+constexpr int kMaxRoundShards = 8;    // chain blocks of the sharded rehearsal (hgx_set_round_shards)
 
 // kStepBatch round steps captured as one hipGraph, replayed with rewritten round arguments
 struct StepGraph {
@@ -211,6 +212,15 @@ class Engine {
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
     int cts_kernel = 1;       // hgx_set_cts_kernel: 1 per-tile blocks (default: measured faster), 2 pipelined (hgx_cts.hip)
     int64_t round_g_runs = 0;   // whole-graph recurrence launches (n <= 16)
+    // the one-GPU rehearsal of a chain-sharded recurrence (hgx_set_round_shards): W > 1
+    // splits the persistent round launch into W chain blocks on W streams and fd_build into W
+    // source-chain blocks
+    int round_shards = 1;
+    hipStream_t sh_stream[kMaxRoundShards] = {};
+    hipEvent_t sh_ev[kMaxRoundShards + 1] = {};
+    hipError_t ensure_shard_streams();
+    bool la_small_used = false;   // the last DivideRounds built lastAncestors with k_la_small
+    int la_small_override = -1;   // 0: never k_la_small (hgx_set_la_kernel 2), else where it applies
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
     int64_t round_p_ovf = 0;
     int32_t round_p_fail_round = -1, round_p_fail_chain = -1;   // the last give-up: round and chain   // candidate rows the persistent launches counted exactly (over 8 bits)

@@ -165,6 +165,12 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
 // null: lane i = chain i of every graph
 // narrow (a resumed call with a few new rows per chain): one-dword column blocks, 4x the workgroups
 bool la_wave_ok(int n, int max_len, int n_active);
+// small graphs (n <= 32 compact / 16 int32, a graph's rows and descriptors within 150 KB of LDS):
+// one workgroup per graph, the whole graph in LDS (hgx_la_wave.hip); la_small_bytes = its LDS
+// bytes for P events per graph, 0 when it does not apply
+size_t la_small_bytes(int n, int compact, int64_t P);
+hipError_t launch_la_small(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, size_t lds,
+                           int32_t* err);
 int la_wave_blocks(int n, int compact);   // column blocks of the time-segment passes (workgroups per segment)
 int la_wave_segments(int n, int compact, int num_cus, int max_segs);   // time segments that fill the device
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
@@ -180,8 +186,9 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
                      int32_t stamp, int64_t* usum, int32_t* out, int32_t* out_next, const int32_t* c_old, int64_t u0);
 // c_old (incremental, else null): only tiles from each chain's first new row; max_new = the
 // most new rows of one chain
+// d_lo / d_hi: the rows of the events of chains [d_lo, d_hi) of every graph only (default all)
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
-                     int max_new);
+                     int max_new, int d_lo = 0, int d_hi = -1);
 // LA rows and FD entries of the new events gids [E0, E0 + m) set to none
 void launch_init_new(hipStream_t s, const DevArrays& a, int64_t E0, int64_t m, int n, int64_t P);
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P);
@@ -205,8 +212,11 @@ bool round_p_ok(int n, int C, int num_cus);
 bool round_g_ok(int n, int nw);
 hipError_t launch_round_g(hipStream_t s, const RoundArgs& A, int32_t* status, int32_t* fin, int r0, int r_end);
 constexpr int kRoundPBufs = 4;   // candidate-row buffers of the persistent recurrence (round s: s % 4)
+// chains [c_lo, c_hi) only (c_hi < 0: all): launches over disjoint chain blocks on concurrent streams
+// sharing FD8p / gran / status are the one-GPU rehearsal of a chain-sharded recurrence;
+// init 2 = the initial rows and granules only
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                          int32_t* fin, int r0, int r_end, int init, int num_cus);
+                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo = 0, int c_hi = -1);
 void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, int r_last);
 // after the persistent launches: rounds of the events, wstat / wflag / active and the candidates'
 // WLA rows of rounds [r_lo, r_hi], from Bm (the persistent loop writes only Bm and the S rows)

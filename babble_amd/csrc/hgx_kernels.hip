@@ -346,7 +346,7 @@ __device__ __forceinline__ int wave_incl_max(int x) {
 template <typename CT>
 __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int n, int nwd,
-                           int FT, int64_t P, const int32_t* __restrict__ c_old) {
+                           int FT, int64_t P, const int32_t* __restrict__ c_old, int d_lo, int d_hi) {
     typedef Coord<CT> K;
     extern __shared__ __attribute__((aligned(16))) int32_t sm[];
     const int c = blockIdx.x;
@@ -428,17 +428,18 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     // gridDim.z > 1 (a resumed call: a few new rows per chain): the target chains are split over
     // z blocks, so a block's serial per-target loop is z times shorter
     const int S = nwaves * (int)gridDim.z;   // target stride
-    for (int d0 = wave + nwaves * (int)blockIdx.z; d0 < n; d0 += S * 64) {
+    // the events' chains d in [d_lo, d_hi) (all of them but in the sharded rehearsal)
+    for (int d0 = d_lo + wave + nwaves * (int)blockIdx.z; d0 < d_hi; d0 += S * 64) {
         const int dq = d0 + S * lane;
         int q_len = 0, q_base = 0, q_off = 0, q_lo = 0, q_hv = 0;
-        if (dq < n) {
+        if (dq < d_hi) {
             q_len = m_len[dq];
             q_base = m_base[dq];
             q_off = m_off[dq];
             q_lo = (k0 > 0) ? K::la(tile[dq]) : q_base - 1;
             if (rows > 0) q_hv = K::la(tile[rows * ld + dq]);
         }
-        const int nq = min(64, (n - d0 + S - 1) / S);
+        const int nq = min(64, (d_hi - d0 + S - 1) / S);
         int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0]) : 0;
         for (int q = 0; q < nq; q++) {
             const int vraw = vnext;
@@ -1844,7 +1845,8 @@ int fd_tile_rows(int n, int compact) {
 }
 
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
-                     int max_new) {
+                     int max_new, int d_lo, int d_hi) {
+    if (d_hi < 0) d_hi = n;
     const int ft = fd_tile_rows(n, a.compact);
     // incremental (c_old): tiles from the one holding each chain's first new row;
     // max_new = the most new rows of a chain
@@ -1856,10 +1858,10 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     const int z = (c_old && max_new <= ft) ? max(1, min(8, n / 64)) : 1;
     if (a.compact)
         hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
+                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi);
     else
         hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old);
+                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi);
 }
 
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {

@@ -428,6 +428,166 @@ hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, con
 }
 }  // namespace
 
+// ---- small graphs: the whole graph in one workgroup's LDS ----------------------------------
+// Every row (n <= 32 coordinates: nwd <= 16 words, padded to NW) and every op descriptor of the graph
+// sit in LDS, packed chain after chain; one wave walks the chains (lane c = chain c, the self-parent
+// row carried in registers) and polls the op chain's progress counter in LDS: a lane takes its next
+// row as soon as prog[op chain] > op row. A row costs ONE LDS round trip: its descriptor (op row's
+// packed index, op chain, op row) was prefetched with the previous row's reads, and the op row, the
+// progress word and the next descriptor are read together. No ring, tags or loader wave. The new
+// rows go to HBM coalesced at the end; rows below c_old (incremental) are read from HBM first.
+template <int NW>
+__global__ void __launch_bounds__(256) k_la_small(uint32_t* __restrict__ LA, const int32_t* __restrict__ p_opk,
+                                                  const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_len,
+                                                  const int32_t* __restrict__ c_base, const int32_t* __restrict__ c_old,
+                                                  int n, int nwd, int compact, int32_t* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int g = blockIdx.x, c0 = g * n, tid = threadIdx.x, nt = blockDim.x;
+    __shared__ int32_t s_P;
+    int32_t* prog = (int32_t*)smem;   // [64] rows done per chain
+    int32_t* cpos = prog + 64;        // [64] chain start in the packed rows
+    if (tid == 0) {
+        int acc = 0;
+        for (int c = 0; c < n; c++) {
+            cpos[c] = acc;
+            acc += c_len[c0 + c];
+        }
+        s_P = acc;
+    }
+    for (int c = tid; c < n; c += nt) prog[c] = c_old ? c_old[c0 + c] : 0;
+    __syncthreads();
+    const int P = s_P;
+    int2* desc = (int2*)(cpos + 64);                       // [P + 1, even] {op row's packed index, p_opk}
+    uint32_t* rows = (uint32_t*)(desc + ((P + 2) & ~1));   // [P][NW], 16-byte aligned
+    for (int c = 0; c < n; c++) {
+        const int o = cpos[c], len = c_len[c0 + c], off = c_off[c0 + c];
+        for (int x = tid; x < len; x += nt) {
+            const int v = p_opk[off + x];
+            desc[o + x] = make_int2(v >= 0 ? cpos[v >> kOpkBits] + (v & ((1 << kOpkBits) - 1)) : -1, v);
+        }
+        if (c_old) {   // final rows of earlier calls
+            const int m = c_old[c0 + c];
+            for (int x = tid; x < m * nwd; x += nt) rows[(size_t)(o + x / nwd) * NW + x % nwd] = LA[(size_t)off * nwd + x];
+        }
+    }
+    if (tid == 0) desc[P] = make_int2(-1, -1);   // (the prefetch past the last row)
+    __syncthreads();
+    if (tid < 64) {
+        const int c = tid;
+        const bool live = c < n;
+        const int len = live ? c_len[c0 + c] : 0, base = live ? cpos[c] : 0;
+        int k = live ? prog[c] : 0;
+        const int own0 = live ? c_base[c0 + c] : 0;
+        // own coordinate: word c / 2 (compact, value + 1 in half c % 2) or word c
+        const int ow = compact ? c >> 1 : c;
+        const uint32_t omask = compact ? (0xFFFFu << ((c & 1) * 16)) : 0xFFFFFFFFu;
+        const uint32_t none = compact ? 0u : 0xFFFFFFFFu;
+        uint32_t carry[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) carry[w] = (k > 0) ? rows[(size_t)(base + k - 1) * NW + w] : none;
+        int2 d = k < len ? desc[base + k] : make_int2(-1, -1);
+        uint32_t guard = 0;
+        while (__any(k < len)) {
+            if (k < len) {
+                const int opc = d.y >= 0 ? d.y >> kOpkBits : 0, opk = d.y & ((1 << kOpkBits) - 1);
+                // one batch: progress word, op row, next descriptor
+                const int pr = prog[opc];
+                uint32_t od[NW];
+                const uint32_t* src = rows + (size_t)(d.x >= 0 ? d.x : 0) * NW;
+                if constexpr (NW % 4 == 0) {
+#pragma unroll
+                    for (int q = 0; q < NW / 4; q++) {
+                        const uint4 x4 = ((const uint4*)src)[q];
+                        od[4 * q] = x4.x; od[4 * q + 1] = x4.y; od[4 * q + 2] = x4.z; od[4 * q + 3] = x4.w;
+                    }
+                } else if constexpr (NW == 2) {
+                    const uint2 x2 = *(const uint2*)src;
+                    od[0] = x2.x; od[1] = x2.y;
+                } else {
+                    od[0] = src[0];
+                }
+                const int2 dn = desc[base + k + 1];
+                if (d.y < 0 || pr > opk) {
+                    uint32_t* dst = rows + (size_t)(base + k) * NW;
+#pragma unroll
+                    for (int w = 0; w < NW; w++) {
+                        const uint32_t o = d.y >= 0 ? od[w] : none;
+                        uint32_t v;
+                        if (compact) {
+                            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                            v = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, carry[w]),
+                                                                                       __builtin_bit_cast(u16x2, o)));
+                            if (w == ow) v = (v & ~omask) | ((((uint32_t)(own0 + k + 1)) & 0xFFFFu) << ((c & 1) * 16));
+                        } else {
+                            v = (uint32_t)max((int32_t)carry[w], (int32_t)o);
+                            if (w == ow) v = (uint32_t)(own0 + k);
+                        }
+                        carry[w] = v;
+                    }
+                    if constexpr (NW % 4 == 0) {
+#pragma unroll
+                        for (int q = 0; q < NW / 4; q++)
+                            ((uint4*)dst)[q] = make_uint4(carry[4 * q], carry[4 * q + 1], carry[4 * q + 2], carry[4 * q + 3]);
+                    } else if constexpr (NW == 2) {
+                        *(uint2*)dst = make_uint2(carry[0], carry[1]);
+                    } else {
+                        dst[0] = carry[0];
+                    }
+                    k++;
+                    prog[c] = k;   // (after the row: a wave's LDS writes land in order)
+                    d = dn;
+                }
+            }
+            if (++guard > (1u << 26)) {   // (a cycle cannot happen on a validated DAG)
+                if (c == 0) atomicOr(err, 1);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < n; c++) {   // the new rows to HBM
+        const int o = cpos[c], k0 = c_old ? c_old[c0 + c] : 0, len = c_len[c0 + c], off = c_off[c0 + c];
+        for (int x = k0 * nwd + tid; x < len * nwd; x += nt)
+            LA[(size_t)off * nwd + x] = rows[(size_t)(o + x / nwd) * NW + x % nwd];
+    }
+}
+
+static int la_small_nw(int nwd) {
+    int nw = 1;
+    while (nw < nwd) nw <<= 1;
+    return nw;
+}
+
+// LDS bytes k_la_small needs for a graph of P events (0: not applicable)
+size_t la_small_bytes(int n, int compact, int64_t P) {
+    const int nwd = compact ? n / 2 : n;
+    if (n > 64 || nwd > 16) return 0;
+    const size_t b = 128 * 4 + (((size_t)P + 2) & ~(size_t)1) * 8 + (size_t)P * la_small_nw(nwd) * 4;
+    return b <= 150 * 1024 ? b : 0;
+}
+
+template <int NW>
+static hipError_t la_small_launch(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, size_t lds,
+                                  int32_t* err) {
+    const hipError_t e = ensure_lds_limit((const void*)k_la_small<NW>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_la_small<NW>, dim3(G), dim3(256), lds, s, (uint32_t*)a.LA, a.p_opk, a.c_off, a.c_len,
+                       a.c_base, c_old, n, a.compact ? n / 2 : n, a.compact, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_la_small(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, size_t lds,
+                           int32_t* err) {
+    switch (la_small_nw(a.compact ? n / 2 : n)) {
+        case 1: return la_small_launch<1>(s, a, G, n, c_old, lds, err);
+        case 2: return la_small_launch<2>(s, a, G, n, c_old, lds, err);
+        case 4: return la_small_launch<4>(s, a, G, n, c_old, lds, err);
+        case 8: return la_small_launch<8>(s, a, G, n, c_old, lds, err);
+        case 16: return la_small_launch<16>(s, a, G, n, c_old, lds, err);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 int la_wave_blocks(int n, int compact) {
     const int nwd = compact ? n / 2 : n;
     return nwd / seg_cfg(n, nwd).dw;

@@ -303,6 +303,7 @@ struct RoundPArgs {
     int32_t* fin;       // [G] the round at which graph g found W'_s empty (-1: not yet, this call)
     int r0, r_end;      // rounds [r0, r_end) at most
     long long tmo;      // one wait's budget in s_memrealtime ticks (100 MHz)
+    int c_lo;           // this launch's first chain (a chain block: the sharded rehearsal)
 };
 
 // One round s of chain c, in the order of its critical path:
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     const RoundArgs& A = P.A;
     const int n = A.n, C = A.C, sm = A.sm;
     const int t = threadIdx.x, lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int gc = blockIdx.x, g = gc / n, cl = gc % n, g0 = g * n;
+    const int gc = P.c_lo + (int)blockIdx.x, g = gc / n, cl = gc % n, g0 = g * n;
     const int j = t / Q, q = t % Q;              // candidate slot and row part of this lane
     const bool jv = j < n && t < K::NC * Q;      // a real chain of the graph
     uint32_t* win = (uint32_t*)(lds + K::O_WIN);
@@ -746,7 +747,7 @@ __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
 }
 
 template <typename CT, int NDW, int Q>
-static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus) {
+static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus, int nblk) {
     typedef RpCfg<CT, NDW, Q> K;
     const void* f = (const void*)k_round_p<CT, NDW, Q>;
     int per_cu = 0;
@@ -755,19 +756,19 @@ static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus) {
     if (e != hipSuccess) return e;
     // every workgroup must be resident at once (they wait for each other): one per CU
     if (per_cu < 1 || P.A.C > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((k_round_p<CT, NDW, Q>), dim3(P.A.C), dim3(K::T), K::LDS, st, P);
+    hipLaunchKernelGGL((k_round_p<CT, NDW, Q>), dim3(nblk), dim3(K::T), K::LDS, st, P);
     return hipGetLastError();
 }
 
 template <typename CT>
-static hipError_t rp_launch_t(hipStream_t st, const RoundPArgs& P, int num_cus) {
+static hipError_t rp_launch_t(hipStream_t st, const RoundPArgs& P, int num_cus, int nblk) {
     switch (round_k_ndw(P.A.n)) {
-        case 2: return rp_launch<CT, 2, 2>(st, P, num_cus);
-        case 4: return rp_launch<CT, 4, 4>(st, P, num_cus);
-        case 8: return rp_launch<CT, 8, 2>(st, P, num_cus);
-        case 16: return rp_launch<CT, 16, 4>(st, P, num_cus);
-        case 32: return rp_launch<CT, 32, 4>(st, P, num_cus);
-        case 64: return rp_launch<CT, 64, 4>(st, P, num_cus);
+        case 2: return rp_launch<CT, 2, 2>(st, P, num_cus, nblk);
+        case 4: return rp_launch<CT, 4, 4>(st, P, num_cus, nblk);
+        case 8: return rp_launch<CT, 8, 2>(st, P, num_cus, nblk);
+        case 16: return rp_launch<CT, 16, 4>(st, P, num_cus, nblk);
+        case 32: return rp_launch<CT, 32, 4>(st, P, num_cus, nblk);
+        case 64: return rp_launch<CT, 64, 4>(st, P, num_cus, nblk);
         default: return hipErrorInvalidValue;
     }
 }
@@ -825,8 +826,11 @@ void launch_round_p_tail(hipStream_t st, const RoundArgs& A, const int32_t* fin,
 }
 
 hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                          int32_t* fin, int r0, int r_end, int init, int num_cus) {
+                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo, int c_hi) {
+    if (c_hi < 0) c_hi = A.C;
+    if (c_lo < 0 || c_hi > A.C || c_lo >= c_hi) return hipErrorInvalidValue;
     RoundPArgs P{};
+    P.c_lo = c_lo;
     P.A = A;
     P.FD8p = FD8p;
     P.gran = gran;
@@ -839,9 +843,9 @@ hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, ui
         if (A.compact) hipLaunchKernelGGL(k_round_p_init<uint16_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
         else hipLaunchKernelGGL(k_round_p_init<int32_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
         const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || init == 2) return e;   // (2: the initial rows only)
     }
-    return A.compact ? rp_launch_t<uint16_t>(st, P, num_cus) : rp_launch_t<int32_t>(st, P, num_cus);
+    return A.compact ? rp_launch_t<uint16_t>(st, P, num_cus, c_hi - c_lo) : rp_launch_t<int32_t>(st, P, num_cus, c_hi - c_lo);
 }
 
 }  // namespace hgx

@@ -573,15 +573,15 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(19, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 19)
+        out = np.zeros(20, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 20)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
                     la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
                     la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]),
                     round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]),
                     round_p_fail_round=int(out[16]), round_p_fail_chain=int(out[17]),
-                    round_g_runs=int(out[18]))
+                    round_g_runs=int(out[18]), la_small=int(out[19]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
@@ -590,8 +590,10 @@ class Hashgraph:
             raise ValueError(f"invalid fame tally {mode}")
 
     def set_la_kernel(self, mode):
-        """DivideRounds lastAncestors: "wave" (default, one dataflow pass) or "sweep" (Gauss-Seidel)."""
-        m = {"wave": 0, "sweep": 1}[mode] if isinstance(mode, str) else int(mode)
+        """DivideRounds lastAncestors: "wave" (default, one dataflow pass; a small graph's whole
+        graph in LDS), "ring" (the dataflow pass without the small-graph form) or "sweep"
+        (Gauss-Seidel)."""
+        m = {"wave": 0, "sweep": 1, "ring": 1025}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_la_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid lastAncestors kernel {mode}")
 
@@ -605,6 +607,12 @@ class Hashgraph:
         m = {"auto": 0, "block": 1, "candidate": 2, "persistent": 3, "graph": 4}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
+
+    def set_round_shards(self, shards: int):
+        """The one-GPU rehearsal of a chain-sharded recurrence: W chain blocks on W streams
+        (hgx_set_round_shards)."""
+        if self.L.hgx_set_round_shards(self.ctx, int(shards)) != 0:
+            raise ValueError(f"invalid shard count {shards}")
 
     def set_cts_kernel(self, mode):
         """FindOrder consensus timestamps: "auto" = "tile" (default: one tile of 8 positions per

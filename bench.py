@@ -539,6 +539,8 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="C3's mode: one graph row-sharded over the ranks (strong scaling) instead of replicas")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--round-shards", type=int, default=1,
+                    help="rehearse a chain-sharded recurrence on one GPU: W chain blocks on W streams (measurement)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -557,6 +559,8 @@ def main():
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
     dev = device_of(local_rank)   # one GPU per rank (ranks share a GPU only in gloo rehearsals)
     h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
+    if args.round_shards > 1:   # the one-GPU rehearsal of a chain-sharded recurrence
+        h.set_round_shards(args.round_shards)
     # the columns as the caller hands them over, built before the clock: hgx_events32 (int32 Index
     # and parents, the coin byte, ntx -1 = nil; 61 B per event) unless --wide (hgx_events, 108 B)
     cols = None if args.wide else compact_columns(tr)
@@ -695,7 +699,9 @@ def main():
                                 "host memory"),
                        "host_columns": "hgx_events (108 B/event)" if args.wide else
                                        "hgx_events32 (int32 Index/parents, coin byte, ntx -1 = nil: 61 B/event)",
-                       "parallelism": f"replicas x{world} (seed-sharded)",
+                       "parallelism": f"replicas x{world} (seed-sharded)" +
+                                      (f"; recurrence rehearsed in {args.round_shards} chain blocks on one GPU"
+                                       if args.round_shards > 1 else ""),
                        "phase_ms_last_step": {k: round(float(v), 3) for k, v in phases.items()},
                        "dominant_kernel": dom},
             "roofline": {"kernel": dom, "bound": BOUND.get(dom, "hbm"), "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -429,9 +429,11 @@ int32_t hgx_set_coord_storage(hgx_ctx* ctx, int32_t mode);
  * kernel, 2 = witness-tiled int8 MFMA. Same results; for measurement. */
 int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds lastAncestors: 0 = one dataflow pass per (graph, column block) where it
- * applies (default: n <= 896, chains < 2^21 rows; hgx_la_wave.hip), 1 = Gauss-Seidel sweeps
- * to the fixed point (hgx_kernels.hip), m >= 2 = the dataflow pass with m time segments on
- * a rebuild (measurement). Same results. */
+ * applies (default: n <= 896, chains < 2^21 rows; hgx_la_wave.hip), and for a small graph
+ * (n <= 32 compact / 16 int32, its rows within 150 KB) the pass with the whole graph in one
+ * workgroup's LDS; 1 = Gauss-Seidel sweeps to the fixed point (hgx_kernels.hip), 2 <= m <= 1024 =
+ * the dataflow pass with m time segments on a rebuild (measurement), 1025 = the dataflow pass
+ * without the small-graph form. Same results. */
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds rounds: 0 = default: the persistent recurrence (hgx_round_p.hip, one resident
  * workgroup per chain runs every round in one launch) where it applies (n <= 256, at most one
@@ -445,6 +447,12 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * (hgx_round_g.hip: one workgroup per graph runs every round in one launch, n <= 16), which mode 0
  * also uses on every call where it applies. Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
+/* The one-GPU rehearsal of a chain-sharded recurrence (measurement): shards = W in
+ * [1, 8] splits the persistent round launch into W launches over disjoint chain blocks on W
+ * concurrent streams that hand candidate rows and granules over through shared HBM buffers (the
+ * stand-in for the peers' xGMI windows), and firstDescendants into W builds of the rows of each
+ * block's events. W > 1 implies the persistent recurrence where it applies. Same results. */
+int32_t hgx_set_round_shards(hgx_ctx* ctx, int32_t shards);
 /* FindOrder consensus timestamps: 0 = default = 1: one tile of 8 positions per block (k_cts_small /
  * k_cts_tile, hgx_kernels.hip); 2 = resident blocks with three tiles' loads in flight behind the
  * selects of a fourth (hgx_cts.hip) where it applies (32 < n <= 512, at most 4096 chains),

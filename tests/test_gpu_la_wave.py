@@ -117,3 +117,62 @@ def test_wave_batched_graphs():
     _same_coords(hw, hs, cat.E, 5)
     for g in range(G):
         _same_results(hw, hs, g)
+
+
+# ---- small graphs: the whole graph in one workgroup's LDS (k_la_small) ----------------------------
+# (sized to the kernel's bound: a graph's events x (words per row + 1) x 4 bytes <= 150 KB)
+SMALL = [(1, 64, 31, 0, 0.0), (2, 300, 32, 0, 0.0), (4, 1024, 1, 0, 0.0), (5, 1500, 33, 1, 0.3),
+         (8, 4000, 34, 0, 0.2), (16, 3000, 35, 5, 0.5), (32, 1000, 36, 0, 0.1)]
+
+
+@pytest.mark.parametrize("n,E,seed,silent,stale", SMALL)
+def test_small_graph_matches_ring_sweeps_and_oracle(n, E, seed, silent, stale):
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=stale, stale_depth=4)
+    h = _run(t, "wave")
+    assert h.phase_times()["la_small"] == 1, "the small-graph lastAncestors kernel did not run"
+    hr = _run(t, "ring")
+    assert hr.phase_times()["la_small"] == 0 and hr.phase_times()["la_wave"] == 1
+    hs = _run(t, "sweep")
+    _same_coords(h, hr, t.E, seed)
+    _same_coords(h, hs, t.E, seed + 1)
+    _same_results(h, hs)
+    b, a = hgref.oracle_run(t).results(), h.results()
+    for key in ("round", "rr", "cts"):
+        assert np.array_equal(np.asarray(a[key]), np.asarray(b[key])), key
+    assert list(a["order"]) == list(b["order"])
+
+
+@pytest.mark.parametrize("n,E,seed,chunk,coord32", [(4, 1024, 41, 100, False), (8, 3000, 42, 250, False),
+                                                    (5, 2000, 43, 300, True), (16, 1500, 44, 200, True)])
+def test_small_graph_incremental(n, E, seed, chunk, coord32):
+    """Calls that resume: the rows of earlier calls are read from HBM into LDS first."""
+    t = gtrace.gossip(n, E, seed, stale_prob=0.2, stale_depth=3)
+    h = _run(t, "wave", coord32=coord32, chunk=chunk)
+    assert h.phase_times()["la_small"] == 1
+    hs = _run(t, "sweep", coord32=coord32, chunk=chunk)
+    _same_coords(h, hs, t.E, seed)
+    _same_results(h, hs)
+    o = hgref.oracle_run(t, chunk).results()
+    assert list(h.results()["order"]) == list(o["order"])
+
+
+def test_small_graph_batched():
+    """One workgroup per graph of a batch."""
+    n, G = 8, 40
+    traces = [gtrace.gossip(n, 500 + 9 * g, 900 + g, stale_prob=0.1 * (g % 3), stale_depth=3) for g in range(G)]
+    t = gtrace.concat_graphs(traces)
+    from babble_amd.hashgraph import Hashgraph
+    h = Hashgraph(n, capacity=t.E, n_graphs=G)
+    h.insert_trace(t)
+    h.RunConsensus()
+    assert h.phase_times()["la_small"] == 1
+    a = h.results()
+    off = 0
+    for g, tg in enumerate(traces):
+        if g % 7 == 0 or g == G - 1:
+            o = hgref.oracle_run(tg).results()
+            sl = slice(off, off + tg.E)
+            for k in ("round", "witness", "famous", "rr", "cts"):
+                assert np.array_equal(np.asarray(a[k])[sl], np.asarray(o[k])), (g, k)
+            assert list(h.ConsensusEvents(g) - off) == list(o["order"]), g
+        off += tg.E

@@ -117,3 +117,37 @@ def test_shard_exchange_through_torch_device_tensors(n, E, chunk):
     libs = sorted({ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln})
     print("HIP runtimes mapped:", libs)
     assert len(libs) == 1, libs   # one HIP runtime in the process (babble_amd._lib._one_hip_runtime)
+
+
+# ---- the one-GPU rehearsal of a chain-sharded recurrence (hgx_set_round_shards) --------
+@pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 81, 2, None), (64, 16000, 82, 4, None),
+                                                   (256, 30000, 83, 2, None), (256, 30000, 84, 4, None),
+                                                   (256, 24000, 85, 4, 6000)])
+def test_chain_sharded_recurrence_rehearsal(n, E, seed, shards, chunk):
+    """W persistent launches over disjoint chain blocks on concurrent streams (each block's
+    firstDescendants rows built by its own fd_build launch), handing candidate rows and granules
+    over through shared buffers: bit-exact with the single launch and with the oracle."""
+    from babble_amd.hashgraph import Hashgraph
+    t = gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3)
+
+    def run(w):
+        h = Hashgraph(n, capacity=E)
+        h.set_round_shards(w)
+        if w == 1:
+            h.set_round_kernel("persistent")
+        for lo in range(0, E, chunk or E):
+            h.insert_trace(t, lo, min(E, lo + (chunk or E)))
+            h.RunConsensus()
+        return h
+
+    hs, h1 = run(shards), run(1)
+    ph = hs.phase_times()
+    assert ph["round_p_runs"] > 0 and ph["round_p_fallbacks"] == 0, ph
+    a, b = hs.results(), h1.results()
+    for k in ("round", "witness", "famous", "rr", "cts"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    assert list(a["order"]) == list(b["order"])
+    o = hgref.oracle_run(t, chunk).results() if chunk else hgref.oracle_run(t).results()
+    for k in ("round", "rr", "cts"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(o[k])), k
+    assert list(a["order"]) == list(o["order"])

@@ -19,10 +19,10 @@ from collections import defaultdict
 
 ROLES = {
     "layout": r"k_layout",
-    "la_sweep": r"k_la_sweep|k_la_wave",
+    "la_sweep": r"k_la_sweep|k_la_wave|k_la_small",
     "fd_build": r"k_fd_build",
-    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin",
-    "round_search": r"k_round_k<|k_round_step|k_round_p<",
+    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin|k_round_p_post|k_round_p_tail",
+    "round_search": r"k_round_k<|k_round_step|k_round_p<|k_round_g<",
     "fame": r"k_fame",
     "threshold": r"k_threshold|k_wla_transpose",
     "round_received": r"k_round_received",
@@ -55,7 +55,9 @@ def main():
         w = [v for k, vs in wr.items() if re.search(rx, k) for v in vs]
         if not f:
             continue
-        corr = 2.0 if role in STREAMING else 1.0
+        # the whole-graph recurrence reads nothing but its 16-byte LDS-DMA staging
+        stream = role in STREAMING or (role == "round_search" and all("k_round_g<" in k for k in fe if re.search(rx, k)))
+        corr = 2.0 if stream else 1.0
         fetch = corr * 1024.0 * sum(f)
         write = 1024.0 * sum(w)
         res[role] = {"bytes_per_pass": fetch + write, "fetch_bytes": fetch, "fetch_correction": corr,
