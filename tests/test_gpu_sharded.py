@@ -120,9 +120,8 @@ def test_shard_exchange_through_torch_device_tensors(n, E, chunk):
 
 
 # ---- the one-GPU rehearsal of a chain-sharded recurrence (hgx_set_round_shards) --------
-@pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 81, 2, None), (64, 16000, 82, 4, None),
-                                                   (256, 30000, 83, 2, None), (256, 30000, 84, 4, None),
-                                                   (256, 24000, 85, 4, 6000)])
+@pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 81, 2, None), (256, 30000, 83, 2, None),
+                                                   (256, 24000, 85, 2, 6000)])
 def test_chain_sharded_recurrence_rehearsal(n, E, seed, shards, chunk):
     """W persistent launches over disjoint chain blocks on concurrent streams (each block's
     firstDescendants rows built by its own fd_build launch), handing candidate rows and granules
@@ -151,3 +150,13 @@ def test_chain_sharded_recurrence_rehearsal(n, E, seed, shards, chunk):
     for k in ("round", "rr", "cts"):
         assert np.array_equal(np.asarray(a[k]), np.asarray(o[k])), k
     assert list(a["order"]) == list(o["order"])
+
+
+@pytest.mark.parametrize("n,E,seed,shards", [(64, 16000, 82, 4), (256, 30000, 84, 4), (256, 30000, 86, 8)])
+def test_chain_sharded_recurrence_rehearsal_more_streams(n, E, seed, shards):
+    """W = 4, 8 shard streams: a child process with GPU_MAX_HW_QUEUES = W + 4 (one hardware queue
+    per shard, so the shards' workgroups are resident together)."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(shards + 4), PYTHONPATH=os.pathsep.join([HERE, os.path.dirname(HERE)]))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "shard_rehearsal_worker.py"), str(n), str(E), str(seed),
+                        str(shards)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), (r.stdout[-2000:], r.stderr[-3000:])

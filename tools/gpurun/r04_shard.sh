@@ -5,8 +5,8 @@ cd "$(dirname "$0")/../.."
 T="timeout -k 10"
 $T 400 python -u -m pytest tests/test_gpu_sharded.py -x -q --timeout 200 --timeout-method thread > gpurun_out/shard_tests.log 2>&1 || { tail -30 gpurun_out/shard_tests.log; exit 1; }
 tail -2 gpurun_out/shard_tests.log
-for w in 1 2 4; do
-  $T 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-chunked --no-check --round-shards $w > gpurun_out/shard_c3_w$w.json 2> gpurun_out/shard_c3_w$w.err || exit 1
+for w in 1 2 4 8; do
+  GPU_MAX_HW_QUEUES=12 $T 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-chunked --no-check --round-shards $w > gpurun_out/shard_c3_w$w.json 2> gpurun_out/shard_c3_w$w.err || exit 1
   python - $w <<'PY'
 import json, sys
 w = sys.argv[1]
