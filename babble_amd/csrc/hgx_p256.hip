@@ -9,10 +9,11 @@
 // Arithmetic: 8 x 32-bit limbs, Montgomery multiplication (CIOS, v_mad_u64_u32) modulo p
 // (field) and modulo N (scalars, s^-1 by Fermat); Jacobian points, a = -3 doubling
 // (dbl-2001-b) and complete-case addition (add-2007-bl, doubling / infinity branches per
-// lane). u1 G + u2 Q by Straus with 4-bit windows over per-key affine tables [1..15]Q built
-// once per distinct key (a sync batch has few creators) and the same table for G, so the
-// window additions are mixed Jacobian + affine (madd-2007-bl, 7M + 4S). The final
-// compare avoids the field inversion: X == r Z^2 or, when r + N < p, X == (r + N) Z^2.
+// lane). u1 G + u2 Q by fixed-base combs: for G and for every key (a context has few, each
+// signing many events) a table of b * 256^j * P for the 32 byte positions j and the 255 digits b,
+// affine, built once when the keys are set (512 KB per key, hgx_set_participant_keys); a verify is
+// then at most 64 mixed Jacobian + affine additions (madd-2007-bl, 7M + 4S) and no doubling. The
+// final compare avoids the field inversion: X == r Z^2 or, when r + N < p, X == (r + N) Z^2.
 // Public keys that are not P-256 points (Go's elliptic.Unmarshal returns nil) give 2.
 #include <hip/hip_runtime.h>
 
@@ -337,29 +338,22 @@ __device__ __forceinline__ void mpow_m2(Fe r, const Fe a, const uint32_t* e, con
     }
 }
 
-// table layout: [key][16][x | y] affine limbs (Montgomery form), entry 0 unused
-constexpr int kTabWords = 16 * 16;
-
-__device__ __forceinline__ void tab_load(Fe x, Fe y, const uint32_t* __restrict__ t) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        x[i] = t[i];
-        y[i] = t[8 + i];
-    }
-}
+// comb table layout: [key][32 byte positions j][256 digits b][x | y] affine limbs (Montgomery form):
+// entry (j, b) = b * 256^j * P; digit 0 unused. 512 KB per key; key nk is the base point G.
+constexpr int kCombPos = 32, kCombDig = 256, kEntWords = 16;
+constexpr size_t kTabWords = (size_t)kCombPos * kCombDig * kEntWords;
 
 }  // namespace p256
 
 using namespace p256;
 
-// one thread per (key, multiple j = 1..15) (keys [0, nk): 65-byte uncompressed points; key nk:
-// the base point G): [j]P by j - 1 additions, stored affine (x = X / Z^2, y = Y / Z^3; a valid
-// point of prime order has no multiple below 16 at infinity). valid[k] = 1 when the key is a
-// P-256 point (0x04 prefix, X, Y < p, Y^2 = X^3 - 3X + b).
-__global__ void __launch_bounds__(64) k_p256_tables(int nk, const uint8_t* __restrict__ keys65,
-                                                    uint32_t* __restrict__ tab, uint8_t* __restrict__ valid) {
+// Tables, step 1: one thread per (key, byte position j): P_j = 256^j P (8 j doublings of the key's
+// point), Jacobian, into base[key][j]; thread j = 0 also checks the key (0x04 prefix, X, Y < p,
+// Y^2 = X^3 - 3X + b) into valid[key]. Key nk is the base point G.
+__global__ void __launch_bounds__(64) k_p256_comb_base(int nk, const uint8_t* __restrict__ keys65,
+                                                       uint32_t* __restrict__ base, uint8_t* __restrict__ valid) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int k = t / 15, j = 1 + t % 15;
+    const int k = t / kCombPos, j = t % kCombPos;
     if (k > nk) return;
     Fe x, y;
     bool ok = true;
@@ -388,25 +382,78 @@ __global__ void __launch_bounds__(64) k_p256_tables(int nk, const uint8_t* __res
         madd<ModP>(r, r, kBm);
         ok = eq(l, r);
     }
-    if (j == 1) valid[k] = ok ? 1 : 0;
+    if (j == 0) valid[k] = ok ? 1 : 0;
     if (!ok) return;
-    uint32_t* tk = tab + (size_t)k * kTabWords;
-    Pt acc = P;
-    for (int m = 2; m <= j; m++) {
-        Pt nx;
-        padd(nx, acc, P);
-        acc = nx;
+    for (int d = 0; d < 8 * j; d++) {
+        Pt t2;
+        pdbl(t2, P);
+        P = t2;
+    }
+    uint32_t* o = base + ((size_t)k * kCombPos + j) * 24;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        o[q] = P.X[q];
+        o[8 + q] = P.Y[q];
+        o[16 + q] = P.Z[q];
+    }
+}
+
+// Tables, step 2: one thread per (key, j, digit b in [1, 255]): b P_j by double-and-add over b's
+// bits, to affine (Z^-1 by Fermat). A valid key's point has prime order, so no b P_j (b < 256, P_j
+// != O) is the point at infinity.
+__global__ void __launch_bounds__(64) k_p256_comb_fill(int nk, const uint32_t* __restrict__ base,
+                                                       const uint8_t* __restrict__ valid, uint32_t* __restrict__ tab) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = 1 + (int)(t % 255);
+    const int64_t kj = t / 255;
+    const int k = (int)(kj / kCombPos), j = (int)(kj % kCombPos);
+    if (k > nk || !valid[k]) return;
+    Pt Pj;
+    const uint32_t* bp = base + ((size_t)k * kCombPos + j) * 24;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        Pj.X[q] = bp[q];
+        Pj.Y[q] = bp[8 + q];
+        Pj.Z[q] = bp[16 + q];
+    }
+    Pt acc = Pj;
+    const int top = 31 - __builtin_clz((unsigned)b);
+    for (int bit = top - 1; bit >= 0; bit--) {
+        Pt t2;
+        pdbl(t2, acc);
+        acc = t2;
+        if ((b >> bit) & 1) {
+            padd(t2, acc, Pj);
+            acc = t2;
+        }
     }
     Fe zi, zi2, tt;
     mpow_m2<ModP>(zi, acc.Z, kPm2, kOneP);
     mmul<ModP>(zi2, zi, zi);
+    uint32_t* e = tab + (size_t)k * kTabWords + ((size_t)j * kCombDig + b) * kEntWords;
     mmul<ModP>(tt, acc.X, zi2);
 #pragma unroll
-    for (int i = 0; i < 8; i++) tk[16 * j + i] = tt[i];
+    for (int q = 0; q < 8; q++) e[q] = tt[q];
     mmul<ModP>(tt, zi2, zi);
     mmul<ModP>(zi, acc.Y, tt);
 #pragma unroll
-    for (int i = 0; i < 8; i++) tk[16 * j + 8 + i] = zi[i];
+    for (int q = 0; q < 8; q++) e[8 + q] = zi[q];
+}
+
+// byte j of a 256-bit scalar (j uniform: selects, not a dynamically indexed array in scratch)
+__device__ __forceinline__ uint32_t byte_at(const Fe u, int j) {
+    const int li = j >> 2;
+    uint32_t w = u[0];
+#pragma unroll
+    for (int q = 1; q < 8; q++) w = li == q ? u[q] : w;
+    return (w >> (8 * (j & 3))) & 255u;
+}
+
+__device__ __forceinline__ void ent_load(Fe x, Fe y, const uint32_t* __restrict__ t) {
+    const uint4* t4 = (const uint4*)t;
+    const uint4 a = t4[0], b = t4[1], c = t4[2], d = t4[3];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    y[0] = c.x; y[1] = c.y; y[2] = c.z; y[3] = c.w; y[4] = d.x; y[5] = d.y; y[6] = d.z; y[7] = d.w;
 }
 
 __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, const int32_t* __restrict__ key_idx,
@@ -439,40 +486,40 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
     mpow_m2<ModN>(w, sm, kNm2, kOneN);
     mmul<ModN>(u1, e, w);   // e s^-1 (plain form)
     mmul<ModN>(u2, r, w);
-    // Straus, 4-bit windows
+    // fixed-base combs for G and for the key: u1 G + u2 Q = sum over the 32 byte positions j of
+    // T_G[j][u1 byte j] + T_Q[j][u2 byte j], at most 64 mixed additions and no doubling; the next
+    // position's two entries are loaded while the current ones are added
     const uint32_t* __restrict__ tg = tab + (size_t)nk * kTabWords;
     const uint32_t* __restrict__ tq = tab + (size_t)k * kTabWords;
     Pt acc;
 #pragma unroll
     for (int q = 0; q < 8; q++) { acc.X[q] = 0; acc.Y[q] = 0; acc.Z[q] = 0; }
-    // limbs outer, nibbles inner
-    for (int li = 7; li >= 0; li--) {
-        const uint32_t w1 = u1[li], w2 = u2[li];
-        for (int sh = 28; sh >= 0; sh -= 4) {
-            if (!is_zero(acc.Z)) {
-                for (int d = 0; d < 4; d++) {
-                    Pt t2;
-                    pdbl(t2, acc);
-                    acc = t2;
-                }
-            }
-            const uint32_t d1 = (w1 >> sh) & 15u;
-            const uint32_t d2 = (w2 >> sh) & 15u;
-            if (d1) {
-                Fe x, y;
-                Pt nx;
-                tab_load(x, y, tg + 16 * d1);
-                pmadd(nx, acc, x, y);
-                acc = nx;
-            }
-            if (d2) {
-                Fe x, y;
-                Pt nx;
-                tab_load(x, y, tq + 16 * d2);
-                pmadd(nx, acc, x, y);
-                acc = nx;
-            }
+    Fe gx, gy, qx, qy;
+    uint32_t d1 = u1[0] & 255u, d2 = u2[0] & 255u;
+    ent_load(gx, gy, tg + (size_t)d1 * kEntWords);
+    ent_load(qx, qy, tq + (size_t)d2 * kEntWords);
+    for (int j = 0; j < kCombPos; j++) {
+        Fe ngx, ngy, nqx, nqy;
+        uint32_t n1 = 0, n2 = 0;
+        if (j + 1 < kCombPos) {
+            n1 = byte_at(u1, j + 1);
+            n2 = byte_at(u2, j + 1);
+            ent_load(ngx, ngy, tg + ((size_t)(j + 1) * kCombDig + n1) * kEntWords);
+            ent_load(nqx, nqy, tq + ((size_t)(j + 1) * kCombDig + n2) * kEntWords);
         }
+        if (d1) {
+            Pt nx;
+            pmadd(nx, acc, gx, gy);
+            acc = nx;
+        }
+        if (d2) {
+            Pt nx;
+            pmadd(nx, acc, qx, qy);
+            acc = nx;
+        }
+        d1 = n1;
+        d2 = n2;
+        cpy(gx, ngx); cpy(gy, ngy); cpy(qx, nqx); cpy(qy, nqy);
     }
     if (is_zero(acc.Z)) {
         out[i] = 0;
@@ -488,9 +535,9 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
         Fe rn;
         uint64_t c = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            c += (uint64_t)r[j] + ModN::n[j];
-            rn[j] = (uint32_t)c;
+        for (int q = 0; q < 8; q++) {
+            c += (uint64_t)r[q] + ModN::n[q];
+            rn[q] = (uint32_t)c;
             c >>= 32;
         }
         if (c == 0 && lt(rn, ModP::n)) {
@@ -502,10 +549,15 @@ __global__ void __launch_bounds__(128) k_p256_verify(int64_t count, int nk, cons
     out[i] = ok ? 1 : 0;
 }
 
-size_t p256_table_bytes(int nk) { return (size_t)(nk + 1) * kTabWords * 4; }
+// the comb tables plus the per-(key, position) base points of step 1 after them
+size_t p256_table_bytes(int nk) { return (size_t)(nk + 1) * (kTabWords + (size_t)kCombPos * 24) * 4; }
 
 void launch_p256_tables(hipStream_t s, int nk, const uint8_t* keys65, uint32_t* tab, uint8_t* valid) {
-    hipLaunchKernelGGL(k_p256_tables, dim3(((nk + 1) * 15 + 63) / 64), dim3(64), 0, s, nk, keys65, tab, valid);
+    uint32_t* base = tab + (size_t)(nk + 1) * kTabWords;
+    hipLaunchKernelGGL(k_p256_comb_base, dim3(((nk + 1) * kCombPos + 63) / 64), dim3(64), 0, s, nk, keys65, base, valid);
+    const int64_t ent = (int64_t)(nk + 1) * kCombPos * 255;
+    hipLaunchKernelGGL(k_p256_comb_fill, dim3((unsigned)((ent + 63) / 64)), dim3(64), 0, s, nk, (const uint32_t*)base,
+                       (const uint8_t*)valid, tab);
 }
 
 void launch_p256_verify(hipStream_t s, int64_t count, int nk, const int32_t* key_idx, const uint8_t* dig,
@@ -532,7 +584,7 @@ bool gfx950(int32_t device) {
            hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
-// device copies of a batch; tables + verify launched `reps` times (the last one's results kept)
+// device copies of a batch: the key tables, then verify launches (the last one's results kept)
 struct P256Run {
     uint8_t *keys = nullptr, *dig = nullptr, *r = nullptr, *s = nullptr, *valid = nullptr, *out = nullptr;
     int32_t* idx = nullptr;
@@ -561,8 +613,11 @@ struct P256Run {
         if (e == hipSuccess) e = hipMemcpyAsync(s, ss, 32 * (size_t)count, hipMemcpyHostToDevice, st);
         return e;
     }
-    hipError_t launch(int32_t nk, int64_t count) {
+    hipError_t tables(int32_t nk) {
         hgx::launch_p256_tables(st, nk, keys, tab, valid);
+        return hipGetLastError();
+    }
+    hipError_t verify(int32_t nk, int64_t count) {
         hgx::launch_p256_verify(st, count, nk, idx, dig, r, s, tab, valid, out);
         return hipGetLastError();
     }
@@ -596,7 +651,8 @@ extern "C" int32_t hgx_p256_verify_batch(int32_t device, const uint8_t* keys65, 
     {
         P256Run run;
         e = run.upload(keys65, n_keys, key_idx, digest32, r32, s32, count);
-        if (e == hipSuccess) e = run.launch(n_keys, count);
+        if (e == hipSuccess) e = run.tables(n_keys);
+        if (e == hipSuccess) e = run.verify(n_keys, count);
         if (e == hipSuccess) e = hipMemcpyAsync(out, run.out, (size_t)count, hipMemcpyDeviceToHost, run.st);
         if (e == hipSuccess) e = hipStreamSynchronize(run.st);
     }
@@ -627,9 +683,11 @@ extern "C" int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, 
         e = run.upload(keys65, n_keys, key_idx, digest32, r32, s32, count);
         if (e == hipSuccess) e = hipEventCreate(&e0);
         if (e == hipSuccess) e = hipEventCreate(&e1);
-        for (int32_t k = 0; e == hipSuccess && k < warmup; k++) e = run.launch(n_keys, count);
+        // the key tables once (a context builds them when its keys are set), then verify launches
+        if (e == hipSuccess) e = run.tables(n_keys);
+        for (int32_t k = 0; e == hipSuccess && k < warmup; k++) e = run.verify(n_keys, count);
         if (e == hipSuccess) e = hipEventRecord(e0, run.st);
-        for (int32_t k = 0; e == hipSuccess && k < iters; k++) e = run.launch(n_keys, count);
+        for (int32_t k = 0; e == hipSuccess && k < iters; k++) e = run.verify(n_keys, count);
         if (e == hipSuccess) e = hipEventRecord(e1, run.st);
         if (e == hipSuccess) e = hipMemcpyAsync(out, run.out, (size_t)count, hipMemcpyDeviceToHost, run.st);
         if (e == hipSuccess) e = hipStreamSynchronize(run.st);

@@ -353,7 +353,8 @@ def p256_leg(count, steps, warmup, device):
     """Side leg (second half): Event.Verify (hashgraph/event.go:142-152) of
     `count` signatures over 6 creator keys (a sync batch), drawn from libcrypto's known answers
     (tests/golden/p256_vectors.txt: valid, corrupted and bad-key rows), HBM-resident; device time
-    per (key tables + verify) launch from HIP events (hgx_p256_verify_bench); every result is
+    per verify launch from HIP events, the key tables built once before (hgx_p256_verify_bench, as a
+    context builds them when its keys are set); every result is
     checked against libcrypto's."""
     from babble_amd.hashgraph import p256_verify_bench
     rows = []

