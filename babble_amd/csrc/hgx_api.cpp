@@ -465,6 +465,12 @@ int32_t hgx_insert_and_run32(hgx_ctx* c, const hgx_events32* ev, int64_t count, 
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
     e = c->eng.payload_begin32(ev->timestamp_ns, ev->coin, ev->sig_s, ev->ntx, out.accepted);
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    // S lands last (FindOrder's sort waits for it); on every way out the caller's S buffer has been
+    // read completely
+    struct WaitS {
+        hgx::Engine& eng;
+        ~WaitS() { (void)eng.payload_wait_S(); }
+    } wait_s{c->eng};
     hgx::InsertOut head = out;
     head.graph_loaded.assign(c->g_loaded.begin(), c->g_loaded.end());
     hgx_error ins_err{};

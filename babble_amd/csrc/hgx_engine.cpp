@@ -579,18 +579,25 @@ hipError_t Engine::payload_begin32(const int64_t* ts, const uint8_t* coin, const
     const size_t c = (size_t)m_ok;
     if (st_ts.n < c) HGX_TRY(st_ts.alloc(c));
     if (st_coin.n < c) HGX_TRY(st_coin.alloc(c));
-    if (st_S.n < 32 * c) HGX_TRY(st_S.alloc(32 * c));
     if (st_ntx.n < c) HGX_TRY(st_ntx.alloc(c));
+    if (!ev_pay_S) HGX_TRY(hipEventCreateWithFlags(&ev_pay_S, hipEventDisableTiming));
+    if (pay_thread.joinable()) pay_thread.join();
     pay_err = hipSuccess;
     pay32 = true;
+    pay_stage = 0;
+    pay_S_pending = true;
     if (m_ok > 0) ids_known = false;
+    uint8_t* S_dst = g_S.p + 32 * (size_t)(E - m_ok);   // the accepted prefix (just appended): gids E - m_ok ..
     pay_thread = std::thread([=]() {
         hipError_t e = hipSetDevice(dev);
         if (c && e == hipSuccess) e = hipMemcpyAsync(st_ts.p, ts, c * 8, hipMemcpyHostToDevice, stream2);
         if (c && e == hipSuccess) e = hipMemcpyAsync(st_coin.p, coin, c, hipMemcpyHostToDevice, stream2);
-        if (c && e == hipSuccess) e = hipMemcpyAsync(st_S.p, S, c * 32, hipMemcpyHostToDevice, stream2);
         if (c && e == hipSuccess) e = hipMemcpyAsync(st_ntx.p, ntx, c * 4, hipMemcpyHostToDevice, stream2);
         if (e == hipSuccess) e = hipEventRecord(ev_pay, stream2);
+        pay_err_a = e;
+        pay_stage.store(1, std::memory_order_release);
+        if (c && e == hipSuccess) e = hipMemcpyAsync(S_dst, S, c * 32, hipMemcpyHostToDevice, stream2);
+        if (e == hipSuccess) e = hipEventRecord(ev_pay_S, stream2);
         if (e == hipSuccess) e = hipStreamSynchronize(stream2);
         pay_err = e;
     });
@@ -609,8 +616,10 @@ hipError_t Engine::payload_begin(const int64_t* ts, const uint8_t* hash, const u
     if (st_S.n < 32 * c) HGX_TRY(st_S.alloc(32 * c));
     if (st_ntx.n < c) HGX_TRY(st_ntx.alloc(c));
     if (st_nil.n < c) HGX_TRY(st_nil.alloc(c));
+    if (pay_thread.joinable()) pay_thread.join();
     pay_err = hipSuccess;
     pay32 = false;
+    pay_S_pending = false;
     // pageable host memory: each copy returns once its source has been consumed, so the copies
     // run on their own host thread (and stream) beside the DivideRounds launches
     pay_thread = std::thread([=]() {
@@ -629,11 +638,16 @@ hipError_t Engine::payload_begin(const int64_t* ts, const uint8_t* hash, const u
 
 hipError_t Engine::payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int32_t wcoin_r0,
                                std::vector<uint64_t>& loaded) {
-    if (pay_thread.joinable()) pay_thread.join();
-    HGX_TRY(pay_err);
+    if (pay_S_pending) {   // the compact payload: its first stage only (S lands in g_S later)
+        while (pay_stage.load(std::memory_order_acquire) == 0) std::this_thread::yield();
+        HGX_TRY(pay_err_a);
+    } else {
+        if (pay_thread.joinable()) pay_thread.join();
+        HGX_TRY(pay_err);
+    }
     HGX_TRY(hipStreamWaitEvent(stream, ev_pay, 0));
     InsertIn in{};
-    in.creator = st_creator.p; in.ts = st_ts.p; in.S = st_S.p; in.ntx = st_ntx.p;
+    in.creator = st_creator.p; in.ts = st_ts.p; in.S = pay_S_pending ? nullptr : st_S.p; in.ntx = st_ntx.p;
     if (split32) { in.index32 = st_index32.p; in.sp32 = st_sp32.p; in.op32 = st_op32.p; }
     else { in.index = st_index.p; in.sp = st_sp.p; in.op = st_op.p; }
     if (pay32) in.coin = st_coin.p;
@@ -650,6 +664,14 @@ hipError_t Engine::payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int3
     loaded.resize(G);
     std::memcpy(loaded.data(), h_ins + ins_gl_off, (size_t)G * 8);
     return hipSuccess;
+}
+
+hipError_t Engine::payload_wait_S() {
+    if (!pay_S_pending) return hipSuccess;
+    pay_S_pending = false;
+    if (pay_thread.joinable()) pay_thread.join();
+    HGX_TRY(pay_err);
+    return hipStreamWaitEvent(stream, ev_pay_S, 0);
 }
 
 hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out, const unsigned long long* fail_sig,
@@ -710,6 +732,7 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
 }
 
 hipError_t Engine::clear() {
+    HGX_TRY(payload_wait_S());
     if (E > 0) HGX_TRY(hipMemsetAsync(succ.p, 0xFF, (size_t)E * 4, stream));
     HGX_TRY(hipMemsetAsync(first_none.p, 0xFF, (size_t)C * 4, stream));
     HGX_TRY(hipMemsetAsync(last_gid_d.p, 0xFF, (size_t)C * 8, stream));   // last_gid, last_index
@@ -792,6 +815,7 @@ hipError_t Engine::get_events(std::vector<int32_t>& creator, std::vector<int32_t
 hipError_t Engine::get_columns(std::vector<int32_t>& creator, std::vector<int32_t>& index, std::vector<int32_t>& sp,
                                std::vector<int32_t>& op, std::vector<int64_t>& ts, std::vector<uint8_t>& S,
                                std::vector<uint8_t>& coin, std::vector<int32_t>& ntx, std::vector<uint8_t>& txnil) {
+    HGX_TRY(payload_wait_S());
     HGX_TRY(get_events(creator, index, sp, op));
     const size_t e = (size_t)E;
     ts.resize(e);
@@ -1557,6 +1581,7 @@ hipError_t Engine::shard_copy(int lo, int hi, void* buf, bool on_device, bool to
 // order_dst (pinned, room for the m received events): the order is copied there with the block
 // tables, in the same host round trip
 hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
+    HGX_TRY(payload_wait_S());   // (the sort's tie-break reads S)
     out.blk_cnt.assign((size_t)G * std::max(R, 1), 0);
     out.blk_ntx.assign((size_t)G * std::max(R, 1), 0);
     out.blk_loaded.assign((size_t)G * std::max(R, 1), 0);

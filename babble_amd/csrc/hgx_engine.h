@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -121,6 +122,9 @@ class Engine {
     hipError_t payload_begin(const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                              const int32_t* nil, int64_t m_ok);
     hipError_t payload_end(int64_t E0, int64_t m_ok, bool laid_out_new, int32_t wcoin_r0, std::vector<uint64_t>& loaded);
+    // the compact payload's S column (copied last, straight into g_S): wait for it (the sort's
+    // tie-break, a read-back, a clear) and for the caller's buffer to be read completely
+    hipError_t payload_wait_S();
     // the same three for the compact columns of hgx_events32 (int32 Index and parents, the coin
     // byte instead of the event id, len(Transactions) with -1 for nil): 61 instead of 108 bytes
     // per event cross PCIe
@@ -234,8 +238,14 @@ class Engine {
     bool pay32 = false;              // the payload in flight is hgx_events32's (coin byte, ntx -1 = nil)
     bool split32 = false;            // the structure columns staged by insert_split_begin32
     hipEvent_t ev_pay = nullptr;
+    // the S column is copied last, straight into g_S: only FindOrder's sort reads it, so DecideFame
+    // and the first FindOrder kernels run while it crosses PCIe (payload_wait_S before the sort)
+    hipEvent_t ev_pay_S = nullptr;
+    std::atomic<int> pay_stage{0};   // 1: ts / coin / ntx (/ hash / nil) issued and ev_pay recorded
+    bool pay_S_pending = false;
     std::thread pay_thread;
     hipError_t pay_err = hipSuccess;
+    hipError_t pay_err_a = hipSuccess;   // the compact payload's first stage (before pay_stage = 1)
     InsertState insert_state();
     void kbeg(int k, bool sample = true, int64_t count = 1);
     void kend(int k, double bytes);

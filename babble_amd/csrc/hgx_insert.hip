@@ -171,10 +171,12 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned
                 const int nt = in.ntx_at(k);
                 const int nil = in.nil_at(k);
                 st.g_ts[gid] = in.ts[k];
-                const uint4* s4 = (const uint4*)(in.S + 32 * k);
-                uint4* d4 = (uint4*)(st.g_S + 32 * gid);
-                d4[0] = s4[0];
-                d4[1] = s4[1];
+                if (in.S) {   // (the split compact payload copies S straight into g_S)
+                    const uint4* s4 = (const uint4*)(in.S + 32 * k);
+                    uint4* d4 = (uint4*)(st.g_S + 32 * gid);
+                    d4[0] = s4[0];
+                    d4[1] = s4[1];
+                }
                 st.g_coin[gid] = (uint8_t)in.coin_at(k);   // middleBit (hashgraph.go:1039-1048)
                 if (in.hash) {   // the event id, for a checkpoint (a compact insert brings only the coin)
                     const uint4* h4 = (const uint4*)(in.hash + 32 * k);
