@@ -136,7 +136,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     cap = std::max<int64_t>(cap_events, 1);
     const size_t P = (size_t)cap;
     // positions: the events plus slack for chains to grow in place between DivideRounds
-    Ppos = cap + std::max<int64_t>(cap / 4, (int64_t)256 * C);
+    Ppos = cap + std::max<int64_t>(cap / 2, (int64_t)256 * C);
     const size_t PP = (size_t)Ppos;
     HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_sp.alloc(P)); HGX_TRY(g_op.alloc(P));
     HGX_TRY(g_ntx.alloc(P)); HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P));
@@ -857,6 +857,53 @@ hipError_t Engine::reserve_rounds(int32_t rounds) {
     return hipStreamSynchronize(stream);
 }
 
+// nb round-step nodes captured as one hipGraph (their round arguments are rewritten per replay)
+hipError_t Engine::capture_steps(StepGraph& sgr, const RoundArgs& args, int kern, int nb) {
+    sgr.drop();
+    sgr.args = args;
+    sgr.kernel = kern;
+    sgr.compact = compact;
+    sgr.nb = nb;
+    HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    hipError_t le = hipSuccess;   // a failed launch ends the capture, then is reported
+    for (int k = 0; k < nb && le == hipSuccess; k++) le = launch_round_step(stream, sgr.args, k, kern);
+    const hipError_t ce = hipStreamEndCapture(stream, &sgr.graph);
+    if (le != hipSuccess) {
+        if (ce == hipSuccess && sgr.graph) (void)hipGraphDestroy(sgr.graph);
+        sgr.graph = nullptr;
+        return le;
+    }
+    HGX_TRY(ce);
+    HGX_TRY(hipGraphInstantiate(&sgr.exec, sgr.graph, nullptr, nullptr, 0));
+    // the step nodes in launch order (a linear chain)
+    size_t nn = 0;
+    HGX_TRY(hipGraphGetNodes(sgr.graph, nullptr, &nn));
+    std::vector<hipGraphNode_t> nodes(nn);
+    HGX_TRY(hipGraphGetNodes(sgr.graph, nodes.data(), &nn));
+    sgr.nodes.clear();
+    sgr.params.clear();
+    hipGraphNode_t nd_cur = nullptr;
+    for (auto nd : nodes) {
+        size_t nd_deps = 0;
+        HGX_TRY(hipGraphNodeGetDependencies(nd, nullptr, &nd_deps));
+        if (nd_deps == 0) nd_cur = nd;
+    }
+    while (nd_cur) {
+        hipKernelNodeParams kp;
+        HGX_TRY(hipGraphKernelNodeGetParams(nd_cur, &kp));
+        sgr.nodes.push_back(nd_cur);
+        sgr.params.push_back(kp);
+        size_t nd_out = 0;
+        HGX_TRY(hipGraphNodeGetDependentNodes(nd_cur, nullptr, &nd_out));
+        if (nd_out == 0) break;
+        std::vector<hipGraphNode_t> outs(nd_out);
+        HGX_TRY(hipGraphNodeGetDependentNodes(nd_cur, outs.data(), &nd_out));
+        nd_cur = outs[0];
+    }
+    if ((int)sgr.nodes.size() != nb) return hipErrorUnknown;
+    return hipSuccess;
+}
+
 // ---- DivideRounds ---------------------------------------------------------------
 // Chains are laid out with slack (positions [c_off[c], c_off[c] + slot)), so that a call
 // after more InsertEvents only appends rows: the events of earlier calls keep their
@@ -887,12 +934,18 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     max_len = new_max_len;
     const size_t csz = compact ? 2 : 4;
     if (rebuild) {
-        // slack shared evenly by the chains
-        const int64_t slack = (Ppos - En) / C;
+        // slack in shares: two for a chain with events, one for a chain without (a silent peer, or
+        // one that has not created an event yet). With even shares c5's 341 silent peers held a
+        // third of the slack and the live chains outgrew theirs two thirds through the run (an
+        // 18.8 ms rebuild call)
+        int act = 0;
+        for (int c = 0; c < C; c++) act += chain_len[c] > 0 ? 1 : 0;
+        const int64_t share = (Ppos - En) / (2 * (int64_t)act + (C - act));
         h_off.assign(C + 1, 0);
-        // slots of multiples of 32 positions (slack >= 256 > 31): every chain starts 64-byte
-        // aligned in the firstDescendants columns (the persistent round kernel's staging)
-        for (int c = 0; c < C; c++) h_off[c + 1] = h_off[c] + ((chain_len[c] + (int32_t)slack) & ~31);
+        // slots of multiples of 32 positions (a share >= 128 > 31: Ppos >= capacity + 256 C): every
+        // chain starts 64-byte aligned in the firstDescendants columns (the round kernels' staging)
+        for (int c = 0; c < C; c++)
+            h_off[c + 1] = h_off[c] + ((chain_len[c] + (int32_t)((chain_len[c] > 0 ? 2 : 1) * share)) & ~31);
         HGX_TRY(hipMemcpyAsync(c_off.p, h_off.data(), (C + 1) * 4, hipMemcpyHostToDevice, stream));
         h_len_div.assign(C, 0);
         last_rebuild = true;
@@ -1269,6 +1322,13 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             r_done = -1;
         }
     }
+    if (r_done >= 0 && rebuild && !graph_ok && !rooted && round_kernel == 0) {
+        // the resumed calls that follow use the per-launch steps: their hipGraphs are captured and
+        // instantiated now, inside this (long) rebuild call, not in the first short resumed one
+        // (c2: a 7 ms first resumed call)
+        for (int i = 1; i <= 2; i++)
+            if (!step_g[i].exec) HGX_TRY(capture_steps(step_g[i], round_args(), 0, i == 1 ? kStepBatchSmall : 2 * kStepBatchSmall));
+    }
     if (r_done < 0) launch_round_k_gather(stream, round_args(), r_lo);   // W'_{r_lo} rebased for k_round_k
     // a rebuild replays kStepBatch steps per hipGraph; a resumed call (a few rounds) 2 or 4: a
     // round holds ~10-14 events per chain, so fewer than 6 new events per chain rarely take
@@ -1290,50 +1350,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             const int kern = (rooted || round_kernel != 1) ? 0 : 1;   // root floors: per-candidate step only
             const RoundArgs cur = round_args();
             if (!sgr.exec || sgr.kernel != kern || sgr.compact != compact || sgr.nb != nb || sgr.args.gB != cur.gB ||
-                sgr.args.gmax != cur.gmax) {
-                sgr.drop();
-                sgr.args = cur;
-                sgr.kernel = kern;
-                sgr.compact = compact;
-                sgr.nb = nb;
-                HGX_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                hipError_t le = hipSuccess;   // a failed launch ends the capture, then is reported
-                for (int k = 0; k < nb && le == hipSuccess; k++) le = launch_round_step(stream, sgr.args, k, kern);
-                const hipError_t ce = hipStreamEndCapture(stream, &sgr.graph);
-                if (le != hipSuccess) {
-                    if (ce == hipSuccess && sgr.graph) (void)hipGraphDestroy(sgr.graph);
-                    sgr.graph = nullptr;
-                    return le;
-                }
-                HGX_TRY(ce);
-                HGX_TRY(hipGraphInstantiate(&sgr.exec, sgr.graph, nullptr, nullptr, 0));
-                // the step nodes in launch order (a linear chain)
-                size_t nn = 0;
-                HGX_TRY(hipGraphGetNodes(sgr.graph, nullptr, &nn));
-                std::vector<hipGraphNode_t> nodes(nn);
-                HGX_TRY(hipGraphGetNodes(sgr.graph, nodes.data(), &nn));
-                sgr.nodes.clear();
-                sgr.params.clear();
-                hipGraphNode_t cur = nullptr;
-                for (auto nd : nodes) {
-                    size_t nd_deps = 0;
-                    HGX_TRY(hipGraphNodeGetDependencies(nd, nullptr, &nd_deps));
-                    if (nd_deps == 0) cur = nd;
-                }
-                while (cur) {
-                    hipKernelNodeParams kp;
-                    HGX_TRY(hipGraphKernelNodeGetParams(cur, &kp));
-                    sgr.nodes.push_back(cur);
-                    sgr.params.push_back(kp);
-                    size_t nd_out = 0;
-                    HGX_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd_out));
-                    if (nd_out == 0) break;
-                    std::vector<hipGraphNode_t> outs(nd_out);
-                    HGX_TRY(hipGraphNodeGetDependentNodes(cur, outs.data(), &nd_out));
-                    cur = outs[0];
-                }
-                if ((int)sgr.nodes.size() != nb) return hipErrorUnknown;
-            }
+                sgr.args.gmax != cur.gmax)
+                HGX_TRY(capture_steps(sgr, cur, kern, nb));
             const int slot = launched & 1;
             // the batch's last step writes round + 1 into this slot's host-mapped flag when a
             // chain still has events beyond its boundary (no D2H copy between the replays)

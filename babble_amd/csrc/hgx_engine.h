@@ -223,6 +223,7 @@ class Engine {
     hipStream_t sh_stream[kMaxRoundShards] = {};
     hipEvent_t sh_ev[kMaxRoundShards + 1] = {};
     hipError_t ensure_shard_streams();
+    hipError_t capture_steps(StepGraph& sgr, const RoundArgs& args, int kern, int nb);
     bool la_small_used = false;   // the last DivideRounds built lastAncestors with k_la_small
     int la_small_override = -1;   // 0: never k_la_small (hgx_set_la_kernel 2), else where it applies
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
