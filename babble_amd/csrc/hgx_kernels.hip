@@ -1080,7 +1080,8 @@ __global__ void __launch_bounds__(256) k_cts_small(const int32_t* __restrict__ f
 // kept in LDS as 32-bit offsets from the event's own timestamp (an event whose offsets
 // do not fit is flagged and redone from global memory in 64 bits). Phase 2, one wave
 // per event: radix select of element floor(m/2) in registers.
-constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8 (round 2); 4: 13.4 vs 8.2 (round 3)
+constexpr int kCtsTile = 8;   // c3: 10.77 ms at 32 positions, 10.35 at 16, 10.05 at 8 (round 2); 4: 13.4 vs 8.2 (round 3);
+                              // round 4 (two levels, runs): 8 -> 7.2 ms, 16 -> 7.6, 4 -> 13.6
 template <int NPAD, typename CT>
 __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu, const int32_t* __restrict__ rcnt,
                                                   const int32_t* __restrict__ p_rr,
@@ -1094,85 +1095,126 @@ __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu
     constexpr int CPL = NPAD / 64;
     extern __shared__ __attribute__((aligned(16))) uint32_t vals[];   // [NPAD][LD] offsets + 2^31
     __shared__ uint32_t mem[T][NPAD / 32];         // membership bits per event
-    __shared__ int32_t e_row[T], e_j[T], e_fb[T], e_g[T];
+    __shared__ int32_t e_row[T];
     __shared__ int64_t e_ts[T];
     __shared__ int32_t e_ovf[T];
     __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
-    __shared__ int32_t s_any;
     // time-major tiles over the newly received events [fu, fu + rcnt) of each chain: block
     // i = tile i / C of chain i % C, so the blocks in flight cover every chain at about the
     // same time and their timestamp gathers (events of other chains at that time) share
     // lines in L2
     const int tc = c_lo + (int)(blockIdx.x % (unsigned)c_cnt), tt = (int)(blockIdx.x / (unsigned)c_cnt);
-    const int64_t p0 = (int64_t)c_off[tc] + fu[tc] + (int64_t)tt * T;
-    const int64_t pend = (int64_t)c_off[tc] + fu[tc] + rcnt[tc];
-    if (threadIdx.x == 0) s_any = 0;
-    for (int k = threadIdx.x; k < T * (NPAD / 32); k += 256) mem[k / (NPAD / 32)][k % (NPAD / 32)] = 0;
-    __syncthreads();
-    if (threadIdx.x < T) {
-        const int e = threadIdx.x;
-        const int64_t p = p0 + e;
-        int row = -1;
-        if (p < pend) {
-            s_any = 1;
-            const int gc = tc, g = gc / n, i = p_rr[p];
-            row = i;
-            e_j[e] = c_base[gc] + (int)(p - c_off[gc]);
-            e_fb[e] = i * C + g * n;   // < 2^31: round tables are int32-indexed
-            e_g[e] = gc;
-            e_ts[e] = p_ts[p];
+    const int64_t q0 = (int64_t)c_off[tc] + fu[tc];
+    const int64_t p0 = q0 + (int64_t)tt * T, pend = q0 + rcnt[tc];
+    if (p0 >= pend) return;   // (block-uniform) no event in this tile
+    // phase 1: lane = event e (32 per half-wave), 8 chain groups over the block. Two dependent
+    // global levels per tile: (1) the event's round received and timestamp, the FD values of its
+    // chains and the chains' position bases; (2) the famous witnesses' lastAncestors (WLAT row of
+    // the round received) beside the timestamp gathers, whose positions need only the FD values
+    // (an FD of a chain that turns out not to be a member gathers a valid timestamp, masked
+    // after). Round 3 read rr / ts in a first level and WLAT and FD in a second, so the gathers
+    // were a third level.
+    constexpr int NG = 256 / T;                                  // chain groups
+    const int e = threadIdx.x & (T - 1), cg = threadIdx.x / T;   // cg in [0, NG)
+    const int64_t p = p0 + e;
+    const bool ev = p < pend;
+    const int64_t pl = ev ? p : p0;   // a valid position for the loads of a missing event
+    const int i = p_rr[pl];
+    const int64_t base = p_ts[pl];
+    const int g = tc / n;
+    const int j = c_base[tc] + (int)(pl - c_off[tc]);
+    // runs of U consecutive chains per thread, every load of a level issued before anything waits
+    // for it (branch-free: non-members load valid dummy addresses and are masked). The kernel is
+    // bound by its vector-memory instruction count (the no-gather / no-select builds: 8.6 ms with
+    // everything, 8.1 without the selects, 4.9 without the gathers too), so the per-chain terms a
+    // thread needs for a run (its chains' position bases c_off - c_base and the WLAT row) are
+    // 16-byte loads, and a run's membership bits are one LDS atomic. The FD values, the chain
+    // bases and the gathered timestamps of a run are live at once: runs of at most 8 chains (16 at
+    // n = 1 024: 227 VGPRs, 2 waves per SIMD, c5 4.2 against 3.7 ms).
+    constexpr int U = (NPAD / NG < 8) ? NPAD / NG : 8;
+    constexpr int NB = NPAD / (NG * U);   // runs per thread (n <= NPAD)
+    constexpr int NBP = NB < 16 / U ? NB : (16 / U > 0 ? 16 / U : 1);   // runs loaded in level 1
+    static_assert(U == 2 || U % 4 == 0, "k_cts_tile: runs of 2 or of a multiple of 4 chains");
+    const bool vec = (n & (U == 2 ? 1 : 3)) == 0;   // rows and runs 8- / 16-byte aligned
+    // o[u] = src[c0 + u] for the run's chains below n (src[0] past n)
+    auto ld_run = [&](const int32_t* __restrict__ src, int c0, int32_t (&o)[U]) {
+        if (vec && c0 + U <= n) {
+            if constexpr (U == 2) {
+                const int2 v = *(const int2*)(src + c0);
+                o[0] = v.x; o[1] = v.y;
+            } else {
+#pragma unroll
+                for (int k = 0; k < U / 4; k++) {
+                    const int4 v = ((const int4*)(src + c0))[k];
+                    o[4 * k] = v.x; o[4 * k + 1] = v.y; o[4 * k + 2] = v.z; o[4 * k + 3] = v.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) o[u] = src[c0 + u < n ? c0 + u : 0];
         }
-        e_row[e] = row;
+    };
+    int32_t fdv[U][NBP], kdv[U][NBP];
+    auto load_fd = [&](int bq, int32_t (&f)[U], int32_t (&kd)[U]) {
+        const int c0 = (bq * NG + cg) * U;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int cc = c0 + u < n ? c0 + u : 0;
+            f[u] = Coord<CT>::fd(FDT[(size_t)cc * Pcap + pl]);
+        }
+        int32_t co[U], cb[U];
+        ld_run(c_off + g * n, c0, co);
+        ld_run(c_base + g * n, c0, cb);
+#pragma unroll
+        for (int u = 0; u < U; u++) kd[u] = co[u] - cb[u];
+    };
+#pragma unroll
+    for (int bq = 0; bq < NBP; bq++) {
+        int32_t f[U], kd[U];
+        load_fd(bq, f, kd);
+#pragma unroll
+        for (int u = 0; u < U; u++) { fdv[u][bq] = f[u]; kdv[u][bq] = kd[u]; }
+    }
+    // the membership words start empty; e_ovf too (after this barrier every wave may set them).
+    // An LDS-only barrier: the loads above stay in flight across it.
+    for (int k = threadIdx.x; k < T * (NPAD / 32); k += 256) mem[k / (NPAD / 32)][k % (NPAD / 32)] = 0;
+    if (threadIdx.x < T) {
+        e_row[e] = (ev && i >= 0) ? i : -1;
+        e_ts[e] = base;
         e_ovf[e] = 0;
     }
-    __syncthreads();
-    if (!s_any) return;
-    // phase 1: lane = event e (32 per half-wave), 8 chain groups over the block
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     {
-        constexpr int NG = 256 / T;                                  // chain groups
-        const int e = threadIdx.x & (T - 1), cg = threadIdx.x / T;   // cg in [0, NG)
-        const int i = e_row[e];
-        const int64_t p = p0 + e;
-        const int gc = (i >= 0) ? e_g[e] : 0;
-        const int g = gc / n;
-        const int j = (i >= 0) ? e_j[e] : 0;
-        const size_t fb = (i >= 0) ? (size_t)e_fb[e] : 0;
-        const size_t wrow = (size_t)(fb + (gc - g * n)) * n;   // WLAT row (i, g, d)
-        const int64_t base = (i >= 0) ? e_ts[e] : 0;
+        const bool evi = ev && i >= 0;
+        const int32_t* __restrict__ wrow = WLAT + ((size_t)(evi ? i : 0) * C + tc) * n;   // WLAT row (i, chain of the event)
         bool ovf = false;
-        // batches of U chains: all independent loads first, then the dependent gathers
-        // (branch-free: non-members gather a valid dummy index and are masked). Up to
-        // 32 chains per batch (every gather of the tile in one batch at n = 256, T = 32)
-        // measured 11.45 -> 10.66 ms at c3 against 4; a per-tile LDS table of the per-chain terms
-        // (thresholds, chain bases) measured slower (14.3 ms: one more dependent round
-        // trip per tile, and the LDS cost a resident block).
-        constexpr int U = (NPAD / NG < 32) ? NPAD / NG : 32;
-        for (int c0 = cg; c0 < n; c0 += NG * U) {
-            // idx < 0 marks a non-member (kept in VGPRs: 32 lane masks would spill SGPRs)
-            int32_t idx[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int c = c0 + NG * u;
-                const bool in = i >= 0 && c < n;
-                const int cc = in ? c : 0;
-                const int ch = g * n + cc;
-                const int32_t w = WLAT[wrow + cc];
-                const int32_t k = c_off[ch] - c_base[ch] + Coord<CT>::fd(FDT[(size_t)cc * Pcap + (in ? p : 0)]);
-                idx[u] = (in & (w >= j)) ? k : -1;
-            }
+        for (int bq = 0; bq < NB; bq++) {
+            const int c0 = (bq * NG + cg) * U;
+            int32_t w[U];
             int64_t x[U];
+            ld_run(wrow, c0, w);
+            int32_t f[U], kd[U];
+            if (bq < NBP) {
 #pragma unroll
-            for (int u = 0; u < U; u++) x[u] = p_ts[max(idx[u], 0)];
-            bool ok[U];
+                for (int u = 0; u < U; u++) { f[u] = fdv[u][bq < NBP ? bq : 0]; kd[u] = kdv[u][bq < NBP ? bq : 0]; }
+            } else {
+                load_fd(bq, f, kd);   // (n > 512: a third level for the later runs)
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) x[u] = p_ts[f[u] != kMaxI32 ? kd[u] + f[u] : 0];
+            uint32_t bits = 0;   // the run's membership bits (a run of <= 8 chains lies in one 32-bit word)
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int c = c0 + NG * u;
-                ok[u] = idx[u] >= 0;
+                const int c = c0 + u;
+                // a member's FD exists: its famous witness descends from the event
+                const bool ok = evi && c < n && w[u] >= j;
                 const int64_t dlt = x[u] - base;
-                ovf |= ok[u] && (dlt < INT32_MIN || dlt > INT32_MAX);
+                ovf |= ok && (dlt < INT32_MIN || dlt > INT32_MAX);
                 if (c < n) vals[c * LD + e] = (uint32_t)(int32_t)dlt ^ 0x80000000u;
-                if (ok[u]) atomicOr(&mem[e][c >> 5], 1u << (c & 31));
+                bits |= (ok ? 1u : 0u) << u;
             }
+            if (bits) atomicOr(&mem[e][c0 >> 5], bits << (c0 & 31));
         }
         if (ovf) e_ovf[e] = 1;
     }
@@ -1198,7 +1240,7 @@ __global__ void __launch_bounds__(256) k_cts_tile(const int32_t* __restrict__ fu
             res = e_ts[e] + (int64_t)(int32_t)(u ^ 0x80000000u);
         } else {   // rare: offsets beyond 32 bits -> regather and select in 64 bits
             const int64_t p = p0 + e;
-            const int gc = e_g[e], g = gc / n;
+            const int g = tc / n;
             uint64_t v[CPL];
 #pragma unroll
             for (int q = 0; q < CPL; q++) {
