@@ -415,7 +415,9 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     }
     __syncthreads();
     const bool last = (k1 == len);
-    const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    // (wave index in an SGPR: the per-target loop bounds below are then scalar, not an exec-masked
+    // loop with a VALU division)
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
     // per target chain d: lane k = tile row k owns d's events j in (v[k-1], v[k]]
     // (v = LA[(c, k0+k)][d], monotone in k; FD[(d,j)][c] = row k). The owner of every
     // position is found without per-lane loops: each non-empty range marks its first
@@ -430,9 +432,9 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     const int ownv = base_c + k0;
     // gridDim.z > 1 (a resumed call: a few new rows per chain): the target chains are split over
     // z blocks, so a block's serial per-target loop is z times shorter
-    const int S = nwaves * (int)gridDim.z;   // target stride
+    const int S = __builtin_amdgcn_readfirstlane(nwaves * (int)gridDim.z);   // target stride
     // the events' chains d in [d_lo, d_hi) (all of them but in the sharded rehearsal)
-    for (int d0 = d_lo + wave + nwaves * (int)blockIdx.z; d0 < d_hi; d0 += S * 64) {
+    for (int d0 = __builtin_amdgcn_readfirstlane(d_lo + wave + nwaves * (int)blockIdx.z); d0 < d_hi; d0 += S * 64) {
         const int dq = d0 + S * lane;
         int q_len = 0, q_base = 0, q_off = 0, q_lo = 0, q_hv = 0;
         if (dq < d_hi) {
@@ -442,7 +444,7 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
             q_lo = (k0 > 0) ? K::la(tile[dq]) : q_base - 1;
             if (rows > 0) q_hv = K::la(tile[rows * ld + dq]);
         }
-        const int nq = min(64, (d_hi - d0 + S - 1) / S);
+        const int nq = __builtin_amdgcn_readfirstlane(min(64, (d_hi - d0 + S - 1) / S));
         int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0]) : 0;
         for (int q = 0; q < nq; q++) {
             const int vraw = vnext;
