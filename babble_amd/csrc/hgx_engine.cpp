@@ -684,10 +684,12 @@ hipError_t Engine::insert_impl(const InsertIn& in, int64_t count, InsertOut& out
         // the kernels take the prefix from the first-failure words, so the batch costs one host
         // round trip (the chunked schedule inserts 1 000 events per call)
         // (ins_fail is ~0 here: set at creation, re-armed by the read-back below)
-        launch_insert_claim(stream, count, E0, cap, C, in, st);
-        launch_insert_check(stream, count, E0, cap, C, n, in, st);
-        launch_insert_commit(stream, count, ins_fail.p, fail_sig, E0, n, in, st, commit_mode);
-        launch_insert_unclaim(stream, count, ins_fail.p, fail_sig, E0, cap, C, in, st);
+        if (!launch_insert_fused(stream, count, fail_sig, E0, cap, C, n, in, st, commit_mode)) {
+            launch_insert_claim(stream, count, E0, cap, C, in, st);
+            launch_insert_check(stream, count, E0, cap, C, n, in, st);
+            launch_insert_commit(stream, count, ins_fail.p, fail_sig, E0, n, in, st, commit_mode);
+            launch_insert_unclaim(stream, count, ins_fail.p, fail_sig, E0, cap, C, in, st);
+        }
         HGX_TRY(copy_to_pinned(h_small, ins_fail.p, 8, 0xFF));
         if (fail_sig) HGX_TRY(copy_to_pinned(h_small + 2, fail_sig, 8));
     }

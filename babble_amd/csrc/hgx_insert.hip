@@ -29,10 +29,8 @@ namespace hgx {
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
-__global__ void __launch_bounds__(256) k_insert_claim(int64_t m, int64_t E0, int64_t cap, int C, InsertIn in,
-                                                      InsertState st) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
+__device__ __forceinline__ void ins_claim(int64_t k, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                                          const InsertState& st) {
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
     const int64_t sp = in.sp_at(k);
@@ -41,6 +39,12 @@ __global__ void __launch_bounds__(256) k_insert_claim(int64_t m, int64_t E0, int
     } else if (sp >= 0 && sp < gid && sp < cap) {
         atomicMin(&st.succ[sp], (uint32_t)gid);
     }
+}
+
+__global__ void __launch_bounds__(256) k_insert_claim(int64_t m, int64_t E0, int64_t cap, int C, InsertIn in,
+                                                      InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) ins_claim(k, E0, cap, C, in, st);
 }
 
 __device__ __forceinline__ int creator_of(int64_t x, int64_t E0, const InsertIn& in, const InsertState& st) {
@@ -76,10 +80,8 @@ __device__ bool others_has(const InsertState& st, const uint8_t* h) {
 
 // other-parent (genesis Root only: "" or a known event of the same graph), capacity,
 // then the RollingIndex rules of SetEvent.
-__global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int64_t cap, int C, int n, InsertIn in,
-                                                      InsertState st) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
+__device__ __forceinline__ void ins_check(int64_t k, int64_t E0, int64_t cap, int C, int n, const InsertIn& in,
+                                          const InsertState& st) {
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
     const int64_t sp = in.sp_at(k), op = in.op_at(k), idx = in.idx_at(k);
@@ -116,6 +118,12 @@ __global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int
     if (code != INS_OK) atomicMin(st.fail, ((unsigned long long)k << 8) | (unsigned long long)code);
 }
 
+__global__ void __launch_bounds__(256) k_insert_check(int64_t m, int64_t E0, int64_t cap, int C, int n, InsertIn in,
+                                                      InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) ins_check(k, E0, cap, C, n, in, st);
+}
+
 // the accepted prefix of a batch of m from the first-failure words (no host round trip between
 // the checks and the commit): Verify comes first in InsertEvent, so at the same event the
 // signature's failure wins; fail == nullptr: all m
@@ -138,14 +146,13 @@ __device__ __forceinline__ int64_t accepted_prefix(int64_t m, const unsigned lon
 // mode: kCommitAll, or the split of hgx_insert_and_run: kCommitStructure (the columns validation
 // and DivideRounds read) now, kCommitPayload (timestamps, S, coin, transactions, IsLoaded and the
 // graphs' loaded counts) once the payload columns have landed
-__global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned long long* fail,
-                                                       const unsigned long long* fail_sig, int64_t E0, int n,
-                                                       InsertIn in, InsertState st, int mode) {
+__device__ __forceinline__ void ins_commit(int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
+                                           int64_t E0, int n, const InsertIn& in, const InsertState& st, int mode,
+                                           int64_t first, int64_t stride) {
     const int64_t m_ok = accepted_prefix(m, fail, fail_sig);
     int acc_g = -1;                 // wave-uniform: the graph whose loaded count is pending
     unsigned long long acc = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < m_ok; k0 += stride) {
+    for (int64_t k0 = first; k0 < m_ok; k0 += stride) {
         const int64_t k = k0 + threadIdx.x;
         bool ld = false;
         int g = -1;
@@ -209,6 +216,12 @@ __global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned
     if (acc_g >= 0 && acc && lane_id() == 0) atomicAdd(&st.graph_loaded[acc_g], acc);
 }
 
+__global__ void __launch_bounds__(256) k_insert_commit(int64_t m, const unsigned long long* fail,
+                                                       const unsigned long long* fail_sig, int64_t E0, int n,
+                                                       InsertIn in, InsertState st, int mode) {
+    ins_commit(m, fail, fail_sig, E0, n, in, st, mode, (int64_t)blockIdx.x * blockDim.x, (int64_t)gridDim.x * blockDim.x);
+}
+
 // p_ts of the events [E0, E0 + m) from their gid-order timestamps (the layout copied them
 // before the payload of hgx_insert_and_run had landed)
 __global__ void k_ts_to_pos(int64_t E0, int64_t m, const int32_t* __restrict__ g_pos, const int64_t* __restrict__ g_ts,
@@ -222,11 +235,8 @@ void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos
 }
 
 // withdraw the claims of the discarded events [m_ok, m)
-__global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, const unsigned long long* fail,
-                                                        const unsigned long long* fail_sig, int64_t E0, int64_t cap,
-                                                        int C, InsertIn in, InsertState st) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m || k < accepted_prefix(m, fail, fail_sig)) return;
+__device__ __forceinline__ void ins_unclaim(int64_t k, int64_t E0, int64_t cap, int C, const InsertIn& in,
+                                            const InsertState& st) {
     const int64_t gid = E0 + k;
     const int cr = in.creator[k];
     const int64_t sp = in.sp_at(k);
@@ -235,6 +245,42 @@ __global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, const unsigne
     } else if (sp >= 0 && sp < gid && sp < cap) {
         if (st.succ[sp] == (uint32_t)gid) st.succ[sp] = kNone32;
     }
+}
+
+__global__ void __launch_bounds__(256) k_insert_unclaim(int64_t m, const unsigned long long* fail,
+                                                        const unsigned long long* fail_sig, int64_t E0, int64_t cap,
+                                                        int C, InsertIn in, InsertState st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m && k >= accepted_prefix(m, fail, fail_sig)) ins_unclaim(k, E0, cap, C, in, st);
+}
+
+// A batch of at most 1 024 events (the chunked schedule's SyncLimit-sized inserts): the four phases
+// above in ONE workgroup, a barrier between them instead of a kernel boundary (three launches fewer
+// per call).
+constexpr int kInsertFusedMax = 1024;
+__global__ void __launch_bounds__(kInsertFusedMax) k_insert_fused(int64_t m, const unsigned long long* fail_sig,
+                                                                  int64_t E0, int64_t cap, int C, int n, InsertIn in,
+                                                                  InsertState st, int mode) {
+    const int64_t k = threadIdx.x;
+    // (each phase's atomics complete at L2 before the barrier: the next phase's loads miss the L1,
+    // which holds no line of succ / first_none / fail before they are read)
+    if (k < m) ins_claim(k, E0, cap, C, in, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (k < m) ins_check(k, E0, cap, C, n, in, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ins_commit(m, st.fail, fail_sig, E0, n, in, st, mode, 0, blockDim.x);
+    __syncthreads();
+    if (k < m && k >= accepted_prefix(m, st.fail, fail_sig)) ins_unclaim(k, E0, cap, C, in, st);
+}
+
+bool launch_insert_fused(hipStream_t s, int64_t m, const unsigned long long* fail_sig, int64_t E0, int64_t cap, int C,
+                         int n, const InsertIn& in, const InsertState& st, int mode) {
+    if (m <= 0 || m > kInsertFusedMax) return false;
+    const unsigned thr = (unsigned)((m + 63) / 64 * 64);
+    hipLaunchKernelGGL(k_insert_fused, dim3(1), dim3(thr), 0, s, m, fail_sig, E0, cap, C, n, in, st, mode);
+    return true;
 }
 
 static inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }

@@ -281,6 +281,9 @@ void launch_insert_commit(hipStream_t s, int64_t m, const unsigned long long* fa
 void launch_ts_to_pos(hipStream_t s, int64_t E0, int64_t m, const int32_t* g_pos, const int64_t* g_ts, int64_t* p_ts);
 void launch_insert_unclaim(hipStream_t s, int64_t m, const unsigned long long* fail, const unsigned long long* fail_sig,
                            int64_t E0, int64_t cap, int C, const InsertIn& in, const InsertState& st);
+// claim + check + commit + unclaim of a batch of at most 1 024 events in one workgroup (false: larger)
+bool launch_insert_fused(hipStream_t s, int64_t m, const unsigned long long* fail_sig, int64_t E0, int64_t cap, int C,
+                         int n, const InsertIn& in, const InsertState& st, int mode);
 // verify results vout[k] (1 valid, 0 invalid, 2 key not a point) -> *fail = min (k << 8 | code)
 void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* creator, const uint8_t* vout,
                              unsigned long long* fail);

@@ -354,16 +354,22 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     extern __shared__ __attribute__((aligned(16))) int32_t sm[];
     const int c = blockIdx.x;
     const int len = c_len[c];
-    // incremental: from the tile holding the chain's first new row (entries of earlier rows
-    // in that tile are rewritten with the same values); new positions start as none
-    int t = blockIdx.y;
+    // new positions start as none (k_init_new)
+    int k0;
     if (c_old) {
+        // incremental: tiles from the chain's first new row itself (not from the 64-aligned tile
+        // holding it): an older row already owns every position up to its own value, so only the
+        // new rows can own a position whose firstDescendant on c changes (a chunked call then
+        // stages its few new rows per chain instead of up to 65)
         if (c_old[c] >= len) return;
-        t += c_old[c] / FT;
+        k0 = c_old[c] + (int)blockIdx.y * FT;
+        if (k0 >= len) return;
+    } else {
+        const int ntiles = max(1, (len + FT - 1) / FT);
+        if ((int)blockIdx.y >= ntiles) return;
+        k0 = (int)blockIdx.y * FT;
     }
-    const int ntiles = max(1, (len + FT - 1) / FT);
-    if (t >= ntiles) return;
-    const int k0 = t * FT, k1 = min(len, k0 + FT), rows = k1 - k0;
+    const int k1 = min(len, k0 + FT), rows = k1 - k0;
     const int off = c_off[c], base_c = c_base[c];
     const int g = c / n, cl = c % n;
     // per target chain d of this graph, then the (FT+1)-row tile (row 0 = row k0-1),
@@ -1906,9 +1912,8 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
                      int max_new, int d_lo, int d_hi) {
     if (d_hi < 0) d_hi = n;
     const int ft = fd_tile_rows(n, a.compact);
-    // incremental (c_old): tiles from the one holding each chain's first new row;
-    // max_new = the most new rows of a chain
-    const int tiles = c_old ? (max_new + ft - 1) / ft + 1 : max(1, (max_len + ft - 1) / ft);
+    // incremental (c_old): tiles from each chain's first new row; max_new = the most new rows of a chain
+    const int tiles = c_old ? max(1, (max_new + ft - 1) / ft) : max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
     // + 8 waves x 64 owner slots
     const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n + 8 * 64) * sizeof(int32_t);
