@@ -99,6 +99,7 @@ def lib():
     _sig(L, "hgx_abi_version", i32, [])
     _sig(L, "hgx_create", p, [i32, i64, i32, E])
     _sig(L, "hgx_create_batch", p, [i32, i32, i64, i32, E])
+    _sig(L, "hgx_create_sharded", p, [i32, i64, i32, p, E])
     _sig(L, "hgx_destroy", None, [p])
     _sig(L, "hgx_insert_events", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_insert_events_device", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])

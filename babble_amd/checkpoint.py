@@ -158,6 +158,8 @@ def read(path: str) -> dict:
             out["keys"] = take(np.uint8, 65 * C, (C, 65))
         if flags & PAYLOADS:
             off = take("<i8", E + 1)
+            if E >= 0 and (off[0] != 0 or np.any(np.diff(off) < 0)):
+                raise ValueError("payload offsets decrease")   # (libhgx rejects the same file)
             blob = take(np.uint8, int(off[-1]) if E >= 0 else 0).tobytes()
             out["payloads"] = [blob[off[i]:off[i + 1]] for i in range(E)]
     except ValueError:

@@ -10,7 +10,9 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hgx.h"
@@ -141,6 +143,14 @@ struct hgx_ctx {
     // commitCh (hashgraph.go:848-854): called for every new block with transactions
     hgx_commit_fn commit_fn = nullptr;
     void* commit_user = nullptr;
+    // a chain-sharded group (hgx_create_sharded / hgx_set_round_shards): this context
+    // is shard 0 and owns the other shards' contexts (each a whole context on its device, driven
+    // with the same calls) and the group; empty / null otherwise
+    std::vector<hgx_ctx*> peers;
+    hgx::ShardGroup* grp = nullptr;
+    void* gx_out = nullptr;   // FindOrder's timestamp exchange: this shard's values (device memory)
+    void* gx_in = nullptr;    // ... another shard's, copied here before the import
+    size_t gx_out_cap = 0, gx_in_cap = 0;
 };
 
 static void set_err(hgx_error* err, int32_t code, const std::string& msg) {
@@ -183,6 +193,50 @@ struct DeviceGuard {
         if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
     }
 };
+
+// ---- chain-sharded group helpers ----------------------------------------
+// f(context, err) on shard 0 (this thread) and on every other shard (a thread each), concurrently:
+// the engines meet at the group's barriers inside DivideRounds. A shard whose call fails breaks the
+// barriers (the others leave with an error too). Shard 0's outcome first, then the first other one.
+template <typename F>
+static int32_t on_shards(hgx_ctx* c, hgx_error* err, F&& f) {
+    hgx::ShardGroup* g = c->grp;
+    g->rearm();
+    const size_t np = c->peers.size();
+    std::vector<int32_t> rc(np, HGX_OK);
+    std::vector<hgx_error> errs(np);
+    std::vector<std::thread> th;
+    th.reserve(np);
+    for (size_t k = 0; k < np; k++)
+        th.emplace_back([&, k] {
+            rc[k] = f(c->peers[k], &errs[k]);
+            if (rc[k]) g->fail();
+        });
+    const int32_t r0 = f(c, err);
+    if (r0) g->fail();
+    for (auto& t : th) t.join();
+    if (r0) return r0;
+    for (size_t k = 0; k < np; k++)
+        if (rc[k]) {
+            if (err) *err = errs[k];
+            return rc[k];
+        }
+    return r0;
+}
+
+template <typename F>
+static void each_shard(hgx_ctx* c, F&& f) {
+    f(c);
+    for (hgx_ctx* q : c->peers) f(q);
+}
+
+static int32_t group_only_one(hgx_ctx* c, hgx_error* err, const char* who) {
+    if (c && c->grp) {
+        set_err(err, HGX_ERR_INVALID, std::string(who) + ": not available on a chain-sharded context");
+        return HGX_ERR_INVALID;
+    }
+    return HGX_OK;
+}
 
 static int32_t ensure_mirror(hgx_ctx* c) {
     if (c->mirror_ok) return HGX_OK;
@@ -266,8 +320,36 @@ hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t dev
     return hgx_create_batch(1, n_participants, capacity_events, device, err);
 }
 
+static void free_gx(hgx_ctx* x) {
+    DeviceGuard dg(x);
+    if (x->gx_out) (void)hipFree(x->gx_out);
+    if (x->gx_in) (void)hipFree(x->gx_in);
+    x->gx_out = x->gx_in = nullptr;
+    x->gx_out_cap = x->gx_in_cap = 0;
+}
+
+// back to one context: the other shards' contexts and the group go
+static void drop_group(hgx_ctx* c) {
+    for (hgx_ctx* q : c->peers) {
+        free_gx(q);
+        DeviceGuard dg(q);
+        delete q;
+    }
+    c->peers.clear();
+    free_gx(c);
+    delete c->grp;
+    c->grp = nullptr;
+    c->eng.grp = nullptr;
+    c->eng.shard = 0;
+    c->shard_rank = 0;
+    c->shard_world = 1;
+    c->eng.shard_lo = 0;
+    c->eng.shard_hi = c->C;
+}
+
 void hgx_destroy(hgx_ctx* ctx) {
     if (!ctx) return;
+    drop_group(ctx);
     DeviceGuard dg(ctx);
     delete ctx;
 }
@@ -343,7 +425,7 @@ static int32_t finish_insert(hgx_ctx* c, const hgx::InsertOut& out, int64_t* n_i
     return rc;
 }
 
-int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+static int32_t insert_events_one(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
     if (n_inserted) *n_inserted = 0;
     if (!c || !ev || count < 0 ||
         (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
@@ -362,6 +444,15 @@ int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64
     hipError_t e = c->eng.insert(in, count, out);
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events");
     return finish_insert(c, out, n_inserted, err);
+}
+
+// a chain-sharded context: every shard inserts the batch (each holds the whole DAG)
+int32_t hgx_insert_events(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (c && c->grp)
+        return on_shards(c, err, [&](hgx_ctx* x, hgx_error* e) {
+            return insert_events_one(x, ev, count, x == c ? n_inserted : nullptr, e);
+        });
+    return insert_events_one(c, ev, count, n_inserted, err);
 }
 
 // Bootstrap / Core.Sync + RunConsensus in one call (hashgraph.go:1008-1037, node/core.go:190-303):
@@ -422,7 +513,7 @@ static bool bad_events32(const hgx_events32* ev, int64_t count) {
                           !ev->coin || !ev->sig_s || !ev->ntx));
 }
 
-int32_t hgx_insert_events32(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+static int32_t insert_events32_one(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
     if (n_inserted) *n_inserted = 0;
     if (!c || bad_events32(ev, count)) {
         set_err(err, HGX_ERR_INVALID, "hgx_insert_events32: bad arguments");
@@ -443,6 +534,14 @@ int32_t hgx_insert_events32(hgx_ctx* c, const hgx_events32* ev, int64_t count, i
     hipError_t e = c->eng.insert(in, count, out);
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events32");
     return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_insert_events32(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
+    if (c && c->grp)
+        return on_shards(c, err, [&](hgx_ctx* x, hgx_error* e) {
+            return insert_events32_one(x, ev, count, x == c ? n_inserted : nullptr, e);
+        });
+    return insert_events32_one(c, ev, count, n_inserted, err);
 }
 
 // hgx_insert_and_run with the compact columns: the structure columns (16 bytes per event) are
@@ -493,7 +592,14 @@ int32_t hgx_insert_and_run32(hgx_ctx* c, const hgx_events32* ev, int64_t count, 
     if (rc) return rc;
     rc = hgx_decide_fame(c, err);
     if (rc) return rc;
-    return hgx_find_order(c, err);
+    rc = hgx_find_order(c, err);
+    if (rc) return rc;
+    // the S copy's outcome is reported here (FindOrder waits for it only when it sorts; a skipped
+    // FindOrder would leave a failed copy unnoticed and g_S stale for a later tie-break); the
+    // guard's wait stays for the early ways out
+    e = c->eng.payload_wait_S();
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    return ok(err);
 }
 
 int32_t hgx_set_participant_keys(hgx_ctx* c, const uint8_t* keys65, hgx_error* err) {
@@ -518,6 +624,7 @@ static int32_t insert_verified(hgx_ctx* c, const hgx_events* ev, const uint8_t* 
         set_err(err, HGX_ERR_INVALID, std::string(who) + ": bad arguments");
         return HGX_ERR_INVALID;
     }
+    if (group_only_one(c, err, who)) return HGX_ERR_INVALID;
     DeviceGuard dg(c);
     if (!c->eng.keys_set) {
         set_err(err, HGX_ERR_INVALID, std::string(who) + ": participant keys not set");
@@ -565,6 +672,7 @@ int32_t hgx_insert_wire_events(hgx_ctx* c, const hgx_wire_events* w, int64_t cou
         set_err(err, HGX_ERR_INVALID, "hgx_insert_wire_events: bad arguments");
         return HGX_ERR_INVALID;
     }
+    if (group_only_one(c, err, "hgx_insert_wire_events")) return HGX_ERR_INVALID;
     DeviceGuard dg(c);
     if (ensure_chains(c)) return dev_err(err, hipErrorUnknown, "hgx_insert_wire_events");
     const int64_t E0 = c->E;
@@ -637,8 +745,8 @@ int32_t hgx_insert_wire_events(hgx_ctx* c, const hgx_wire_events* w, int64_t cou
     return HGX_OK;
 }
 
-int32_t hgx_insert_events_device(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted,
-                                 hgx_error* err) {
+static int32_t insert_events_device_one(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted,
+                                        hgx_error* err) {
     if (n_inserted) *n_inserted = 0;
     if (!c || !ev || count < 0 ||
         (count > 0 && (!ev->creator || !ev->index || !ev->self_parent || !ev->other_parent || !ev->timestamp_ns ||
@@ -656,7 +764,18 @@ int32_t hgx_insert_events_device(hgx_ctx* c, const hgx_events* ev, int64_t count
     return finish_insert(c, out, n_inserted, err);
 }
 
-int32_t hgx_clear(hgx_ctx* c) {
+// a chain-sharded context: the columns are device pointers of shard 0's device; the other shards'
+// kernels read them through the peer mapping
+int32_t hgx_insert_events_device(hgx_ctx* c, const hgx_events* ev, int64_t count, int64_t* n_inserted,
+                                 hgx_error* err) {
+    if (c && c->grp)
+        return on_shards(c, err, [&](hgx_ctx* x, hgx_error* e) {
+            return insert_events_device_one(x, ev, count, x == c ? n_inserted : nullptr, e);
+        });
+    return insert_events_device_one(c, ev, count, n_inserted, err);
+}
+
+static int32_t clear_one(hgx_ctx* c) {
     if (!c) return HGX_ERR_INVALID;
     DeviceGuard dg(c);
     if (c->eng.clear() != hipSuccess) return HGX_ERR_DEVICE;
@@ -688,6 +807,11 @@ int32_t hgx_clear(hgx_ctx* c) {
         if (c->eng.set_roots(c->root_round, c->root_y_ext) != hipSuccess) return HGX_ERR_DEVICE;
     }
     return HGX_OK;
+}
+
+int32_t hgx_clear(hgx_ctx* c) {
+    if (c && c->grp) return on_shards(c, nullptr, [](hgx_ctx* x, hgx_error*) { return clear_one(x); });
+    return clear_one(c);
 }
 
 // ---- checkpoint file + Bootstrap (hashgraph.go:1008-1037, badger_store.go:345-386) ----------
@@ -845,6 +969,7 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
         set_err(err, HGX_ERR_INVALID, "hgx_bootstrap: bad arguments");
         return HGX_ERR_INVALID;
     }
+    if (group_only_one(c, err, "hgx_bootstrap")) return HGX_ERR_INVALID;
     auto bad = [&](const std::string& why) {
         set_err(err, HGX_ERR_INVALID, "hgx_bootstrap: " + why);
         return HGX_ERR_INVALID;
@@ -884,10 +1009,12 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
     if (E > c->eng.cap) return bad("the file has " + std::to_string(E) + " events, the context's capacity is " +
                                    std::to_string(c->eng.cap));
     const size_t Ez = (size_t)E, Cz = (size_t)c->C;
+    // every section is parsed and validated into locals first; the context is touched (Reset,
+    // Root.Others, the kept state, keys, events) only once the whole file is accepted
     std::vector<uint8_t> others;
     std::vector<hgx_ctx::Kept> kept;
+    std::vector<int32_t> ri(Cz), rr(Cz), ry(Cz);
     if (flags & kCkRooted) {
-        std::vector<int32_t> ri(Cz), rr(Cz), ry(Cz);
         std::vector<uint8_t> y((Cz + 3) & ~(size_t)3);
         if (!r.get(ri.data(), Cz * 4) || !r.get(rr.data(), Cz * 4) || !r.get(y.data(), y.size())) return bad("truncated file");
         for (size_t p = 0; p < Cz; p++) ry[p] = y[p];
@@ -918,24 +1045,6 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
                     b.first = -1;
                 }
             }
-        }
-        const int32_t rc = hgx_reset(c, ri.data(), rr.data(), ry.data(), err);
-        if (rc) return rc;
-        if (!others.empty()) {
-            const int32_t rc2 = hgx_set_root_others(c, others.data(), (int64_t)(others.size() / 32), err);
-            if (rc2) return rc2;
-        }
-        if (version >= 2) {   // what Reset kept at the saved context
-            for (int g = 0; g < G; g++) {
-                GraphState& s = c->gs[g];
-                const hgx_ctx::Kept& k = kept[(size_t)g];
-                s.has_lcr = k.has_lcr;
-                s.lcr = k.lcr;
-                s.lcre = k.lcre;
-                s.consensus_tx = k.consensus_tx;
-                s.blocks = k.blocks;
-            }
-            c->reset_kept = kept;
         }
     }
     std::vector<int32_t> creator(Ez), ntx(Ez), nil(Ez);
@@ -971,6 +1080,26 @@ int32_t hgx_bootstrap(hgx_ctx* c, const char* path, hgx_error* err) {
         if (!r.get(pblob.data(), pblob.size())) return bad("truncated file");
     }
     if (r.pos != r.buf.size()) return bad("size mismatch");
+    if (flags & kCkRooted) {
+        const int32_t rc = hgx_reset(c, ri.data(), rr.data(), ry.data(), err);
+        if (rc) return rc;
+        if (!others.empty()) {
+            const int32_t rc2 = hgx_set_root_others(c, others.data(), (int64_t)(others.size() / 32), err);
+            if (rc2) return rc2;
+        }
+        if (version >= 2) {   // what Reset kept at the saved context
+            for (int g = 0; g < G; g++) {
+                GraphState& s = c->gs[g];
+                const hgx_ctx::Kept& k = kept[(size_t)g];
+                s.has_lcr = k.has_lcr;
+                s.lcr = k.lcr;
+                s.lcre = k.lcre;
+                s.consensus_tx = k.consensus_tx;
+                s.blocks = k.blocks;
+            }
+            c->reset_kept = kept;
+        }
+    }
     if (!keys.empty()) {
         const int32_t rc = hgx_set_participant_keys(c, keys.data(), err);
         if (rc) return rc;
@@ -1032,6 +1161,7 @@ int32_t hgx_reset(hgx_ctx* c, const int32_t* root_index, const int32_t* root_rou
         set_err(err, HGX_ERR_INVALID, "hgx_reset: bad arguments");
         return HGX_ERR_INVALID;
     }
+    if (group_only_one(c, err, "hgx_reset")) return HGX_ERR_INVALID;
     DeviceGuard dg(c);
     std::vector<int32_t> rr(root_round, root_round + c->C);
     std::vector<uint8_t> ye(c->C);
@@ -1167,7 +1297,7 @@ int32_t hgx_get_frame(hgx_ctx* c, int64_t* events, int64_t events_cap, int64_t* 
 }
 
 // ---- DivideRounds (hashgraph.go:616-646) -----------------------------------------
-int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
+static int32_t divide_rounds_one(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     if (c->divided && c->E_div == c->E) return ok(err);   // nothing new: AddEvent is idempotent
     DeviceGuard dg(c);
@@ -1222,6 +1352,13 @@ int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
     return ok(err);
 }
 
+// a chain-sharded context: the shards run DivideRounds together (their recurrence launches hand
+// rows to each other)
+int32_t hgx_divide_rounds(hgx_ctx* c, hgx_error* err) {
+    if (c && c->grp) return on_shards(c, err, [](hgx_ctx* x, hgx_error* e) { return divide_rounds_one(x, e); });
+    return divide_rounds_one(c, err);
+}
+
 static bool is_witness(const hgx_ctx* c, int32_t r, int gc) {
     return r >= 0 && r < c->rh.R && c->rh.wflag[(size_t)r * c->C + gc] == 2;
 }
@@ -1236,7 +1373,7 @@ static bool witnesses_decided(const hgx_ctx* c, int g, int32_t r) {
 }
 
 // ---- DecideFame (hashgraph.go:649-750) -------------------------------------------
-int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
+static int32_t decide_fame_one(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     DeviceGuard dg(c);
     std::vector<int8_t>& dev = c->fame_dev;   // kept between calls (rows below the first undecided one unused)
@@ -1289,11 +1426,16 @@ int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
     return ok(err);
 }
 
+int32_t hgx_decide_fame(hgx_ctx* c, hgx_error* err) {
+    if (c && c->grp) return on_shards(c, err, [](hgx_ctx* x, hgx_error* e) { return decide_fame_one(x, e); });
+    return decide_fame_one(c, err);
+}
+
 // ---- FindOrder (hashgraph.go:801-858) --------------------------------------------
 // In two halves: begin = DecideRoundReceived and the consensus timestamps of this context's
 // shard of chains (all chains unless hgx_set_shard); end = the ConsensusSorter order and the
 // blocks. A row-sharded graph exchanges the shards' timestamps in between.
-int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
+static int32_t find_order_begin_one(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     c->fo_open = false;
     if (!c->divided) return ok(err);
@@ -1364,7 +1506,7 @@ int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
     return ok(err);
 }
 
-int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
+static int32_t find_order_end_one(hgx_ctx* c, hgx_error* err) {
     if (!c) { set_err(err, HGX_ERR_INVALID, "null context"); return HGX_ERR_INVALID; }
     if (!c->fo_open) return ok(err);
     c->fo_open = false;
@@ -1455,15 +1597,82 @@ int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
     return ok(err);
 }
 
+int32_t hgx_find_order_begin(hgx_ctx* c, hgx_error* err) {
+    const int32_t rc = group_only_one(c, err, "hgx_find_order_begin");
+    return rc ? rc : find_order_begin_one(c, err);
+}
+
+int32_t hgx_find_order_end(hgx_ctx* c, hgx_error* err) {
+    const int32_t rc = group_only_one(c, err, "hgx_find_order_end");
+    return rc ? rc : find_order_end_one(c, err);
+}
+
+static int32_t shard_xfer(hgx_ctx* c, int32_t rank, void* buf, int32_t on_device, bool to_buf);
+
+static int32_t grow_dev(hgx_ctx* c, void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return HGX_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, std::max<size_t>(bytes, 1 << 16)) != hipSuccess) return HGX_ERR_DEVICE;
+    *cap = std::max<size_t>(bytes, 1 << 16);
+    (void)c;
+    return HGX_OK;
+}
+
+// FindOrder of a chain-sharded context: every shard's begin (round received for every event, the
+// consensus timestamps of its own chains' events: its firstDescendants are valid there only), the
+// timestamps exchanged (each shard's values copied device to device into every other shard and
+// imported there), every shard's end (sort, blocks)
+static int32_t group_find_order(hgx_ctx* c, hgx_error* err) {
+    int32_t rc = on_shards(c, err, [](hgx_ctx* x, hgx_error* e) { return find_order_begin_one(x, e); });
+    if (rc) return rc;
+    std::vector<hgx_ctx*> sh{c};
+    sh.insert(sh.end(), c->peers.begin(), c->peers.end());
+    const int W = (int)sh.size();
+    if (c->fo_open) {
+        std::vector<int64_t> cnt(W);
+        for (int k = 0; k < W; k++) {   // shard k's values into its own device buffer
+            hgx_ctx* x = sh[k];
+            DeviceGuard dg(x);
+            cnt[k] = hgx_shard_values(x, k);
+            if (cnt[k] == 0) continue;
+            if (grow_dev(x, &x->gx_out, &x->gx_out_cap, (size_t)cnt[k] * 8) ||
+                shard_xfer(x, k, x->gx_out, 1, true)) {
+                set_err(err, HGX_ERR_DEVICE, "hgx_find_order: shard timestamp export failed");
+                return HGX_ERR_DEVICE;
+            }
+        }
+        for (int j = 0; j < W; j++) {   // ... copied to every other shard and imported there
+            hgx_ctx* x = sh[j];
+            DeviceGuard dg(x);
+            for (int k = 0; k < W; k++) {
+                if (k == j || cnt[k] == 0) continue;
+                // (on the importing engine's stream: a device-to-device copy on the null stream returns
+                // before it completes, and the engine's non-blocking stream does not wait for it)
+                if (grow_dev(x, &x->gx_in, &x->gx_in_cap, (size_t)cnt[k] * 8) ||
+                    hipMemcpyPeerAsync(x->gx_in, x->eng.dev, sh[k]->gx_out, sh[k]->eng.dev, (size_t)cnt[k] * 8,
+                                       x->eng.stream) != hipSuccess ||
+                    shard_xfer(x, k, x->gx_in, 1, false)) {
+                    set_err(err, HGX_ERR_DEVICE, "hgx_find_order: shard timestamp import failed");
+                    return HGX_ERR_DEVICE;
+                }
+            }
+        }
+    }
+    return on_shards(c, err, [](hgx_ctx* x, hgx_error* e) { return find_order_end_one(x, e); });
+}
+
 int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
+    if (c && c->grp) return group_find_order(c, err);
     if (c && c->shard_world > 1) {
         set_err(err, HGX_ERR_INVALID, "hgx_find_order: a sharded context exchanges timestamps between "
                                       "hgx_find_order_begin and hgx_find_order_end");
         return HGX_ERR_INVALID;
     }
-    const int32_t rc = hgx_find_order_begin(c, err);
+    const int32_t rc = find_order_begin_one(c, err);
     if (rc) return rc;
-    return hgx_find_order_end(c, err);
+    return find_order_end_one(c, err);
 }
 
 // ---- row-sharded graph --------------------------------------------------
@@ -1473,7 +1682,7 @@ static void shard_range(const hgx_ctx* c, int32_t rank, int* lo, int* hi) {
 }
 
 int32_t hgx_set_shard(hgx_ctx* c, int32_t rank, int32_t world) {
-    if (!c || world < 1 || rank < 0 || rank >= world || world > c->C) return HGX_ERR_INVALID;
+    if (!c || c->grp || world < 1 || rank < 0 || rank >= world || world > c->C) return HGX_ERR_INVALID;
     c->shard_rank = rank;
     c->shard_world = world;
     shard_range(c, rank, &c->eng.shard_lo, &c->eng.shard_hi);
@@ -1513,7 +1722,7 @@ int32_t hgx_run_consensus(hgx_ctx* c, hgx_error* err) {
     return hgx_find_order(c, err);
 }
 
-int32_t hgx_reset_consensus(hgx_ctx* c) {
+static int32_t reset_consensus_one(hgx_ctx* c) {
     if (!c) return HGX_ERR_INVALID;
     DeviceGuard dg(c);
     for (int g = 0; g < c->G; g++) {
@@ -1529,6 +1738,11 @@ int32_t hgx_reset_consensus(hgx_ctx* c) {
     c->E_div = 0;
     c->rounds_cached = c->recv_cached = false;
     return c->eng.reset_received() == hipSuccess ? HGX_OK : HGX_ERR_DEVICE;
+}
+
+int32_t hgx_reset_consensus(hgx_ctx* c) {
+    if (c && c->grp) return on_shards(c, nullptr, [](hgx_ctx* x, hgx_error*) { return reset_consensus_one(x); });
+    return reset_consensus_one(c);
 }
 
 // ---- state getters ----------------------------------------------------------------
@@ -1927,19 +2141,19 @@ int32_t hgx_reset_stats(hgx_ctx* c) {
 
 int32_t hgx_set_coord_storage(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
-    c->eng.force_coord32 = mode == 1;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.force_coord32 = mode == 1; });
     return HGX_OK;
 }
 
 int32_t hgx_set_kernel_timing(hgx_ctx* c, int32_t on) {
     if (!c) return HGX_ERR_INVALID;
-    c->eng.time_mask = (uint32_t)on;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.time_mask = (uint32_t)on; });
     return HGX_OK;
 }
 
 int32_t hgx_set_fame_tally(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
-    c->eng.fame_tally = mode;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.fame_tally = mode; });
     return HGX_OK;
 }
 
@@ -1978,9 +2192,11 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
 
 int32_t hgx_set_la_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 1025) return HGX_ERR_INVALID;
-    c->eng.la_kernel = mode == 1 ? 1 : 0;
-    c->eng.la_segs_override = (mode >= 2 && mode <= 1024) ? mode : 0;
-    c->eng.la_small_override = mode == 1025 ? 0 : -1;
+    each_shard(c, [&](hgx_ctx* x) {
+        x->eng.la_kernel = mode == 1 ? 1 : 0;
+        x->eng.la_segs_override = (mode >= 2 && mode <= 1024) ? mode : 0;
+        x->eng.la_small_override = mode == 1025 ? 0 : -1;
+    });
     return HGX_OK;
 }
 
@@ -1989,6 +2205,7 @@ int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t cou
         set_err(err, HGX_ERR_INVALID, "hgx_set_root_others: bad arguments");
         return HGX_ERR_INVALID;
     }
+    if (group_only_one(c, err, "hgx_set_root_others")) return HGX_ERR_INVALID;
     if (!c->rooted && count > 0) {
         set_err(err, HGX_ERR_INVALID, "hgx_set_root_others: no roots installed (hgx_reset)");
         return HGX_ERR_INVALID;
@@ -2002,19 +2219,129 @@ int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t cou
 
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 4) return HGX_ERR_INVALID;
-    c->eng.round_kernel = mode;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.round_kernel = mode; });
     return HGX_OK;
 }
 
+// W shards of one graph: shard 0 is `c` (on devs[0] == its device), shard k a new
+// context on devs[k]; every shard holds the whole DAG, shard k owns chains [C k / W, C (k + 1) / W)
+static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error* err) {
+    auto bad = [&](const std::string& why) {
+        set_err(err, HGX_ERR_INVALID, "chain-sharded context: " + why);
+        return HGX_ERR_INVALID;
+    };
+    if (W < 1 || W > hgx::kMaxShards) return bad("1 to 8 shards");
+    if (c->E != 0) return bad("shards are set up on an empty context (before the first insert)");
+    if (W == 1) {
+        drop_group(c);
+        return ok(err);
+    }
+    if (c->G != 1) return bad("one graph per context (hgx_create)");
+    if (c->rooted) return bad("not after a Reset");
+    if (W > c->C || c->n > 256) return bad("at most one shard per chain and n <= 256 (the persistent recurrence)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return bad("no HIP device");
+    if (devs[0] != c->eng.dev) return bad("shard 0 runs on the context's own device");
+    // every shard's launch of the recurrence waits for the others' granules, so the shards that share
+    // a device need a hardware queue each besides the ones HIP keeps for itself
+    const char* qenv = std::getenv("GPU_MAX_HW_QUEUES");
+    const int queues = qenv ? std::max(1, std::atoi(qenv)) : 4;
+    for (int k = 0; k < W; k++) {
+        if (devs[k] < 0 || devs[k] >= ndev) return bad("invalid device ordinal " + std::to_string(devs[k]));
+        int same = 0;
+        for (int j = 0; j < W; j++) same += devs[j] == devs[k];
+        if (same > 1 && same > queues - 2)
+            return bad(std::to_string(same) + " shards on device " + std::to_string(devs[k]) +
+                       " need GPU_MAX_HW_QUEUES >= " + std::to_string(same + 2) + " (set before the HIP runtime starts)");
+    }
+    // peer mappings between the shards' devices (window stores, round-row and timestamp copies)
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (int a = 0; a < W; a++)
+        for (int b = 0; b < W; b++) {
+            if (devs[a] == devs[b]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devs[a], devs[b]) != hipSuccess || !can) {
+                if (prev >= 0) (void)hipSetDevice(prev);
+                return bad("device " + std::to_string(devs[a]) + " cannot map device " + std::to_string(devs[b]));
+            }
+            (void)hipSetDevice(devs[a]);
+            const hipError_t e = hipDeviceEnablePeerAccess(devs[b], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                if (prev >= 0) (void)hipSetDevice(prev);
+                return dev_err(err, e, "hipDeviceEnablePeerAccess");
+            }
+            (void)hipGetLastError();
+        }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    drop_group(c);
+    auto* g = new (std::nothrow) hgx::ShardGroup();
+    if (!g) return bad("out of host memory");
+    g->W = W;
+    for (int k = 0; k < W; k++) {
+        g->dev[k] = devs[k];
+        g->c_split[k] = (int32_t)((int64_t)c->C * k / W);
+    }
+    g->c_split[W] = c->C;
+    c->grp = g;
+    for (int k = 1; k < W; k++) {
+        hgx_ctx* q = hgx_create_batch(1, c->n, c->cap, devs[k], err);
+        if (!q) {
+            drop_group(c);
+            return err ? err->code : HGX_ERR_DEVICE;
+        }
+        // the shard 0 settings (hgx_set_*) so far
+        q->eng.force_coord32 = c->eng.force_coord32;
+        q->eng.time_mask = c->eng.time_mask;
+        q->eng.fame_tally = c->eng.fame_tally;
+        q->eng.la_kernel = c->eng.la_kernel;
+        q->eng.la_segs_override = c->eng.la_segs_override;
+        q->eng.la_small_override = c->eng.la_small_override;
+        q->eng.round_kernel = c->eng.round_kernel;
+        q->eng.cts_kernel = c->eng.cts_kernel;
+        q->eng.incremental = c->eng.incremental;
+        q->grp = nullptr;
+        c->peers.push_back(q);
+    }
+    std::vector<hgx_ctx*> sh{c};
+    sh.insert(sh.end(), c->peers.begin(), c->peers.end());
+    for (int k = 0; k < W; k++) {
+        g->eng[k] = &sh[k]->eng;
+        sh[k]->eng.grp = g;
+        sh[k]->eng.shard = k;
+        sh[k]->shard_rank = k;
+        sh[k]->shard_world = W;
+        sh[k]->eng.shard_lo = g->c_split[k];
+        sh[k]->eng.shard_hi = g->c_split[k + 1];
+    }
+    return ok(err);
+}
+
 int32_t hgx_set_round_shards(hgx_ctx* c, int32_t shards) {
-    if (!c || shards < 1 || shards > hgx::kMaxRoundShards) return HGX_ERR_INVALID;
-    c->eng.round_shards = shards;
-    return HGX_OK;
+    if (!c || shards < 1 || shards > hgx::kMaxShards) return HGX_ERR_INVALID;
+    if (shards == (c->grp ? c->grp->W : 1)) return HGX_OK;
+    std::vector<int32_t> devs((size_t)shards, c->eng.dev);   // every shard on this context's device
+    return setup_group(c, shards, devs.data(), nullptr);
+}
+
+hgx_ctx* hgx_create_sharded(int32_t n_participants, int64_t capacity_events, int32_t n_shards, const int32_t* devices,
+                            hgx_error* err) {
+    if (n_shards < 1 || n_shards > hgx::kMaxShards || !devices) {
+        set_err(err, HGX_ERR_INVALID, "hgx_create_sharded: 1 to 8 shards, one device ordinal each");
+        return nullptr;
+    }
+    hgx_ctx* c = hgx_create_batch(1, n_participants, capacity_events, devices[0], err);
+    if (!c) return nullptr;
+    if (setup_group(c, n_shards, devices, err) != HGX_OK) {
+        hgx_destroy(c);
+        return nullptr;
+    }
+    return c;
 }
 
 int32_t hgx_set_cts_kernel(hgx_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 2) return HGX_ERR_INVALID;
-    c->eng.cts_kernel = mode == 0 ? 1 : mode;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.cts_kernel = mode == 0 ? 1 : mode; });
     return HGX_OK;
 }
 
@@ -2027,16 +2354,19 @@ int32_t hgx_set_commit_callback(hgx_ctx* c, hgx_commit_fn fn, void* user) {
 
 int32_t hgx_set_incremental(hgx_ctx* c, int32_t on) {
     if (!c || on < 0 || on > 1) return HGX_ERR_INVALID;
-    c->eng.incremental = on != 0;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.incremental = on != 0; });
     return HGX_OK;
 }
 
 int32_t hgx_reserve_rounds(hgx_ctx* c, int32_t rounds) {
     if (!c || rounds < 1 || c->divided) return HGX_ERR_INVALID;   // before the first DivideRounds only
-    DeviceGuard dg(c);
-    if (c->eng.reserve_rounds(rounds) != hipSuccess) return HGX_ERR_DEVICE;
-    c->rounds_cached = c->recv_cached = false;
-    return HGX_OK;
+    int32_t rc = HGX_OK;
+    each_shard(c, [&](hgx_ctx* x) {
+        DeviceGuard dg(x);
+        if (x->eng.reserve_rounds(rounds) != hipSuccess) rc = HGX_ERR_DEVICE;
+        x->rounds_cached = x->recv_cached = false;
+    });
+    return rc;
 }
 
 }  // extern "C"

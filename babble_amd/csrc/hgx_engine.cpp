@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -62,23 +63,62 @@ static int bitlen(uint64_t v) {
     return b;
 }
 
-hipError_t Engine::ensure_shard_streams() {
-    if (round_shards < 1 || round_shards > kMaxRoundShards) return hipErrorInvalidValue;
-    for (int k = 0; k <= round_shards; k++)
-        if (!sh_ev[k]) HGX_TRY(hipEventCreateWithFlags(&sh_ev[k], hipEventDisableTiming));
-    for (int k = 0; k < round_shards; k++)
-        if (!sh_stream[k]) HGX_TRY(hipStreamCreateWithFlags(&sh_stream[k], hipStreamNonBlocking));
-    return hipSuccess;
+// ---- chain-sharded group -------------------------------------------------
+bool ShardGroup::wait() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) return false;
+    const uint64_t g = gen;
+    if (++count == W) {
+        count = 0;
+        gen++;
+        cv.notify_all();
+        return true;
+    }
+    // (a shard that failed breaks the barrier; the time limit only guards against a lost thread)
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; })) broken = true;
+    if (broken) cv.notify_all();
+    return !broken;
+}
+
+void ShardGroup::fail() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = true;
+    cv.notify_all();
+}
+
+void ShardGroup::rearm() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = false;
+    count = 0;
+}
+
+hipError_t Engine::share_round_rows(int32_t r_a, int32_t r_b) {
+    if (!grp || grp->W < 2) return hipSuccess;
+    const int lo = grp->c_split[shard], hi = grp->c_split[shard + 1];
+    if (hi <= lo || r_b < r_a) return hipSuccess;
+    const int32_t r_s = std::min(r_b, r_cap - 1);   // rows of the [r_cap x C] tables
+    const size_t Cz = (size_t)C, w = (size_t)(hi - lo);
+    for (int k = 0; k < grp->W; k++) {
+        if (k == shard) continue;
+        Engine* q = grp->eng[k];
+        // the peer's tables have the same shapes (identical calls, identical growth)
+        if (q->r_cap != r_cap) return hipErrorInvalidValue;
+        HGX_TRY(hipMemcpy2DAsync(q->Bm.p + (size_t)r_a * Cz + lo, Cz * 4, Bm.p + (size_t)r_a * Cz + lo, Cz * 4, w * 4,
+                                 (size_t)(r_b - r_a + 1), hipMemcpyDefault, stream));
+        if (r_s >= r_a) {
+            const size_t rows = (size_t)(r_s - r_a + 1);
+            HGX_TRY(hipMemcpy2DAsync(q->Smat.p + ((size_t)r_a * Cz + lo) * nw, Cz * nw * 8, Smat.p + ((size_t)r_a * Cz + lo) * nw,
+                                     Cz * nw * 8, w * nw * 8, rows, hipMemcpyDefault, stream));
+            HGX_TRY(hipMemcpy2DAsync(q->wstat.p + (size_t)r_a * Cz + lo, Cz, wstat.p + (size_t)r_a * Cz + lo, Cz, w, rows,
+                                     hipMemcpyDefault, stream));
+            HGX_TRY(hipMemcpy2DAsync(q->wflag.p + (size_t)r_a * Cz + lo, Cz, wflag.p + (size_t)r_a * Cz + lo, Cz, w, rows,
+                                     hipMemcpyDefault, stream));
+        }
+    }
+    return hipStreamSynchronize(stream);
 }
 
 Engine::~Engine() {
-    for (auto& q : sh_stream)
-        if (q) {
-            (void)hipStreamSynchronize(q);
-            (void)hipStreamDestroy(q);
-        }
-    for (auto e : sh_ev)
-        if (e) (void)hipEventDestroy(e);
     if (pay_thread.joinable()) pay_thread.join();
     if (stream2) (void)hipStreamSynchronize(stream2);
     if (ev_pay) (void)hipEventDestroy(ev_pay);
@@ -140,7 +180,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     const size_t PP = (size_t)Ppos;
     HGX_TRY(g_creator.alloc(P)); HGX_TRY(g_index.alloc(P)); HGX_TRY(g_sp.alloc(P)); HGX_TRY(g_op.alloc(P));
     HGX_TRY(g_ntx.alloc(P)); HGX_TRY(g_rr.alloc(P)); HGX_TRY(g_pos.alloc(P)); HGX_TRY(g_ts.alloc(P));
-    HGX_TRY(g_cts.alloc(P)); HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
+    HGX_TRY(g_cts.alloc(P)); HGX_TRY(g_ck.alloc(P)); HGX_TRY(g_S.alloc(P * 32)); HGX_TRY(g_coin.alloc(P)); HGX_TRY(g_loaded.alloc(P));
     HGX_TRY(g_txnil.alloc(P)); HGX_TRY(g_id.alloc(P * 32));
     // insert state: no claims, no events per creator
     HGX_TRY(succ.alloc(P)); HGX_TRY(first_none.alloc(C));
@@ -234,7 +274,7 @@ DevArrays Engine::arrays() {
     DevArrays a;
     a.g_creator = g_creator.p; a.g_index = g_index.p; a.g_op = g_op.p; a.g_ntx = g_ntx.p;
     a.g_ts = g_ts.p; a.g_S = g_S.p; a.g_coin = g_coin.p; a.g_loaded = g_loaded.p; a.g_txnil = g_txnil.p;
-    a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p;
+    a.g_rr = g_rr.p; a.g_pos = g_pos.p; a.g_cts = g_cts.p; a.g_ck = g_ck.p;
     a.c_off = c_off.p; a.c_len = c_len.p; a.c_base = c_base.p;
     a.p_gid = p_gid.p; a.p_chain = p_chain.p; a.p_op = p_op.p; a.p_opu = p_opu.p; a.p_opk = p_opk.p; a.p_round = p_round.p; a.p_rr = p_rr.p;
     a.p_ts = p_ts.p; a.p_cts = p_cts.p;
@@ -1100,9 +1140,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         HGX_TRY(run_sweeps(1));
     }
     kbeg(K_FD_BUILD);
-    if (round_shards > 1) {   // the sharded rehearsal: each shard builds the rows of its own chains' events
-        for (int k = 0; k < round_shards; k++)
-            launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new, n * k / round_shards, n * (k + 1) / round_shards);
+    if (grp) {   // a chain-sharded group (one graph): the firstDescendants of this shard's chains' events
+        launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new, grp->c_split[shard], grp->c_split[shard + 1]);
     } else {
         launch_fd_build(stream, a, C, n, max_len, fd_ld, cold, max_new);
     }
@@ -1221,6 +1260,32 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         int32_t* fin = rp_st.p + 4;
         HGX_TRY(hipMemsetAsync(rp_gran.p, 0, (size_t)4 * C * 8, stream));   // no tag survives a call
         HGX_TRY(hipMemsetAsync(fin, 0xFF, (size_t)G * 4, stream));          // no graph finished yet
+        // a chain-sharded group: this shard's chain block, its candidate rows and granules written into
+        // every shard's window; the host threads of the W shards meet at the barriers
+        const bool sh = grp && grp->W > 1;
+        int c_lo = 0, c_hi = C;
+        RoundPWindows win;
+        auto gwait = [&]() -> hipError_t { return grp->wait() ? hipSuccess : hipErrorUnknown; };
+        if (sh) {
+            c_lo = grp->c_split[shard];
+            c_hi = grp->c_split[shard + 1];
+            HGX_TRY(hipStreamSynchronize(stream));
+            HGX_TRY(gwait());   // every window is cleared and registered (its engine's FD8p / gran / st)
+            win.nwin = grp->W;
+            for (int k = 0; k <= grp->W; k++) win.c_split[k] = grp->c_split[k];
+            for (int k = 0; k < grp->W; k++) {
+                Engine* q = grp->eng[k];
+                win.FD8p[k] = q->FD8p.p;
+                win.gran[k] = q->rp_gran.p;
+                win.st[k] = q->rp_st.p;
+                win.FDT[k] = q->FDT.p;
+                if (grp->dev[k] != dev) win.remote |= 1u << k;
+            }
+            if (rp_win.n < sizeof(RoundPWindows)) HGX_TRY(rp_win.alloc(sizeof(RoundPWindows)));
+            HGX_TRY(hipMemcpyAsync(rp_win.p, &win, sizeof(RoundPWindows), hipMemcpyHostToDevice, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+        }
+        const RoundPWindows* win_d = sh ? (const RoundPWindows*)rp_win.p : nullptr;
         int32_t s = r_lo, last = -1;
         int finished = 0;
         for (int init = 1;; init = 0) {
@@ -1229,38 +1294,45 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 a = arrays();
             }
             HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
-            kbeg(K_ROUND_SEARCH);
-            if (round_shards > 1) {
-                // the one-GPU rehearsal of a chain-sharded recurrence: W launches over
-                // disjoint chain blocks on W streams, handing rows and granules over through the shared
-                // buffers that stand in for the peers' xGMI windows
-                HGX_TRY(ensure_shard_streams());
-                if (init) HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus));
-                HGX_TRY(hipEventRecord(sh_ev[0], stream));
-                for (int k = 0; k < round_shards; k++) {
-                    HGX_TRY(hipStreamWaitEvent(sh_stream[k], sh_ev[0], 0));
-                    const int lo = C * k / round_shards, hi = C * (k + 1) / round_shards;
-                    if (hi > lo)
-                        HGX_TRY(launch_round_p(sh_stream[k], round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 0,
-                                               num_cus, lo, hi));
-                    HGX_TRY(hipEventRecord(sh_ev[1 + k], sh_stream[k]));
-                    HGX_TRY(hipStreamWaitEvent(stream, sh_ev[1 + k], 0));
-                }
-            } else {
-                HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, init, num_cus));
+            if (sh && init) {
+                // W'_{r_lo} of this shard's chains into every window; every shard's launch starts once
+                // every window holds the whole W'_{r_lo}
+                HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus,
+                                       c_lo, c_hi, win_d, win.nwin));
+                HGX_TRY(hipStreamSynchronize(stream));
+                HGX_TRY(gwait());
             }
+            kbeg(K_ROUND_SEARCH);
+            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, sh ? 0 : init,
+                                   num_cus, c_lo, c_hi, win_d, sh ? win.nwin : 1));
             kend(K_ROUND_SEARCH, 0);
             HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipStreamSynchronize(stream));
             round_p_runs++;
             round_p_ovf += h_small[59];
-            if (h_small[56] != 0) {   // a workgroup gave up waiting: st[0] = 1 + its chain, st[3] its round
-                round_p_fail_chain = h_small[56] - 1;
-                round_p_fail_round = h_small[59];
+            int32_t st0 = h_small[56], st1 = h_small[57], st2 = h_small[58], st3 = h_small[59];
+            if (sh) {
+                // every shard's outcome; then this shard's round rows into every shard's tables
+                for (int k = 0; k < 4; k++) grp->st[shard][k] = h_small[56 + k];
+                HGX_TRY(gwait());
+                for (int k = 0; k < grp->W; k++) {
+                    if (grp->st[k][0] != 0 && st0 == 0) {
+                        st0 = grp->st[k][0];
+                        st3 = grp->st[k][3];
+                    }
+                    st1 = std::max(st1, grp->st[k][1]);
+                    st2 = std::max(st2, grp->st[k][2]);
+                }
+                if (st0 == 0) HGX_TRY(share_round_rows(s, std::min(st1 + 1, r_cap)));
+                HGX_TRY(gwait());
+            }
+            if (st0 != 0) {   // a workgroup gave up waiting: st[0] = 1 + its chain, st[3] its round
+                round_p_fail_chain = st0 - 1;
+                round_p_fail_round = st3;
                 return hipErrorLaunchTimeOut;
             }
-            last = std::max(last, h_small[57]);
-            finished += h_small[58];
+            last = std::max(last, st1);
+            finished += st2;
             if (finished >= G) {
                 r_done = last + 1;
                 // graphs that finished earlier: empty rows up to the last round (k_last_round,
@@ -1271,7 +1343,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 kend(K_ROUND_GATHER, (double)(last - r_lo + 1) * C * n * (sizeof(int32_t) + (compact ? 2 : 4)));
                 return hipGetLastError();
             }
-            s = h_small[57];   // the round tables' capacity: continue from there
+            s = st1;   // the round tables' capacity: continue from there
         }
     };
     // the whole-graph recurrence (hgx_round_g.hip, n <= 16): one workgroup per graph, every round
@@ -1309,11 +1381,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             s = h_small[57];   // the round tables' capacity: continue from there
         }
     };
-    const bool graph_ok = !rooted && round_g_ok(n, nw) && (round_kernel == 0 || round_kernel == 4) && round_shards == 1;
+    const bool graph_ok = !rooted && round_g_ok(n, nw) && (round_kernel == 0 || round_kernel == 4) && !grp;
     if (graph_ok) HGX_TRY(run_graph());
     // the persistent launch pays a fixed cost (every chain's window staged, 256 resident
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
-    if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild) || round_shards > 1) &&
+    // (a chain-sharded group always runs it: its shards build firstDescendants for their own chains only)
+    if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild) || grp) &&
         round_p_ok(n, C, num_cus)) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
@@ -1322,6 +1395,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             if (pe != hipErrorLaunchTimeOut && pe != hipErrorCooperativeLaunchTooLarge) return pe;
             round_p_fallbacks++;
             r_done = -1;
+            if (grp) {
+                // the steps read every candidate's firstDescendants: this shard built its own chains'
+                // only, so the whole table is rebuilt here, and W'_{r_lo} gathered again from it
+                launch_fd_build(stream, a, C, n, max_len, fd_ld, nullptr, 0);
+                launch_round_gather(stream, a, r_lo, C, n, fd_ld);
+            }
         }
     }
     if (r_done >= 0 && rebuild && !graph_ok && !rooted && round_kernel == 0) {
@@ -1368,8 +1447,11 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 kp.extra = nullptr;
                 HGX_TRY(hipGraphExecKernelNodeSetParams(sgr.exec, sgr.nodes[k], &kp));
             }
-            // nb step kernels per replay; one replay in 4 is bracketed by timing events
-            const bool sample = (launched & 3) == 0;
+            // nb step kernels per replay, every replay bracketed by timing events when the round
+            // search is timed (a sample of replays misjudged the pass: the first replays' rounds hold
+            // most of the events, the last ones' steps find little left -- c5: 19.4 ms sampled
+            // against 12.8 ms in the rocprofv3 trace)
+            const bool sample = true;
             kbeg(K_ROUND_SEARCH, sample, nb);
             HGX_TRY(hipGraphLaunch(sgr.exec, stream));
             if (sample) kend(K_ROUND_SEARCH, 0);

@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <string>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -17,7 +19,6 @@ namespace hgx {
 
 constexpr int kStepBatch = 16;        // round steps per hipGraph replay (a full DivideRounds)
 constexpr int kStepBatchSmall = 2;    // ... when resuming at the lowest changed round
-constexpr int kMaxRoundShards = 8;    // chain blocks of the sharded rehearsal (hgx_set_round_shards)
 
 // kStepBatch round steps captured as one hipGraph, replayed with rewritten round arguments
 struct StepGraph {
@@ -89,6 +90,32 @@ struct InsertOut {
     // per-creator state after the batch ([C]) and loaded events per graph ([G], cumulative)
     std::vector<int32_t> last_gid, last_index, chain_base;
     std::vector<unsigned long long> graph_loaded;
+};
+
+class Engine;
+
+// A chain-sharded group (hgx_create_sharded / hgx_set_round_shards): W engines in one
+// process, shard k's on device dev[k] (devices may repeat), each holding the whole DAG. Shard k
+// builds the firstDescendants of its chains' events [c_split[k], c_split[k+1]), runs the persistent
+// recurrence for those chains and their consensus timestamps, and hands its candidate rows and
+// granules to every shard through that shard's window (peer-mapped device memory, write-through);
+// the round outputs of its chains are copied to every shard after each launch. The W engines' host
+// threads meet at the group's barriers.
+struct ShardGroup {
+    int W = 1;
+    int dev[kMaxShards] = {};
+    int32_t c_split[kMaxShards + 1] = {};
+    Engine* eng[kMaxShards] = {};
+    int32_t st[kMaxShards][4] = {};   // every shard's status words after its last persistent launch
+    bool wait();                      // false: a shard failed (or 120 s passed): leave with an error
+    void fail();
+    void rearm();                     // before a group call (no thread inside the group)
+   private:
+    std::mutex m;
+    std::condition_variable cv;
+    int count = 0;
+    uint64_t gen = 0;
+    bool broken = false;
 };
 
 class Engine {
@@ -216,13 +243,12 @@ class Engine {
                               // else per-launch per-candidate steps; 1 block-search steps; 2 per-candidate steps
     int cts_kernel = 1;       // hgx_set_cts_kernel: 1 per-tile blocks (default: measured faster), 2 pipelined (hgx_cts.hip)
     int64_t round_g_runs = 0;   // whole-graph recurrence launches (n <= 16)
-    // the one-GPU rehearsal of a chain-sharded recurrence (hgx_set_round_shards): W > 1
-    // splits the persistent round launch into W chain blocks on W streams and fd_build into W
-    // source-chain blocks
-    int round_shards = 1;
-    hipStream_t sh_stream[kMaxRoundShards] = {};
-    hipEvent_t sh_ev[kMaxRoundShards + 1] = {};
-    hipError_t ensure_shard_streams();
+    // shard `shard` of a chain-sharded group (nullptr: not sharded)
+    ShardGroup* grp = nullptr;
+    int shard = 0;
+    // the round outputs of this shard's chains (Bm rows [r_a, r_b], S rows / witness flags [r_a,
+    // min(r_b, capacity - 1)]) copied into every other shard's tables (after its launches)
+    hipError_t share_round_rows(int32_t r_a, int32_t r_b);
     hipError_t capture_steps(StepGraph& sgr, const RoundArgs& args, int kern, int nb);
     bool la_small_used = false;   // the last DivideRounds built lastAncestors with k_la_small
     int la_small_override = -1;   // 0: never k_la_small (hgx_set_la_kernel 2), else where it applies
@@ -269,7 +295,7 @@ class Engine {
     DBuf<int64_t> sh_buf;              // ... and staging of host buffers
     // gid order
     DBuf<int32_t> g_creator, g_index, g_sp, g_op, g_ntx, g_rr, g_pos;
-    DBuf<int64_t> g_ts, g_cts;
+    DBuf<int64_t> g_ts, g_cts, g_ck;   // g_ck: (creator << 32) | chain offset (k_ck_pack, the layout's op lookups)
     DBuf<uint8_t> g_S, g_coin, g_loaded, g_txnil, g_id;
     // insert state (hgx_insert.hip)
     DBuf<uint32_t> succ, first_none;
@@ -323,6 +349,7 @@ class Engine {
     DBuf<uint32_t> FD8p;  // [kRoundPBufs][C][ndw] the same, row-major, self-validating (k_round_p)
     DBuf<uint64_t> rp_gran;   // [4][C] k_round_p hand-off granules
     DBuf<int32_t> rp_st;      // k_round_p status: abort, rounds done, finished
+    DBuf<uint8_t> rp_win;     // a chain-sharded group's RoundPWindows (device copy read by k_round_p)
     DBuf<int32_t> la_lmap;          // k_la_wave lanes -> chains with events (one graph, n > 896)
     std::vector<int32_t> h_lmap;
     DBuf<int32_t> ovf;    // [r_cap + 2]

@@ -18,6 +18,7 @@ struct DevArrays {
     const int64_t* g_ts;
     const uint8_t *g_S, *g_coin, *g_loaded, *g_txnil;
     int32_t *g_rr, *g_pos;
+    int64_t* g_ck;   // [E] (creator << 32) | (Index - chain base) of every event: the layout's op lookups
     int64_t* g_cts;
     // chains
     const int32_t *c_off, *c_len, *c_base;
@@ -212,11 +213,29 @@ bool round_p_ok(int n, int C, int num_cus);
 bool round_g_ok(int n, int nw);
 hipError_t launch_round_g(hipStream_t s, const RoundArgs& A, int32_t* status, int32_t* fin, int r0, int r_end);
 constexpr int kRoundPBufs = 4;   // candidate-row buffers of the persistent recurrence (round s: s % 4)
-// chains [c_lo, c_hi) only (c_hi < 0: all): launches over disjoint chain blocks on concurrent streams
-// sharing FD8p / gran / status are the one-GPU rehearsal of a chain-sharded recurrence;
-// init 2 = the initial rows and granules only
+constexpr int kRoundPShift = 2;  // validity bit of round s's rows: (s >> kRoundPShift) & 1
+constexpr int kMaxShards = 8;    // shards of a chain-sharded recurrence (hgx_create_sharded)
+// The hand-off windows of a chain-sharded recurrence: every shard's candidate rows,
+// granules and abort word, each written by every shard (write-through; system scope into a window
+// on another device, through the peer mapping), and every shard's firstDescendants (valid for the
+// positions of its own chains [c_split[w], c_split[w + 1])). nwin = 0: one launch over every chain,
+// its own buffers only.
+struct RoundPWindows {
+    int nwin = 0;
+    uint32_t remote = 0;   // bit w: window w lies on another device
+    uint32_t* FD8p[kMaxShards] = {};
+    uint64_t* gran[kMaxShards] = {};
+    int32_t* st[kMaxShards] = {};
+    const void* FDT[kMaxShards] = {};
+    int32_t c_split[kMaxShards + 1] = {};
+};
+// chains [c_lo, c_hi) only (c_hi < 0: all): shard k of a chain-sharded recurrence launches its chain
+// block with its nwin = W windows (win_dev: a RoundPWindows in device memory; the W shards' launches
+// run concurrently, on W devices or W streams of one); init 2 = the initial rows and granules only
+// (of the launch's chains, into every window)
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo = 0, int c_hi = -1);
+                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo = 0, int c_hi = -1,
+                          const RoundPWindows* win_dev = nullptr, int nwin = 1);
 void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, int r_last);
 // after the persistent launches: rounds of the events, wstat / wflag / active and the candidates'
 // WLA rows of rounds [r_lo, r_hi], from Bm (the persistent loop writes only Bm and the S rows)

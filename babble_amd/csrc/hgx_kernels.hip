@@ -32,8 +32,20 @@ namespace hgx {
 constexpr int kLayoutB = 4096;   // gids per block
 constexpr int kLayoutH = 1024;   // chain-id range a block can group (else direct scatter)
 
+// The op parent's (chain, chain offset) come from ONE 8-byte read of g_ck (k_ck_pack) instead of two
+// gathers (its creator and its Index) from different arrays: an op parent is an arbitrary earlier event,
+// so each gather was a line of its own (c4: 204 bytes fetched per laid-out event)
+__global__ void __launch_bounds__(256) k_ck_pack(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
+                                                 const int32_t* __restrict__ g_index, const int32_t* __restrict__ c_base,
+                                                 int64_t* __restrict__ g_ck) {
+    const int64_t gid = E0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= E) return;
+    const int c = g_creator[gid];
+    g_ck[gid] = ((int64_t)c << 32) | (uint32_t)(g_index[gid] - c_base[c]);
+}
+
 __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __restrict__ g_creator,
-                                           const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                           const int64_t* __restrict__ g_ck, const int32_t* __restrict__ g_op,
                                            const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
                                            const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
                                            const int32_t* __restrict__ c_base, int32_t* __restrict__ p_gid,
@@ -45,8 +57,9 @@ __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __
     const int op = g_op[gid];
     int opp = -1, opu = -1, opk = -1;
     if (op >= 0) {
-        const int oc = g_creator[op];
-        const int ok = g_index[op] - c_base[oc];
+        const int64_t ck = g_ck[op];
+        const int oc = (int)(ck >> 32);
+        const int ok = (int)(uint32_t)ck;
         opp = c_off[oc] + ok;
         opu = (ok / seg) * C + oc;   // lastAncestors unit of the op row (k_la_sweep)
         // op chain within the graph | op row (k_la_wave; only used when rows < 2^kOpkBits)
@@ -65,7 +78,8 @@ __device__ __forceinline__ void layout_one(int64_t gid, int p, const int32_t* __
 // a few thousand new events (the incremental schedule): one thread per event, direct scatter
 // (a 4 096-event block of k_layout would run the whole batch on one CU)
 __global__ void __launch_bounds__(256) k_layout_direct(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
-                                                       const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                                       const int32_t* __restrict__ g_index, const int64_t* __restrict__ g_ck,
+                                                       const int32_t* __restrict__ g_op,
                                                        const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
                                                        const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
                                                        const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
@@ -79,12 +93,13 @@ __global__ void __launch_bounds__(256) k_layout_direct(int64_t E0, int64_t E, co
     const int c = g_creator[gid];
     const int p = c_off[c] + g_index[gid] - c_base[c];
     g_pos[gid] = p;
-    layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu, p_opk,
+    layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu, p_opk,
                p_ts, p_rr, p_cts, C, n, seg);
 }
 
 __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
-                                                const int32_t* __restrict__ g_index, const int32_t* __restrict__ g_op,
+                                                const int32_t* __restrict__ g_index, const int64_t* __restrict__ g_ck,
+                                                const int32_t* __restrict__ g_op,
                                                 const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
                                                 const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
                                                 const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
@@ -96,7 +111,12 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
     __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
     __shared__ int32_t s_slot[kLayoutB];   // slot -> gid offset in the block
     __shared__ int32_t s_lo, s_hi;
-    const int64_t g0 = E0 + (int64_t)blockIdx.x * kLayoutB;
+    // XCD-grouped block order: blocks b, b + 8, b + 16, ... run on one XCD (the dispatcher's b % 8
+    // placement, for speed only), so each XCD takes one contiguous eighth of the gids in order and
+    // the op parents its blocks look up (mostly recent events) sit in its own L2
+    const int nbk = (int)gridDim.x, q8 = nbk / 8, r8 = nbk % 8, x8 = (int)blockIdx.x % 8;
+    const int lb = x8 * q8 + min(x8, r8) + (int)blockIdx.x / 8;   // XCD x8's j-th block (a bijection)
+    const int64_t g0 = E0 + (int64_t)lb * kLayoutB;
     const int nb = (int)min<int64_t>(kLayoutB, E - g0);
     if (threadIdx.x == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
     for (int h = threadIdx.x; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
@@ -117,7 +137,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
             const int c = g_creator[gid];
             const int p = c_off[c] + g_index[gid] - c_base[c];
             g_pos[gid] = p;
-            layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
+            layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
                        p_opu, p_opk, p_ts, p_rr, p_cts, C, n, seg);
         }
         return;
@@ -161,7 +181,7 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
         const int64_t gid = g0 + s_slot[sl];
         const int c = g_creator[gid];
         const int p = c_off[c] + g_index[gid] - c_base[c];
-        layout_one(gid, p, g_creator, g_index, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu,
+        layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu,
                    p_opk, p_ts, p_rr, p_cts, C, n, seg);
     }
 }
@@ -1860,13 +1880,15 @@ void launch_copy_many(hipStream_t s, const CopyRange* r, int count) {
 
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
     if (E <= E0) return;
+    hipLaunchKernelGGL(k_ck_pack, dim3(nblk(E - E0, 256)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.c_base,
+                       a.g_ck);
     if (E - E0 <= 8 * kLayoutB) {
         hipLaunchKernelGGL(k_layout_direct, dim3(nblk(E - E0, 256)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index,
-                           a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
+                           a.g_ck, a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
                            a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
         return;
     }
-    hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_op, a.g_ts,
+    hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_ck, a.g_op, a.g_ts,
                        a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_opk,
                        a.p_ts, a.p_rr, a.p_cts, C, n, seg);
 }

@@ -144,6 +144,13 @@ __device__ __forceinline__ void rp_st_gran(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ void rp_st_sc1(uint32_t* p, uint32_t v) {
     asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
+// the same into a window on another device (peer mapping): system scope
+__device__ __forceinline__ void rp_st_sys(uint32_t* p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void rp_st_gran_sys(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint32_t rp_ld_abort(const int32_t* p) {
     return (uint32_t)__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -303,7 +310,12 @@ struct RoundPArgs {
     int32_t* fin;       // [G] the round at which graph g found W'_s empty (-1: not yet, this call)
     int r0, r_end;      // rounds [r0, r_end) at most
     long long tmo;      // one wait's budget in s_memrealtime ticks (100 MHz)
-    int c_lo;           // this launch's first chain (a chain block: the sharded rehearsal)
+    int c_lo;           // this launch's first chain (a shard's chain block)
+    // the windows every candidate row and granule is written to (device memory; nwin = 1: FD8p / gran
+    // alone, Wd unused). Kept out of the kernel arguments: the loop's SGPRs are already spilled, and
+    // more arguments made the compiler reload arguments inside the round loop (c2 rounds +0.9 ms)
+    int nwin;
+    const RoundPWindows* Wd;
 };
 
 // One round s of chain c, in the order of its critical path:
@@ -316,7 +328,9 @@ struct RoundPArgs {
 //  (e) wave 0 publishes W'_{s+1} of chain c (row rebased to base(s+1), granule) at once, while the
 //      other waves rebase the next window [kstar, kstar + 31) to base(s+1); one barrier; the poll
 //      loads of round s + 1 go out.
-template <typename CT, int NDW, int Q>
+// SH: a shard's launch of a chain-sharded group (W windows); the plain launch over every
+// chain is a separate instantiation, so its loop keeps the code (and registers) it had without windows
+template <typename CT, int NDW, int Q, bool SH>
 __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round_p(RoundPArgs P) {
     typedef RpCfg<CT, NDW, Q> K;
     constexpr int HD = K::HD, T = K::T, WS = K::WS, NW = K::NW;
@@ -458,6 +472,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     rp_vm_drain();
     rp_lds_barrier();
     if (b < len) rebase(b, min(kRpP, len - b), bases(P.r0 - 1), t, T);
+    rp_lds_barrier();   // the first window is rebased (every later round: the barrier ending (e))
     // the first poll's loads (each round issues the next round's)
     auto gran_at = [&](int r) { return P.gran + (size_t)(r % kRpSlots) * C + g0 + (jv ? j : 0); };
     auto row_at = [&](int r) { return P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD; };
@@ -473,15 +488,18 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
 
         // (a) this lane's candidate granule and row part (W'_s): reload until the granule carries
         // tag s + 1 and, when the candidate exists, every byte of the row part carries v(s)
-        const uint32_t vbit = ((s >> 2) & 1) ? 0x80808080u : 0u;
+        const uint32_t vbit = ((s >> kRoundPShift) & 1) ? 0x80808080u : 0u;
         bool wfail = false;
-        uint64_t gv;
+        uint64_t gv = 0;
         uint32_t fd[HD];
         {
             const uint64_t* gp = gran_at(s);
             const uint32_t* rowp = row_at(s);
             const long long tw = __builtin_amdgcn_s_memrealtime();
             bool ok = false;
+            // the poll at the top priority: the waves whose candidates arrived search meanwhile, and
+            // the youngest waves (last in the age order) would otherwise issue their loads last
+            __builtin_amdgcn_s_setprio(3);
             for (int spins = 0;; spins++) {
                 if (!ok) rp_ld_cand<HD>(gp, rowp, gv, fd);   // (a lane whose candidate is complete keeps it)
                 uint32_t bad = 0;
@@ -496,6 +514,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         RP_PROF(1);
         RP_TRACE(0);
@@ -514,7 +533,8 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         }
         if (wfail && lane == 0) misc[3] = 1;
         if (cand && q == 0) misc[2] = 1;   // (same value from every writer)
-        rp_lds_barrier();   // this window's rebase (round s - 1's other waves) is complete
+        // (no barrier here: the window was rebased before the barrier ending round s - 1, and each
+        // wave searches as soon as its own candidates arrived; c3 rounds 20.7 -> 19.3 ms)
         // round s + 1's histogram and flags start empty: their buffers were last read in round
         // s - 1 (before this barrier) and are next written in round s + 1's poll (after round s's
         // histogram barrier)
@@ -558,8 +578,16 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                         // exact int32 compares of this part of the row (hashgraph.go:191-197)
                         const int i_lo = q * HD * 4, i_hi = min(n, (q + 1) * HD * 4);
                         const size_t pos = (size_t)coff[j] + bmj;
+                        // candidate j's firstDescendants are its owner shard's (valid for that
+                        // shard's chains only; a peer-mapped read when it lies on another device)
+                        const CT* __restrict__ fdt = (const CT*)A.FDT;
+                        if (SH) {
+                            int ow = 0;
+                            while (ow + 1 < P.nwin && g0 + j >= P.Wd->c_split[ow + 1]) ow++;
+                            fdt = (const CT*)P.Wd->FDT[ow];
+                        }
                         for (int i = i_lo; i < i_hi; i++) {
-                            const int32_t fdv = Coord<CT>::fd(((const CT*)A.FDT)[(size_t)i * A.Pcap + pos]);
+                            const int32_t fdv = Coord<CT>::fd(fdt[(size_t)i * A.Pcap + pos]);
                             const int32_t lav = min(Coord<CT>::la(raw_at(kb + mid, i)), kMaxI32 - 1);
                             cnt += lav >= fdv ? 1u : 0u;
                         }
@@ -631,8 +659,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         if (wave == 0) {
             bool of = false;
             if (nx) {
-                const uint32_t vb1 = (((s + 1) >> 2) & 1) ? 0x80808080u : 0u;
-                uint32_t* dst = P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
+                const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
+                const size_t roff = ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
+                static_assert(NDW <= 64, "k_round_p: one row dword per lane of wave 0");
                 for (int d = lane; d < NDW; d += 64) {
                     // every LDS read first (4 firstDescendants, 4 bases), then the byte arithmetic
                     CT f[4];
@@ -649,13 +678,33 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                         of |= real && x > 126;
                         w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
                     }
-                    rp_st_sc1(dst + d, w | vb1);
+                    // into every shard's window (one: the launch's own buffers, whose address the
+                    // kernel arguments hold in SGPRs: no scalar load ahead of the store)
+                    if (!SH) {
+                        rp_st_sc1(P.FD8p + roff + d, w | vb1);
+                    } else {
+                        const RoundPWindows* __restrict__ Wd = P.Wd;
+                        for (int wi = 0; wi < P.nwin; wi++) {
+                            if ((Wd->remote >> wi) & 1u) rp_st_sys(Wd->FD8p[wi] + roff + d, w | vb1);
+                            else rp_st_sc1(Wd->FD8p[wi] + roff + d, w | vb1);
+                        }
+                    }
                 }
             }
             of = __any(of);
-            if (lane == 0)
-                rp_st_gran(P.gran + (size_t)((s + 1) % kRpSlots) * C + gc,
-                           ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u));
+            if (lane == 0) {
+                const uint64_t gw = ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u);
+                const size_t go = (size_t)((s + 1) % kRpSlots) * C + gc;
+                if (!SH) {
+                    rp_st_gran(P.gran + go, gw);
+                } else {
+                    const RoundPWindows* __restrict__ Wd = P.Wd;
+                    for (int wi = 0; wi < P.nwin; wi++) {
+                        if ((Wd->remote >> wi) & 1u) rp_st_gran_sys(Wd->gran[wi] + go, gw);
+                        else rp_st_gran(Wd->gran[wi] + go, gw);
+                    }
+                }
+            }
             if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
         if (NW == 1) {
@@ -678,6 +727,10 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             s_k = kstar;
         }
         b = kstar;
+        // the next window's rebase, the S-row slices and the publish are complete before any wave
+        // polls: each wave then searches as soon as its own candidates arrived (no barrier between
+        // the poll and the search; the histogram barrier joins the waves)
+        rp_lds_barrier();
         RP_PROF(5);
         RP_TRACE_W(s, 1);
         RP_TRACE_STORE(s);
@@ -690,20 +743,28 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     if (failed) {
         // the first workgroup to give up records its chain and round (st[3] then holds the
         // round, not the exact-row count: the launch is redone anyway)
-        if (t == 0 && atomicCAS((int32_t*)P.st, 0, gc + 1) == 0) atomicExch(&P.st[3], s);
+        if (t == 0 && atomicCAS((int32_t*)P.st, 0, gc + 1) == 0) {
+            atomicExch(&P.st[3], s);
+            // every other shard gives up too (its workgroups wait for this shard's granules)
+            for (int wi = 0; SH && wi < P.nwin; wi++)
+                if (P.Wd->st[wi] != P.st)
+                    __hip_atomic_store((gu32*)P.Wd->st[wi], (uint32_t)(gc + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         return;
     }
+    // the launch's first workgroup of a graph reports (a shard's chain block starts mid-graph)
+    const bool rep = cl == 0 || (SH && gc == P.c_lo);
     if (t == 0) {
         if (s < P.r_end) {   // W'_s empty: round s has no events (the per-launch step's outputs)
             A.wstat[(size_t)s * C + gc] = 0;
             A.wflag[(size_t)(s + 1) * C + gc] = 0;
             A.Bm[(size_t)(s + 1) * C + gc] = len;
-            if (cl == 0) {
+            if (rep) {
                 P.fin[g] = s;
                 atomicAdd(&P.st[2], 1);
             }
         }
-        if (cl == 0) atomicMax(&P.st[1], s);
+        if (rep) atomicMax(&P.st[1], s);
     }
 }
 
@@ -714,7 +775,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
 template <typename CT>
 __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
     const RoundArgs& A = P.A;
-    const int gc = blockIdx.x, n = A.n, C = A.C, g = gc / n, r = P.r0;
+    const int gc = P.c_lo + (int)blockIdx.x, n = A.n, C = A.C, g = gc / n, r = P.r0;
     const int b = A.Bm[(size_t)r * C + gc];
     const bool have = b < A.c_len[gc];
     bool of = false;
@@ -735,40 +796,55 @@ __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
             }
             w |= v << (8 * u);
         }
-        P.FD8p[((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d] = w | ((((r >> 2) & 1) ? 0x80808080u : 0u));
-        for (int k = 1; k < kRoundPBufs; k++)
-            P.FD8p[((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d] =
-                (((r + k) >> 2) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu;   // bit 7 = !v(r + k)
+        // into every shard's window (write-through; the launches that read them start after this
+        // kernel has completed on every shard)
+        for (int wi = 0; wi < P.nwin; wi++) {
+            const bool rem = P.nwin > 1 && ((P.Wd->remote >> wi) & 1u);
+            uint32_t* fw = P.nwin > 1 ? P.Wd->FD8p[wi] : P.FD8p;
+            const uint32_t v0 = w | ((((r >> kRoundPShift) & 1) ? 0x80808080u : 0u));
+            uint32_t* p0 = fw + ((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d;
+            if (rem) rp_st_sys(p0, v0); else rp_st_sc1(p0, v0);
+            for (int k = 1; k < kRoundPBufs; k++) {
+                uint32_t* pk = fw + ((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d;
+                const uint32_t vk = (((r + k) >> kRoundPShift) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu;   // bit 7 = !v(r + k)
+                if (rem) rp_st_sys(pk, vk); else rp_st_sc1(pk, vk);
+            }
+        }
     }
     of = __any(of);
-    if (threadIdx.x == 0)
-        P.gran[(size_t)(r % kRpSlots) * C + gc] =
-            ((uint64_t)(uint32_t)(r + 1) << 32) | (uint32_t)b | (have ? kRpEx : 0u) | (of ? kRpOv : 0u);
+    if (threadIdx.x == 0) {
+        const uint64_t gw = ((uint64_t)(uint32_t)(r + 1) << 32) | (uint32_t)b | (have ? kRpEx : 0u) | (of ? kRpOv : 0u);
+        for (int wi = 0; wi < P.nwin; wi++) {
+            uint64_t* gw_p = (P.nwin > 1 ? P.Wd->gran[wi] : P.gran) + (size_t)(r % kRpSlots) * C + gc;
+            if (P.nwin > 1 && ((P.Wd->remote >> wi) & 1u)) rp_st_gran_sys(gw_p, gw);
+            else rp_st_gran(gw_p, gw);
+        }
+    }
 }
 
-template <typename CT, int NDW, int Q>
+template <typename CT, int NDW, int Q, bool SH>
 static hipError_t rp_launch(hipStream_t st, const RoundPArgs& P, int num_cus, int nblk) {
     typedef RpCfg<CT, NDW, Q> K;
-    const void* f = (const void*)k_round_p<CT, NDW, Q>;
+    const void* f = (const void*)k_round_p<CT, NDW, Q, SH>;
     int per_cu = 0;
     hipError_t e = ensure_lds_limit(f, K::LDS);
     if (e == hipSuccess) e = blocks_per_cu(f, K::T, K::LDS, &per_cu);
     if (e != hipSuccess) return e;
     // every workgroup must be resident at once (they wait for each other): one per CU
     if (per_cu < 1 || P.A.C > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((k_round_p<CT, NDW, Q>), dim3(nblk), dim3(K::T), K::LDS, st, P);
+    hipLaunchKernelGGL((k_round_p<CT, NDW, Q, SH>), dim3(nblk), dim3(K::T), K::LDS, st, P);
     return hipGetLastError();
 }
 
-template <typename CT>
+template <typename CT, bool SH>
 static hipError_t rp_launch_t(hipStream_t st, const RoundPArgs& P, int num_cus, int nblk) {
     switch (round_k_ndw(P.A.n)) {
-        case 2: return rp_launch<CT, 2, 2>(st, P, num_cus, nblk);
-        case 4: return rp_launch<CT, 4, 4>(st, P, num_cus, nblk);
-        case 8: return rp_launch<CT, 8, 2>(st, P, num_cus, nblk);
-        case 16: return rp_launch<CT, 16, 4>(st, P, num_cus, nblk);
-        case 32: return rp_launch<CT, 32, 4>(st, P, num_cus, nblk);
-        case 64: return rp_launch<CT, 64, 4>(st, P, num_cus, nblk);
+        case 2: return rp_launch<CT, 2, 2, SH>(st, P, num_cus, nblk);
+        case 4: return rp_launch<CT, 4, 4, SH>(st, P, num_cus, nblk);
+        case 8: return rp_launch<CT, 8, 2, SH>(st, P, num_cus, nblk);
+        case 16: return rp_launch<CT, 16, 4, SH>(st, P, num_cus, nblk);
+        case 32: return rp_launch<CT, 32, 4, SH>(st, P, num_cus, nblk);
+        case 64: return rp_launch<CT, 64, 4, SH>(st, P, num_cus, nblk);
         default: return hipErrorInvalidValue;
     }
 }
@@ -835,11 +911,15 @@ void launch_round_p_tail(hipStream_t st, const RoundArgs& A, const int32_t* fin,
 }
 
 hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo, int c_hi) {
+                          int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo, int c_hi,
+                          const RoundPWindows* win_dev, int nwin) {
     if (c_hi < 0) c_hi = A.C;
     if (c_lo < 0 || c_hi > A.C || c_lo >= c_hi) return hipErrorInvalidValue;
     RoundPArgs P{};
     P.c_lo = c_lo;
+    if (nwin > kMaxShards || (nwin > 1 && !win_dev)) return hipErrorInvalidValue;
+    P.nwin = nwin > 1 ? nwin : 1;   // 1: one launch over every chain, its own buffers
+    P.Wd = nwin > 1 ? win_dev : nullptr;
     P.A = A;
     P.FD8p = FD8p;
     P.gran = gran;
@@ -849,12 +929,17 @@ hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, ui
     P.r_end = r_end;
     P.tmo = 5000000;   // 50 ms per wait (a round takes microseconds)
     if (init) {
-        if (A.compact) hipLaunchKernelGGL(k_round_p_init<uint16_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
-        else hipLaunchKernelGGL(k_round_p_init<int32_t>, dim3(A.C), dim3(64), 0, st, P, round_k_ndw(A.n));
+        const dim3 grid(c_hi - c_lo);
+        if (A.compact) hipLaunchKernelGGL(k_round_p_init<uint16_t>, grid, dim3(64), 0, st, P, round_k_ndw(A.n));
+        else hipLaunchKernelGGL(k_round_p_init<int32_t>, grid, dim3(64), 0, st, P, round_k_ndw(A.n));
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess || init == 2) return e;   // (2: the initial rows only)
     }
-    return A.compact ? rp_launch_t<uint16_t>(st, P, num_cus, c_hi - c_lo) : rp_launch_t<int32_t>(st, P, num_cus, c_hi - c_lo);
+    if (P.nwin > 1)
+        return A.compact ? rp_launch_t<uint16_t, true>(st, P, num_cus, c_hi - c_lo)
+                         : rp_launch_t<int32_t, true>(st, P, num_cus, c_hi - c_lo);
+    return A.compact ? rp_launch_t<uint16_t, false>(st, P, num_cus, c_hi - c_lo)
+                     : rp_launch_t<int32_t, false>(st, P, num_cus, c_hi - c_lo);
 }
 
 }  // namespace hgx

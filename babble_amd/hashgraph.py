@@ -41,12 +41,21 @@ class Hashgraph:
     participant ids g*n .. g*n+n-1); per-graph getters take `graph`.
     """
 
-    def __init__(self, n_participants: int, capacity: int = 1 << 16, device: int = 0, n_graphs: int = 1):
+    def __init__(self, n_participants: int, capacity: int = 1 << 16, device: int = 0, n_graphs: int = 1,
+                 shard_devices: Optional[Sequence[int]] = None):
+        """shard_devices: one graph whose round recurrence is chain-sharded over these devices
+        (hgx_create_sharded; shard 0 on shard_devices[0], ordinals may repeat)."""
         self.L = _lib.lib()
         self.n = n_participants
         self.G = n_graphs
         err = hgx_error()
-        self.ctx = self.L.hgx_create_batch(n_graphs, n_participants, capacity, device, C.byref(err))
+        if shard_devices is not None:
+            if n_graphs != 1:
+                raise ValueError("a chain-sharded context holds one graph")
+            devs = np.ascontiguousarray(list(shard_devices), np.int32)
+            self.ctx = self.L.hgx_create_sharded(n_participants, capacity, len(devs), ptr(devs), C.byref(err))
+        else:
+            self.ctx = self.L.hgx_create_batch(n_graphs, n_participants, capacity, device, C.byref(err))
         if not self.ctx:
             raise HgxError(err.code, err.msg.decode(errors="replace"))
         self.capacity = capacity
@@ -261,7 +270,10 @@ class Hashgraph:
         self._call(lambda ctx, e: self.L.hgx_save(ctx, os.fsencode(path), e))
 
     def save_with_payloads(self, path: str, payloads: Sequence[bytes]):
-        """Checkpoint with the caller's per-event bytes (hgx_save_ex), one entry per event."""
+        """Checkpoint with the caller's per-event bytes (hgx_save_ex), one entry per event
+        (ValueError otherwise: hgx_save_ex reads E + 1 offsets and that many blob bytes)."""
+        if len(payloads) != self.num_events():
+            raise ValueError(f"save_with_payloads: {len(payloads)} payloads for {self.num_events()} events")
         off = np.zeros(len(payloads) + 1, np.int64)
         off[1:] = np.cumsum([len(b) for b in payloads]) if len(payloads) else []
         blob = np.frombuffer(b"".join(payloads) or b"\0", np.uint8).copy()
@@ -609,10 +621,12 @@ class Hashgraph:
             raise ValueError(f"invalid round kernel {mode}")
 
     def set_round_shards(self, shards: int):
-        """The one-GPU rehearsal of a chain-sharded recurrence: W chain blocks on W streams
-        (hgx_set_round_shards)."""
+        """hgx_create_sharded's chain-sharded recurrence with every shard on this context's device
+        (hgx_set_round_shards): on an empty context; W shards on one device need
+        GPU_MAX_HW_QUEUES >= W + 2."""
         if self.L.hgx_set_round_shards(self.ctx, int(shards)) != 0:
-            raise ValueError(f"invalid shard count {shards}")
+            raise ValueError(f"invalid shard count {shards} (an empty context, 1..8 shards, "
+                             f"GPU_MAX_HW_QUEUES >= shards + 2 for shards sharing a device)")
 
     def set_cts_kernel(self, mode):
         """FindOrder consensus timestamps: "auto" = "tile" (default: one tile of 8 positions per

@@ -77,9 +77,10 @@ def make_trace(cfg, rank):
                                 for s in seeds]), G
 
 
-def kernel_bytes(name, n, E, m, compact):
+def kernel_bytes(name, n, E, m, compact, sort_passes=1):
     """SURVEY §8(d) algorithmic bytes of one pass, per kernel: E events,
-    m events received by the pass, coordinates of `cb` bytes (2 compact, 4 int32)."""
+    m events received by the pass, coordinates of `cb` bytes (2 compact, 4 int32); the sort moves
+    2 x 44 bytes per consensus event in each of its radix passes."""
     cb = 2 if compact else 4
     return {
         "la_sweep": (3 * cb * n + 16) * E,      # la_build: read 2 parent rows, write the row (12n+16 int32)
@@ -87,9 +88,23 @@ def kernel_bytes(name, n, E, m, compact):
         "round_search": (4 * n + 16) * E,       # round_assign: 4n+16 per event (witness rows amortised)
         "round_received": 16 * E,
         "cts_median": (cb * n + 8 * n + 12) * m,  # FD row + <= n timestamp gathers + outputs
-        "order_sort": 2 * 44 * m,
+        "order_sort": 2 * 44 * m * sort_passes,
         "layout": 64 * E,
     }.get(name)
+
+
+def host_cpu():
+    """The host's CPU model (/proc/cpuinfo) and its logical CPU count (nproc)."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
 
 
 def cpu_baseline(t, n, budget_note, ordered_frac=None):
@@ -122,10 +137,11 @@ def cpu_baseline(t, n, budget_note, ordered_frac=None):
                 f"orders)")
     elif not ordered:
         note = " (no round is decided within the sample: no rate is reported)"
-    base = dict(value=value, unit="consensus-ordered events/s", cores=1, kind="port",
+    model, nproc = host_cpu()
+    base = dict(value=value, unit="consensus-ordered events/s", cores=1, kind="port", cpu_model=model, nproc=nproc,
                 sample=f"first {t.E} events of the {budget_note} trace (seed 1), oracle InsertEvent+DivideRounds+"
-                       f"DecideFame+FindOrder single-threaded, {ordered} events ordered in {dt:.2f}s on "
-                       f"{platform.processor() or platform.machine()}{note}")
+                       f"DecideFame+FindOrder single-threaded (1 of the host's {nproc} logical CPUs, {model}), "
+                       f"{ordered} events ordered in {dt:.2f}s{note}")
     return base, o
 
 
@@ -392,44 +408,33 @@ def p256_leg(count, steps, warmup, device):
     return out
 
 
-def _valid_signature_pool():
-    """libcrypto's valid (key, digest, r, s) rows of tests/golden/p256_vectors.txt, by key."""
-    pool = {}
-    with open(os.path.join(ROOT, "tests", "golden", "p256_vectors.txt")) as f:
-        for line in f:
-            pub, dg, r, s, exp, kok, _ = line.split()
-            if int(exp) == 1 and int(kok):
-                pool.setdefault(pub, []).append((dg, r, s))
-    return [(k, pool[k]) for k in sorted(pool)]
+def _signature_pool():
+    """libcrypto signatures of tests/golden/p256_pool256.npz (tests/golden/make_p256_pool.py): 256
+    keys, 16 valid signatures each. Returns keys [K, 65] and digest / r / s [K, 16, 32]."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "p256_pool256.npz"))
+    return z["keys"], z["digest"], z["r"], z["s"]
 
 
 def insert_verify_leg(h, tr, steps, ref, sha_ms, device):
     """InsertEvent with Event.Verify (hashgraph.go:356-363, event.go:142-152) over the whole
     headline trace: clear -> hgx_insert_events_verified_device (batched P-256 verify of every
     event merged with the parent/index checks' first-failure rule) -> DivideRounds -> DecideFame
-    -> FindOrder, columns HBM-resident. Participant c signs with libcrypto fixture key c % K and
-    event (c, Index) carries that key's valid fixture signature number Index % len (the S column
-    is the signature's S, so the consensus tie-break runs on these S). Checked: every event is
-    accepted, and rounds / round received / timestamps equal the headline run's (they do not
-    depend on S). `ref` = (rr, cts) of the headline run."""
+    -> FindOrder, columns HBM-resident. Participant c signs with its own libcrypto key c % 256 (c3:
+    256 distinct keys, the context's key footprint: 256 comb tables) and event (c, Index) carries
+    that key's signature number Index % 16 (the S column is the signature's S, so the consensus
+    tie-break runs on these S). Checked: every event is accepted, and rounds / round received /
+    timestamps equal the headline run's (they do not depend on S). `ref` = (rr, cts) of the
+    headline run."""
     from babble_amd.hashgraph import DeviceBuffer, DeviceTrace
     from babble_amd import trace as gtrace
-    pool = _valid_signature_pool()
-    nk = len(pool)
-    keys = np.stack([np.frombuffer(bytes.fromhex(pool[c % nk][0]), np.uint8) for c in range(h.n)])
-    per_key = [np.stack([np.stack([np.frombuffer(bytes.fromhex(x), np.uint8) for x in row]) for row in rows])
-               for _, rows in pool]                  # [K][rows][3][32]: digest, r, s
+    pk, pdig, pr, ps = _signature_pool()
+    nk, per = pk.shape[0], pdig.shape[1]
+    keys = np.stack([pk[c % nk] for c in range(h.n)])
     kk = (tr.creator % h.n) % nk
-    dig = np.empty((tr.E, 32), np.uint8)
-    sr = np.empty((tr.E, 32), np.uint8)
-    ss = np.empty((tr.E, 32), np.uint8)
-    for k in range(nk):
-        sel = np.nonzero(kk == k)[0]
-        if len(sel) == 0:
-            continue
-        rows = per_key[k]
-        pick = rows[tr.index[sel] % len(rows)]
-        dig[sel], sr[sel], ss[sel] = pick[:, 0], pick[:, 1], pick[:, 2]
+    pick = tr.index % per
+    dig = np.ascontiguousarray(pdig[kk, pick])
+    sr = np.ascontiguousarray(pr[kk, pick])
+    ss = np.ascontiguousarray(ps[kk, pick])
     t2 = gtrace.GossipTrace(**{**tr.__dict__, "s": ss})
     dtr, dd, dr = DeviceTrace(t2, device=device), DeviceBuffer(dig, device), DeviceBuffer(sr, device)
     del dig, sr, ss
@@ -456,11 +461,12 @@ def insert_verify_leg(h, tr, steps, ref, sha_ms, device):
         raise SystemExit(f"INSERT-VERIFY CHECK FAILURE: accepted {ins} of {tr.E}, rr/cts equal to the headline: "
                          f"{np.array_equal(rr, ref[0])}/{np.array_equal(cts, ref[1])}")
     res = {"value": ordered / el, "unit": "consensus-ordered events/s", "ms_per_step": el * 1e3,
-           "signatures_verified_per_step": int(tr.E), "keys": nk,
+           "signatures_verified_per_step": int(tr.E), "keys": int(min(nk, h.n)),
            "step": "clear + InsertEvent with Event.Verify (batched P-256 verify + parent/index checks, device) + "
                    "DivideRounds + DecideFame + FindOrder, columns HBM-resident",
            "check": "every event accepted; rounds received and consensus timestamps equal the headline run's",
-           "signatures": "libcrypto 3.0.2 fixture signatures (tests/golden/p256_vectors.txt), cycled per key"}
+           "signatures": "libcrypto 3.0.2 signatures (tests/golden/p256_pool256.npz: one key per participant, 16 "
+                         "signatures per key, cycled by Index)"}
     if sha_ms:
         res["with_event_ids_ms"] = el * 1e3 + sha_ms
         res["with_event_ids_value"] = ordered / (el + sha_ms * 1e-3)
@@ -478,11 +484,65 @@ def device_of(local_rank):
     return local_rank % nd if nd > 0 else local_rank
 
 
-def run_sharded(args, red, world, rank, local_rank):
-    """C3's north-star mode (BASELINE configs[2]): ONE graph row-sharded over the ranks. Every
-    rank holds the whole DAG (the same trace) and runs the replicated phases; the consensus
-    timestamps are computed per creator block and all-gathered (RCCL on GPUs). Strong scaling:
-    value = the graph's ordered events / the slowest rank's time."""
+def run_sharded(args):
+    """C3's north-star single-graph mode (BASELINE configs[2]): ONE graph whose round recurrence is
+    chain-sharded over `--gpus` devices in one process (hgx_create_sharded): shard k
+    builds its chains' firstDescendants, runs their workgroups of the persistent recurrence (its
+    candidate rows and granules written into every shard's window over the peer mapping) and their
+    consensus timestamps; inserts, lastAncestors, fame, round received and the sort are replicated.
+    With fewer devices than shards, shards share a device (the same code: its windows are then local).
+    Strong scaling: value = the graph's ordered events per step / the step's wall time."""
+    from babble_amd import trace
+    from babble_amd.hashgraph import Hashgraph, compact_columns
+    import torch
+    n, E, G, silent, stale, depth, desc = CONFIGS[args.config]
+    if G != 1:
+        raise SystemExit("--sharded: one graph per run (c1, c2, c3, c5)")
+    ndev = max(1, torch.cuda.device_count())
+    devs = [k % ndev for k in range(args.gpus)]
+    tr = trace.gossip(n, E, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
+    h = Hashgraph(n, capacity=tr.E, shard_devices=devs)
+    cols = compact_columns(tr)
+
+    def step():
+        h.clear()
+        h.insert_and_run32(cols)
+        return int(h.L.hgx_consensus_events_count(h.ctx, 0))
+
+    for w in range(max(1, args.warmup)):
+        tw = time.time()
+        ordered = step()
+        log(f"[sharded x{len(devs)}] warmup {w}: {ordered} ordered in {time.time() - tw:.2f}s  {h.phase_times()}")
+    t0 = time.perf_counter()
+    ordered = 0
+    for _ in range(args.steps):
+        ordered = step()
+    t_el = time.perf_counter() - t0
+    ph = h.phase_times()
+    if ph["round_p_fallbacks"]:
+        raise SystemExit(f"--sharded: the sharded recurrence fell back to per-launch steps: {ph}")
+    checks = {"full_size": "skipped"}
+    if not args.no_check:
+        checks["full_size"] = full_size_checks(h, tr, 1)
+    print(json.dumps({
+        "metric": "consensus-ordered events/sec at N=256 peers (1 GPU and 8-GPU batched sims)",
+        "value": ordered * args.steps / t_el, "unit": "consensus-ordered events/s", "n_gpus": len(set(devs)),
+        "shards": len(devs), "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_el * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (seeded random-gossip trace), in host RAM at the start of every step",
+        "config": {"workload": desc, "config": args.config, "peers": n, "events": int(tr.E),
+                   "shard_devices": devs,
+                   "parallelism": f"one graph, round recurrence chain-sharded x{len(devs)} over devices {devs} "
+                                  f"(firstDescendants, recurrence workgroups and consensus timestamps per chain "
+                                  f"block; the rest replicated), one process",
+                   "phase_ms_last_step": {k: round(float(v), 3) for k, v in ph.items()}},
+        "checks": checks}), flush=True)
+
+
+def run_sharded_ranks(args, red, world, rank, local_rank):
+    """The multi-process form of C3's mode (torch.distributed ranks, RCCL): every rank holds the
+    whole DAG and runs every phase but the consensus-timestamp medians, computed per creator block
+    and all-gathered between the halves of FindOrder (hgx_set_shard). Strong scaling."""
     from babble_amd import trace
     from babble_amd.hashgraph import DeviceTrace, Hashgraph
     n, E, G, silent, stale, depth, desc = CONFIGS[args.config]
@@ -538,20 +598,31 @@ def main():
     ap.add_argument("--wide", action="store_true", help="hand the events over as hgx_events (108 B/event) "
                                                         "instead of hgx_events32 (61 B/event)")
     ap.add_argument("--sharded", action="store_true",
-                    help="C3's mode: one graph row-sharded over the ranks (strong scaling) instead of replicas")
+                    help="C3's single-graph mode in one process: the round recurrence chain-sharded over --gpus devices "
+                         "(shards share a device when there are fewer; strong scaling) instead of replicas")
+    ap.add_argument("--sharded-ranks", action="store_true",
+                    help="C3's mode over torch.distributed ranks: consensus timestamps per creator block, all-gathered")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--round-shards", type=int, default=1,
-                    help="rehearse a chain-sharded recurrence on one GPU: W chain blocks on W streams (measurement)")
+                    help="the chain-sharded recurrence with W shards on this rank's GPU (measurement)")
     args = ap.parse_args()
+    if args.sharded or args.round_shards > 1:
+        # shards that share a device need a hardware queue each (their launches wait for each
+        # other): set before the HIP runtime starts
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(args.gpus, args.round_shards) + 4))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    red = Reducer(world, local_rank, backend=args.backend)
     if args.sharded:
+        if world > 1:
+            raise SystemExit("--sharded runs one process over --gpus devices (not under torch.distributed.run)")
+        return run_sharded(args)
+    red = Reducer(world, local_rank, backend=args.backend)
+    if args.sharded_ranks:
         if world < 2:
-            raise SystemExit("--sharded needs torch.distributed.run with >= 2 ranks")
-        return run_sharded(args, red, world, rank, local_rank)
+            raise SystemExit("--sharded-ranks needs torch.distributed.run with >= 2 ranks")
+        return run_sharded_ranks(args, red, world, rank, local_rank)
 
     from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns
     n, E, G, *_ = CONFIGS[args.config]
@@ -642,9 +713,12 @@ def main():
                 tj_all = json.load(open(tf))
             except Exception:
                 tj_all = {}
+        # the radix sort's passes in the per-kernel pass (libhgx counts 24 bytes per event and pass)
+        srt = ks_w.get("order_sort", {})
+        sort_passes = max(1, round(srt.get("bytes", 0) / (24.0 * m_pass))) if m_pass else 1
         for k, v in ks_w.items():
             ms = v["ms"] / nw
-            b = kernel_bytes(k, n, tr.E, m_pass, phases["compact"])
+            b = kernel_bytes(k, n, tr.E, m_pass, phases["compact"], sort_passes)
             pmc = tj_all.get(k, {}).get("bytes_per_pass") if isinstance(tj_all.get(k), dict) else None
             per_pass[k] = {"ms": round(ms, 4), "launches": v["launches"] // nw,
                            "algorithmic_bytes": b, "GB_per_s": (b / (ms * 1e-3) / 1e9) if (b and ms > 0) else None,
@@ -653,7 +727,7 @@ def main():
                            "pmc_GB_per_s": (pmc / (ms * 1e-3) / 1e9) if (pmc and ms > 0) else None}
         r = ks.get(dom, {"ms": 0, "launches": 0})
         dom_ms = r["ms"] / max(1, args.steps)
-        dom_bytes = kernel_bytes(dom, n, tr.E, m_pass, phases["compact"])
+        dom_bytes = kernel_bytes(dom, n, tr.E, m_pass, phases["compact"], sort_passes)
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and dom_bytes else 0.0
         traffic, valu = None, None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -715,6 +789,7 @@ def main():
                                  "for wide streaming kernels, Infinity-Cache hits included); valu = VALU issue "
                                  "rate from SQ_INSTS_VALU (profiles/valu_<cfg>.json)"},
             "kernels_per_pass": per_pass,
+            "sort_radix_passes": sort_passes,
             "hbm_resident": {"value": total // max(1, args.steps) / t_hbm, "unit": "consensus-ordered events/s",
                              "ms_per_step": t_hbm * 1e3,
                              "note": "the same step with the event columns already in HBM (hgx_insert_events_device, "

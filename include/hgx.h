@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define HGX_ABI_VERSION 3   /* 3: HGX_ROOT_OTHER needs its key registered (hgx_set_root_others) */
+#define HGX_ABI_VERSION 4   /* 4: hgx_create_sharded (chain-sharded recurrence over devices);
+                              3: HGX_ROOT_OTHER needs its key registered (hgx_set_root_others) */
 
 /* Error codes. 1..5 mirror common.StoreErrType + 1 (common/errors.go:7-13). */
 enum {
@@ -92,6 +93,20 @@ hgx_ctx* hgx_create(int32_t n_participants, int64_t capacity_events, int32_t dev
 /* n_graphs independent hashgraphs of n_participants each (seed-sharded simulations) */
 hgx_ctx* hgx_create_batch(int32_t n_graphs, int32_t n_participants, int64_t capacity_events,
                           int32_t device, hgx_error* err);
+/* One graph whose round recurrence is chain-sharded over n_shards devices (the north star's
+ * single-graph mode; no reference counterpart: the Go Hashgraph is one object on one
+ * core). devices[k] = shard k's HIP device (ordinals may repeat: shards that share a device need
+ * GPU_MAX_HW_QUEUES >= shards on it + 2, set before the HIP runtime starts); shard 0 is the returned
+ * context. Every shard holds the whole DAG (inserts, lastAncestors, fame, round received, sort:
+ * replicated); shard k owns chains [C k / W, C (k + 1) / W): it builds their events'
+ * firstDescendants, runs their workgroups of the persistent recurrence (writing each candidate row and
+ * granule write-through into every shard's window, over the peer mapping when the shard lies on
+ * another device) and their events' consensus timestamps, which FindOrder exchanges device to device.
+ * The drop-in calls and getters work as on one context, with the same results; n <= 256, one graph;
+ * hgx_reset, hgx_bootstrap, verified and wire inserts, hgx_set_shard and the public FindOrder halves
+ * return HGX_ERR_INVALID on it. */
+hgx_ctx* hgx_create_sharded(int32_t n_participants, int64_t capacity_events, int32_t n_shards,
+                            const int32_t* devices, hgx_error* err);
 void hgx_destroy(hgx_ctx* ctx);
 
 /* ---- the four drop-in calls ------------------------------------------------ */
@@ -448,11 +463,9 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * (hgx_round_g.hip: one workgroup per graph runs every round in one launch, n <= 16), which mode 0
  * also uses on every call where it applies. Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
-/* The one-GPU rehearsal of a chain-sharded recurrence (measurement): shards = W in
- * [1, 8] splits the persistent round launch into W launches over disjoint chain blocks on W
- * concurrent streams that hand candidate rows and granules over through shared HBM buffers (the
- * stand-in for the peers' xGMI windows), and firstDescendants into W builds of the rows of each
- * block's events. W > 1 implies the persistent recurrence where it applies. Same results. */
+/* hgx_create_sharded's shards on this context's own device: shards = W in [1, 8] (1 = back to one
+ * context), on an empty context only (before the first insert). W shards on one device need
+ * GPU_MAX_HW_QUEUES >= W + 2 (HGX_ERR_INVALID otherwise). Same results. */
 int32_t hgx_set_round_shards(hgx_ctx* ctx, int32_t shards);
 /* FindOrder consensus timestamps: 0 = default = 1: one tile of 8 positions per block (k_cts_small /
  * k_cts_tile, hgx_kernels.hip); 2 = resident blocks with three tiles' loads in flight behind the

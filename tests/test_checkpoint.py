@@ -95,3 +95,28 @@ def test_rejections(tmp_path, how):
     p.write_bytes(bytes(raw))
     with pytest.raises(ValueError):
         checkpoint.read(str(p))
+
+
+@pytest.mark.parametrize("bad", ["decrease", "nonzero_start"])
+def test_payload_offsets_rejected(tmp_path, bad):
+    """Payload offsets that do not start at 0 or decrease: libhgx's hgx_bootstrap rejects the file
+    ("payload offsets decrease"), and so does the host reader."""
+    t = gtrace.gossip(4, 50, 12)
+    pay = [b"p%d" % i for i in range(t.E)]
+    data = bytearray(checkpoint.encode(4, 1, t.creator, t.index, t.sp, t.op, t.ts, t.s, t.hash[:, 16], t.ntx,
+                                       t.txnil, payloads=pay))
+    # the offsets section is the last E + 1 int64 before the blob and the checksum
+    blob = sum(len(x) for x in pay)
+    at = len(data) - 8 - blob - 8 * (t.E + 1)
+    off = np.frombuffer(bytes(data[at:at + 8 * (t.E + 1)]), "<i8").copy()
+    assert off[0] == 0 and off[-1] == blob
+    if bad == "decrease":
+        off[5], off[6] = off[6], off[5]
+    else:
+        off[0] = 1
+    data[at:at + 8 * (t.E + 1)] = off.tobytes()
+    data[-8:] = checkpoint.fnv1a(bytes(data[:-8])).to_bytes(8, "little")
+    p = tmp_path / "p.ckpt"
+    p.write_bytes(bytes(data))
+    with pytest.raises(ValueError):
+        checkpoint.read(str(p))

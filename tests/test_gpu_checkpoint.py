@@ -147,6 +147,19 @@ def test_rooted_context_round_trip(tmp_path):
     p2 = str(tmp_path / "rooted2.ckpt")
     h2.save(p2)
     assert open(p2, "rb").read() == open(p, "rb").read()
+    # a checksum-valid file whose last section is inconsistent (one byte too many) is refused before
+    # the context is touched: no roots, no kept state, and the same context then bootstraps the good file
+    from babble_amd._lib import HgxError
+    raw = open(p, "rb").read()
+    body = raw[:-8] + b"\0"
+    p3 = str(tmp_path / "rooted_bad.ckpt")
+    open(p3, "wb").write(body + checkpoint.fnv1a(body).to_bytes(8, "little"))
+    h3 = _hg(n, E)
+    with pytest.raises(HgxError, match="size mismatch"):
+        h3.Bootstrap(p3)
+    assert h3.LastConsensusRound() is None and h3.num_events() == 0 and h3.Blocks() == []
+    h3.Bootstrap(p)
+    assert list(h3.ConsensusEvents()) == list(h2.ConsensusEvents())
 
 
 def test_bootstrap_restores_node_state(tmp_path):
@@ -165,6 +178,8 @@ def test_bootstrap_restores_node_state(tmp_path):
     h.RunConsensus()
     p = str(tmp_path / "node.ckpt")
     h.save_with_payloads(p, pay)
+    with pytest.raises(ValueError):
+        h.save_with_payloads(str(tmp_path / "short.ckpt"), pay[:-1])   # one payload per event
     r = checkpoint.read(p)
     assert np.array_equal(r["ids"], t.hash) and np.array_equal(r["keys"], keys) and r["payloads"] == pay
     h2 = _hg(n, E)

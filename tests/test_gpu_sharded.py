@@ -119,13 +119,18 @@ def test_shard_exchange_through_torch_device_tensors(n, E, chunk):
     assert len(libs) == 1, libs   # one HIP runtime in the process (babble_amd._lib._one_hip_runtime)
 
 
-# ---- the one-GPU rehearsal of a chain-sharded recurrence (hgx_set_round_shards) --------
+# ---- the chain-sharded recurrence (hgx_create_sharded / hgx_set_round_shards) ---------
+# W shard contexts in one process, each holding the whole DAG; shard k builds its chains' events'
+# firstDescendants, launches its chains' workgroups of the persistent recurrence (candidate rows and
+# granules written into every shard's window), computes its events' consensus timestamps. Here every
+# shard is on device 0 (the box has one GPU): the same code as shards on separate devices, whose windows
+# are peer-mapped.
 @pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 81, 2, None), (256, 30000, 83, 2, None),
                                                    (256, 24000, 85, 2, 6000)])
 def test_chain_sharded_recurrence_rehearsal(n, E, seed, shards, chunk):
-    """W persistent launches over disjoint chain blocks on concurrent streams (each block's
-    firstDescendants rows built by its own fd_build launch), handing candidate rows and granules
-    over through shared buffers: bit-exact with the single launch and with the oracle."""
+    """W shard contexts whose persistent launches over disjoint chain blocks (on W streams) hand
+    candidate rows and granules to each other through the shards' windows: bit-exact with the single
+    context and with the oracle, no fallback."""
     from babble_amd.hashgraph import Hashgraph
     t = gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3)
 
@@ -160,3 +165,77 @@ def test_chain_sharded_recurrence_rehearsal_more_streams(n, E, seed, shards):
     r = subprocess.run([sys.executable, os.path.join(HERE, "shard_rehearsal_worker.py"), str(n), str(E), str(seed),
                         str(shards)], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), (r.stdout[-2000:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("n,E,seed,chunk", [(64, 12000, 91, None), (256, 24000, 93, 4000)])
+def test_sharded_context_device_placement(n, E, seed, chunk):
+    """hgx_create_sharded with an explicit device per shard (both 0 here): the drop-in calls on the
+    one handle, bit-exact with a plain context and the oracle (rounds, witnesses, fame, round
+    received, timestamps, order, blocks, UndecidedRounds, LastConsensusRound)."""
+    from babble_amd.hashgraph import Hashgraph
+    t = gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=2)
+    hs = Hashgraph(n, capacity=E, shard_devices=[0, 0])
+    h1 = Hashgraph(n, capacity=E)
+    for lo in range(0, E, chunk or E):
+        hi = min(E, lo + (chunk or E))
+        for h in (hs, h1):
+            h.insert_trace(t, lo, hi)
+            h.RunConsensus()
+    ph = hs.phase_times()
+    assert ph["round_p_runs"] > 0 and ph["round_p_fallbacks"] == 0, ph
+    a, b = hs.results(), h1.results()
+    for k in ("round", "witness", "famous", "rr", "cts"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    for k in ("order", "undecided", "lcr", "lcre", "last_round"):
+        assert list(np.atleast_1d(a[k])) == list(np.atleast_1d(b[k])), k
+    assert hs.Blocks() == h1.Blocks()
+    o = hgref.oracle_run(t, chunk).results() if chunk else hgref.oracle_run(t).results()
+    assert list(a["order"]) == list(o["order"])
+    assert len(a["order"]) > 0
+
+
+def test_sharded_context_rules():
+    """What a chain-sharded context refuses: shards beyond the hardware queues of a shared device, an
+    insert before the shards are set up, batched graphs, and the calls it does not serve."""
+    import ctypes as C
+    from babble_amd.hashgraph import Hashgraph
+    from babble_amd._lib import HgxError
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    h = Hashgraph(16, capacity=1000)
+    with pytest.raises(ValueError):
+        h.set_round_shards(q - 1)   # q - 1 shards on one device need q + 1 queues
+    t = gtrace.gossip(16, 500, 5)
+    h.insert_trace(t, 0, 100)
+    with pytest.raises(ValueError):
+        h.set_round_shards(2)       # not on a context holding events
+    with pytest.raises(ValueError):
+        Hashgraph(16, capacity=1000, n_graphs=2, shard_devices=[0, 0])
+    hs = Hashgraph(16, capacity=1000, shard_devices=[0, 0])
+    err = C.create_string_buffer(256)
+    assert hs.L.hgx_find_order_begin(hs.ctx, err) != 0
+    assert hs.L.hgx_set_shard(hs.ctx, 0, 2) != 0
+    with pytest.raises(HgxError):
+        hs.Reset(np.zeros(16, np.int32), np.zeros(16, np.int32), np.zeros(16, np.int32))
+    hs.insert_trace(t)
+    hs.RunConsensus()
+    h1 = Hashgraph(16, capacity=1000)
+    h1.insert_trace(t)
+    h1.RunConsensus()
+    assert list(hs.results()["order"]) == list(h1.results()["order"])
+    with pytest.raises(ValueError):
+        hs.set_round_shards(1)      # back to one context is refused too: it holds events
+
+
+def test_bench_sharded_line():
+    """bench.py --sharded: C3's single-graph mode in one process, the recurrence chain-sharded over
+    --gpus devices (two shards on the box's one GPU), full-size property checks on the result."""
+    import json
+    root = os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--sharded", "--gpus", "2", "--config", "c2",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["shards"] == 2 and line["scaling"] == "strong" and line["value"] > 0, line
+    assert line["checks"]["full_size"]["result"] == "pass"
+    ph = line["config"]["phase_ms_last_step"]
+    assert ph["round_p_runs"] > 0 and ph["round_p_fallbacks"] == 0, ph

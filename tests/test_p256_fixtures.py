@@ -35,3 +35,24 @@ def test_libcrypto_agrees_with_vectors():
         pytest.skip(f"cannot build oracle/p256_ref (gcc + libcrypto): {e}")
     out = subprocess.run([os.path.join(ROOT, "oracle", "p256_ref"), "check", VEC], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_libcrypto_verifies_the_256_key_pool(tmp_path):
+    """tests/golden/p256_pool256.npz (bench.py insert_verify at c3's 256 keys; written by
+    tests/golden/make_p256_pool.py through libcrypto): every signature re-verified by libcrypto."""
+    import numpy as np
+    try:
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "p256_ref"])
+    except (OSError, subprocess.CalledProcessError) as e:
+        pytest.skip(f"cannot build oracle/p256_ref (gcc + libcrypto): {e}")
+    z = np.load(os.path.join(ROOT, "tests", "golden", "p256_pool256.npz"))
+    keys, dg, r, s = z["keys"], z["digest"], z["r"], z["s"]
+    assert keys.shape == (256, 65) and dg.shape == (256, 16, 32) and len({k.tobytes() for k in keys}) == 256
+    f = tmp_path / "pool.txt"
+    with open(f, "w") as o:
+        for k in range(256):
+            for i in range(16):
+                o.write(f"{keys[k].tobytes().hex()} {dg[k, i].tobytes().hex()} {r[k, i].tobytes().hex()} "
+                        f"{s[k, i].tobytes().hex()} 1 1 pool\n")
+    out = subprocess.run([os.path.join(ROOT, "oracle", "p256_ref"), "check", str(f)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
