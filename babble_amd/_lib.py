@@ -165,6 +165,7 @@ def lib():
     _sig(L, "hgx_set_coord_storage", i32, [p, i32])
     _sig(L, "hgx_set_fame_tally", i32, [p, i32])
     _sig(L, "hgx_set_round_kernel", i32, [p, i32])
+    _sig(L, "hgx_set_sort_kernel", i32, [p, i32])
     _sig(L, "hgx_set_round_shards", i32, [p, i32])
     _sig(L, "hgx_set_cts_kernel", i32, [p, i32])
     _sig(L, "hgx_set_root_others", i32, [p, p, i64, p])

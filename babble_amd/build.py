@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libhgx.so")
-SOURCES = ["hgx_kernels.hip", "hgx_rounds.hip", "hgx_round_k.hip", "hgx_round_p.hip", "hgx_round_g.hip", "hgx_la_wave.hip", "hgx_insert.hip", "hgx_sha256.hip", "hgx_p256.hip", "hgx_cts.hip", "hgx_engine.cpp", "hgx_api.cpp", "hgx_goenc.cpp", "hgx_trace.cpp"]
+SOURCES = ["hgx_kernels.hip", "hgx_rounds.hip", "hgx_round_k.hip", "hgx_round_p.hip", "hgx_round_pb.hip", "hgx_round_g.hip", "hgx_la_wave.hip", "hgx_insert.hip", "hgx_sha256.hip", "hgx_p256.hip", "hgx_cts.hip", "hgx_engine.cpp", "hgx_api.cpp", "hgx_goenc.cpp", "hgx_trace.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
          "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]

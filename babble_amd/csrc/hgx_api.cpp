@@ -2105,15 +2105,16 @@ int32_t hgx_witness(hgx_ctx* c, int64_t x) {
 // ---- instrumentation / knobs ----------------------------------------------------------
 int32_t hgx_phase_times(hgx_ctx* c, double* out, int32_t cap) {
     if (!c || !out) return 0;
-    const int32_t m = std::min<int32_t>(cap, 20);
-    double v[20] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
+    const int32_t m = std::min<int32_t>(cap, 22);
+    double v[22] = {c->eng.phase_ms[0], c->eng.phase_ms[1], c->eng.phase_ms[2], c->eng.phase_ms[3],
                     (double)c->eng.la_sweeps, (double)c->eng.R, (double)c->eng.compact,
                     (double)c->eng.la_rows, c->eng.last_rebuild ? 1.0 : 0.0, (double)c->rh.r_lo,
                     c->eng.la_wave_used ? 1.0 : 0.0, (double)c->eng.la_wave_fallbacks,
                     (double)(c->eng.la_wave_used ? c->eng.la_wave_segs : 0), (double)c->eng.round_p_runs,
                     (double)c->eng.round_p_fallbacks, (double)c->eng.round_p_ovf,
                     (double)c->eng.round_p_fail_round, (double)c->eng.round_p_fail_chain,
-                    (double)c->eng.round_g_runs, c->eng.la_small_used ? 1.0 : 0.0};
+                    (double)c->eng.round_g_runs, c->eng.la_small_used ? 1.0 : 0.0,
+                    c->eng.la_verified ? 1.0 : 0.0, (double)c->eng.sort_seg_runs};
     for (int32_t i = 0; i < m; i++) out[i] = v[i];
     return m;
 }
@@ -2191,11 +2192,12 @@ int32_t hgx_device_copy(int32_t device, void* dst, const void* src, int64_t byte
 }
 
 int32_t hgx_set_la_kernel(hgx_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 1025) return HGX_ERR_INVALID;
+    if (!c || mode < 0 || mode > 1026) return HGX_ERR_INVALID;
     each_shard(c, [&](hgx_ctx* x) {
         x->eng.la_kernel = mode == 1 ? 1 : 0;
         x->eng.la_segs_override = (mode >= 2 && mode <= 1024) ? mode : 0;
         x->eng.la_small_override = mode == 1025 ? 0 : -1;
+        x->eng.la_verify_always = mode == 1026;
     });
     return HGX_OK;
 }
@@ -2217,9 +2219,18 @@ int32_t hgx_set_root_others(hgx_ctx* c, const uint8_t* event_hash32, int64_t cou
     return ok(err);
 }
 
+int32_t hgx_set_sort_kernel(hgx_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return HGX_ERR_INVALID;
+    each_shard(c, [&](hgx_ctx* x) { x->eng.sort_seg_enabled = mode == 0; });
+    return HGX_OK;
+}
+
 int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 4) return HGX_ERR_INVALID;
-    each_shard(c, [&](hgx_ctx* x) { x->eng.round_kernel = mode; });
+    if (!c || mode < 0 || mode > 5) return HGX_ERR_INVALID;
+    each_shard(c, [&](hgx_ctx* x) {
+        x->eng.round_kernel = mode == 5 ? 0 : mode;
+        x->eng.round_pb_enabled = mode != 5;
+    });
     return HGX_OK;
 }
 
@@ -2298,6 +2309,8 @@ static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error
         q->eng.la_segs_override = c->eng.la_segs_override;
         q->eng.la_small_override = c->eng.la_small_override;
         q->eng.round_kernel = c->eng.round_kernel;
+        q->eng.round_pb_enabled = c->eng.round_pb_enabled;
+        q->eng.sort_seg_enabled = c->eng.sort_seg_enabled;
         q->eng.cts_kernel = c->eng.cts_kernel;
         q->eng.incremental = c->eng.incremental;
         q->grp = nullptr;

@@ -218,7 +218,7 @@ hipError_t Engine::init(int device, int n_graphs, int n_part, int64_t cap_events
     HGX_TRY(scan_part.alloc((size_t)256 * ((P + 2047) / 2048 + 1) / 2048 + 64));
     HGX_TRY(key_a.alloc(P)); HGX_TRY(key_b.alloc(P)); HGX_TRY(val_a.alloc(P)); HGX_TRY(val_b.alloc(P));
     HGX_TRY(hist.alloc((size_t)256 * ((P + 2047) / 2048 + 1)));
-    HGX_TRY(minmax.alloc(2));
+    HGX_TRY(minmax.alloc(3));
     HGX_TRY(lr.alloc(G));
     for (auto& e : la_ev) HGX_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HGX_TRY(hipEventCreateWithFlags(&flag_ev[0], hipEventDisableTiming));
@@ -1133,7 +1133,18 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(hipMemcpyAsync(h_small + 48, counters.p + 6, 4, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipMemsetAsync(counters.p + 6, 0, 4, stream));
         }
-        if (la_wave_segs > 1) HGX_TRY(run_sweeps(2));   // verify sweep + dirty sweeps (counted there)
+        if (la_wave_segs > 1) {
+            // the verify sweep (+ dirty sweeps, counted there) only when the segments' exactness check
+            // fails (k_la_seg_check): c3 1.6 ms per pass otherwise
+            const size_t nt = (size_t)(la_wave_segs + 1) * n;
+            if (la_chk.n < nt + 1) HGX_TRY(la_chk.alloc(nt + 1));
+            HGX_TRY(hipMemsetAsync(la_chk.p, 0, 4, stream));
+            HGX_TRY(launch_la_seg_check(stream, a, n, En, la_wave_segs, kLaHeadRows, la_chk.p + 1, la_chk.p));
+            HGX_TRY(hipMemcpyAsync(h_small + 50, la_chk.p, 4, hipMemcpyDeviceToHost, stream));
+            HGX_TRY(hipStreamSynchronize(stream));
+            la_verified = h_small[50] != 0 || la_verify_always;
+            if (la_verified) HGX_TRY(run_sweeps(2));
+        }
         la_sweeps++;
         la_rows += (int64_t)rows;
     } else {
@@ -1286,6 +1297,18 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             HGX_TRY(hipStreamSynchronize(stream));
         }
         const RoundPWindows* win_d = sh ? (const RoundPWindows*)rp_win.p : nullptr;
+        // n > 256 (one graph): k_round_pb, a workgroup per chain with events (hgx_round_pb.hip)
+        const bool big = n > 256;
+        int na = 0;
+        if (big) {
+            h_amap.clear();
+            for (int c = 0; c < C; c++)
+                if (chain_len[c] > 0) h_amap.push_back(c);
+            na = (int)h_amap.size();
+            if (na == 0) return hipErrorCooperativeLaunchTooLarge;   // (nothing to step: the steps' path)
+            if (rp_amap.n < (size_t)C) HGX_TRY(rp_amap.alloc((size_t)C));
+            HGX_TRY(hipMemcpyAsync(rp_amap.p, h_amap.data(), (size_t)na * 4, hipMemcpyHostToDevice, stream));
+        }
         int32_t s = r_lo, last = -1;
         int finished = 0;
         for (int init = 1;; init = 0) {
@@ -1294,7 +1317,13 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 a = arrays();
             }
             HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
-            if (sh && init) {
+            if (big) {
+                if (init) HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus));
+                kbeg(K_ROUND_SEARCH);
+                HGX_TRY(launch_round_pb(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, rp_amap.p, na, s, r_cap - 1,
+                                        num_cus));
+                kend(K_ROUND_SEARCH, 0);
+            } else if (sh && init) {
                 // W'_{r_lo} of this shard's chains into every window; every shard's launch starts once
                 // every window holds the whole W'_{r_lo}
                 HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus,
@@ -1302,10 +1331,12 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 HGX_TRY(hipStreamSynchronize(stream));
                 HGX_TRY(gwait());
             }
-            kbeg(K_ROUND_SEARCH);
-            HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, sh ? 0 : init,
-                                   num_cus, c_lo, c_hi, win_d, sh ? win.nwin : 1));
-            kend(K_ROUND_SEARCH, 0);
+            if (!big) {
+                kbeg(K_ROUND_SEARCH);
+                HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, sh ? 0 : init,
+                                       num_cus, c_lo, c_hi, win_d, sh ? win.nwin : 1));
+                kend(K_ROUND_SEARCH, 0);
+            }
             HGX_TRY(hipMemcpyAsync(h_small + 56, rp_st.p, 16, hipMemcpyDeviceToHost, stream));
             HGX_TRY(hipStreamSynchronize(stream));
             round_p_runs++;
@@ -1338,6 +1369,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 // graphs that finished earlier: empty rows up to the last round (k_last_round,
                 // fame and the host copies read every graph's rows of every round)
                 launch_round_p_tail(stream, round_args(), fin, last);
+                if (big) launch_round_pb_silent(stream, round_args(), r_lo, last);
                 kbeg(K_ROUND_GATHER);
                 launch_round_p_post(stream, round_args(), r_lo, last);
                 kend(K_ROUND_GATHER, (double)(last - r_lo + 1) * C * n * (sizeof(int32_t) + (compact ? 2 : 4)));
@@ -1387,7 +1419,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // workgroups) that a call resuming for a few rounds does not recover: those use the steps
     // (a chain-sharded group always runs it: its shards build firstDescendants for their own chains only)
     if (!graph_ok && !rooted && (round_kernel == 3 || (round_kernel == 0 && rebuild) || grp) &&
-        round_p_ok(n, C, num_cus)) {
+        (round_p_ok(n, C, num_cus) || (round_pb_ok(n, G) && !grp && round_pb_enabled))) {
         const hipError_t pe = run_persistent();
         if (pe != hipSuccess) {
             // redo the rounds with the per-launch steps (a timed-out launch left partial rows)
@@ -1708,12 +1740,22 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         launch_sort_small(stream, a, m, n, &vals);
         kend(K_SORT, (double)m * 24.0);
     } else {
-        // sort keys: cts range, then (graph, rr)
-        const unsigned long long init[2] = {~0ull, 0ull};
-        HGX_TRY(hipMemcpyAsync(minmax.p, init, 16, hipMemcpyHostToDevice, stream));
+        // sort keys: cts range, then (graph, rr); and the (graph, rr) buckets' sizes (the segmented
+        // sort's condition), read back in the same round trip
+        const unsigned long long init[3] = {~0ull, 0ull, 0ull};
+        HGX_TRY(hipMemcpyAsync(minmax.p, init, 24, hipMemcpyHostToDevice, stream));
         launch_minmax(stream, a, m);
-        unsigned long long mm[2];
-        HGX_TRY(hipMemcpyAsync(mm, minmax.p, 16, hipMemcpyDeviceToHost, stream));
+        const int64_t nseg64 = (int64_t)G * R;
+        const bool seg_try = sort_seg_enabled && nseg64 >= 1 && nseg64 <= (int64_t)1 << 24;
+        const int nseg = (int)nseg64;
+        if (seg_try) {
+            if (seg_off.n < (size_t)nseg + 1) HGX_TRY(seg_off.alloc((size_t)nseg + 1));
+            if (seg_cur.n < (size_t)nseg + 1) HGX_TRY(seg_cur.alloc((size_t)nseg + 1));
+            HGX_TRY(hipMemsetAsync(seg_off.p, 0, (size_t)nseg * 4, stream));
+            launch_seg_count(stream, a, m, R, n, nseg, seg_off.p, (unsigned long long*)minmax.p + 2);
+        }
+        unsigned long long mm[3];
+        HGX_TRY(hipMemcpyAsync(mm, minmax.p, 24, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
         const int64_t cmin = (int64_t)(mm[0] ^ 0x8000000000000000ull);
         const int64_t cmax = (int64_t)(mm[1] ^ 0x8000000000000000ull);
@@ -1721,10 +1763,16 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         const int seg_bits = bitlen((uint64_t)G * (uint64_t)R - 1);
         uint64_t* keys = nullptr;
         kbeg(K_SORT);
-        launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
-        kend(K_SORT, (double)m * 24.0 *
-                         (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
-                                                    : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+        if (seg_try && cts_bits + seg_bits <= 64 && mm[2] >= 1 && mm[2] <= (unsigned long long)seg_sort_cap()) {
+            launch_sort_seg(stream, a, m, cmin, cts_bits, R, n, nseg, seg_off.p, seg_cur.p, (int)mm[2], &vals, &keys);
+            sort_seg_runs++;
+            kend(K_SORT, (double)m * 24.0 * 2);   // (bucket scatter + in-LDS sort: two passes' bytes)
+        } else {
+            launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
+            kend(K_SORT, (double)m * 24.0 *
+                             (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
+                                                        : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
+        }
     }
     // a large order (a full pass: 40 MB at c3) is written by k_finish_order straight into the
     // pinned host arena (coalesced writes over the host link while the kernel runs) instead of a

@@ -230,6 +230,8 @@ class Engine {
     static constexpr int kLaHeadRows = 64;   // rows per chain rebuilt at the start of each time segment
     static constexpr int kLaSegMinRows = 512;   // time segments only when the graph has >= this many rows per chain
     int64_t la_wave_fallbacks = 0;   // k_la_wave gave up and the sweeps redid the pass
+    bool la_verified = false;        // the last time-segmented pass ran the verify sweep (its exactness check failed)
+    bool la_verify_always = false;   // hgx_set_la_kernel(1026): the verify sweep after every segmented pass (tests)
     int compact = 0;             // coordinates of the last DivideRounds stored as uint16
     bool force_coord32 = false;  // hgx_set_coord_storage(1)
     int64_t la_rows = 0;   // rows recomputed over all sweeps of the last divide_rounds
@@ -252,6 +254,9 @@ class Engine {
     hipError_t capture_steps(StepGraph& sgr, const RoundArgs& args, int kern, int nb);
     bool la_small_used = false;   // the last DivideRounds built lastAncestors with k_la_small
     int la_small_override = -1;   // 0: never k_la_small (hgx_set_la_kernel 2), else where it applies
+    bool sort_seg_enabled = true;      // FindOrder's bucketed sort (hgx_set_sort_kernel)
+    int64_t sort_seg_runs = 0;         // FindOrders sorted by buckets
+    bool round_pb_enabled = true;   // n > 256: k_round_pb (hgx_set_round_kernel 5 turns it off)
     int64_t round_p_runs = 0, round_p_fallbacks = 0;   // persistent launches / calls redone per launch
     int64_t round_p_ovf = 0;
     int32_t round_p_fail_round = -1, round_p_fail_chain = -1;   // the last give-up: round and chain   // candidate rows the persistent launches counted exactly (over 8 bits)
@@ -349,8 +354,12 @@ class Engine {
     DBuf<uint32_t> FD8p;  // [kRoundPBufs][C][ndw] the same, row-major, self-validating (k_round_p)
     DBuf<uint64_t> rp_gran;   // [4][C] k_round_p hand-off granules
     DBuf<int32_t> rp_st;      // k_round_p status: abort, rounds done, finished
+    DBuf<uint32_t> seg_off, seg_cur;   // the segmented order sort's bucket starts / cursors
+    DBuf<int32_t> rp_amap;    // k_round_pb: the chains with events
+    std::vector<int32_t> h_amap;
     DBuf<uint8_t> rp_win;     // a chain-sharded group's RoundPWindows (device copy read by k_round_p)
     DBuf<int32_t> la_lmap;          // k_la_wave lanes -> chains with events (one graph, n > 896)
+    DBuf<int32_t> la_chk;           // k_la_seg_check: [0] flag, then the segments' first rows [(nts + 1) x n]
     std::vector<int32_t> h_lmap;
     DBuf<int32_t> ovf;    // [r_cap + 2]
     DBuf<int8_t> fame;

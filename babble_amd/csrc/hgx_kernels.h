@@ -174,6 +174,10 @@ hipError_t launch_la_small(hipStream_t s, const DevArrays& a, int G, int n, cons
                            int32_t* err);
 int la_wave_blocks(int n, int compact);   // column blocks of the time-segment passes (workgroups per segment)
 int la_wave_segments(int n, int compact, int num_cus, int max_segs);   // time segments that fill the device
+// exactness check of a time-segmented lastAncestors pass plus its head pass (one graph): *flag
+// |= 1 unless every row is provably exact (then no verify sweep is needed); tbl: (nts + 1) x n ints
+hipError_t launch_la_seg_check(hipStream_t s, const DevArrays& a, int n, int64_t E, int nts, int head, int32_t* tbl,
+                               int32_t* flag);
 hipError_t launch_la_wave(hipStream_t s, const DevArrays& a, int G, int n, const int32_t* c_old, int64_t E, int nts,
                           int head, int32_t* err, const int32_t* lmap = nullptr, int na = 0,
                           bool narrow = false);
@@ -240,6 +244,15 @@ void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, 
 // after the persistent launches: rounds of the events, wstat / wflag / active and the candidates'
 // WLA rows of rounds [r_lo, r_hi], from Bm (the persistent loop writes only Bm and the S rows)
 void launch_round_p_post(hipStream_t s, const RoundArgs& A, int r_lo, int r_hi);
+// persistent recurrence for 256 < n <= 1024, one graph (hgx_round_pb.hip): one resident workgroup
+// per chain WITH events (amap: their indices, na of them), rows / granules / status / fin as
+// launch_round_p's (its init = 2 writes W'_{r0}); hipErrorCooperativeLaunchTooLarge when the na
+// workgroups cannot all be resident. launch_round_pb_silent then writes the silent chains' Bm rows
+// of rounds [r_lo, r_hi + 1] (0), before launch_round_p_post.
+bool round_pb_ok(int n, int G);
+hipError_t launch_round_pb(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
+                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus);
+void launch_round_pb_silent(hipStream_t s, const RoundArgs& A, int r_lo, int r_hi);
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,
@@ -250,6 +263,7 @@ void launch_last_round(hipStream_t s, int rs, int R, int G, int C, int n, const 
 void step_prof_dump();     // -DHGX_STEP_PROF builds only
 void round_k_prof_dump();  // -DHGX_STEP_PROF builds only
 void round_p_prof_dump();  // -DHGX_STEP_PROF builds only
+void round_pb_prof_dump(); // -DHGX_STEP_PROF builds only
 void round_g_prof_dump();  // -DHGX_STEP_PROF builds only
 // tally: 0 = witness-tiled popcount (default), 1 = per-round popcount kernel, 2 = witness-tiled int8 MFMA
 // rounds [r0, R) (r0 = the first undecided round)
@@ -275,6 +289,15 @@ void launch_cts_shard_copy(hipStream_t s, const DevArrays& a, int lo, int hi, co
 void launch_minmax(hipStream_t s, const DevArrays& a, int32_t m);
 void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                  int seg_bits, uint32_t** final_vals, uint64_t** final_keys);
+// the segmented sort (round 5): launch_seg_count counts the received events per (graph, rr) bucket
+// into segc[G R] (zeroed by the caller) and their largest bucket into *max_out (atomicMax); if that
+// is <= seg_sort_cap() and the combined key fits 64 bits, launch_sort_seg buckets the list and sorts
+// every bucket in LDS (segoff = the counts, scanned in place; segcur = [nseg] scratch)
+int seg_sort_cap();
+void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n, int nseg, uint32_t* segc,
+                      unsigned long long* max_out);
+void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
+                     uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys);
 // m <= 4096: one block sorts (graph, rr, cts, S) (no cts range needed)
 bool sort_small_ok(int32_t m);
 void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals);

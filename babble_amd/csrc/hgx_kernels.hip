@@ -1461,6 +1461,122 @@ __global__ void k_keys_seg(int32_t m, const uint32_t* __restrict__ vals, const i
     keys[i] = (uint64_t)(p_chain[p] / n) * (uint64_t)R + (uint64_t)p_rr[p];
 }
 
+// ---------------------------------------------------------------------------------
+// order, segmented (round 5): the received events bucketed by (graph, rr) -- one counting pass and
+// one scatter -- and every bucket then sorted by its combined key in one workgroup's LDS (bitonic),
+// instead of 5-6 LSD radix passes over the whole list (c4: 4.8 GB of sort traffic per pass, 6.6x the
+// one-pass bytes). A bucket holds the events received in one round (c3 ~3 500, c4 ~120); a list with a
+// bucket over kSegSortCap takes the radix sort (consensus_sorter.go:5-52, hashgraph.go:822-823).
+constexpr int kSegSortCap = 8192;
+
+// runs of equal segments among a wave's lanes [0, nvalid) (the list is chain-major with rr
+// non-decreasing along a chain, so a wave holds a few runs): the run head's lane, the run length
+__device__ __forceinline__ void wave_seg_runs(bool valid, int seg, bool& head, int& head_lane, int& run_len) {
+    const int lane = lane_id();
+    const int prev = __shfl_up(seg, 1);
+    head = valid && (lane == 0 || prev != seg);
+    const uint64_t hm = __ballot(head), vm = __ballot(valid);
+    const int nv = __popcll(vm);   // (valid lanes are a prefix)
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t above = hm & ~upto;
+    run_len = (above ? (int)__builtin_ctzll(above) : nv) - lane;
+    const uint64_t below = hm & upto;
+    head_lane = below ? 63 - (int)__builtin_clzll(below) : 0;
+}
+
+__global__ void __launch_bounds__(256) k_seg_count(int32_t m, const int32_t* __restrict__ list,
+                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+                                                   int R, int n, uint32_t* __restrict__ segc) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v = i < m;
+    int seg = -1;
+    if (v) {
+        const int p = list[i];
+        seg = (p_chain[p] / n) * R + p_rr[p];
+    }
+    bool head;
+    int hl, len;
+    wave_seg_runs(v, seg, head, hl, len);
+    if (head) atomicAdd(&segc[seg], (uint32_t)len);
+}
+
+__global__ void __launch_bounds__(256) k_seg_max(int nseg, const uint32_t* __restrict__ segc,
+                                                 unsigned long long* __restrict__ out) {
+    uint32_t mx = 0;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) mx = max(mx, segc[s]);
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+    if (lane_id() == 0 && mx) atomicMax(out, (unsigned long long)mx);
+}
+
+// (key, value) into its bucket: slot = bucket start + a per-bucket cursor (one atomic per run)
+__global__ void __launch_bounds__(256) k_seg_scatter(int32_t m, const uint64_t* __restrict__ kin,
+                                                     const uint32_t* __restrict__ vin, int cts_bits,
+                                                     const uint32_t* __restrict__ segoff, uint32_t* __restrict__ segcur,
+                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v = i < m;
+    const uint64_t key = v ? kin[i] : 0ull;
+    const int seg = v ? (int)(key >> cts_bits) : -1;
+    bool head;
+    int hl, len;
+    wave_seg_runs(v, seg, head, hl, len);
+    uint32_t base = 0;
+    if (head) base = atomicAdd(&segcur[seg], (uint32_t)len);
+    base = (uint32_t)__shfl((int)base, hl);
+    if (v) {
+        const uint32_t slot = segoff[seg] + base + (uint32_t)(lane_id() - hl);
+        kout[slot] = key;
+        vout[slot] = vin[i];
+    }
+}
+
+// one bucket per workgroup: bitonic sort of its (key, value) pairs in LDS (cap = the largest bucket
+// rounded up to a power of two; ties in the key are ordered by S afterwards, k_tiefix_rank)
+__global__ void __launch_bounds__(256) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
+                                                  const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                  uint64_t* __restrict__ kout, uint32_t* __restrict__ vout, int cap) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
+    uint32_t* sv = (uint32_t*)(sk + cap);
+    const int sgi = blockIdx.x;
+    const int o = (int)segoff[sgi], e = sgi + 1 < nseg ? (int)segoff[sgi + 1] : m, len = e - o;
+    const int t = threadIdx.x, T = blockDim.x;
+    if (len <= 1) {
+        if (len == 1 && t == 0) {
+            kout[o] = kin[o];
+            vout[o] = vin[o];
+        }
+        return;
+    }
+    int P = 2;
+    while (P < len) P <<= 1;
+    for (int i = t; i < P; i += T) {
+        sk[i] = i < len ? kin[o + i] : ~0ull;
+        sv[i] = i < len ? vin[o + i] : 0u;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = t; q < (P >> 1); q += T) {
+                const int lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
+                const bool asc = (lo & k) == 0;
+                const uint64_t a = sk[lo], b = sk[hi];
+                if ((a > b) == asc) {
+                    sk[lo] = b;
+                    sk[hi] = a;
+                    const uint32_t x = sv[lo];
+                    sv[lo] = sv[hi];
+                    sv[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < len; i += T) {
+        kout[o + i] = sk[i];
+        vout[o + i] = sv[i];
+    }
+}
+
 // grid-stride min/max of the received events' timestamps (biased to unsigned order);
 // one atomic pair per block
 __global__ void __launch_bounds__(256) k_minmax_cts(int32_t m, const int32_t* __restrict__ list,
@@ -2156,6 +2272,36 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
     }
     hipLaunchKernelGGL(k_tiefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_cts, a.p_gid, a.g_S);
     *final_vals = va;
+    *final_keys = ka;
+}
+
+int seg_sort_cap() { return kSegSortCap; }
+
+void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n, int nseg, uint32_t* segc,
+                      unsigned long long* max_out) {
+    hipLaunchKernelGGL(k_seg_count, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_chain, a.p_rr, R, n, segc);
+    hipLaunchKernelGGL(k_seg_max, dim3(std::max(1, std::min(256, (nseg + 255) / 256))), dim3(256), 0, s, nseg, segc,
+                       max_out);
+}
+
+void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
+                     uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys) {
+    uint64_t *ka = a.key_a, *kb = a.key_b;
+    uint32_t *va = a.val_a, *vb = a.val_b;
+    hipLaunchKernelGGL(k_keys_comb, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr,
+                       cmin, cts_bits, R, n, ka, va);
+    scan_u32(s, a, segoff, nseg);   // bucket counts -> bucket starts
+    (void)hipMemsetAsync(segcur, 0, (size_t)nseg * 4, s);
+    hipLaunchKernelGGL(k_seg_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, ka, va, cts_bits, segoff, segcur, kb, vb);
+    int cap = 2;
+    while (cap < max_seg) cap <<= 1;
+    const size_t lds = (size_t)cap * 12;
+    (void)ensure_lds_limit((const void*)k_seg_sort, lds);
+    hipLaunchKernelGGL(k_seg_sort, dim3(nseg), dim3(256), lds, s, nseg, m, segoff, kb, vb, ka, va, cap);
+    // runs of equal keys ordered by S, as after the radix sort (kb / vb are free again)
+    hipLaunchKernelGGL(k_tie_prefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_gid, a.g_S, kb);
+    hipLaunchKernelGGL(k_tiefix_rank, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, vb, ka, kb, a.p_gid, a.g_S);
+    *final_vals = vb;
     *final_keys = ka;
 }
 

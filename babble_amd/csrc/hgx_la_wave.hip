@@ -604,6 +604,76 @@ int la_wave_segments(int n, int compact, int num_cus, int max_segs) {
     return std::max(1, std::min(max_segs, per_cu * num_cus / la_wave_blocks(n, compact)));
 }
 
+// ---- exactness check of the time-segmented pass (one graph; replaces the verify sweep when it holds)
+// The segment pass (MODE 2) gives row x of segment t the max over x's ancestors y IN segment t
+// (every path from such a y to x stays in the segment: parents have smaller gids), per chain c':
+// L'[x][c'] = max index of an ancestor of x on c' with gid >= the segment start. Indices and gids
+// both grow along a chain, so whenever x has ANY ancestor on c' inside the segment, the largest one
+// is inside too and L'[x][c'] is exact; only a coordinate left "none" can be wrong, and only if c'
+// has events before the segment. Rows grow along a chain, so if the first row after the head rows
+// (the rows MODE 3 rebuilds) has no such coordinate, every later row of the chain in the segment is
+// exact. The head rows are rebuilt from exact parents if every parent they read from memory is a
+// non-head row (exact by the above) or a segment-0 row, i.e. never another segment's head row,
+// which the same launch rebuilds concurrently. Both conditions hold -> every row is exact and the
+// verify sweep is skipped; either fails -> *flag = 1 and the sweep runs.
+__global__ void __launch_bounds__(256) k_la_seg_bounds(const int32_t* __restrict__ p_gid, const int32_t* __restrict__ c_off,
+                                                       const int32_t* __restrict__ c_len, int64_t E, int nts, int n,
+                                                       int32_t* __restrict__ tbl) {
+    const int t = blockIdx.x;   // [0, nts]: first row of each chain in segment t (nts: the chain's length)
+    for (int c = threadIdx.x; c < n; c += blockDim.x) {
+        const int len = c_len[c];
+        tbl[(size_t)t * n + c] = t == 0 ? 0 : t == nts ? len : chain_lower_bound(p_gid, c_off[c], len, E * t / nts);
+    }
+}
+
+template <typename CT>
+__global__ void __launch_bounds__(256) k_la_seg_check(const CT* __restrict__ LA, const int32_t* __restrict__ p_gid,
+                                                      const int32_t* __restrict__ p_op, const int32_t* __restrict__ p_chain,
+                                                      const int32_t* __restrict__ c_off, const int32_t* __restrict__ tbl,
+                                                      int64_t E, int nts, int n, int head, int32_t* __restrict__ flag) {
+    const int t = 1 + (int)blockIdx.x / n, c = (int)blockIdx.x % n;   // segment t >= 1, chain c
+    const int o = tbl[(size_t)t * n + c], e = tbl[(size_t)(t + 1) * n + c], off = c_off[c];
+    bool bad = false;
+    // (a) the first row after the head rows: no "none" coordinate of a chain with events before t
+    if (e - o > head) {
+        const CT* __restrict__ row = LA + (size_t)(off + o + head) * n;
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            if (Coord<CT>::la(row[i]) < 0 && tbl[(size_t)t * n + i] > 0) bad = true;
+    }
+    // (b) every head row's parent outside the rebuilt region is not another segment's head row
+    const int kh = min(e, o + head);
+    for (int k = o + (int)threadIdx.x; k < kh; k += blockDim.x) {
+        if (k == o && k > 0) {   // the self-parent: the chain's last row before segment t
+            int tz = t - 1;
+            while (tz > 0 && tbl[(size_t)tz * n + c] > k - 1) tz--;
+            if (tz >= 1 && k - 1 < tbl[(size_t)tz * n + c] + head) bad = true;
+        }
+        const int opp = p_op[off + k];
+        if (opp >= 0) {
+            const int d = p_chain[opp], r = opp - c_off[d];
+            const int64_t gz = p_gid[opp];
+            int tz = (int)min<int64_t>(nts - 1, gz * nts / E);   // the segment holding gid gz
+            while (tz > 0 && E * tz / nts > gz) tz--;
+            while (tz + 1 < nts && E * (tz + 1) / nts <= gz) tz++;
+            if (tz >= 1 && tz < t && r < tbl[(size_t)tz * n + d] + head) bad = true;
+        }
+    }
+    if (bad) atomicOr(flag, 1);
+}
+
+hipError_t launch_la_seg_check(hipStream_t s, const DevArrays& a, int n, int64_t E, int nts, int head, int32_t* tbl,
+                               int32_t* flag) {
+    if (nts < 2) return hipSuccess;
+    hipLaunchKernelGGL(k_la_seg_bounds, dim3(nts + 1), dim3(256), 0, s, a.p_gid, a.c_off, a.c_len, E, nts, n, tbl);
+    if (a.compact)
+        hipLaunchKernelGGL(k_la_seg_check<uint16_t>, dim3((nts - 1) * n), dim3(256), 0, s, (const uint16_t*)a.LA,
+                           a.p_gid, a.p_op, a.p_chain, a.c_off, tbl, E, nts, n, head, flag);
+    else
+        hipLaunchKernelGGL(k_la_seg_check<int32_t>, dim3((nts - 1) * n), dim3(256), 0, s, (const int32_t*)a.LA,
+                           a.p_gid, a.p_op, a.p_chain, a.c_off, tbl, E, nts, n, head, flag);
+    return hipGetLastError();
+}
+
 // one workgroup holds every chain of a graph plus the loader waves (<= 1024 threads)
 bool la_wave_ok(int n, int max_len, int n_active) {
     return n >= 1 && n <= 1024 && n_active <= 896 && max_len < (1 << kOpkBits);

@@ -1,0 +1,616 @@
+// Persistent round recurrence for 256 < n <= 1024 (one graph): the k_round_p design (every round in
+// one launch, candidate rows and granules handed over write-through and self-validating; RoundInc
+// hashgraph.go:285-305, StronglySee :170-198) for candidate rows too large for one workgroup's
+// registers. DESIGN.md §3.3.
+//
+//  * one workgroup of 1 024 threads per PP = 3 chains WITH events (the "probers"; silent chains have
+//    no candidate in any round and no workgroup, their granules are never polled). Every prober's
+//    31-probe window lives in LDS rebased to 8 bits (as k_round_p);
+//  * 8 lanes per candidate (each holds a 1/8 part of the candidate's 8-bit rebased row, the counts
+//    combined by DPP inside the wave), so a pass covers 128 candidates: the candidates come in chunks
+//    of 128 (8 at n = 1 024), each chunk polled, validated and then searched against the PP windows
+//    at once (three binary searches per loaded row). A candidate row crosses the fabric once per
+//    workgroup and round: with one prober per workgroup the polls of c5 moved ~700 MB per round and
+//    took 190 us of the ~350 us round (tools/probe, prof build);
+//  * per (prober, candidate) its K(w) and "seen in an earlier window" bit go to LDS (the S row is
+//    assembled from them once the boundary is known); per prober a K(w) histogram gives the boundary;
+//  * the windows' raw lastAncestors rows and the new candidates' firstDescendants come straight from
+//    HBM (at n = 1 024 a 32-position staging segment is 64 KB).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hgx_device.h"
+#include "hgx_kernels.h"
+
+namespace hgx {
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+constexpr int kPbP = 31;   // probes per window
+constexpr int kPbSlots = 4;
+constexpr int kPbPP = 3;   // probers (chains) per workgroup
+constexpr uint32_t kPbEx = 1u << 31, kPbOv = 1u << 30, kPbBm = (1u << 30) - 1;
+
+__device__ __forceinline__ void pb_st_sc1(uint32_t* p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void pb_st_gran(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t pb_ld_abort(const int32_t* p) {
+    return (uint32_t)__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pb_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void pb_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// a candidate's granule and this lane's HD dwords of its row (sc1 loads, issued and waited for in one
+// asm statement: see rp_ld_cand, hgx_round_p.hip)
+template <int HD>
+__device__ __forceinline__ void pb_ld_cand(const uint64_t* gp, const uint32_t* p, uint64_t& gv, uint32_t (&v)[HD]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    static_assert(HD == 16 || HD == 32, "pb_ld_cand: HD in {16, 32}");
+    u32x4 a, b, c, d;
+    asm volatile(
+        "global_load_dwordx2 %0, %5, off sc1\n\t"
+        "global_load_dwordx4 %1, %6, off sc1\n\t"
+        "global_load_dwordx4 %2, %6, off offset:16 sc1\n\t"
+        "global_load_dwordx4 %3, %6, off offset:32 sc1\n\t"
+        "global_load_dwordx4 %4, %6, off offset:48 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(p) : "memory");
+    const u32x4 q4[4] = {a, b, c, d};
+#pragma unroll
+    for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
+    if constexpr (HD == 32) {
+        u32x4 e, f, g, h;
+        asm volatile(
+            "global_load_dwordx4 %0, %4, off offset:64 sc1\n\t"
+            "global_load_dwordx4 %1, %4, off offset:80 sc1\n\t"
+            "global_load_dwordx4 %2, %4, off offset:96 sc1\n\t"
+            "global_load_dwordx4 %3, %4, off offset:112 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(e), "=&v"(f), "=&v"(g), "=&v"(h) : "v"(p) : "memory");
+        const u32x4 r4[4] = {e, f, g, h};
+#pragma unroll
+        for (int k = 0; k < 4; k++) { v[16 + 4 * k] = r4[k].x; v[17 + 4 * k] = r4[k].y; v[18 + 4 * k] = r4[k].z; v[19 + 4 * k] = r4[k].w; }
+    }
+}
+
+__device__ __forceinline__ uint32_t pb_combine8(uint32_t x) {   // sum over the 8 lanes of a candidate
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);    // quad_perm xor 1
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false);    // quad_perm xor 2
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xf, 0xf, false);   // half-row mirror
+    return x;
+}
+
+constexpr int pb_part_stride(int hd) {   // smallest stride >= hd that is 8 or 24 (mod 32)
+    int ps = hd;
+    while (ps % 32 != 8 && ps % 32 != 24) ps++;
+    return ps;
+}
+
+template <int NDW>
+struct PbCfg {
+    static constexpr int Q = 8, T = 1024, NW = T / 64, PP = kPbPP;
+    static constexpr int HD = NDW / Q;          // row dwords per lane (16 or 32)
+    static constexpr int CPB = T / Q;           // candidates per pass (128)
+    static constexpr int NC = 4 * NDW;          // chains (padded)
+    static constexpr int NCH = NC / CPB;        // chunks
+    static constexpr int PS = pb_part_stride(HD);
+    static constexpr int WS = Q * PS + 4;       // window row stride (dwords)
+    static constexpr int WIN = kPbP * WS;       // window (dwords)
+    // LDS (bytes)
+    static constexpr int O_WIN = 0;                       // [PP][kPbP][WS] rebased probes
+    static constexpr int O_BS = O_WIN + PP * WIN * 4;     // [2][NC] c_base + Bm, by round parity
+    static constexpr int O_KST = O_BS + 2 * NC * 4;       // [PP][NC] bytes: K | done << 5 | cand << 6
+    static constexpr int O_HIST = O_KST + PP * NC;        // [PP][32]
+    static constexpr int O_POF = O_HIST + PP * 32 * 4;    // [PP] the published row's overflow flag
+    static constexpr int O_MISC = O_POF + PP * 4;         // [8]: [2] any, [3] fail
+    static constexpr int LDS = O_MISC + 32;
+    static_assert(LDS <= 160 * 1024, "k_round_pb: LDS carve exceeds a CU's 160 KB");
+};
+
+struct RoundPbArgs {
+    RoundArgs A;
+    uint32_t* FD8p;   // [4][C][ndw], bit 7 of every byte = v(s) = (s >> 2) & 1 (round s: buffer s % 4)
+    uint64_t* gran;   // [4][C]
+    int32_t* st;      // [0] abort, [1] max round stopped, [2] finished, [3] rows counted exactly
+    int32_t* fin;     // [1]
+    const int32_t* amap;   // [na] the chains with events
+    int na;
+    int r0, r_end;
+    long long tmo;
+};
+
+}  // namespace
+
+// Optional phase clocks (-DHGX_STEP_PROF, build variant "prof"): thread 0 of each workgroup adds
+// clock deltas per phase: 1 polls, 2 searches (both summed over the chunks), 3 histogram barrier,
+// 4 scan + later windows, 5 publish + S rows, 6 publish barrier, 7 next windows' rebase + end barrier;
+// 15 = block-rounds
+#ifdef HGX_STEP_PROF
+__device__ unsigned long long hgx_pb_prof[16];
+#define PB_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[16] = {}
+#define PB_PROF(i)                                    \
+    do {                                              \
+        if (threadIdx.x == 0) {                       \
+            const long long _t = clock64();           \
+            _pa[i] += (unsigned long long)(_t - _pt); \
+            _pt = _t;                                 \
+            if ((i) == 7) _pa[15] += 1;               \
+        }                                             \
+    } while (0)
+#define PB_PROF_END()                                              \
+    do {                                                           \
+        if (threadIdx.x == 0)                                      \
+            for (int _i = 0; _i < 16; _i++)                        \
+                if (_pa[_i]) atomicAdd(&hgx_pb_prof[_i], _pa[_i]); \
+    } while (0)
+void round_pb_prof_dump() {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_pb_prof), sizeof(h)) != hipSuccess) return;
+    if (!h[15]) return;
+    const double r = (double)h[15];
+    fprintf(stderr, "[hgx] k_round_pb clk per block-round (thread 0): polls %.0f searches %.0f hist-barrier %.0f "
+            "scan+windows %.0f publish %.0f pub-barrier %.0f rebase+barrier %.0f | block-rounds %llu\n",
+            h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / r, h[6] / r, h[7] / r, h[15]);
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_pb_prof), z, sizeof(z));
+}
+#else
+#define PB_PROF_BEGIN() (void)0
+#define PB_PROF(i) (void)0
+#define PB_PROF_END() (void)0
+void round_pb_prof_dump() {}
+#endif
+
+template <typename CT, int NDW>
+__global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
+    typedef PbCfg<NDW> K;
+    constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, PS = K::PS, CPB = K::CPB;
+    constexpr int NCH = K::NCH, NC = K::NC;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const RoundArgs& A = P.A;
+    const int n = A.n, C = A.C, sm = A.sm;
+    const int t = threadIdx.x, lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int jl = t / Q, q = t % Q;   // candidate slot in a pass, row part
+    auto winp = [&](int k) { return (uint32_t*)(lds + K::O_WIN) + k * K::WIN; };
+    auto bpar = [&](int r) { return (int32_t*)(lds + K::O_BS) + (r & 1) * NC; };   // c_base + Bm[r]
+    auto kstp = [&](int k) { return lds + K::O_KST + k * NC; };
+    auto histp = [&](int k) { return (int32_t*)(lds + K::O_HIST) + k * 32; };
+    int32_t* pof = (int32_t*)(lds + K::O_POF);
+    int32_t* misc = (int32_t*)(lds + K::O_MISC);
+    if (P.fin[0] >= 0) return;   // finished in an earlier launch of this DivideRounds
+    const CT* __restrict__ LA = (const CT*)A.LA;
+    const CT* __restrict__ FDT = (const CT*)A.FDT;
+    // the probers (block-uniform)
+    int gcs[PP], lens[PP], offs[PP], bs[PP];
+    bool valid[PP];
+#pragma unroll
+    for (int k = 0; k < PP; k++) {
+        const int a = (int)blockIdx.x * PP + k;
+        valid[k] = a < P.na;
+        gcs[k] = __builtin_amdgcn_readfirstlane(valid[k] ? P.amap[a] : 0);
+        lens[k] = __builtin_amdgcn_readfirstlane(valid[k] ? A.c_len[gcs[k]] : 0);
+        offs[k] = __builtin_amdgcn_readfirstlane(A.c_off[gcs[k]]);
+        bs[k] = __builtin_amdgcn_readfirstlane(valid[k] ? A.Bm[(size_t)P.r0 * C + gcs[k]] : 0);
+    }
+    for (int i = t; i < NC; i += T) {
+        // (a silent chain's Bm rows are written after the launches: 0 = its length)
+        const bool li = i < n && A.c_len[i] > 0;
+        bpar(P.r0 - 1)[i] = (i < n ? A.c_base[i] : 0) + (P.r0 > 0 && li ? A.Bm[(size_t)(P.r0 - 1) * C + i] : 0);
+    }
+    if (t < PP * 32) ((int32_t*)(lds + K::O_HIST))[t] = 0;
+    if (t < PP) pof[t] = 0;
+    if (t < 8) misc[t] = 0;
+    // rebased 8-bit window rows of prober k's positions [kb, kb + np) against bases bq, straight from
+    // HBM: rb_load issues a thread's raw loads, rb_store rebases them into the window
+    // (T a multiple of NDW: a thread keeps its dword d = t % NDW, rows p = (t + kT) / NDW)
+    constexpr int PER = (kPbP * NDW + T - 1) / T;
+    constexpr int NR = sizeof(CT) == 2 ? 2 : 4;   // raw dwords per row dword
+    typedef uint32_t RawRows[PER][NR];
+    auto rb_load = [&](RawRows& raw, int off, int kb, int np) {
+        const int d = t % NDW;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int p = (t + k * T) / NDW;
+#pragma unroll
+            for (int u = 0; u < NR; u++) raw[k][u] = 0u;
+            if (p < np) {
+                const CT* row = LA + (size_t)(off + kb + p) * n;
+                if constexpr (sizeof(CT) == 2) {   // (compact: n even)
+                    const uint32_t* rw = (const uint32_t*)row;
+                    if (4 * d < n) raw[k][0] = rw[2 * d];
+                    if (4 * d + 2 < n) raw[k][1] = rw[2 * d + 1];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) raw[k][u] = 4 * d + u < n ? (uint32_t)row[4 * d + u] : 0u;
+                }
+            }
+        }
+    };
+    auto rb_store = [&](const RawRows& raw, uint32_t* win, int np, const int32_t* bq) {
+        const int d = t % NDW;
+        if (t / NDW >= np) return;
+        int32_t bq4[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) bq4[u] = 4 * d + u < n ? bq[4 * d + u] : 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int p = (t + k * T) / NDW;
+            if (p >= np) continue;
+            int32_t la[4];
+            if constexpr (sizeof(CT) == 2) {
+                la[0] = (int32_t)(raw[k][0] & 0xFFFFu) - 1; la[1] = (int32_t)(raw[k][0] >> 16) - 1;
+                la[2] = (int32_t)(raw[k][1] & 0xFFFFu) - 1; la[3] = (int32_t)(raw[k][1] >> 16) - 1;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; u++) la[u] = (int32_t)raw[k][u];
+            }
+            uint32_t w = 0x80808080u;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (4 * d + u < n) {
+                    const int32_t x = la[u] - bq4[u] + 1;
+                    w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
+                }
+            }
+            win[p * WS + (d / HD) * PS + d % HD] = w;
+        }
+    };
+    auto rebase = [&](uint32_t* win, int off, int kb, int np, const int32_t* bq) {
+        RawRows raw;
+        rb_load(raw, off, kb, np);
+        rb_store(raw, win, np, bq);
+    };
+    pb_lds_barrier();   // the bases (a rebase reads other threads' entries)
+#pragma unroll
+    for (int k = 0; k < PP; k++)
+        if (valid[k] && bs[k] < lens[k]) rebase(winp(k), offs[k], bs[k], min(kPbP, lens[k] - bs[k]), bpar(P.r0 - 1));
+    pb_lds_barrier();
+    PB_PROF_BEGIN();
+    int s = P.r0;
+    bool failed = false;
+    for (;; s++) {
+        if (s >= P.r_end) break;
+        bool have[PP], act[PP];
+        int kb[PP], np[PP], kstar[PP], B[PP], carried[PP];
+#pragma unroll
+        for (int k = 0; k < PP; k++) {
+            have[k] = valid[k] && bs[k] < lens[k];
+            act[k] = have[k];
+            kb[k] = bs[k];
+            np[k] = have[k] ? min(kPbP, lens[k] - bs[k]) : 0;
+            kstar[k] = lens[k];
+            B[k] = -1;
+            carried[k] = 0;
+        }
+        const uint32_t vbit = ((s >> kRoundPShift) & 1) ? 0x80808080u : 0u;
+        bool any = false;
+        for (int w_it = 0;; w_it++) {
+            // every chunk of 128 candidates: poll (reload in a later window), search every active window
+            for (int ch = 0; ch < NCH; ch++) {
+                const int j = ch * CPB + jl;
+                const bool jv = j < n;
+                const bool live = jv && A.c_len[j] > 0;   // silent chains publish nothing
+                uint64_t gv = 0;
+                uint32_t fd[HD];
+                const uint64_t* gp = P.gran + (size_t)(s % kPbSlots) * C + (live ? j : 0);
+                const uint32_t* rowp = P.FD8p + ((size_t)(s & (kRoundPBufs - 1)) * C + (live ? j : 0)) * NDW + q * HD;
+                // (a wave of this workgroup gave up: no further waits)
+                bool wfail = *(volatile int32_t*)&misc[3] != 0;
+                if (!wfail && __any(live)) {
+                    const long long tw = __builtin_amdgcn_s_memrealtime();
+                    bool ok = false;
+                    for (int spins = 0;; spins++) {
+                        if (!ok) pb_ld_cand<HD>(gp, rowp, gv, fd);
+                        uint32_t bad = 0;
+#pragma unroll
+                        for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
+                        const bool tag_ok = (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
+                        ok = !live || (tag_ok && (!((uint32_t)gv & kPbEx) || bad == 0));
+                        if (__all(ok)) break;
+                        if ((spins & 31) == 31) {
+                            const long long now = __builtin_amdgcn_s_memrealtime();
+                            if (now - tw > P.tmo || pb_ld_abort(P.st) != 0) { wfail = true; break; }
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                PB_PROF(1);
+                const uint32_t gval = (uint32_t)gv;
+                const bool cand = live && !wfail && (gval & kPbEx);
+                const bool ov = cand && (gval & kPbOv);
+                if (w_it == 0 && jv && q == 0 && !wfail) bpar(s)[j] = A.c_base[j] + (live ? (int)(gval & kPbBm) : 0);
+                if (wfail && lane == 0) misc[3] = 1;
+                if (cand && q == 0) misc[2] = 1;
+#pragma unroll
+                for (int d = 0; d < HD; d++) fd[d] = cand ? (fd[d] & 0x7F7F7F7Fu) : 0x7F7F7F7Fu;
+                bool done[PP], srch[PP];
+                int lo[PP], hi[PP];
+                const bool wc = __any(cand);
+#pragma unroll
+                for (int k = 0; k < PP; k++) {
+                    done[k] = w_it > 0 && jv && ((kstp(k)[j] >> 5) & 1);   // seen in an earlier window
+                    srch[k] = act[k] && wc;
+                    lo[k] = 0;
+                    hi[k] = kPbP;
+                }
+                bool srch_any = false;
+#pragma unroll
+                for (int k = 0; k < PP; k++) srch_any |= srch[k];
+#pragma unroll 1
+                for (int it = 0; it < (srch_any ? 5 : 0); it++) {
+                    int mid[PP];
+                    uint32_t cnt[PP];
+#pragma unroll
+                    for (int k = 0; k < PP; k++) {
+                        mid[k] = (lo[k] + hi[k]) >> 1;
+                        cnt[k] = 0;
+                    }
+                    if (!ov) {
+                        // this lane's part of each active window's probe row, 8 dwords at a time
+#pragma unroll
+                        for (int k = 0; k < PP; k++) {
+                            if (!srch[k]) continue;
+                            const uint4* rp = (const uint4*)(winp(k) + mid[k] * WS + q * PS);
+#pragma unroll
+                            for (int h = 0; h < HD / 8; h++) {
+                                const uint4 v0 = rp[2 * h], v1 = rp[2 * h + 1];
+                                const uint32_t* f8 = fd + 8 * h;
+                                cnt[k] += __builtin_popcount((v0.x - f8[0]) & 0x80808080u) +
+                                          __builtin_popcount((v0.y - f8[1]) & 0x80808080u) +
+                                          __builtin_popcount((v0.z - f8[2]) & 0x80808080u) +
+                                          __builtin_popcount((v0.w - f8[3]) & 0x80808080u) +
+                                          __builtin_popcount((v1.x - f8[4]) & 0x80808080u) +
+                                          __builtin_popcount((v1.y - f8[5]) & 0x80808080u) +
+                                          __builtin_popcount((v1.z - f8[6]) & 0x80808080u) +
+                                          __builtin_popcount((v1.w - f8[7]) & 0x80808080u);
+                            }
+                        }
+                    } else {
+                        // exact int32 compares of this part of the row (hashgraph.go:191-197)
+                        const int i_lo = q * HD * 4, i_hi = min(n, (q + 1) * HD * 4);
+                        const size_t pos = (size_t)A.c_off[j] + (gval & kPbBm);
+#pragma unroll
+                        for (int k = 0; k < PP; k++) {
+                            if (!srch[k] || done[k] || mid[k] >= np[k]) continue;
+                            for (int i = i_lo; i < i_hi; i++) {
+                                const int32_t fdv = Coord<CT>::fd(FDT[(size_t)i * A.Pcap + pos]);
+                                const int32_t lav =
+                                    min(Coord<CT>::la(LA[(size_t)(offs[k] + kb[k] + mid[k]) * n + i]), kMaxI32 - 1);
+                                cnt[k] += lav >= fdv ? 1u : 0u;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < PP; k++) {
+                        if (!srch[k]) continue;
+                        const uint32_t c8 = pb_combine8(cnt[k]);
+                        const bool seen = done[k] || mid[k] >= np[k] || ((int)c8 >= sm && !(j == gcs[k] && kb[k] + mid[k] == bs[k]));
+                        if (seen) hi[k] = mid[k]; else lo[k] = mid[k] + 1;
+                    }
+                }
+                PB_PROF(2);
+#pragma unroll
+                for (int k = 0; k < PP; k++) {
+                    if (!act[k]) continue;   // (a prober whose boundary is known keeps its K)
+                    const int Kw = srch[k] ? lo[k] : 0;
+                    if (cand && q == 0 && !done[k] && Kw < np[k]) atomicAdd(&histp(k)[Kw], 1);
+                    // K of this window, seen-earlier bit, candidate bit (the S row's inputs)
+                    if (jv && q == 0) kstp(k)[j] = (uint8_t)(min(Kw, 31) | (done[k] ? 32 : 0) | (cand ? 64 : 0));
+                }
+            }
+            // the histograms are complete: every wave scans them (the boundary: first probe where
+            // #{K <= p} (+ seen in earlier windows) >= SM)
+            pb_lds_barrier();
+            PB_PROF(3);
+            any = misc[2] != 0;
+            const bool fail = misc[3] != 0;
+            bool more = false, nxt[PP];
+            int tot[PP];
+#pragma unroll
+            for (int k = 0; k < PP; k++) {
+                nxt[k] = false;
+                tot[k] = 0;
+                if (!act[k]) continue;
+                const uint32_t v = lane < np[k] ? (uint32_t)histp(k)[lane] : 0u;
+                const uint32_t inc = wave_scan_add_u32(v) + (uint32_t)carried[k];
+                const uint64_t m = __ballot(lane < np[k] && (int)inc >= sm);
+                tot[k] = __builtin_amdgcn_readlane((int)inc, 63);
+                B[k] = __builtin_amdgcn_readfirstlane(m ? (int)__builtin_ctzll(m) : -1);
+                if (B[k] >= 0) kstar[k] = kb[k] + B[k];
+                // no boundary in this window (rare): the next one, if the chain has more events
+                nxt[k] = B[k] < 0 && any && !fail && kb[k] + np[k] < lens[k];
+                more |= nxt[k];
+            }
+            if (!more) break;
+            pb_lds_barrier();   // every wave has scanned the histograms and read kst
+#pragma unroll
+            for (int k = 0; k < PP; k++) {
+                if (!nxt[k]) {
+                    act[k] = false;
+                    continue;
+                }
+                // the candidates seen in this window are seen at every later probe
+                uint8_t* ks = kstp(k);
+                for (int jj = t; jj < n; jj += T) {
+                    const uint8_t k8 = ks[jj];
+                    if ((k8 & 64) && (k8 & 31) < np[k]) ks[jj] = (uint8_t)(k8 | 32);
+                }
+                if (t < 32) histp(k)[t] = 0;
+                carried[k] = tot[k];
+                kb[k] += np[k];
+                np[k] = min(kPbP, lens[k] - kb[k]);
+                rebase(winp(k), offs[k], kb[k], np[k], bpar(s - 1));
+            }
+            pb_lds_barrier();
+        }
+        PB_PROF(4);
+        if (misc[3] != 0) { failed = true; break; }
+        if (!any) break;   // W'_s is empty: no round s
+        // the next windows' raw rows (compact coordinates: every prober's loads in flight beside the
+        // publish's gathers; int32 rows are loaded after the publish, one prober at a time)
+        constexpr bool kMerged = sizeof(CT) == 2;
+        RawRows rawn[kMerged ? PP : 1];
+        int np1[PP];
+#pragma unroll
+        for (int k = 0; k < PP; k++) {
+            np1[k] = valid[k] && kstar[k] < lens[k] ? min(kPbP, lens[k] - kstar[k]) : 0;
+            if constexpr (kMerged) rb_load(rawn[k], offs[k], kstar[k], np1[k]);
+        }
+        // W'_{s+1} of each prober: the firstDescendants row of position kstar rebased to
+        // base(s+1) = c_base + Bm[s] (bit 7 = v(s + 1)), straight from the FDT columns
+        {
+            const int k = t / NDW, d = t % NDW;
+            int kk = -1;   // (a register-indexed prober: its scalars by an unrolled select)
+#pragma unroll
+            for (int x = 0; x < PP; x++)
+                if (k == x && valid[x] && kstar[x] < lens[x]) kk = x;
+            if (kk >= 0) {
+                int off = 0, kst_ = 0, gc = 0;
+#pragma unroll
+                for (int x = 0; x < PP; x++)
+                    if (kk == x) { off = offs[x]; kst_ = kstar[x]; gc = gcs[x]; }
+                const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
+                const int32_t* bs1 = bpar(s);
+                CT f[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) f[u] = FDT[(size_t)min(4 * d + u, n - 1) * A.Pcap + off + kst_];
+                uint32_t w = 0;
+                bool of = false;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int32_t fv = Coord<CT>::fd(f[u]);
+                    const bool real = 4 * d + u < n && fv != kMaxI32;
+                    const int32_t x = fv - (real ? bs1[4 * d + u] : 0) + 1;
+                    of |= real && x > 126;
+                    w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
+                }
+                pb_st_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + d, w | vb1);
+                if (of) pof[kk] = 1;
+            }
+        }
+        // the S rows (DecideFame, hashgraph.go:688-705): bit j = the new candidate strongly sees
+        // candidate j of W'_s, i.e. j was seen in an earlier window or K(j) <= B
+        constexpr int WPR = NC / 64;   // 64-bit words per S row
+        for (int task = wave; task < PP * WPR; task += NW) {
+            const int k = task / WPR, w = task % WPR;
+            int Bk = -1, gc = 0;
+            bool nx = false;
+#pragma unroll
+            for (int x = 0; x < PP; x++)
+                if (k == x) { Bk = B[x]; gc = gcs[x]; nx = valid[x] && kstar[x] < lens[x]; }
+            if (!nx || w >= A.nw) continue;   // (wave-uniform)
+            const int jj = w * 64 + lane;
+            const uint8_t k8 = jj < n ? kstp(k)[jj] : 0;
+            const uint64_t m = __ballot((k8 & 64) && ((k8 & 32) || (int)(k8 & 31) <= Bk));
+            if (lane == 0) A.Smat[((size_t)(s + 1) * C + gc) * A.nw + w] = m;
+        }
+#pragma unroll
+        for (int k = 0; k < PP; k++)
+            if (t == k && valid[k]) A.Bm[(size_t)(s + 1) * C + gcs[k]] = kstar[k];
+        PB_PROF(5);
+        pb_lds_barrier();   // the rows' overflow flags, every search read of the windows, kst reads
+        PB_PROF(6);
+#pragma unroll
+        for (int k = 0; k < PP; k++) {
+            if (t == k && valid[k]) {
+                const bool of = pof[k] != 0;
+                const bool nx = kstar[k] < lens[k];
+                pb_st_gran(P.gran + (size_t)((s + 1) % kPbSlots) * C + gcs[k],
+                           ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar[k] | (nx ? kPbEx : 0u) |
+                               (of ? kPbOv : 0u));
+                if (of) atomicAdd(&P.st[3], 1);
+                pof[k] = 0;   // (same thread: read before)
+            }
+        }
+        if (t >= 64 && t < 64 + PP * 32) ((int32_t*)(lds + K::O_HIST))[t - 64] = 0;
+        if (t == 200) misc[2] = 0;
+#pragma unroll
+        for (int k = 0; k < PP; k++) {
+            if constexpr (kMerged) rb_store(rawn[k], winp(k), np1[k], bpar(s));
+            else if (np1[k] > 0) rebase(winp(k), offs[k], kstar[k], np1[k], bpar(s));
+            bs[k] = kstar[k];
+        }
+        pb_lds_barrier();
+        PB_PROF(7);
+    }
+    PB_PROF_END();
+    pb_vm_drain();
+    if (failed) {
+        if (t == 0 && atomicCAS((int32_t*)P.st, 0, gcs[0] + 1) == 0) atomicExch(&P.st[3], s);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < PP; k++) {
+        if (t != k || !valid[k]) continue;
+        const bool rep = blockIdx.x == 0 && k == 0;
+        if (s < P.r_end) {   // W'_s empty: round s has no events (the per-launch step's outputs)
+            A.wstat[(size_t)s * C + gcs[k]] = 0;
+            A.wflag[(size_t)(s + 1) * C + gcs[k]] = 0;
+            A.Bm[(size_t)(s + 1) * C + gcs[k]] = lens[k];
+            if (rep) {
+                P.fin[0] = s;
+                atomicAdd(&P.st[2], 1);
+            }
+        }
+        if (rep) atomicMax(&P.st[1], s);
+    }
+}
+
+// the rows of silent chains (no events, no workgroup) for rounds [r_lo, r_hi]: Bm = 0 (= len)
+__global__ void k_round_pb_silent(RoundArgs A, int r_lo, int r_hi) {
+    const int gc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gc >= A.C || A.c_len[gc] != 0) return;
+    for (int r = r_lo; r <= r_hi + 1; r++) A.Bm[(size_t)r * A.C + gc] = 0;
+}
+
+namespace {
+template <typename CT, int NDW>
+hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus) {
+    typedef PbCfg<NDW> K;
+    const void* f = (const void*)k_round_pb<CT, NDW>;
+    int per_cu = 0;
+    hipError_t e = ensure_lds_limit(f, K::LDS);
+    if (e == hipSuccess) e = blocks_per_cu(f, K::T, K::LDS, &per_cu);
+    if (e != hipSuccess) return e;
+    const int nblk = (P.na + K::PP - 1) / K::PP;
+    // every workgroup must be resident at once (they wait for each other)
+    if (per_cu < 1 || nblk > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL((k_round_pb<CT, NDW>), dim3(nblk), dim3(K::T), K::LDS, st, P);
+    return hipGetLastError();
+}
+}  // namespace
+
+bool round_pb_ok(int n, int G) { return G == 1 && n > 256 && n <= 1024; }
+
+hipError_t launch_round_pb(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
+                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus) {
+    if (!round_pb_ok(A.n, A.C / A.n) || na < 1) return hipErrorInvalidValue;
+    RoundPbArgs P{};
+    P.A = A;
+    P.FD8p = FD8p;
+    P.gran = gran;
+    P.st = status;
+    P.fin = fin;
+    P.amap = amap;
+    P.na = na;
+    P.r0 = r0;
+    P.r_end = r_end;
+    P.tmo = 5000000;   // 50 ms per wait
+    const int ndw = round_k_ndw(A.n);
+    if (A.compact) return ndw == 128 ? pb_launch<uint16_t, 128>(st, P, num_cus) : pb_launch<uint16_t, 256>(st, P, num_cus);
+    return ndw == 128 ? pb_launch<int32_t, 128>(st, P, num_cus) : pb_launch<int32_t, 256>(st, P, num_cus);
+}
+
+void launch_round_pb_silent(hipStream_t st, const RoundArgs& A, int r_lo, int r_hi) {
+    if (r_hi < r_lo) return;
+    hipLaunchKernelGGL(k_round_pb_silent, dim3((A.C + 255) / 256), dim3(256), 0, st, A, r_lo, r_hi);
+}
+
+}  // namespace hgx

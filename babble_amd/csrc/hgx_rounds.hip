@@ -788,6 +788,7 @@ void step_prof_dump() {
     fprintf(stderr, "\n");
     round_k_prof_dump();
     round_p_prof_dump();
+    round_pb_prof_dump();
     round_g_prof_dump();
 }
 #else

@@ -585,15 +585,16 @@ class Hashgraph:
                     pending_loaded=self.PendingLoadedEvents(graph), blocks=self.Blocks(graph))
 
     def phase_times(self):
-        out = np.zeros(20, np.float64)
-        self.L.hgx_phase_times(self.ctx, ptr(out), 20)
+        out = np.zeros(22, np.float64)
+        self.L.hgx_phase_times(self.ctx, ptr(out), 22)
         return dict(coords_ms=out[0], rounds_ms=out[1], fame_ms=out[2], order_ms=out[3],
                     la_sweeps=int(out[4]), rounds=int(out[5]), compact=int(out[6]),
                     la_rows=int(out[7]), rebuild=int(out[8]), r_lo=int(out[9]),
                     la_wave=int(out[10]), la_wave_fallbacks=int(out[11]), la_wave_segs=int(out[12]),
                     round_p_runs=int(out[13]), round_p_fallbacks=int(out[14]), round_p_ovf=int(out[15]),
                     round_p_fail_round=int(out[16]), round_p_fail_chain=int(out[17]),
-                    round_g_runs=int(out[18]), la_small=int(out[19]))
+                    round_g_runs=int(out[18]), la_small=int(out[19]), la_verify=int(out[20]),
+                    sort_seg=int(out[21]))
 
     def set_fame_tally(self, mode):
         """DecideFame tally: "popc" (default), "vote" (per-round kernel) or "mfma" (int8 MFMA)."""
@@ -604,8 +605,9 @@ class Hashgraph:
     def set_la_kernel(self, mode):
         """DivideRounds lastAncestors: "wave" (default, one dataflow pass; a small graph's whole
         graph in LDS), "ring" (the dataflow pass without the small-graph form) or "sweep"
-        (Gauss-Seidel)."""
-        m = {"wave": 0, "sweep": 1, "ring": 1025}[mode] if isinstance(mode, str) else int(mode)
+        (Gauss-Seidel); "wave+verify" runs the verify sweep after every time-segmented pass (by default
+        only when the segments' exactness check fails)."""
+        m = {"wave": 0, "sweep": 1, "ring": 1025, "wave+verify": 1026}[mode] if isinstance(mode, str) else int(mode)
         if self.L.hgx_set_la_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid lastAncestors kernel {mode}")
 
@@ -614,11 +616,20 @@ class Hashgraph:
         out anew, where it applies, else per-round "candidate" launches; the whole-graph
         recurrence on every call for n <= 16), "persistent" (the persistent recurrence on every
         call where it applies), "graph" (one workgroup per graph of n <= 16 on every call),
-        "block" (block binary search per round) or "candidate" (one launch per round, one lane
-        per candidate)."""
-        m = {"auto": 0, "block": 1, "candidate": 2, "persistent": 3, "graph": 4}[mode] if isinstance(mode, str) else int(mode)
+        "block" (block binary search per round), "candidate" (one launch per round, one lane
+        per candidate) or "auto-steps" ("auto" without the big-n persistent recurrence: n > 256
+        runs the "candidate" steps)."""
+        m = ({"auto": 0, "block": 1, "candidate": 2, "persistent": 3, "graph": 4, "auto-steps": 5}[mode]
+             if isinstance(mode, str) else int(mode))
         if self.L.hgx_set_round_kernel(self.ctx, m) != 0:
             raise ValueError(f"invalid round kernel {mode}")
+
+    def set_sort_kernel(self, mode):
+        """FindOrder's sort: "auto" (default: buckets by (graph, roundReceived), each sorted in LDS,
+        where every bucket holds <= 8 192 events) or "radix" (LSD radix passes over the whole list)."""
+        m = {"auto": 0, "radix": 1}[mode] if isinstance(mode, str) else int(mode)
+        if self.L.hgx_set_sort_kernel(self.ctx, m) != 0:
+            raise ValueError(f"invalid sort kernel {mode}")
 
     def set_round_shards(self, shards: int):
         """hgx_create_sharded's chain-sharded recurrence with every shard on this context's device

@@ -603,6 +603,8 @@ def main():
     ap.add_argument("--sharded-ranks", action="store_true",
                     help="C3's mode over torch.distributed ranks: consensus timestamps per creator block, all-gathered")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--round-kernel", default="auto",
+                    help="DivideRounds' round kernel (Hashgraph.set_round_kernel; measurement A/B, e.g. auto-steps)")
     ap.add_argument("--round-shards", type=int, default=1,
                     help="the chain-sharded recurrence with W shards on this rank's GPU (measurement)")
     args = ap.parse_args()
@@ -631,6 +633,8 @@ def main():
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
     dev = device_of(local_rank)   # one GPU per rank (ranks share a GPU only in gloo rehearsals)
     h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
+    if args.round_kernel != "auto":
+        h.set_round_kernel(args.round_kernel)
     if args.round_shards > 1:   # the one-GPU rehearsal of a chain-sharded recurrence
         h.set_round_shards(args.round_shards)
     # the columns as the caller hands them over, built before the clock: hgx_events32 (int32 Index

@@ -449,11 +449,14 @@ int32_t hgx_set_fame_tally(hgx_ctx* ctx, int32_t mode);
  * (n <= 32 compact / 16 int32, its rows within 150 KB) the pass with the whole graph in one
  * workgroup's LDS; 1 = Gauss-Seidel sweeps to the fixed point (hgx_kernels.hip), 2 <= m <= 1024 =
  * the dataflow pass with m time segments on a rebuild (measurement), 1025 = the dataflow pass
- * without the small-graph form. Same results. */
+ * without the small-graph form, 1026 = the default with the verify sweep after every time-segmented
+ * pass (by default it runs only when the segments' exactness check fails). Same results
+ * (DESIGN.md §3.1). */
 int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
 /* DivideRounds rounds: 0 = default: the persistent recurrence (hgx_round_p.hip, one resident
  * workgroup per chain runs every round in one launch) where it applies (n <= 256, at most one
- * chain per compute unit, no roots) on a call that lays the DAG out anew (a call resuming after
+ * chain per compute unit, no roots; for 256 < n <= 1024 and one graph hgx_round_pb.hip, one
+ * resident workgroup per chain with events) on a call that lays the DAG out anew (a call resuming after
  * a few inserts runs a few rounds: one launch per round of mode 2 there, and wherever the
  * persistent launch does not apply); 3 = the persistent recurrence on every call where it
  * applies;
@@ -461,8 +464,14 @@ int32_t hgx_set_la_kernel(hgx_ctx* ctx, int32_t mode);
  * above n = 256); 2 = one launch per round, one lane per candidate, 8-bit rebased compares
  * (hgx_round_k.hip; candidates in chunks of 128 above n = 256); 4 = the whole-graph recurrence
  * (hgx_round_g.hip: one workgroup per graph runs every round in one launch, n <= 16), which mode 0
- * also uses on every call where it applies. Same results. */
+ * also uses on every call where it applies; 5 = mode 0 without hgx_round_pb.hip (n > 256: the
+ * steps of mode 2). Same results. */
 int32_t hgx_set_round_kernel(hgx_ctx* ctx, int32_t mode);
+/* FindOrder's sort of the received events by (graph, roundReceived, consensus timestamp, S): 0 =
+ * default: bucketed by (graph, roundReceived) and every bucket sorted in one workgroup's LDS where
+ * every bucket holds at most 8 192 events (else as 1); 1 = LSD radix passes over the whole list.
+ * Same results. */
+int32_t hgx_set_sort_kernel(hgx_ctx* ctx, int32_t mode);
 /* hgx_create_sharded's shards on this context's own device: shards = W in [1, 8] (1 = back to one
  * context), on an empty context only (before the first insert). W shards on one device need
  * GPU_MAX_HW_QUEUES >= W + 2 (HGX_ERR_INVALID otherwise). Same results. */

@@ -106,6 +106,36 @@ def test_wave_time_segments(n, E, seed, coord32):
     _same_results(hw, hs)
 
 
+@pytest.mark.parametrize("n,E,seed", [(256, 600000, 35), (64, 100000, 36)])
+def test_wave_segments_exactness_check(n, E, seed):
+    """The time-segmented pass on large gossip graphs (more than the 64 head rows per chain in each
+    segment): the exactness check (k_la_seg_check) proves every row exact, so the verify sweep is
+    skipped; coordinates and consensus equal the sweeps'."""
+    t = gtrace.gossip(n, E, seed, stale_prob=0.2, stale_depth=4)
+    hw = _run(t, "wave")
+    pt = hw.phase_times()
+    assert pt["la_wave_segs"] > 1 and pt["la_verify"] == 0 and pt["la_wave_fallbacks"] == 0, pt
+    hv = _run(t, "wave+verify")
+    assert hv.phase_times()["la_verify"] == 1
+    hs = _run(t, "sweep")
+    _same_coords(hw, hs, t.E, seed, k=3000)
+    _same_coords(hw, hv, t.E, seed + 1, k=3000)
+    _same_results(hw, hs)
+
+
+@pytest.mark.parametrize("n,E,seed,segs", [(16, 20000, 37, 48), (32, 30000, 38, 200)])
+def test_wave_segments_check_fails_safe(n, E, seed, segs):
+    """Segments so short that head rows read other segments' head rows: the check fails and the verify
+    sweep runs; the result still equals the sweeps'."""
+    t = gtrace.gossip(n, E, seed, stale_prob=0.3, stale_depth=4)
+    hw = _run(t, segs)
+    pt = hw.phase_times()
+    assert pt["la_wave_segs"] == segs and pt["la_verify"] == 1, pt
+    hs = _run(t, "sweep")
+    _same_coords(hw, hs, t.E, seed, k=1500)
+    _same_results(hw, hs)
+
+
 def test_wave_batched_graphs():
     """One workgroup per (graph, column block): 8 independent 16-peer graphs."""
     n, G, E = 16, 8, 3000

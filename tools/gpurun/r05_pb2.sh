@@ -1,0 +1,17 @@
+# k_round_pb v2 (3 probers per workgroup) + the segmented order sort: probes, tests, bench lines
+set -o pipefail
+mkdir -p gpurun_out/r05
+O=gpurun_out/r05
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sort_seg.py -x -v --timeout 200 --timeout-method thread > $O/pb2_sort_tests.log 2>&1 || { tail -40 $O/pb2_sort_tests.log; exit 1; }
+tail -1 $O/pb2_sort_tests.log
+for c in c5 c4 c3; do
+  timeout -k 10 300 python -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked \
+    > $O/pb2_$c.json 2> $O/pb2_$c.log || exit $?
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_per_pass']; p=d['config']['phase_ms_last_step']; print(sys.argv[2], 'ms/step %.2f' % d['ms_per_step'], 'rounds %.2f order %.2f' % (p['rounds_ms'], p['order_ms']), 'seg', p.get('sort_seg'), 'rp', p['round_p_runs'], p['round_p_fallbacks'], {x: round(k[x]['ms'],3) for x in ('layout','order_sort','cts_median')})" $O/pb2_$c.json $c
+done
+HGX_LIB=libhgx_prof.so timeout -k 10 300 python -u tools/phase_timing.py c5 2 > $O/pb2_ph_c5.log 2>&1 || { tail -20 $O/pb2_ph_c5.log; exit 1; }
+grep -E "k_round_pb clk" $O/pb2_ph_c5.log | tail -1
+PYTHONPATH=. timeout -k 10 400 python -u tools/probe/pb_diff.py > $O/pb2_diff.log 2>&1 || { tail -30 $O/pb2_diff.log; exit 1; }
+grep -c "mismatch=0" $O/pb2_diff.log
+timeout -k 10 900 python -u -m pytest tests/test_gpu_round_pb.py -x -v --timeout 200 --timeout-method thread > $O/pb2_tests.log 2>&1 || { tail -40 $O/pb2_tests.log; exit 1; }
+tail -1 $O/pb2_tests.log

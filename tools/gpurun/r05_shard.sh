@@ -10,3 +10,7 @@ for c in c3 c2; do
     > $O/shard_$c.json 2> $O/shard_$c.log || exit $?
   python -c "import json,sys; d=json.load(open(sys.argv[1])); p=d['config']['phase_ms_last_step']; print(sys.argv[2], 'ms/step %.2f' % d['ms_per_step'], 'value %.1f M' % (d['value']/1e6), 'coords %.2f rounds %.2f fame %.2f order %.2f' % (p['coords_ms'], p['rounds_ms'], p['fame_ms'], p['order_ms']))" $O/shard_$c.json $c
 done
+# the layout change at c4 (PMC-free timing from the bench line's kernel table)
+timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked \
+  > $O/shard_c4.json 2> $O/shard_c4.log || exit $?
+python -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_per_pass']; print('c4 ms/step %.2f' % d['ms_per_step'], {x: k[x]['ms'] for x in ('layout','order_sort','round_search','la_sweep')})" $O/shard_c4.json
