@@ -186,6 +186,133 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
     }
 }
 
+// Round 5: the same grouping, with every input column read in gid order (coalesced) into an LDS
+// stage and written out in slot order (coalesced): the slot-order pass of k_layout read six columns
+// scattered over its 4 096 gids while ~190 blocks per XCD were in flight, so most of those reads
+// missed L2 (c4 PMC: 3.97 GB fetched per pass, 473 bytes per event against 40 read).
+constexpr int kLayoutB2 = 2048;   // gids per block
+__global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
+                                                       const int32_t* __restrict__ g_index, const int64_t* __restrict__ g_ck,
+                                                       const int32_t* __restrict__ g_op, const int64_t* __restrict__ g_ts,
+                                                       const int32_t* __restrict__ g_rr, const int64_t* __restrict__ g_cts,
+                                                       const int32_t* __restrict__ c_off, const int32_t* __restrict__ c_base,
+                                                       int32_t* __restrict__ g_pos, int32_t* __restrict__ p_gid,
+                                                       int32_t* __restrict__ p_chain, int32_t* __restrict__ p_op,
+                                                       int32_t* __restrict__ p_opu, int32_t* __restrict__ p_opk,
+                                                       int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
+                                                       int64_t* __restrict__ p_cts, int C, int n, int seg) {
+    constexpr int B = kLayoutB2;
+    __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
+    __shared__ int32_t s_slot[B];   // slot -> gid offset in the block
+    __shared__ int32_t s_cr[B], s_ix[B];
+    __shared__ __attribute__((aligned(16))) int64_t s_stg[B];
+    __shared__ int32_t s_lo, s_hi;
+    const int nbk = (int)gridDim.x, q8 = nbk / 8, r8 = nbk % 8, x8 = (int)blockIdx.x % 8;
+    const int lb = x8 * q8 + min(x8, r8) + (int)blockIdx.x / 8;   // XCD-grouped block order (k_layout)
+    const int64_t g0 = E0 + (int64_t)lb * B;
+    const int nb = (int)min<int64_t>(B, E - g0);
+    const int t0 = threadIdx.x;
+    if (t0 == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
+    for (int h = t0; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
+    __syncthreads();
+    int lo = 0x7FFFFFFF, hi = -1;
+    for (int t = t0; t < nb; t += 256) {
+        const int c = g_creator[g0 + t];
+        s_cr[t] = c;
+        s_ix[t] = g_index[g0 + t];
+        lo = min(lo, c);
+        hi = max(hi, c);
+    }
+    for (int o = 32; o >= 1; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
+    if ((t0 & 63) == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    __syncthreads();
+    const int clo = s_lo;
+    if (s_hi - clo >= kLayoutH) {   // block-uniform: too many chains to group, direct scatter
+        for (int t = t0; t < nb; t += 256) {
+            const int64_t gid = g0 + t;
+            const int c = s_cr[t];
+            const int p = c_off[c] + s_ix[t] - c_base[c];
+            g_pos[gid] = p;
+            layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
+                       p_opu, p_opk, p_ts, p_rr, p_cts, C, n, seg);
+        }
+        return;
+    }
+    for (int t = t0; t < nb; t += 256) {
+        const int h = s_cr[t] - clo;
+        atomicAdd(&s_cnt[h], 1);
+        atomicMin(&s_min[h], s_ix[t]);
+    }
+    __syncthreads();
+    if (t0 < 64) {   // exclusive scan of the counts (one wave)
+        constexpr int PER = kLayoutH / 64;
+        int v[PER], sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) { v[k] = s_cnt[t0 * PER + k]; sum += v[k]; }
+        int incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (t0 >= o) incl += y;
+        }
+        int run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < PER; k++) { s_cnt[t0 * PER + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    for (int t = t0; t < nb; t += 256) {
+        const int c = s_cr[t], h = c - clo, idx = s_ix[t];
+        s_slot[s_cnt[h] + idx - s_min[h]] = t;
+        g_pos[g0 + t] = c_off[c] + idx - c_base[c];
+    }
+    __syncthreads();
+    // slot sl -> (gid offset, position): consecutive slots = consecutive positions of a chain's run
+    auto pos_of = [&](int t) { const int c = s_cr[t]; return c_off[c] + s_ix[t] - c_base[c]; };
+    // the op parent's (chain, offset) -> p_op, p_opu, p_opk (g_ck read in gid order: recent events)
+    for (int t = t0; t < nb; t += 256) {
+        const int op = g_op[g0 + t];
+        s_stg[t] = op >= 0 ? g_ck[op] : -1ll;
+    }
+    __syncthreads();
+    for (int sl = t0; sl < nb; sl += 256) {
+        const int t = s_slot[sl], p = pos_of(t);
+        const int64_t ck = s_stg[t];
+        int opp = -1, opu = -1, opk = -1;
+        if (ck >= 0) {
+            const int oc = (int)(ck >> 32), ok = (int)(uint32_t)ck;
+            opp = c_off[oc] + ok;
+            opu = (ok / seg) * C + oc;
+            opk = ((oc % n) << kOpkBits) | (ok & ((1 << kOpkBits) - 1));
+        }
+        p_op[p] = opp;
+        p_opu[p] = opu;
+        p_opk[p] = opk;
+        p_gid[p] = (int32_t)(g0 + t);
+        p_chain[p] = s_cr[t];
+    }
+    __syncthreads();
+    for (int t = t0; t < nb; t += 256) s_stg[t] = g_ts[g0 + t];
+    __syncthreads();
+    for (int sl = t0; sl < nb; sl += 256) {
+        const int t = s_slot[sl];
+        p_ts[pos_of(t)] = s_stg[t];
+    }
+    __syncthreads();
+    for (int t = t0; t < nb; t += 256) s_stg[t] = g_cts[g0 + t];
+    __syncthreads();
+    for (int sl = t0; sl < nb; sl += 256) {
+        const int t = s_slot[sl];
+        p_cts[pos_of(t)] = s_stg[t];
+    }
+    __syncthreads();
+    int32_t* s_rr = (int32_t*)s_stg;
+    for (int t = t0; t < nb; t += 256) s_rr[t] = g_rr[g0 + t];
+    __syncthreads();
+    for (int sl = t0; sl < nb; sl += 256) {
+        const int t = s_slot[sl];
+        p_rr[pos_of(t)] = s_rr[t];
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // lastAncestors: in-place monotone sweeps (Gauss-Seidel) over units, with dirty tracking.
 // LA[x] = max(LA[sp(x)], LA[op(x)]), LA[x][cr(x)] = Index(x)   (hashgraph.go:470-496)
@@ -1530,33 +1657,54 @@ __global__ void __launch_bounds__(256) k_seg_scatter(int32_t m, const uint64_t* 
     }
 }
 
-// one bucket per workgroup: bitonic sort of its (key, value) pairs in LDS (cap = the largest bucket
-// rounded up to a power of two; ties in the key are ordered by S afterwards, k_tiefix_rank)
+// equal (graph, rr, cts) runs are ordered by S (big-endian 256-bit; consensus_sorter.go:37-42)
+__device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
+    for (int k = 0; k < 32; k++)
+        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return 0;
+}
+
+// One bucket per group of GS threads (a workgroup, GS = 256, or a wave, GS = 64, four buckets per
+// workgroup when every bucket holds <= 512 events): bitonic sort of its (key, value) pairs in LDS
+// (cap = the largest bucket rounded up to a power of two), then the runs of equal keys (same graph,
+// rr and timestamp) ordered by S in the same kernel: a run's members get the first 8 bytes of their S
+// (big-endian) in place of the key they share, and each member's place in its run is its rank by
+// (S prefix, full S on equal prefixes, index) -- the radix path's k_tie_prefix / k_tiefix_rank, with
+// the run in LDS (consensus_sorter.go:36-51). Writes the final values.
+template <int GS>
 __global__ void __launch_bounds__(256) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
                                                   const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                  uint64_t* __restrict__ kout, uint32_t* __restrict__ vout, int cap) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
-    uint32_t* sv = (uint32_t*)(sk + cap);
-    const int sgi = blockIdx.x;
-    const int o = (int)segoff[sgi], e = sgi + 1 < nseg ? (int)segoff[sgi + 1] : m, len = e - o;
-    const int t = threadIdx.x, T = blockDim.x;
-    if (len <= 1) {
-        if (len == 1 && t == 0) {
-            kout[o] = kin[o];
-            vout[o] = vin[o];
-        }
+                                                  const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S,
+                                                  uint32_t* __restrict__ vout, int cap) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    constexpr int NG = 256 / GS;   // groups (buckets) per workgroup
+    const int grp = (int)threadIdx.x / GS, t = (int)threadIdx.x % GS;
+    uint64_t* sk = smem + (size_t)grp * cap;                               // [cap] keys, then S prefixes
+    uint32_t* sv = (uint32_t*)(smem + (size_t)NG * cap) + (size_t)grp * cap;   // [cap] values
+    uint16_t* rs = (uint16_t*)((uint32_t*)(smem + (size_t)NG * cap) + (size_t)NG * cap) + (size_t)grp * 2 * cap;   // [2][cap]
+    auto sync = [&]() {
+        if constexpr (GS == 64) wave_lds_fence(); else __syncthreads();
+    };
+    const int sgi = (int)blockIdx.x * NG + grp;
+    int o = 0, len = 0;
+    if (sgi < nseg) {
+        o = (int)segoff[sgi];
+        len = (sgi + 1 < nseg ? (int)segoff[sgi + 1] : m) - o;
+    }
+    if (len <= 1) {   // (group-uniform)
+        if (len == 1 && t == 0) vout[o] = vin[o];
         return;
     }
     int P = 2;
     while (P < len) P <<= 1;
-    for (int i = t; i < P; i += T) {
+    for (int i = t; i < P; i += GS) {
         sk[i] = i < len ? kin[o + i] : ~0ull;
         sv[i] = i < len ? vin[o + i] : 0u;
     }
-    __syncthreads();
+    sync();
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = t; q < (P >> 1); q += T) {
+            for (int q = t; q < (P >> 1); q += GS) {
                 const int lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
                 const bool asc = (lo & k) == 0;
                 const uint64_t a = sk[lo], b = sk[hi];
@@ -1568,12 +1716,61 @@ __global__ void __launch_bounds__(256) k_seg_sort(int nseg, int32_t m, const uin
                     sv[hi] = x;
                 }
             }
-            __syncthreads();
+            sync();
         }
     }
-    for (int i = t; i < len; i += T) {
-        kout[o + i] = sk[i];
-        vout[o + i] = sv[i];
+    // run starts: inclusive max-scan of (head ? i : 0) over [0, len), ping-pong between rs[0] and rs[1]
+    bool tie_any = false;
+    for (int i = t; i < len; i += GS) {
+        const bool head = i == 0 || sk[i - 1] != sk[i];
+        rs[i] = (uint16_t)(head ? i : 0);
+        tie_any |= !head;
+    }
+    if constexpr (GS == 64) tie_any = __any(tie_any); else tie_any = __syncthreads_or(tie_any);
+    if (!tie_any) {   // (group-uniform) every key distinct: the values are final
+        for (int i = t; i < len; i += GS) vout[o + i] = sv[i];
+        return;
+    }
+    sync();
+    int cur = 0;
+    for (int d = 1; d < len; d <<= 1) {
+        const uint16_t* src = rs + cur * cap;
+        uint16_t* dst = rs + (cur ^ 1) * cap;
+        for (int i = t; i < len; i += GS) dst[i] = i >= d ? max(src[i], src[i - d]) : src[i];
+        sync();
+        cur ^= 1;
+    }
+    const uint16_t* st = rs + cur * cap;
+    // run members: the S prefix in place of the shared key (a member is not its run's only element)
+    for (int i = t; i < len; i += GS) {
+        const int s0 = st[i];
+        const bool member = s0 != i || (i + 1 < len && st[i + 1] == i);
+        if (member) {
+            const uint8_t* sp = g_S + (size_t)p_gid[sv[i]] * 32;
+            uint64_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 8; b++) v = (v << 8) | sp[b];
+            sk[i] = v;
+        }
+    }
+    sync();
+    for (int i = t; i < len; i += GS) {
+        const int s0 = st[i];
+        const bool member = s0 != i || (i + 1 < len && st[i + 1] == i);
+        if (!member) {
+            vout[o + i] = sv[i];
+            continue;
+        }
+        const uint64_t my = sk[i];
+        const uint32_t vi = sv[i];
+        const uint8_t* si = g_S + (size_t)p_gid[vi] * 32;
+        int rank = 0;
+        for (int jx = s0; jx < len && st[jx] == s0; jx++) {
+            const uint64_t pj = sk[jx];
+            const int c = pj != my ? (pj < my ? -1 : 1) : (jx == i ? 0 : cmp_s(g_S + (size_t)p_gid[sv[jx]] * 32, si));
+            rank += c < 0 || (c == 0 && jx < i);   // equal S (never in a valid trace): stable
+        }
+        vout[o + s0 + rank] = vi;
     }
 }
 
@@ -1604,12 +1801,6 @@ __global__ void __launch_bounds__(256) k_minmax_cts(int32_t m, const int32_t* __
     }
 }
 
-// equal (graph, rr, cts) runs are ordered by S (big-endian 256-bit; consensus_sorter.go:37-42)
-__device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
-    for (int k = 0; k < 32; k++)
-        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
-    return 0;
-}
 
 // runs of equal combined keys (same graph, rr and timestamp) ordered by S (256-bit
 // big-endian, consensus_sorter.go:36-51 with the zero whitening).
@@ -1995,6 +2186,8 @@ void launch_copy_many(hipStream_t s, const CopyRange* r, int count) {
 }
 
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
+    // (HGX_LAYOUT_ROUND4=1 in the environment: the round-4 k_layout, for A/B measurements)
+    static const bool layout_staged = getenv("HGX_LAYOUT_ROUND4") == nullptr;
     if (E <= E0) return;
     hipLaunchKernelGGL(k_ck_pack, dim3(nblk(E - E0, 256)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.c_base,
                        a.g_ck);
@@ -2004,9 +2197,14 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
                            a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
         return;
     }
-    hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_ck, a.g_op, a.g_ts,
-                       a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu, a.p_opk,
-                       a.p_ts, a.p_rr, a.p_cts, C, n, seg);
+    if (layout_staged)
+        hipLaunchKernelGGL(k_layout_staged, dim3(nblk(E - E0, kLayoutB2)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index,
+                           a.g_ck, a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
+                           a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
+    else
+        hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_ck,
+                           a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu,
+                           a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
 }
 
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
@@ -2295,14 +2493,19 @@ void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin,
     hipLaunchKernelGGL(k_seg_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, ka, va, cts_bits, segoff, segcur, kb, vb);
     int cap = 2;
     while (cap < max_seg) cap <<= 1;
-    const size_t lds = (size_t)cap * 12;
-    (void)ensure_lds_limit((const void*)k_seg_sort, lds);
-    hipLaunchKernelGGL(k_seg_sort, dim3(nseg), dim3(256), lds, s, nseg, m, segoff, kb, vb, ka, va, cap);
-    // runs of equal keys ordered by S, as after the radix sort (kb / vb are free again)
-    hipLaunchKernelGGL(k_tie_prefix, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, ka, a.p_gid, a.g_S, kb);
-    hipLaunchKernelGGL(k_tiefix_rank, dim3(nblk(m, 256)), dim3(256), 0, s, m, va, vb, ka, kb, a.p_gid, a.g_S);
-    *final_vals = vb;
-    *final_keys = ka;
+    // (the runs of equal keys are ordered by S inside k_seg_sort: the final values land in va)
+    if (cap <= 512) {   // a wave per bucket, four per workgroup
+        const size_t lds = (size_t)4 * cap * 16;
+        hipLaunchKernelGGL(k_seg_sort<64>, dim3((nseg + 3) / 4), dim3(256), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
+                           a.g_S, va, cap);
+    } else {
+        const size_t lds = (size_t)cap * 16;
+        (void)ensure_lds_limit((const void*)k_seg_sort<256>, lds);
+        hipLaunchKernelGGL(k_seg_sort<256>, dim3(nseg), dim3(256), lds, s, nseg, m, segoff, kb, vb, a.p_gid, a.g_S,
+                           va, cap);
+    }
+    *final_vals = va;
+    *final_keys = kb;
 }
 
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,

@@ -87,21 +87,17 @@ __device__ __forceinline__ uint32_t pb_combine8(uint32_t x) {   // sum over the 
     return x;
 }
 
-constexpr int pb_part_stride(int hd) {   // smallest stride >= hd that is 8 or 24 (mod 32)
-    int ps = hd;
-    while (ps % 32 != 8 && ps % 32 != 24) ps++;
-    return ps;
-}
-
 template <int NDW>
 struct PbCfg {
     static constexpr int Q = 8, T = 1024, NW = T / 64, PP = kPbPP;
     static constexpr int HD = NDW / Q;          // row dwords per lane (16 or 32)
     static constexpr int CPB = T / Q;           // candidates per pass (128)
     static constexpr int NC = 4 * NDW;          // chains (padded)
-    static constexpr int NCH = NC / CPB;        // chunks
-    static constexpr int PS = pb_part_stride(HD);
-    static constexpr int WS = Q * PS + 4;       // window row stride (dwords)
+    // window rows: dword 8h + e of part q (what lane q of a candidate compares) at h * 64 + 8 q + e, so
+    // part q lies in banks 8q .. 8q + 7 of every row whatever the row; a ds_read_b128 lane group holds
+    // two candidates per part, which read the part's two halves in opposite orders (the candidates
+    // 2, 3 (mod 4) of a wave high half first): conflict-free whatever rows they probe
+    static constexpr int WS = NDW;              // window row stride (dwords)
     static constexpr int WIN = kPbP * WS;       // window (dwords)
     // LDS (bytes)
     static constexpr int O_WIN = 0;                       // [PP][kPbP][WS] rebased probes
@@ -110,7 +106,8 @@ struct PbCfg {
     static constexpr int O_HIST = O_KST + PP * NC;        // [PP][32]
     static constexpr int O_POF = O_HIST + PP * 32 * 4;    // [PP] the published row's overflow flag
     static constexpr int O_MISC = O_POF + PP * 4;         // [8]: [2] any, [3] fail
-    static constexpr int LDS = O_MISC + 32;
+    static constexpr int O_AMAP = O_MISC + 32;            // [NC] the chains with events (candidates)
+    static constexpr int LDS = O_AMAP + NC * 4;
     static_assert(LDS <= 160 * 1024, "k_round_pb: LDS carve exceeds a CU's 160 KB");
 };
 
@@ -171,19 +168,21 @@ void round_pb_prof_dump() {}
 template <typename CT, int NDW>
 __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
     typedef PbCfg<NDW> K;
-    constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, PS = K::PS, CPB = K::CPB;
-    constexpr int NCH = K::NCH, NC = K::NC;
+    constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, CPB = K::CPB;
+    constexpr int NC = K::NC;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const RoundArgs& A = P.A;
     const int n = A.n, C = A.C, sm = A.sm;
     const int t = threadIdx.x, lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int jl = t / Q, q = t % Q;   // candidate slot in a pass, row part
+    const int hsw = (jl >> 1) & 1;     // this candidate reads each 8-dword piece high half first
     auto winp = [&](int k) { return (uint32_t*)(lds + K::O_WIN) + k * K::WIN; };
     auto bpar = [&](int r) { return (int32_t*)(lds + K::O_BS) + (r & 1) * NC; };   // c_base + Bm[r]
     auto kstp = [&](int k) { return lds + K::O_KST + k * NC; };
     auto histp = [&](int k) { return (int32_t*)(lds + K::O_HIST) + k * 32; };
     int32_t* pof = (int32_t*)(lds + K::O_POF);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
+    int32_t* amapl = (int32_t*)(lds + K::O_AMAP);
     if (P.fin[0] >= 0) return;   // finished in an earlier launch of this DivideRounds
     const CT* __restrict__ LA = (const CT*)A.LA;
     const CT* __restrict__ FDT = (const CT*)A.FDT;
@@ -200,10 +199,15 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         bs[k] = __builtin_amdgcn_readfirstlane(valid[k] ? A.Bm[(size_t)P.r0 * C + gcs[k]] : 0);
     }
     for (int i = t; i < NC; i += T) {
-        // (a silent chain's Bm rows are written after the launches: 0 = its length)
+        // (a silent chain's Bm rows are written after the launches: 0 = its length; its bases never
+        // change and its candidate bits stay 0: only the chains with events are polled)
         const bool li = i < n && A.c_len[i] > 0;
-        bpar(P.r0 - 1)[i] = (i < n ? A.c_base[i] : 0) + (P.r0 > 0 && li ? A.Bm[(size_t)(P.r0 - 1) * C + i] : 0);
+        const int32_t cb = i < n ? A.c_base[i] : 0;
+        bpar(P.r0 - 1)[i] = cb + (P.r0 > 0 && li ? A.Bm[(size_t)(P.r0 - 1) * C + i] : 0);
+        if (!li) bpar(P.r0)[i] = cb;
+        if (i < P.na) amapl[i] = P.amap[i];
     }
+    for (int i = t; i < PP * NC; i += T) lds[K::O_KST + i] = 0;
     if (t < PP * 32) ((int32_t*)(lds + K::O_HIST))[t] = 0;
     if (t < PP) pof[t] = 0;
     if (t < 8) misc[t] = 0;
@@ -259,7 +263,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                     w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
                 }
             }
-            win[p * WS + (d / HD) * PS + d % HD] = w;
+            win[p * WS + ((d % HD) >> 3) * 64 + (d / HD) * 8 + (d & 7)] = w;
         }
     };
     auto rebase = [&](uint32_t* win, int off, int kb, int np, const int32_t* bq) {
@@ -290,13 +294,27 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             carried[k] = 0;
         }
         const uint32_t vbit = ((s >> kRoundPShift) & 1) ? 0x80808080u : 0u;
+        // the firstDescendants lines (and address translations) the publish will gather: the round's
+        // new candidate lies in the window, whose middle position's column entries share a page and
+        // mostly a line with it (each coordinate's column is its own 2 MB page: without this the
+        // publish's 1 024 gathers per prober each took a translation miss, 26 us per c5 round); the
+        // loads complete behind this round's first poll, which waits for the candidates anyway
+        uint32_t pfx = 0;
+        if (t < n) {
+#pragma unroll
+            for (int k = 0; k < PP; k++)
+                if (have[k]) pfx += (uint32_t)FDT[(size_t)t * A.Pcap + offs[k] + min(bs[k] + kPbP / 2, lens[k] - 1)];
+        }
         bool any = false;
         for (int w_it = 0;; w_it++) {
             // every chunk of 128 candidates: poll (reload in a later window), search every active window
-            for (int ch = 0; ch < NCH; ch++) {
-                const int j = ch * CPB + jl;
-                const bool jv = j < n;
-                const bool live = jv && A.c_len[j] > 0;   // silent chains publish nothing
+            // (chunks over the chains with events only: c5's 341 silent peers cost no chunk slots)
+            const int nch = (P.na + CPB - 1) / CPB;
+            for (int ch = 0; ch < nch; ch++) {
+                const int ja = ch * CPB + jl;
+                const bool jv = ja < P.na;
+                const int j = jv ? amapl[ja] : 0;   // candidate chain
+                const bool live = jv;
                 uint64_t gv = 0;
                 uint32_t fd[HD];
                 const uint64_t* gp = P.gran + (size_t)(s % kPbSlots) * C + (live ? j : 0);
@@ -330,6 +348,17 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 if (cand && q == 0) misc[2] = 1;
 #pragma unroll
                 for (int d = 0; d < HD; d++) fd[d] = cand ? (fd[d] & 0x7F7F7F7Fu) : 0x7F7F7F7Fu;
+                // (candidates 2, 3 (mod 4) read each 8-dword piece high half first: their registers too)
+                if (hsw) {
+#pragma unroll
+                    for (int h = 0; h < HD / 8; h++)
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            const uint32_t x = fd[8 * h + e];
+                            fd[8 * h + e] = fd[8 * h + 4 + e];
+                            fd[8 * h + 4 + e] = x;
+                        }
+                }
                 bool done[PP], srch[PP];
                 int lo[PP], hi[PP];
                 const bool wc = __any(cand);
@@ -357,10 +386,10 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
 #pragma unroll
                         for (int k = 0; k < PP; k++) {
                             if (!srch[k]) continue;
-                            const uint4* rp = (const uint4*)(winp(k) + mid[k] * WS + q * PS);
+                            const uint4* rp = (const uint4*)(winp(k) + mid[k] * WS + q * 8) + hsw;
 #pragma unroll
                             for (int h = 0; h < HD / 8; h++) {
-                                const uint4 v0 = rp[2 * h], v1 = rp[2 * h + 1];
+                                const uint4 v0 = rp[16 * h], v1 = rp[16 * h + 1 - 2 * hsw];
                                 const uint32_t* f8 = fd + 8 * h;
                                 cnt[k] += __builtin_popcount((v0.x - f8[0]) & 0x80808080u) +
                                           __builtin_popcount((v0.y - f8[1]) & 0x80808080u) +
@@ -453,34 +482,29 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         PB_PROF(4);
         if (misc[3] != 0) { failed = true; break; }
         if (!any) break;   // W'_s is empty: no round s
-        // the next windows' raw rows (compact coordinates: every prober's loads in flight beside the
-        // publish's gathers; int32 rows are loaded after the publish, one prober at a time)
+        // W'_{s+1} of each prober: the firstDescendants row of position kstar rebased to
+        // base(s+1) = c_base + Bm[s] (bit 7 = v(s + 1)), straight from the FDT columns; then the next
+        // windows' raw rows (compact coordinates: every prober's loads at once; int32 rows are loaded
+        // after the barrier, one prober at a time)
         constexpr bool kMerged = sizeof(CT) == 2;
         RawRows rawn[kMerged ? PP : 1];
         int np1[PP];
-#pragma unroll
-        for (int k = 0; k < PP; k++) {
-            np1[k] = valid[k] && kstar[k] < lens[k] ? min(kPbP, lens[k] - kstar[k]) : 0;
-            if constexpr (kMerged) rb_load(rawn[k], offs[k], kstar[k], np1[k]);
-        }
-        // W'_{s+1} of each prober: the firstDescendants row of position kstar rebased to
-        // base(s+1) = c_base + Bm[s] (bit 7 = v(s + 1)), straight from the FDT columns
         {
             const int k = t / NDW, d = t % NDW;
             int kk = -1;   // (a register-indexed prober: its scalars by an unrolled select)
 #pragma unroll
             for (int x = 0; x < PP; x++)
                 if (k == x && valid[x] && kstar[x] < lens[x]) kk = x;
-            if (kk >= 0) {
-                int off = 0, kst_ = 0, gc = 0;
+            int off = 0, kst_ = 0, gc = 0;
 #pragma unroll
-                for (int x = 0; x < PP; x++)
-                    if (kk == x) { off = offs[x]; kst_ = kstar[x]; gc = gcs[x]; }
-                const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
-                const int32_t* bs1 = bpar(s);
+            for (int x = 0; x < PP; x++)
+                if (kk == x) { off = offs[x]; kst_ = kstar[x]; gc = gcs[x]; }
+            if (kk >= 0) {
                 CT f[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) f[u] = FDT[(size_t)min(4 * d + u, n - 1) * A.Pcap + off + kst_];
+                const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
+                const int32_t* bs1 = bpar(s);
                 uint32_t w = 0;
                 bool of = false;
 #pragma unroll
@@ -493,6 +517,13 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 }
                 pb_st_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + d, w | vb1);
                 if (of) pof[kk] = 1;
+            }
+            // (the next windows' rows: issued after the publish, which waits for its gathers alone, and
+            // in flight behind the S rows, the barrier and the granules)
+#pragma unroll
+            for (int x = 0; x < PP; x++) {
+                np1[x] = valid[x] && kstar[x] < lens[x] ? min(kPbP, lens[x] - kstar[x]) : 0;
+                if constexpr (kMerged) rb_load(rawn[x], offs[x], kstar[x], np1[x]);
             }
         }
         // the S rows (DecideFame, hashgraph.go:688-705): bit j = the new candidate strongly sees
@@ -537,6 +568,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             else if (np1[k] > 0) rebase(winp(k), offs[k], kstar[k], np1[k], bpar(s));
             bs[k] = kstar[k];
         }
+        if (pfx == 0xFFFFFFFFu) misc[7] = 1;   // (the prefetch's use: never true, keeps the loads)
         pb_lds_barrier();
         PB_PROF(7);
     }

@@ -18,16 +18,16 @@ import sys
 from collections import defaultdict
 
 ROLES = {
-    "layout": r"k_layout",
+    "layout": r"k_layout|k_ck_pack",
     "la_sweep": r"k_la_sweep|k_la_wave|k_la_small",
     "fd_build": r"k_fd_build",
-    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin|k_round_p_post|k_round_p_tail",
-    "round_search": r"k_round_k<|k_round_step|k_round_p<|k_round_g<",
+    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin|k_round_p_post|k_round_p_tail|k_round_p_init|k_round_pb_silent",
+    "round_search": r"k_round_k<|k_round_step|k_round_p<|k_round_pb<|k_round_g<",
     "fame": r"k_fame",
     "threshold": r"k_threshold|k_wla_transpose",
     "round_received": r"k_round_received",
     "cts_median": r"k_cts",
-    "order_sort": r"k_radix|k_sort_small|k_sort_rank|k_sort_place|k_tie|k_keys|k_scan|k_minmax|k_finish_order",
+    "order_sort": r"k_radix|k_sort_small|k_sort_rank|k_sort_place|k_tie|k_keys|k_scan|k_minmax|k_seg_|k_finish_order",
     # ingest legs (bench.py p256_leg / ingest_leg; not in a consensus pass)
     "p256_verify": r"k_p256_verify",
     "sha256": r"k_sha256",
