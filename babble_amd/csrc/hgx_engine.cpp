@@ -1318,10 +1318,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
             }
             HGX_TRY(hipMemsetAsync(rp_st.p, 0, 16, stream));
             if (big) {
-                if (init) HGX_TRY(launch_round_p(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, s, r_cap - 1, 2, num_cus));
                 kbeg(K_ROUND_SEARCH);
                 HGX_TRY(launch_round_pb(stream, round_args(), FD8p.p, rp_gran.p, rp_st.p, fin, rp_amap.p, na, s, r_cap - 1,
-                                        num_cus));
+                                        num_cus, init != 0));
                 kend(K_ROUND_SEARCH, 0);
             } else if (sh && init) {
                 // W'_{r_lo} of this shard's chains into every window; every shard's launch starts once
@@ -1744,15 +1743,16 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         // sort's condition), read back in the same round trip
         const unsigned long long init[3] = {~0ull, 0ull, 0ull};
         HGX_TRY(hipMemcpyAsync(minmax.p, init, 24, hipMemcpyHostToDevice, stream));
-        launch_minmax(stream, a, m);
         const int64_t nseg64 = (int64_t)G * R;
         const bool seg_try = sort_seg_enabled && nseg64 >= 1 && nseg64 <= (int64_t)1 << 24;
         const int nseg = (int)nseg64;
-        if (seg_try) {
+        if (seg_try) {   // (the bucket counts with the timestamp range, one pass)
             if (seg_off.n < (size_t)nseg + 1) HGX_TRY(seg_off.alloc((size_t)nseg + 1));
             if (seg_cur.n < (size_t)nseg + 1) HGX_TRY(seg_cur.alloc((size_t)nseg + 1));
             HGX_TRY(hipMemsetAsync(seg_off.p, 0, (size_t)nseg * 4, stream));
             launch_seg_count(stream, a, m, R, n, nseg, seg_off.p, (unsigned long long*)minmax.p + 2);
+        } else {
+            launch_minmax(stream, a, m);
         }
         unsigned long long mm[3];
         HGX_TRY(hipMemcpyAsync(mm, minmax.p, 24, hipMemcpyDeviceToHost, stream));

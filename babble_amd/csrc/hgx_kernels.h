@@ -246,12 +246,13 @@ void launch_round_p_tail(hipStream_t s, const RoundArgs& A, const int32_t* fin, 
 void launch_round_p_post(hipStream_t s, const RoundArgs& A, int r_lo, int r_hi);
 // persistent recurrence for 256 < n <= 1024, one graph (hgx_round_pb.hip): one resident workgroup
 // per chain WITH events (amap: their indices, na of them), rows / granules / status / fin as
-// launch_round_p's (its init = 2 writes W'_{r0}); hipErrorCooperativeLaunchTooLarge when the na
+// launch_round_p's (init: W'_{r0}'s rows first, compressed to the chains with events);
+// hipErrorCooperativeLaunchTooLarge when the na
 // workgroups cannot all be resident. launch_round_pb_silent then writes the silent chains' Bm rows
 // of rounds [r_lo, r_hi + 1] (0), before launch_round_p_post.
 bool round_pb_ok(int n, int G);
 hipError_t launch_round_pb(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus);
+                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus, bool init);
 void launch_round_pb_silent(hipStream_t s, const RoundArgs& A, int r_lo, int r_hi);
 // root floors (hgx_reset): per position G = max over chains i whose first event it sees of
 // Root.Round(i) + 1, then gB[r][c] = first offset of chain c with G >= r, r in [0, gmax]

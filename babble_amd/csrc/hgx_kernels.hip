@@ -186,10 +186,12 @@ __global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int
     }
 }
 
-// Round 5: the same grouping, with every input column read in gid order (coalesced) into an LDS
-// stage and written out in slot order (coalesced): the slot-order pass of k_layout read six columns
-// scattered over its 4 096 gids while ~190 blocks per XCD were in flight, so most of those reads
-// missed L2 (c4 PMC: 3.97 GB fetched per pass, 473 bytes per event against 40 read).
+// Round 5: the same grouping, with every input column read in gid order (coalesced) and written out in
+// slot order (coalesced) through an LDS stage: the slot-order pass of k_layout read six columns scattered
+// over its 4 096 gids while ~190 blocks per XCD were in flight, so most of those reads missed L2 (c4 PMC:
+// 3.97 GB fetched per pass, 473 bytes per event against 40 read). A thread's 8 events have all their
+// columns loaded at once (one global round trip, then one for the op parents' packed words), then each
+// output column goes through the stage in turn.
 constexpr int kLayoutB2 = 2048;   // gids per block
 __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
                                                        const int32_t* __restrict__ g_index, const int64_t* __restrict__ g_ck,
@@ -201,7 +203,7 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
                                                        int32_t* __restrict__ p_opu, int32_t* __restrict__ p_opk,
                                                        int64_t* __restrict__ p_ts, int32_t* __restrict__ p_rr,
                                                        int64_t* __restrict__ p_cts, int C, int n, int seg) {
-    constexpr int B = kLayoutB2;
+    constexpr int B = kLayoutB2, PT = B / 256;   // events per thread
     __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
     __shared__ int32_t s_slot[B];   // slot -> gid offset in the block
     __shared__ int32_t s_cr[B], s_ix[B];
@@ -212,17 +214,37 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
     const int64_t g0 = E0 + (int64_t)lb * B;
     const int nb = (int)min<int64_t>(B, E - g0);
     const int t0 = threadIdx.x;
+    // every column of this thread's events at once
+    int32_t cr[PT], ix[PT], op[PT], rr[PT];
+    int64_t ts[PT], cts[PT], ck[PT];
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const int t = t0 + 256 * k;
+        const bool v = t < nb;
+        const int64_t gid = g0 + (v ? t : 0);
+        cr[k] = g_creator[gid];
+        ix[k] = g_index[gid];
+        op[k] = g_op[gid];
+        rr[k] = g_rr[gid];
+        ts[k] = g_ts[gid];
+        cts[k] = g_cts[gid];
+    }
+#pragma unroll
+    for (int k = 0; k < PT; k++) ck[k] = op[k] >= 0 ? g_ck[op[k]] : -1ll;   // (op parents: recent events)
     if (t0 == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
     for (int h = t0; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
-    __syncthreads();
     int lo = 0x7FFFFFFF, hi = -1;
-    for (int t = t0; t < nb; t += 256) {
-        const int c = g_creator[g0 + t];
-        s_cr[t] = c;
-        s_ix[t] = g_index[g0 + t];
-        lo = min(lo, c);
-        hi = max(hi, c);
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const int t = t0 + 256 * k;
+        if (t < nb) {
+            s_cr[t] = cr[k];
+            s_ix[t] = ix[k];
+            lo = min(lo, cr[k]);
+            hi = max(hi, cr[k]);
+        }
     }
+    __syncthreads();
     for (int o = 32; o >= 1; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
     if ((t0 & 63) == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
     __syncthreads();
@@ -238,10 +260,14 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
         }
         return;
     }
-    for (int t = t0; t < nb; t += 256) {
-        const int h = s_cr[t] - clo;
-        atomicAdd(&s_cnt[h], 1);
-        atomicMin(&s_min[h], s_ix[t]);
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const int t = t0 + 256 * k;
+        if (t < nb) {
+            const int h = cr[k] - clo;
+            atomicAdd(&s_cnt[h], 1);
+            atomicMin(&s_min[h], ix[k]);
+        }
     }
     __syncthreads();
     if (t0 < 64) {   // exclusive scan of the counts (one wave)
@@ -259,26 +285,25 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
         for (int k = 0; k < PER; k++) { s_cnt[t0 * PER + k] = run; run += v[k]; }
     }
     __syncthreads();
-    for (int t = t0; t < nb; t += 256) {
-        const int c = s_cr[t], h = c - clo, idx = s_ix[t];
-        s_slot[s_cnt[h] + idx - s_min[h]] = t;
-        g_pos[g0 + t] = c_off[c] + idx - c_base[c];
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const int t = t0 + 256 * k;
+        if (t < nb) {
+            const int h = cr[k] - clo;
+            s_slot[s_cnt[h] + ix[k] - s_min[h]] = t;
+            g_pos[g0 + t] = c_off[cr[k]] + ix[k] - c_base[cr[k]];
+        }
+        if (t < nb) s_stg[t] = ck[k];
     }
     __syncthreads();
     // slot sl -> (gid offset, position): consecutive slots = consecutive positions of a chain's run
     auto pos_of = [&](int t) { const int c = s_cr[t]; return c_off[c] + s_ix[t] - c_base[c]; };
-    // the op parent's (chain, offset) -> p_op, p_opu, p_opk (g_ck read in gid order: recent events)
-    for (int t = t0; t < nb; t += 256) {
-        const int op = g_op[g0 + t];
-        s_stg[t] = op >= 0 ? g_ck[op] : -1ll;
-    }
-    __syncthreads();
-    for (int sl = t0; sl < nb; sl += 256) {
+    for (int sl = t0; sl < nb; sl += 256) {   // the op parent's (chain, offset) -> p_op, p_opu, p_opk
         const int t = s_slot[sl], p = pos_of(t);
-        const int64_t ck = s_stg[t];
+        const int64_t cki = s_stg[t];
         int opp = -1, opu = -1, opk = -1;
-        if (ck >= 0) {
-            const int oc = (int)(ck >> 32), ok = (int)(uint32_t)ck;
+        if (cki >= 0) {
+            const int oc = (int)(cki >> 32), ok = (int)(uint32_t)cki;
             opp = c_off[oc] + ok;
             opu = (ok / seg) * C + oc;
             opk = ((oc % n) << kOpkBits) | (ok & ((1 << kOpkBits) - 1));
@@ -290,14 +315,18 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
         p_chain[p] = s_cr[t];
     }
     __syncthreads();
-    for (int t = t0; t < nb; t += 256) s_stg[t] = g_ts[g0 + t];
+#pragma unroll
+    for (int k = 0; k < PT; k++)
+        if (t0 + 256 * k < nb) s_stg[t0 + 256 * k] = ts[k];
     __syncthreads();
     for (int sl = t0; sl < nb; sl += 256) {
         const int t = s_slot[sl];
         p_ts[pos_of(t)] = s_stg[t];
     }
     __syncthreads();
-    for (int t = t0; t < nb; t += 256) s_stg[t] = g_cts[g0 + t];
+#pragma unroll
+    for (int k = 0; k < PT; k++)
+        if (t0 + 256 * k < nb) s_stg[t0 + 256 * k] = cts[k];
     __syncthreads();
     for (int sl = t0; sl < nb; sl += 256) {
         const int t = s_slot[sl];
@@ -305,7 +334,9 @@ __global__ void __launch_bounds__(256) k_layout_staged(int64_t E0, int64_t E, co
     }
     __syncthreads();
     int32_t* s_rr = (int32_t*)s_stg;
-    for (int t = t0; t < nb; t += 256) s_rr[t] = g_rr[g0 + t];
+#pragma unroll
+    for (int k = 0; k < PT; k++)
+        if (t0 + 256 * k < nb) s_rr[t0 + 256 * k] = rr[k];
     __syncthreads();
     for (int sl = t0; sl < nb; sl += 256) {
         const int t = s_slot[sl];
@@ -1611,20 +1642,73 @@ __device__ __forceinline__ void wave_seg_runs(bool valid, int seg, bool& head, i
     head_lane = below ? 63 - (int)__builtin_clzll(below) : 0;
 }
 
-__global__ void __launch_bounds__(256) k_seg_count(int32_t m, const int32_t* __restrict__ list,
-                                                   const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
-                                                   int R, int n, uint32_t* __restrict__ segc) {
+// the bucket counts and the timestamp range in one pass over the received list (the range read back
+// decides the key width; grid-stride, one atomic pair per block for the range)
+__global__ void __launch_bounds__(256) k_seg_count_mm(int32_t m, const int32_t* __restrict__ list,
+                                                      const int64_t* __restrict__ p_cts,
+                                                      const int32_t* __restrict__ p_chain, const int32_t* __restrict__ p_rr,
+                                                      int R, int n, uint32_t* __restrict__ segc,
+                                                      unsigned long long* __restrict__ mm) {
+    __shared__ unsigned long long slo[4], shi[4];
+    unsigned long long lo = ~0ull, hi = 0ull;
+    const int stride = gridDim.x * blockDim.x;
+    for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += stride) {   // (wave-uniform trip count)
+        const int i = i0 + (int)threadIdx.x;
+        const bool v = i < m;
+        int seg = -1;
+        if (v) {
+            const int p = list[i];
+            seg = (p_chain[p] / n) * R + p_rr[p];
+            const unsigned long long u = (unsigned long long)p_cts[p] ^ 0x8000000000000000ull;
+            lo = min(lo, u);
+            hi = max(hi, u);
+        }
+        bool head;
+        int hl, len;
+        wave_seg_runs(v, seg, head, hl, len);
+        if (head) atomicAdd(&segc[seg], (uint32_t)len);
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        lo = min(lo, (unsigned long long)__shfl_xor(lo, o));
+        hi = max(hi, (unsigned long long)__shfl_xor(hi, o));
+    }
+    if (lane_id() == 0) { slo[threadIdx.x >> 6] = lo; shi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < 4; w++) { lo = min(lo, slo[w]); hi = max(hi, shi[w]); }
+        atomicMin(&mm[0], lo);
+        atomicMax(&mm[1], hi);
+    }
+}
+
+// the combined key of every received event straight into its bucket (k_keys_comb + k_seg_scatter)
+__global__ void __launch_bounds__(256) k_seg_keys_scatter(int32_t m, const int32_t* __restrict__ list,
+                                                          const int64_t* __restrict__ p_cts,
+                                                          const int32_t* __restrict__ p_chain,
+                                                          const int32_t* __restrict__ p_rr, int64_t cmin, int cts_bits,
+                                                          int R, int n, const uint32_t* __restrict__ segoff,
+                                                          uint32_t* __restrict__ segcur, uint64_t* __restrict__ kout,
+                                                          uint32_t* __restrict__ vout) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool v = i < m;
-    int seg = -1;
+    int seg = -1, p = 0;
+    uint64_t key = 0;
     if (v) {
-        const int p = list[i];
+        p = list[i];
         seg = (p_chain[p] / n) * R + p_rr[p];
+        key = ((uint64_t)seg << cts_bits) | (uint64_t)(p_cts[p] - cmin);
     }
     bool head;
     int hl, len;
     wave_seg_runs(v, seg, head, hl, len);
-    if (head) atomicAdd(&segc[seg], (uint32_t)len);
+    uint32_t base = 0;
+    if (head) base = atomicAdd(&segcur[seg], (uint32_t)len);
+    base = (uint32_t)__shfl((int)base, hl);
+    if (v) {
+        const uint32_t slot = segoff[seg] + base + (uint32_t)(lane_id() - hl);
+        kout[slot] = key;
+        vout[slot] = (uint32_t)p;
+    }
 }
 
 __global__ void __launch_bounds__(256) k_seg_max(int nseg, const uint32_t* __restrict__ segc,
@@ -1635,28 +1719,6 @@ __global__ void __launch_bounds__(256) k_seg_max(int nseg, const uint32_t* __res
     if (lane_id() == 0 && mx) atomicMax(out, (unsigned long long)mx);
 }
 
-// (key, value) into its bucket: slot = bucket start + a per-bucket cursor (one atomic per run)
-__global__ void __launch_bounds__(256) k_seg_scatter(int32_t m, const uint64_t* __restrict__ kin,
-                                                     const uint32_t* __restrict__ vin, int cts_bits,
-                                                     const uint32_t* __restrict__ segoff, uint32_t* __restrict__ segcur,
-                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool v = i < m;
-    const uint64_t key = v ? kin[i] : 0ull;
-    const int seg = v ? (int)(key >> cts_bits) : -1;
-    bool head;
-    int hl, len;
-    wave_seg_runs(v, seg, head, hl, len);
-    uint32_t base = 0;
-    if (head) base = atomicAdd(&segcur[seg], (uint32_t)len);
-    base = (uint32_t)__shfl((int)base, hl);
-    if (v) {
-        const uint32_t slot = segoff[seg] + base + (uint32_t)(lane_id() - hl);
-        kout[slot] = key;
-        vout[slot] = vin[i];
-    }
-}
-
 // equal (graph, rr, cts) runs are ordered by S (big-endian 256-bit; consensus_sorter.go:37-42)
 __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
     for (int k = 0; k < 32; k++)
@@ -1664,20 +1726,21 @@ __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
     return 0;
 }
 
-// One bucket per group of GS threads (a workgroup, GS = 256, or a wave, GS = 64, four buckets per
-// workgroup when every bucket holds <= 512 events): bitonic sort of its (key, value) pairs in LDS
+// One bucket per group of GS threads (a workgroup of 1 024 threads, or a wave, GS = 64, four buckets
+// per workgroup when every bucket holds <= 512 events: 256 threads per bucket at c3 left the LDS latency
+// of the compare-exchange stages exposed, 1.14 ms per pass): bitonic sort of its (key, value) pairs in LDS
 // (cap = the largest bucket rounded up to a power of two), then the runs of equal keys (same graph,
 // rr and timestamp) ordered by S in the same kernel: a run's members get the first 8 bytes of their S
 // (big-endian) in place of the key they share, and each member's place in its run is its rank by
 // (S prefix, full S on equal prefixes, index) -- the radix path's k_tie_prefix / k_tiefix_rank, with
 // the run in LDS (consensus_sorter.go:36-51). Writes the final values.
-template <int GS>
-__global__ void __launch_bounds__(256) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
+template <int GS, int TB>
+__global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
                                                   const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                   const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S,
                                                   uint32_t* __restrict__ vout, int cap) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    constexpr int NG = 256 / GS;   // groups (buckets) per workgroup
+    constexpr int NG = TB / GS;   // groups (buckets) per workgroup
     const int grp = (int)threadIdx.x / GS, t = (int)threadIdx.x % GS;
     uint64_t* sk = smem + (size_t)grp * cap;                               // [cap] keys, then S prefixes
     uint32_t* sv = (uint32_t*)(smem + (size_t)NG * cap) + (size_t)grp * cap;   // [cap] values
@@ -2477,32 +2540,33 @@ int seg_sort_cap() { return kSegSortCap; }
 
 void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n, int nseg, uint32_t* segc,
                       unsigned long long* max_out) {
-    hipLaunchKernelGGL(k_seg_count, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_chain, a.p_rr, R, n, segc);
+    // (with the timestamp range: minmax[0..1], as launch_minmax)
+    hipLaunchKernelGGL(k_seg_count_mm, dim3(std::min(2048u, nblk(m, 256))), dim3(256), 0, s, m, a.recv_list, a.p_cts,
+                       a.p_chain, a.p_rr, R, n, segc, (unsigned long long*)a.minmax);
     hipLaunchKernelGGL(k_seg_max, dim3(std::max(1, std::min(256, (nseg + 255) / 256))), dim3(256), 0, s, nseg, segc,
                        max_out);
 }
 
 void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
                      uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys) {
-    uint64_t *ka = a.key_a, *kb = a.key_b;
+    uint64_t* kb = a.key_b;
     uint32_t *va = a.val_a, *vb = a.val_b;
-    hipLaunchKernelGGL(k_keys_comb, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr,
-                       cmin, cts_bits, R, n, ka, va);
     scan_u32(s, a, segoff, nseg);   // bucket counts -> bucket starts
     (void)hipMemsetAsync(segcur, 0, (size_t)nseg * 4, s);
-    hipLaunchKernelGGL(k_seg_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, ka, va, cts_bits, segoff, segcur, kb, vb);
+    hipLaunchKernelGGL(k_seg_keys_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain,
+                       a.p_rr, cmin, cts_bits, R, n, segoff, segcur, kb, vb);
     int cap = 2;
     while (cap < max_seg) cap <<= 1;
     // (the runs of equal keys are ordered by S inside k_seg_sort: the final values land in va)
     if (cap <= 512) {   // a wave per bucket, four per workgroup
         const size_t lds = (size_t)4 * cap * 16;
-        hipLaunchKernelGGL(k_seg_sort<64>, dim3((nseg + 3) / 4), dim3(256), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
-                           a.g_S, va, cap);
+        hipLaunchKernelGGL((k_seg_sort<64, 256>), dim3((nseg + 3) / 4), dim3(256), lds, s, nseg, m, segoff, kb, vb,
+                           a.p_gid, a.g_S, va, cap);
     } else {
         const size_t lds = (size_t)cap * 16;
-        (void)ensure_lds_limit((const void*)k_seg_sort<256>, lds);
-        hipLaunchKernelGGL(k_seg_sort<256>, dim3(nseg), dim3(256), lds, s, nseg, m, segoff, kb, vb, a.p_gid, a.g_S,
-                           va, cap);
+        (void)ensure_lds_limit((const void*)k_seg_sort<1024, 1024>, lds);
+        hipLaunchKernelGGL((k_seg_sort<1024, 1024>), dim3(nseg), dim3(1024), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
+                           a.g_S, va, cap);
     }
     *final_vals = va;
     *final_keys = kb;

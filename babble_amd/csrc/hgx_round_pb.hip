@@ -52,7 +52,7 @@ __device__ __forceinline__ void pb_lds_barrier() { asm volatile("s_waitcnt lgkmc
 template <int HD>
 __device__ __forceinline__ void pb_ld_cand(const uint64_t* gp, const uint32_t* p, uint64_t& gv, uint32_t (&v)[HD]) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    static_assert(HD == 16 || HD == 32, "pb_ld_cand: HD in {16, 32}");
+    static_assert(HD == 16 || HD == 24 || HD == 32, "pb_ld_cand: HD in {16, 24, 32}");
     u32x4 a, b, c, d;
     asm volatile(
         "global_load_dwordx2 %0, %5, off sc1\n\t"
@@ -77,6 +77,16 @@ __device__ __forceinline__ void pb_ld_cand(const uint64_t* gp, const uint32_t* p
         const u32x4 r4[4] = {e, f, g, h};
 #pragma unroll
         for (int k = 0; k < 4; k++) { v[16 + 4 * k] = r4[k].x; v[17 + 4 * k] = r4[k].y; v[18 + 4 * k] = r4[k].z; v[19 + 4 * k] = r4[k].w; }
+    } else if constexpr (HD == 24) {
+        u32x4 e, f;
+        asm volatile(
+            "global_load_dwordx4 %0, %2, off offset:64 sc1\n\t"
+            "global_load_dwordx4 %1, %2, off offset:80 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(e), "=&v"(f) : "v"(p) : "memory");
+        const u32x4 r4[2] = {e, f};
+#pragma unroll
+        for (int k = 0; k < 2; k++) { v[16 + 4 * k] = r4[k].x; v[17 + 4 * k] = r4[k].y; v[18 + 4 * k] = r4[k].z; v[19 + 4 * k] = r4[k].w; }
     }
 }
 
@@ -87,12 +97,16 @@ __device__ __forceinline__ uint32_t pb_combine8(uint32_t x) {   // sum over the 
     return x;
 }
 
-template <int NDW>
+// Rows are COMPRESSED to the chains with events: coordinate slot i < na is chain amap[i] (c5's 341
+// silent peers, whose coordinates are "none" everywhere and never count, take no bytes: 768 instead of
+// 1 024 coordinate slots per row).
+template <int HD_>
 struct PbCfg {
     static constexpr int Q = 8, T = 1024, NW = T / 64, PP = kPbPP;
-    static constexpr int HD = NDW / Q;          // row dwords per lane (16 or 32)
+    static constexpr int HD = HD_;              // row dwords per lane (16, 24 or 32)
+    static constexpr int NDW = Q * HD;          // row dwords (4 coordinate slots each)
     static constexpr int CPB = T / Q;           // candidates per pass (128)
-    static constexpr int NC = 4 * NDW;          // chains (padded)
+    static constexpr int NC = 1024;             // chains (bases, K, map)
     // window rows: dword 8h + e of part q (what lane q of a candidate compares) at h * 64 + 8 q + e, so
     // part q lies in banks 8q .. 8q + 7 of every row whatever the row; a ds_read_b128 lane group holds
     // two candidates per part, which read the part's two halves in opposite orders (the candidates
@@ -153,8 +167,9 @@ void round_pb_prof_dump() {
     if (!h[15]) return;
     const double r = (double)h[15];
     fprintf(stderr, "[hgx] k_round_pb clk per block-round (thread 0): polls %.0f searches %.0f hist-barrier %.0f "
-            "scan+windows %.0f publish %.0f pub-barrier %.0f rebase+barrier %.0f | block-rounds %llu\n",
-            h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / r, h[6] / r, h[7] / r, h[15]);
+            "scan+windows %.0f publish: gathers+store %.0f window loads %.0f S rows %.0f pub-barrier %.0f "
+            "rebase+barrier %.0f | block-rounds %llu\n",
+            h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[6] / r, h[7] / r, h[15]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_pb_prof), z, sizeof(z));
 }
@@ -165,10 +180,10 @@ void round_pb_prof_dump() {
 void round_pb_prof_dump() {}
 #endif
 
-template <typename CT, int NDW>
+template <typename CT, int HD_>
 __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
-    typedef PbCfg<NDW> K;
-    constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, CPB = K::CPB;
+    typedef PbCfg<HD_> K;
+    constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, CPB = K::CPB, NDW = K::NDW;
     constexpr int NC = K::NC;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const RoundArgs& A = P.A;
@@ -213,39 +228,48 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
     if (t < 8) misc[t] = 0;
     // rebased 8-bit window rows of prober k's positions [kb, kb + np) against bases bq, straight from
     // HBM: rb_load issues a thread's raw loads, rb_store rebases them into the window
-    // (T a multiple of NDW: a thread keeps its dword d = t % NDW, rows p = (t + kT) / NDW)
-    constexpr int PER = (kPbP * NDW + T - 1) / T;
-    constexpr int NR = sizeof(CT) == 2 ? 2 : 4;   // raw dwords per row dword
+    // (a thread keeps its dword d = t % NDW of rows p = t / NDW + k RPP; threads past RPP rows idle)
+    constexpr int RPP = T / NDW;                  // rows per pass
+    constexpr int PER = (kPbP + RPP - 1) / RPP;   // passes
+    constexpr int NR = sizeof(CT) == 2 ? 2 : 4;   // raw dwords per row dword (compact: two coordinates each)
     typedef uint32_t RawRows[PER][NR];
-    auto rb_load = [&](RawRows& raw, int off, int kb, int np) {
+    // the chains of this thread's dword's 4 coordinate slots (-1: no coordinate)
+    int dch[4];
+    {
         const int d = t % NDW;
 #pragma unroll
+        for (int u = 0; u < 4; u++) dch[u] = 4 * d + u < P.na ? P.amap[4 * d + u] : -1;
+    }
+    auto rb_load = [&](RawRows& raw, int off, int kb, int np) {
+        const int p0 = t / NDW;
+#pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int p = (t + k * T) / NDW;
+            const int p = p0 + k * RPP;
 #pragma unroll
             for (int u = 0; u < NR; u++) raw[k][u] = 0u;
-            if (p < np) {
+            if (p0 < RPP && p < np) {
                 const CT* row = LA + (size_t)(off + kb + p) * n;
-                if constexpr (sizeof(CT) == 2) {   // (compact: n even)
-                    const uint32_t* rw = (const uint32_t*)row;
-                    if (4 * d < n) raw[k][0] = rw[2 * d];
-                    if (4 * d + 2 < n) raw[k][1] = rw[2 * d + 1];
+                if constexpr (sizeof(CT) == 2) {   // (two 16-bit coordinates per register)
+                    const uint32_t a0 = dch[0] >= 0 ? (uint32_t)row[dch[0]] : 0u, a1 = dch[1] >= 0 ? (uint32_t)row[dch[1]] : 0u;
+                    const uint32_t a2 = dch[2] >= 0 ? (uint32_t)row[dch[2]] : 0u, a3 = dch[3] >= 0 ? (uint32_t)row[dch[3]] : 0u;
+                    raw[k][0] = a0 | (a1 << 16);
+                    raw[k][1] = a2 | (a3 << 16);
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 4; u++) raw[k][u] = 4 * d + u < n ? (uint32_t)row[4 * d + u] : 0u;
+                    for (int u = 0; u < 4; u++) raw[k][u] = dch[u] >= 0 ? (uint32_t)row[dch[u]] : 0u;
                 }
             }
         }
     };
     auto rb_store = [&](const RawRows& raw, uint32_t* win, int np, const int32_t* bq) {
-        const int d = t % NDW;
-        if (t / NDW >= np) return;
+        const int d = t % NDW, p0 = t / NDW;
+        if (p0 >= RPP || p0 >= np) return;
         int32_t bq4[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) bq4[u] = 4 * d + u < n ? bq[4 * d + u] : 0;
+        for (int u = 0; u < 4; u++) bq4[u] = dch[u] >= 0 ? bq[dch[u]] : 0;
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int p = (t + k * T) / NDW;
+            const int p = p0 + k * RPP;
             if (p >= np) continue;
             int32_t la[4];
             if constexpr (sizeof(CT) == 2) {
@@ -258,7 +282,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             uint32_t w = 0x80808080u;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                if (4 * d + u < n) {
+                if (dch[u] >= 0) {
                     const int32_t x = la[u] - bq4[u] + 1;
                     w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
                 }
@@ -300,17 +324,37 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         // publish's 1 024 gathers per prober each took a translation miss, 26 us per c5 round); the
         // loads complete behind this round's first poll, which waits for the candidates anyway
         uint32_t pfx = 0;
-        if (t < n) {
+        if (t < P.na) {
+            const int ch = amapl[t];
 #pragma unroll
             for (int k = 0; k < PP; k++)
-                if (have[k]) pfx += (uint32_t)FDT[(size_t)t * A.Pcap + offs[k] + min(bs[k] + kPbP / 2, lens[k] - 1)];
+                if (have[k]) pfx += (uint32_t)FDT[(size_t)ch * A.Pcap + offs[k] + min(bs[k] + kPbP / 2, lens[k] - 1)];
         }
         bool any = false;
         for (int w_it = 0;; w_it++) {
             // every chunk of 128 candidates: poll (reload in a later window), search every active window
-            // (chunks over the chains with events only: c5's 341 silent peers cost no chunk slots)
+            // (chunks over the chains with events only: c5's 341 silent peers cost no chunk slots). A wave
+            // takes its chunks in the order their candidates arrive: a chunk whose rows are not complete
+            // yet is passed over and retried after the others, so a late candidate delays its own chunk's
+            // search only, not the searches of the chunks after it (with the chunks in order, the wave
+            // holding the round's last candidate searched every later chunk after it arrived)
             const int nch = (P.na + CPB - 1) / CPB;
-            for (int ch = 0; ch < nch; ch++) {
+            uint32_t pend = (1u << nch) - 1u;   // (nch <= 8)
+            const long long tw = __builtin_amdgcn_s_memrealtime();
+            bool wfail_w = false;
+            for (int spins = 0; pend; spins++) {
+              if (spins > 0) {   // a pass with nothing new: a pause and the bounded-wait checks
+                if ((spins & 7) == 7) {
+                    const long long now = __builtin_amdgcn_s_memrealtime();
+                    if (now - tw > P.tmo || pb_ld_abort(P.st) != 0) {
+                        wfail_w = true;
+                        if (lane == 0) misc[3] = 1;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+              for (int ch = 0; ch < nch; ch++) {
+                if (!((pend >> ch) & 1u)) continue;
                 const int ja = ch * CPB + jl;
                 const bool jv = ja < P.na;
                 const int j = jv ? amapl[ja] : 0;   // candidate chain
@@ -320,25 +364,18 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 const uint64_t* gp = P.gran + (size_t)(s % kPbSlots) * C + (live ? j : 0);
                 const uint32_t* rowp = P.FD8p + ((size_t)(s & (kRoundPBufs - 1)) * C + (live ? j : 0)) * NDW + q * HD;
                 // (a wave of this workgroup gave up: no further waits)
-                bool wfail = *(volatile int32_t*)&misc[3] != 0;
+                bool wfail = wfail_w || *(volatile int32_t*)&misc[3] != 0;
                 if (!wfail && __any(live)) {
-                    const long long tw = __builtin_amdgcn_s_memrealtime();
-                    bool ok = false;
-                    for (int spins = 0;; spins++) {
-                        if (!ok) pb_ld_cand<HD>(gp, rowp, gv, fd);
-                        uint32_t bad = 0;
+                    pb_ld_cand<HD>(gp, rowp, gv, fd);
+                    uint32_t bad = 0;
 #pragma unroll
-                        for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
-                        const bool tag_ok = (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
-                        ok = !live || (tag_ok && (!((uint32_t)gv & kPbEx) || bad == 0));
-                        if (__all(ok)) break;
-                        if ((spins & 31) == 31) {
-                            const long long now = __builtin_amdgcn_s_memrealtime();
-                            if (now - tw > P.tmo || pb_ld_abort(P.st) != 0) { wfail = true; break; }
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
+                    for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
+                    const bool tag_ok = (uint32_t)(gv >> 32) == (uint32_t)(s + 1);
+                    const bool ok = !live || (tag_ok && (!((uint32_t)gv & kPbEx) || bad == 0));
+                    if (!__all(ok)) continue;   // not complete yet: the next pending chunk
                 }
+                pend &= ~(1u << ch);
+                spins = 0;
                 PB_PROF(1);
                 const uint32_t gval = (uint32_t)gv;
                 const bool cand = live && !wfail && (gval & kPbEx);
@@ -403,15 +440,17 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                         }
                     } else {
                         // exact int32 compares of this part of the row (hashgraph.go:191-197)
-                        const int i_lo = q * HD * 4, i_hi = min(n, (q + 1) * HD * 4);
+                        // (this lane's coordinate slots, each a chain with events)
+                        const int i_lo = q * HD * 4, i_hi = min(P.na, (q + 1) * HD * 4);
                         const size_t pos = (size_t)A.c_off[j] + (gval & kPbBm);
 #pragma unroll
                         for (int k = 0; k < PP; k++) {
                             if (!srch[k] || done[k] || mid[k] >= np[k]) continue;
                             for (int i = i_lo; i < i_hi; i++) {
-                                const int32_t fdv = Coord<CT>::fd(FDT[(size_t)i * A.Pcap + pos]);
+                                const int ch = amapl[i];
+                                const int32_t fdv = Coord<CT>::fd(FDT[(size_t)ch * A.Pcap + pos]);
                                 const int32_t lav =
-                                    min(Coord<CT>::la(LA[(size_t)(offs[k] + kb[k] + mid[k]) * n + i]), kMaxI32 - 1);
+                                    min(Coord<CT>::la(LA[(size_t)(offs[k] + kb[k] + mid[k]) * n + ch]), kMaxI32 - 1);
                                 cnt[k] += lav >= fdv ? 1u : 0u;
                             }
                         }
@@ -433,6 +472,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                     // K of this window, seen-earlier bit, candidate bit (the S row's inputs)
                     if (jv && q == 0) kstp(k)[j] = (uint8_t)(min(Kw, 31) | (done[k] ? 32 : 0) | (cand ? 64 : 0));
                 }
+              }
             }
             // the histograms are complete: every wave scans them (the boundary: first probe where
             // #{K <= p} (+ seen in earlier windows) >= SM)
@@ -502,7 +542,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             if (kk >= 0) {
                 CT f[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) f[u] = FDT[(size_t)min(4 * d + u, n - 1) * A.Pcap + off + kst_];
+                for (int u = 0; u < 4; u++) f[u] = FDT[(size_t)(dch[u] >= 0 ? dch[u] : 0) * A.Pcap + off + kst_];
                 const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
                 const int32_t* bs1 = bpar(s);
                 uint32_t w = 0;
@@ -510,14 +550,15 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int32_t fv = Coord<CT>::fd(f[u]);
-                    const bool real = 4 * d + u < n && fv != kMaxI32;
-                    const int32_t x = fv - (real ? bs1[4 * d + u] : 0) + 1;
+                    const bool real = dch[u] >= 0 && fv != kMaxI32;
+                    const int32_t x = fv - (real ? bs1[dch[u]] : 0) + 1;
                     of |= real && x > 126;
                     w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
                 }
                 pb_st_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + d, w | vb1);
                 if (of) pof[kk] = 1;
             }
+            PB_PROF(8);
             // (the next windows' rows: issued after the publish, which waits for its gathers alone, and
             // in flight behind the S rows, the barrier and the granules)
 #pragma unroll
@@ -525,6 +566,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 np1[x] = valid[x] && kstar[x] < lens[x] ? min(kPbP, lens[x] - kstar[x]) : 0;
                 if constexpr (kMerged) rb_load(rawn[x], offs[x], kstar[x], np1[x]);
             }
+            PB_PROF(9);
         }
         // the S rows (DecideFame, hashgraph.go:688-705): bit j = the new candidate strongly sees
         // candidate j of W'_s, i.e. j was seen in an earlier window or K(j) <= B
@@ -595,6 +637,47 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
     }
 }
 
+// W'_{r0}'s compressed rows (rebased to base(r0), bit 7 = v(r0)) and granules of the chains with events,
+// from the WFD rows of launch_round_gather (k_round_p_init's job, for the compressed slots); the three
+// other buffers get the invalid bit for the rounds r0 + 1 .. r0 + 3 that will use them. One workgroup per
+// chain with events.
+template <typename CT>
+__global__ void __launch_bounds__(64) k_round_pb_init(RoundPbArgs P, int ndw) {
+    const RoundArgs& A = P.A;
+    const int gc = P.amap[blockIdx.x], n = A.n, C = A.C, r = P.r0;
+    const int b = A.Bm[(size_t)r * C + gc];
+    const bool have = b < A.c_len[gc];
+    bool of = false;
+    const CT* __restrict__ row = (const CT*)A.WFD + ((size_t)r * C + gc) * n;
+    for (int d = threadIdx.x; d < ndw; d += 64) {
+        uint32_t w = 0;
+        for (int u = 0; u < 4; u++) {
+            const int i = 4 * d + u;
+            uint32_t v = 127u;
+            if (have && i < P.na) {
+                const int ch = P.amap[i];
+                const int32_t f = Coord<CT>::fd(row[ch]);
+                if (f != kMaxI32) {
+                    const int32_t bs = A.c_base[ch] + (r > 0 ? A.Bm[(size_t)(r - 1) * C + ch] : 0);
+                    const int32_t x = f - bs + 1;
+                    if (x > 126) of = true;
+                    else v = (uint32_t)x;
+                }
+            }
+            w |= v << (8 * u);
+        }
+        pb_st_sc1(P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d,
+                  w | (((r >> kRoundPShift) & 1) ? 0x80808080u : 0u));
+        for (int k = 1; k < kRoundPBufs; k++)
+            pb_st_sc1(P.FD8p + ((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d,
+                      (((r + k) >> kRoundPShift) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu);   // bit 7 = !v(r + k)
+    }
+    of = __any(of);
+    if (threadIdx.x == 0)
+        pb_st_gran(P.gran + (size_t)(r % kPbSlots) * C + gc,
+                   ((uint64_t)(uint32_t)(r + 1) << 32) | (uint32_t)b | (have ? kPbEx : 0u) | (of ? kPbOv : 0u));
+}
+
 // the rows of silent chains (no events, no workgroup) for rounds [r_lo, r_hi]: Bm = 0 (= len)
 __global__ void k_round_pb_silent(RoundArgs A, int r_lo, int r_hi) {
     const int gc = blockIdx.x * blockDim.x + threadIdx.x;
@@ -603,10 +686,10 @@ __global__ void k_round_pb_silent(RoundArgs A, int r_lo, int r_hi) {
 }
 
 namespace {
-template <typename CT, int NDW>
-hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus) {
-    typedef PbCfg<NDW> K;
-    const void* f = (const void*)k_round_pb<CT, NDW>;
+template <typename CT, int HD>
+hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus, bool init) {
+    typedef PbCfg<HD> K;
+    const void* f = (const void*)k_round_pb<CT, HD>;
     int per_cu = 0;
     hipError_t e = ensure_lds_limit(f, K::LDS);
     if (e == hipSuccess) e = blocks_per_cu(f, K::T, K::LDS, &per_cu);
@@ -614,7 +697,12 @@ hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus) {
     const int nblk = (P.na + K::PP - 1) / K::PP;
     // every workgroup must be resident at once (they wait for each other)
     if (per_cu < 1 || nblk > num_cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((k_round_pb<CT, NDW>), dim3(nblk), dim3(K::T), K::LDS, st, P);
+    if (init) {
+        hipLaunchKernelGGL(k_round_pb_init<CT>, dim3(P.na), dim3(64), 0, st, P, K::NDW);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_round_pb<CT, HD>), dim3(nblk), dim3(K::T), K::LDS, st, P);
     return hipGetLastError();
 }
 }  // namespace
@@ -622,7 +710,7 @@ hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus) {
 bool round_pb_ok(int n, int G) { return G == 1 && n > 256 && n <= 1024; }
 
 hipError_t launch_round_pb(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
-                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus) {
+                           int32_t* fin, const int32_t* amap, int na, int r0, int r_end, int num_cus, bool init) {
     if (!round_pb_ok(A.n, A.C / A.n) || na < 1) return hipErrorInvalidValue;
     RoundPbArgs P{};
     P.A = A;
@@ -635,9 +723,14 @@ hipError_t launch_round_pb(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, u
     P.r0 = r0;
     P.r_end = r_end;
     P.tmo = 5000000;   // 50 ms per wait
-    const int ndw = round_k_ndw(A.n);
-    if (A.compact) return ndw == 128 ? pb_launch<uint16_t, 128>(st, P, num_cus) : pb_launch<uint16_t, 256>(st, P, num_cus);
-    return ndw == 128 ? pb_launch<int32_t, 128>(st, P, num_cus) : pb_launch<int32_t, 256>(st, P, num_cus);
+    // row dwords per lane by the chains with events (coordinate slots = 32 HD)
+    if (na > 1024) return hipErrorInvalidValue;
+    const int hd = na <= 512 ? 16 : na <= 768 ? 24 : 32;
+    if (A.compact)
+        return hd == 16 ? pb_launch<uint16_t, 16>(st, P, num_cus, init)
+                        : hd == 24 ? pb_launch<uint16_t, 24>(st, P, num_cus, init) : pb_launch<uint16_t, 32>(st, P, num_cus, init);
+    return hd == 16 ? pb_launch<int32_t, 16>(st, P, num_cus, init)
+                    : hd == 24 ? pb_launch<int32_t, 24>(st, P, num_cus, init) : pb_launch<int32_t, 32>(st, P, num_cus, init);
 }
 
 void launch_round_pb_silent(hipStream_t st, const RoundArgs& A, int r_lo, int r_hi) {
