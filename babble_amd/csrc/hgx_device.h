@@ -9,6 +9,28 @@ namespace hgx {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// Strongly-see count of 8-bit rebased coordinates, 4 per dword: window bytes hold LA' in [0, 126], the
+// candidate's bytes nf = 128 - FD' with FD' in [1, 127] (127 = none), so LA' + nf lies in [1, 253]: no
+// carry leaves a byte, and bit 7 is set exactly when LA' >= FD'. With no carries the add may span 64
+// bits (one v_lshl_add_u64 per 8 coordinates instead of a v_sub per 4).
+template <int HD>
+__device__ __forceinline__ uint32_t swar_ge_count(const uint32_t (&v)[HD], const uint32_t (&nf)[HD]) {
+    uint32_t c = 0;
+    if constexpr (HD % 2 == 0) {
+#pragma unroll
+        for (int i = 0; i < HD / 2; i++) {
+            const uint64_t s = ((((uint64_t)v[2 * i + 1]) << 32) | v[2 * i]) + ((((uint64_t)nf[2 * i + 1]) << 32) | nf[2 * i]);
+            c += __builtin_popcount((uint32_t)s & 0x80808080u) + __builtin_popcount((uint32_t)(s >> 32) & 0x80808080u);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < HD; d++) c += __builtin_popcount((v[d] + nf[d]) & 0x80808080u);
+    }
+    return c;
+}
+// a candidate row dword (bytes FD' with the validity bit cleared) as its nf bytes (128 - FD'); 127 = none -> 1
+__device__ __forceinline__ uint32_t swar_nf(uint32_t fd7) { return 0x80808080u - fd7; }
+
 __device__ __forceinline__ uint64_t group_mask(int gs, int grp) {
     return (gs >= 64) ? ~0ull : (((1ull << gs) - 1ull) << (gs * grp));
 }

@@ -101,10 +101,10 @@ void round_p_prof_dump() {
     unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
     const double r = h[15] ? (double)h[15] : 1.0;
-    fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): poll %.0f barrier %.0f search-levels %.0f "
-            "drain+barrier %.0f scan %.0f publish..poll-issue %.0f | block-rounds %llu, synchronous stagings %llu, "
-            "later windows %llu\n",
-            h[1] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[5] / r, h[15], h[10], h[11]);
+    fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): poll %.0f bases+flags %.0f S row %.0f staging issue %.0f "
+            "search-levels %.0f drain+barrier %.0f scan %.0f publish..poll-issue %.0f | block-rounds %llu, synchronous "
+            "stagings %llu, later windows %llu\n",
+            h[1] / r, h[6] / r, h[7] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[5] / r, h[15], h[10], h[11]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
     if (const char* path = getenv("HGX_RP_TRACE_FILE")) {
@@ -147,6 +147,24 @@ __device__ __forceinline__ void rp_st_sc1(uint32_t* p, uint32_t v) {
 // the same into a window on another device (peer mapping): system scope
 __device__ __forceinline__ void rp_st_sys(uint32_t* p, uint32_t v) {
     asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+// 16-byte forms (a write-through store is one fabric write per lane: per byte a dword store costs
+// ~6x a dwordx4 one, MI355X_MICROARCH.md)
+__device__ __forceinline__ void rp_st4_sc1(uint32_t* p, uint4 v) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+__device__ __forceinline__ void rp_st4_sys(uint32_t* p, uint4 v) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+}
+// a wave's row dwords w (lane d = dword d) as 16-byte pieces: lane l < 16 gets dwords 4l .. 4l + 3
+__device__ __forceinline__ uint4 rp_gather4(uint32_t w) {
+    const int src = (4 * lane_id()) & 63;
+    return make_uint4((uint32_t)__shfl((int)w, src), (uint32_t)__shfl((int)w, src + 1),
+                      (uint32_t)__shfl((int)w, src + 2), (uint32_t)__shfl((int)w, src + 3));
 }
 __device__ __forceinline__ void rp_st_gran_sys(uint64_t* p, uint64_t v) {
     __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -408,7 +426,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     auto raw_at = [&](int p, int i) -> CT {   // staged lastAncestors row of chain offset p
         return ((const CT*)(lds + K::O_RAW))[(p % RR) * n + i];
     };
-    // rebased 8-bit window rows (0x80 | clamp(LA - base + 1, 0, 126)) of the window [kb, kb + np),
+    // rebased 8-bit window rows (clamp(LA - base + 1, 0, 126), swar_ge_count) of the window [kb, kb + np),
     // by threads [0, nthr) (tid = this thread's), bases bq = c_base + Bm of the previous round
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     auto rebase = [&](int kb, int np, const int32_t* bsp, int tid, int nthr) {
@@ -428,10 +446,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     const u16x2 cap = {126, 126};
                     const u16x2 y01 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r01), b01), cap);
                     const u16x2 y23 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, r23), b23), cap);
-                    w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23), __builtin_bit_cast(uint32_t, y01), 0x06040200u) |
-                        0x80808080u;
+                    w = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y23), __builtin_bit_cast(uint32_t, y01), 0x06040200u);
                 } else {
-                    w = 0x80808080u;
+                    w = 0u;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         if (i0 + u < n) {
@@ -526,10 +543,11 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         if (jv && q == 0 && !wfail) bases(s)[j] = cbase[j] + bmj;   // base(s + 1)[j]
         if (cand && have) {
 #pragma unroll
-            for (int d = 0; d < HD; d++) fd[d] &= 0x7F7F7F7Fu;   // the validity bits off: rebased values
+            for (int d = 0; d < HD; d++) fd[d] = swar_nf(fd[d] & 0x7F7F7F7Fu);   // validity bits off, as 128 - FD'
+
         } else {
 #pragma unroll
-            for (int d = 0; d < HD; d++) fd[d] = 0x7F7F7F7Fu;   // never seen
+            for (int d = 0; d < HD; d++) fd[d] = 0x01010101u;   // never seen (FD' = 127)
         }
         if (wfail && lane == 0) misc[3] = 1;
         if (cand && q == 0) misc[2] = 1;   // (same value from every writer)
@@ -540,10 +558,12 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         // histogram barrier)
         if (t >= T - 32) hist_of(s + 1)[t - (T - 32)] = 0;
         if (t < 8) misc_of(s + 1)[t] = 0;
+        RP_PROF(6);
         if (s_r >= 0) {   // round s - 1's S row: every wave set its slice before this barrier
             if (wave == 0) s_row(s_r, s_k);
             s_r = -1;
         }
+        RP_PROF(7);
         // the ring ahead (segments up to b / SEG + NSEG - 1), behind the poll (a wave's loads return
         // in order: staging issued before the poll would hold it back) and behind the LDS writes
         // above (the compiler waits for an LDS-DMA before the next LDS access it cannot tell
@@ -572,8 +592,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     if (!ov) {
                         uint32_t v[HD];
                         rp_lds_row<HD>(win + mid * WS + q * K::PS, v);
-#pragma unroll
-                        for (int d = 0; d < HD; d++) cnt += __builtin_popcount((v[d] - fd[d]) & 0x80808080u);
+                        cnt = swar_ge_count<HD>(v, fd);
                     } else if (!done && mid < np) {
                         // exact int32 compares of this part of the row (hashgraph.go:191-197)
                         const int i_lo = q * HD * 4, i_hi = min(n, (q + 1) * HD * 4);
@@ -662,14 +681,15 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
                 const size_t roff = ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
                 static_assert(NDW <= 64, "k_round_p: one row dword per lane of wave 0");
-                for (int d = lane; d < NDW; d += 64) {
+                const int d = lane;
+                uint32_t w = 0;
+                if (d < NDW) {
                     // every LDS read first (4 firstDescendants, 4 bases), then the byte arithmetic
                     CT f[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) f[u] = fd_at(min(4 * d + u, n - 1), kstar);
                     const int4 bq = *(const int4*)(bs1 + 4 * d);
                     const int32_t bqa[4] = {bq.x, bq.y, bq.z, bq.w};
-                    uint32_t w = 0;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         const int32_t fv = Coord<CT>::fd(f[u]);
@@ -678,15 +698,31 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                         of |= real && x > 126;
                         w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
                     }
-                    // into every shard's window (one: the launch's own buffers, whose address the
-                    // kernel arguments hold in SGPRs: no scalar load ahead of the store)
+                }
+                w |= vb1;
+                // into every shard's window (one: the launch's own buffers, whose address the kernel
+                // arguments hold in SGPRs: no scalar load ahead of the store), 16 bytes per lane
+                if constexpr (NDW % 4 == 0) {
+                    const uint4 w4 = rp_gather4(w);
+                    if (lane < NDW / 4) {
+                        if (!SH) {
+                            rp_st4_sc1(P.FD8p + roff + 4 * lane, w4);
+                        } else {
+                            const RoundPWindows* __restrict__ Wd = P.Wd;
+                            for (int wi = 0; wi < P.nwin; wi++) {
+                                if ((Wd->remote >> wi) & 1u) rp_st4_sys(Wd->FD8p[wi] + roff + 4 * lane, w4);
+                                else rp_st4_sc1(Wd->FD8p[wi] + roff + 4 * lane, w4);
+                            }
+                        }
+                    }
+                } else if (d < NDW) {
                     if (!SH) {
-                        rp_st_sc1(P.FD8p + roff + d, w | vb1);
+                        rp_st_sc1(P.FD8p + roff + d, w);
                     } else {
                         const RoundPWindows* __restrict__ Wd = P.Wd;
                         for (int wi = 0; wi < P.nwin; wi++) {
-                            if ((Wd->remote >> wi) & 1u) rp_st_sys(Wd->FD8p[wi] + roff + d, w | vb1);
-                            else rp_st_sc1(Wd->FD8p[wi] + roff + d, w | vb1);
+                            if ((Wd->remote >> wi) & 1u) rp_st_sys(Wd->FD8p[wi] + roff + d, w);
+                            else rp_st_sc1(Wd->FD8p[wi] + roff + d, w);
                         }
                     }
                 }

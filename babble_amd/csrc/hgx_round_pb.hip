@@ -30,13 +30,19 @@ namespace {
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 
-constexpr int kPbP = 31;   // probes per window
+// kst bytes: K(w) (0..63) | seen in an earlier window | candidate
+constexpr uint8_t kPbKM = 63, kPbDone = 64, kPbCand = 128;
 constexpr int kPbSlots = 4;
 constexpr int kPbPP = 3;   // probers (chains) per workgroup
 constexpr uint32_t kPbEx = 1u << 31, kPbOv = 1u << 30, kPbBm = (1u << 30) - 1;
 
 __device__ __forceinline__ void pb_st_sc1(uint32_t* p, uint32_t v) {
     asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void pb_st4_sc1(uint32_t* p, uint4 v) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
 }
 __device__ __forceinline__ void pb_st_gran(uint64_t* p, uint64_t v) {
     __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -100,9 +106,13 @@ __device__ __forceinline__ uint32_t pb_combine8(uint32_t x) {   // sum over the 
 // Rows are COMPRESSED to the chains with events: coordinate slot i < na is chain amap[i] (c5's 341
 // silent peers, whose coordinates are "none" everywhere and never count, take no bytes: 768 instead of
 // 1 024 coordinate slots per row).
-template <int HD_>
+template <int HD_, int NP_>
 struct PbCfg {
     static constexpr int Q = 8, T = 1024, NW = T / 64, PP = kPbPP;
+    // probes per window (31: 5 search levels; 63: 6): c5's chains have ~38 events per round, so a
+    // 31-probe window rarely held the boundary and most rounds searched two windows
+    static constexpr int NP = NP_, LV = NP_ == 31 ? 5 : 6;
+    static_assert(NP_ == 31 || NP_ == 63, "k_round_pb: windows of 31 or 63 probes");
     static constexpr int HD = HD_;              // row dwords per lane (16, 24 or 32)
     static constexpr int NDW = Q * HD;          // row dwords (4 coordinate slots each)
     static constexpr int CPB = T / Q;           // candidates per pass (128)
@@ -112,13 +122,13 @@ struct PbCfg {
     // two candidates per part, which read the part's two halves in opposite orders (the candidates
     // 2, 3 (mod 4) of a wave high half first): conflict-free whatever rows they probe
     static constexpr int WS = NDW;              // window row stride (dwords)
-    static constexpr int WIN = kPbP * WS;       // window (dwords)
+    static constexpr int WIN = NP * WS;         // window (dwords)
     // LDS (bytes)
-    static constexpr int O_WIN = 0;                       // [PP][kPbP][WS] rebased probes
+    static constexpr int O_WIN = 0;                       // [PP][NP][WS] rebased probes
     static constexpr int O_BS = O_WIN + PP * WIN * 4;     // [2][NC] c_base + Bm, by round parity
     static constexpr int O_KST = O_BS + 2 * NC * 4;       // [PP][NC] bytes: K | done << 5 | cand << 6
-    static constexpr int O_HIST = O_KST + PP * NC;        // [PP][32]
-    static constexpr int O_POF = O_HIST + PP * 32 * 4;    // [PP] the published row's overflow flag
+    static constexpr int O_HIST = O_KST + PP * NC;        // [PP][64]
+    static constexpr int O_POF = O_HIST + PP * 64 * 4;    // [PP] the published row's overflow flag
     static constexpr int O_MISC = O_POF + PP * 4;         // [8]: [2] any, [3] fail
     static constexpr int O_AMAP = O_MISC + 32;            // [NC] the chains with events (candidates)
     static constexpr int LDS = O_AMAP + NC * 4;
@@ -168,8 +178,9 @@ void round_pb_prof_dump() {
     const double r = (double)h[15];
     fprintf(stderr, "[hgx] k_round_pb clk per block-round (thread 0): polls %.0f searches %.0f hist-barrier %.0f "
             "scan+windows %.0f publish: gathers+store %.0f window loads %.0f S rows %.0f pub-barrier %.0f "
-            "rebase+barrier %.0f | block-rounds %llu\n",
-            h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[6] / r, h[7] / r, h[15]);
+            "granules %.0f rebase k=0 %.0f k=1 %.0f k=2 %.0f end barrier %.0f | block-rounds %llu\n",
+            h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[6] / r, h[10] / r, h[11] / r,
+            h[12] / r, h[13] / r, h[7] / r, h[15]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_pb_prof), z, sizeof(z));
 }
@@ -180,9 +191,10 @@ void round_pb_prof_dump() {
 void round_pb_prof_dump() {}
 #endif
 
-template <typename CT, int HD_>
+template <typename CT, int HD_, int NP_>
 __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
-    typedef PbCfg<HD_> K;
+    typedef PbCfg<HD_, NP_> K;
+    constexpr int kPbP = K::NP;
     constexpr int Q = K::Q, T = K::T, NW = K::NW, PP = K::PP, HD = K::HD, WS = K::WS, CPB = K::CPB, NDW = K::NDW;
     constexpr int NC = K::NC;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -194,7 +206,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
     auto winp = [&](int k) { return (uint32_t*)(lds + K::O_WIN) + k * K::WIN; };
     auto bpar = [&](int r) { return (int32_t*)(lds + K::O_BS) + (r & 1) * NC; };   // c_base + Bm[r]
     auto kstp = [&](int k) { return lds + K::O_KST + k * NC; };
-    auto histp = [&](int k) { return (int32_t*)(lds + K::O_HIST) + k * 32; };
+    auto histp = [&](int k) { return (int32_t*)(lds + K::O_HIST) + k * 64; };
     int32_t* pof = (int32_t*)(lds + K::O_POF);
     int32_t* misc = (int32_t*)(lds + K::O_MISC);
     int32_t* amapl = (int32_t*)(lds + K::O_AMAP);
@@ -223,74 +235,92 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         if (i < P.na) amapl[i] = P.amap[i];
     }
     for (int i = t; i < PP * NC; i += T) lds[K::O_KST + i] = 0;
-    if (t < PP * 32) ((int32_t*)(lds + K::O_HIST))[t] = 0;
+    if (t < PP * 64) ((int32_t*)(lds + K::O_HIST))[t] = 0;
     if (t < PP) pof[t] = 0;
     if (t < 8) misc[t] = 0;
     // rebased 8-bit window rows of prober k's positions [kb, kb + np) against bases bq, straight from
-    // HBM: rb_load issues a thread's raw loads, rb_store rebases them into the window
-    // (a thread keeps its dword d = t % NDW of rows p = t / NDW + k RPP; threads past RPP rows idle)
-    constexpr int RPP = T / NDW;                  // rows per pass
-    constexpr int PER = (kPbP + RPP - 1) / RPP;   // passes
-    constexpr int NR = sizeof(CT) == 2 ? 2 : 4;   // raw dwords per row dword (compact: two coordinates each)
-    typedef uint32_t RawRows[PER][NR];
-    // the chains of this thread's dword's 4 coordinate slots (-1: no coordinate)
-    int dch[4];
+    // HBM: rb_load issues a thread's raw loads, rb_store rebases them into the window. A thread takes
+    // GS = 16 bytes of coordinate slots (8 compact, 4 int32: 2 or 1 window dwords) of rows
+    // p = t / NG + k RPP; threads past RPP rows idle. Where its slots are GS consecutive chains from an
+    // aligned one (c5: every slot), a row's slots are ONE 16-byte load (the per-slot gathers issued 26
+    // dword loads per thread and window and took ~20 us per window at c5, the memory pipeline's
+    // request rate, not its bytes); otherwise one gather per slot
+    constexpr int GS = 16 / (int)sizeof(CT);       // slots per thread
+    constexpr int GD = GS / 4;                     // window dwords per thread
+    constexpr int NG = NDW / GD;                   // threads per row
+    constexpr int RPP = T / NG;                    // rows per pass
+    constexpr int PER = (kPbP + RPP - 1) / RPP;    // passes
+    typedef uint32_t RawRows[PER][4];
+    const int ge = t % NG, gp0 = t / NG;           // slot group, first row
+    int g_c0;                                      // first chain of an aligned run (vector loads), else -1
     {
-        const int d = t % NDW;
+        const int i0 = GS * ge;
+        bool vec = i0 < P.na && n % GS == 0;
+        const int c0 = vec ? P.amap[i0] : -1;
+        vec = vec && c0 % GS == 0;
 #pragma unroll
-        for (int u = 0; u < 4; u++) dch[u] = 4 * d + u < P.na ? P.amap[4 * d + u] : -1;
+        for (int u = 1; u < GS; u++) vec = vec && (i0 + u >= P.na || P.amap[i0 + u] == c0 + u);
+        g_c0 = vec ? c0 : -1;
     }
-    auto rb_load = [&](RawRows& raw, int off, int kb, int np) {
-        const int p0 = t / NDW;
+    auto slot_chain = [&](int u) __attribute__((always_inline)) -> int {   // chain of slot GS ge + u (-1: no coordinate)
+        const int i = GS * ge + u;
+        return i < P.na ? (g_c0 >= 0 ? g_c0 + u : amapl[i]) : -1;
+    };
+    auto rb_load = [&](RawRows& raw, int off, int kb, int np) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int p = p0 + k * RPP;
+            const int p = gp0 + k * RPP;
 #pragma unroll
-            for (int u = 0; u < NR; u++) raw[k][u] = 0u;
-            if (p0 < RPP && p < np) {
+            for (int u = 0; u < 4; u++) raw[k][u] = 0u;
+            if (gp0 < RPP && p < np) {
                 const CT* row = LA + (size_t)(off + kb + p) * n;
-                if constexpr (sizeof(CT) == 2) {   // (two 16-bit coordinates per register)
-                    const uint32_t a0 = dch[0] >= 0 ? (uint32_t)row[dch[0]] : 0u, a1 = dch[1] >= 0 ? (uint32_t)row[dch[1]] : 0u;
-                    const uint32_t a2 = dch[2] >= 0 ? (uint32_t)row[dch[2]] : 0u, a3 = dch[3] >= 0 ? (uint32_t)row[dch[3]] : 0u;
-                    raw[k][0] = a0 | (a1 << 16);
-                    raw[k][1] = a2 | (a3 << 16);
+                if (g_c0 >= 0) {
+                    const uint4 v = *(const uint4*)(row + g_c0);
+                    raw[k][0] = v.x; raw[k][1] = v.y; raw[k][2] = v.z; raw[k][3] = v.w;
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 4; u++) raw[k][u] = dch[u] >= 0 ? (uint32_t)row[dch[u]] : 0u;
+                    for (int u = 0; u < GS; u++) {
+                        const int ch = slot_chain(u);
+                        const uint32_t a = ch >= 0 ? (uint32_t)row[ch] : 0u;
+                        if constexpr (sizeof(CT) == 2) raw[k][u >> 1] |= a << (16 * (u & 1));
+                        else raw[k][u] = a;
+                    }
                 }
             }
         }
     };
-    auto rb_store = [&](const RawRows& raw, uint32_t* win, int np, const int32_t* bq) {
-        const int d = t % NDW, p0 = t / NDW;
-        if (p0 >= RPP || p0 >= np) return;
-        int32_t bq4[4];
+    auto rb_store = [&](const RawRows& raw, uint32_t* win, int np, const int32_t* bq) __attribute__((always_inline)) {
+        if (gp0 >= RPP || gp0 >= np) return;
+        int32_t bqv[GS];
+        bool sv[GS];
 #pragma unroll
-        for (int u = 0; u < 4; u++) bq4[u] = dch[u] >= 0 ? bq[dch[u]] : 0;
+        for (int u = 0; u < GS; u++) {
+            const int ch = slot_chain(u);
+            sv[u] = ch >= 0;
+            bqv[u] = ch >= 0 ? bq[ch] : 0;
+        }
+        const int d = GD * ge;   // first window dword (GD consecutive ones share an 8-dword piece)
+        const int wa = ((d % HD) >> 3) * 64 + (d / HD) * 8 + (d & 7);
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int p = p0 + k * RPP;
+            const int p = gp0 + k * RPP;
             if (p >= np) continue;
-            int32_t la[4];
-            if constexpr (sizeof(CT) == 2) {
-                la[0] = (int32_t)(raw[k][0] & 0xFFFFu) - 1; la[1] = (int32_t)(raw[k][0] >> 16) - 1;
-                la[2] = (int32_t)(raw[k][1] & 0xFFFFu) - 1; la[3] = (int32_t)(raw[k][1] >> 16) - 1;
-            } else {
+            uint32_t w[GD];
 #pragma unroll
-                for (int u = 0; u < 4; u++) la[u] = (int32_t)raw[k][u];
-            }
-            uint32_t w = 0x80808080u;
+            for (int x = 0; x < GD; x++) w[x] = 0u;   // (swar_ge_count's window bytes)
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (dch[u] >= 0) {
-                    const int32_t x = la[u] - bq4[u] + 1;
-                    w |= (uint32_t)min(max(x, 0), 126) << (8 * u);
-                }
+            for (int u = 0; u < GS; u++) {
+                int32_t la;
+                if constexpr (sizeof(CT) == 2) la = (int32_t)((raw[k][u >> 1] >> (16 * (u & 1))) & 0xFFFFu) - 1;
+                else la = (int32_t)raw[k][u];
+                const int32_t x = la - bqv[u] + 1;
+                if (sv[u]) w[u >> 2] |= (uint32_t)min(max(x, 0), 126) << (8 * (u & 3));
             }
-            win[p * WS + ((d % HD) >> 3) * 64 + (d / HD) * 8 + (d & 7)] = w;
+            if constexpr (GD == 2) *(uint2*)(win + p * WS + wa) = make_uint2(w[0], w[1]);
+            else win[p * WS + wa] = w[0];
         }
     };
-    auto rebase = [&](uint32_t* win, int off, int kb, int np, const int32_t* bq) {
+    auto rebase = [&](uint32_t* win, int off, int kb, int np, const int32_t* bq) __attribute__((always_inline)) {
         RawRows raw;
         rb_load(raw, off, kb, np);
         rb_store(raw, win, np, bq);
@@ -384,7 +414,8 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 if (wfail && lane == 0) misc[3] = 1;
                 if (cand && q == 0) misc[2] = 1;
 #pragma unroll
-                for (int d = 0; d < HD; d++) fd[d] = cand ? (fd[d] & 0x7F7F7F7Fu) : 0x7F7F7F7Fu;
+                for (int d = 0; d < HD; d++) fd[d] = cand ? swar_nf(fd[d] & 0x7F7F7F7Fu) : 0x01010101u;   // 128 - FD'
+
                 // (candidates 2, 3 (mod 4) read each 8-dword piece high half first: their registers too)
                 if (hsw) {
 #pragma unroll
@@ -401,7 +432,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 const bool wc = __any(cand);
 #pragma unroll
                 for (int k = 0; k < PP; k++) {
-                    done[k] = w_it > 0 && jv && ((kstp(k)[j] >> 5) & 1);   // seen in an earlier window
+                    done[k] = w_it > 0 && jv && (kstp(k)[j] & kPbDone);   // seen in an earlier window
                     srch[k] = act[k] && wc;
                     lo[k] = 0;
                     hi[k] = kPbP;
@@ -410,7 +441,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
 #pragma unroll
                 for (int k = 0; k < PP; k++) srch_any |= srch[k];
 #pragma unroll 1
-                for (int it = 0; it < (srch_any ? 5 : 0); it++) {
+                for (int it = 0; it < (srch_any ? K::LV : 0); it++) {
                     int mid[PP];
                     uint32_t cnt[PP];
 #pragma unroll
@@ -427,15 +458,10 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
 #pragma unroll
                             for (int h = 0; h < HD / 8; h++) {
                                 const uint4 v0 = rp[16 * h], v1 = rp[16 * h + 1 - 2 * hsw];
-                                const uint32_t* f8 = fd + 8 * h;
-                                cnt[k] += __builtin_popcount((v0.x - f8[0]) & 0x80808080u) +
-                                          __builtin_popcount((v0.y - f8[1]) & 0x80808080u) +
-                                          __builtin_popcount((v0.z - f8[2]) & 0x80808080u) +
-                                          __builtin_popcount((v0.w - f8[3]) & 0x80808080u) +
-                                          __builtin_popcount((v1.x - f8[4]) & 0x80808080u) +
-                                          __builtin_popcount((v1.y - f8[5]) & 0x80808080u) +
-                                          __builtin_popcount((v1.z - f8[6]) & 0x80808080u) +
-                                          __builtin_popcount((v1.w - f8[7]) & 0x80808080u);
+                                const uint32_t v8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                                const uint32_t f8[8] = {fd[8 * h], fd[8 * h + 1], fd[8 * h + 2], fd[8 * h + 3],
+                                                        fd[8 * h + 4], fd[8 * h + 5], fd[8 * h + 6], fd[8 * h + 7]};
+                                cnt[k] += swar_ge_count<8>(v8, f8);
                             }
                         }
                     } else {
@@ -470,7 +496,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                     const int Kw = srch[k] ? lo[k] : 0;
                     if (cand && q == 0 && !done[k] && Kw < np[k]) atomicAdd(&histp(k)[Kw], 1);
                     // K of this window, seen-earlier bit, candidate bit (the S row's inputs)
-                    if (jv && q == 0) kstp(k)[j] = (uint8_t)(min(Kw, 31) | (done[k] ? 32 : 0) | (cand ? 64 : 0));
+                    if (jv && q == 0) kstp(k)[j] = (uint8_t)(min(Kw, (int)kPbKM) | (done[k] ? kPbDone : 0) | (cand ? kPbCand : 0));
                 }
               }
             }
@@ -509,9 +535,9 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 uint8_t* ks = kstp(k);
                 for (int jj = t; jj < n; jj += T) {
                     const uint8_t k8 = ks[jj];
-                    if ((k8 & 64) && (k8 & 31) < np[k]) ks[jj] = (uint8_t)(k8 | 32);
+                    if ((k8 & kPbCand) && (k8 & kPbKM) < np[k]) ks[jj] = (uint8_t)(k8 | kPbDone);
                 }
-                if (t < 32) histp(k)[t] = 0;
+                if (t < 64) histp(k)[t] = 0;
                 carried[k] = tot[k];
                 kb[k] += np[k];
                 np[k] = min(kPbP, lens[k] - kb[k]);
@@ -526,8 +552,15 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         // base(s+1) = c_base + Bm[s] (bit 7 = v(s + 1)), straight from the FDT columns; then the next
         // windows' raw rows (compact coordinates: every prober's loads at once; int32 rows are loaded
         // after the barrier, one prober at a time)
-        constexpr bool kMerged = sizeof(CT) == 2;
-        RawRows rawn[kMerged ? PP : 1];
+        // (63-probe windows: prober 0's rows now, the others' after the barrier, one row set in registers)
+        constexpr bool kMerged = sizeof(CT) == 2 && kPbP == 31;
+        constexpr bool kPipe = sizeof(CT) == 2 && kPbP == 63;
+#ifdef HGX_PB_PIPE2
+        constexpr int kPipeBufs = 2;   // (experiment: the next prober's rows in flight during a rebase)
+#else
+        constexpr int kPipeBufs = 1;   // (two row sets spilled and measured no faster)
+#endif
+        RawRows rawn[kMerged ? PP : kPipe ? kPipeBufs : 1];
         int np1[PP];
         {
             const int k = t / NDW, d = t % NDW;
@@ -540,6 +573,9 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             for (int x = 0; x < PP; x++)
                 if (kk == x) { off = offs[x]; kst_ = kstar[x]; gc = gcs[x]; }
             if (kk >= 0) {
+                int dch[4];   // the chains of this dword's 4 coordinate slots (-1: none)
+#pragma unroll
+                for (int u = 0; u < 4; u++) dch[u] = 4 * d + u < P.na ? amapl[4 * d + u] : -1;
                 CT f[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) f[u] = FDT[(size_t)(dch[u] >= 0 ? dch[u] : 0) * A.Pcap + off + kst_];
@@ -555,7 +591,15 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                     of |= real && x > 126;
                     w |= (real && x <= 126 ? (uint32_t)x : 127u) << (8 * u);
                 }
-                pb_st_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + d, w | vb1);
+                // (16 bytes per lane: a prober's NDW threads fill whole waves, so its 64 consecutive dwords of
+                // a wave go out as 16 dwordx4 write-through stores, ~6x cheaper per byte than dword ones)
+                static_assert(NDW % 64 == 0, "k_round_pb: a prober's row dwords fill whole waves");
+                const int src = (4 * lane) & 63;
+                const uint32_t wv = w | vb1;
+                const uint4 w4 = make_uint4((uint32_t)__shfl((int)wv, src), (uint32_t)__shfl((int)wv, src + 1),
+                                            (uint32_t)__shfl((int)wv, src + 2), (uint32_t)__shfl((int)wv, src + 3));
+                if (lane < 16)
+                    pb_st4_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + (d - lane) + 4 * lane, w4);
                 if (of) pof[kk] = 1;
             }
             PB_PROF(8);
@@ -566,6 +610,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 np1[x] = valid[x] && kstar[x] < lens[x] ? min(kPbP, lens[x] - kstar[x]) : 0;
                 if constexpr (kMerged) rb_load(rawn[x], offs[x], kstar[x], np1[x]);
             }
+            if constexpr (kPipe) rb_load(rawn[0], offs[0], kstar[0], np1[0]);
             PB_PROF(9);
         }
         // the S rows (DecideFame, hashgraph.go:688-705): bit j = the new candidate strongly sees
@@ -581,7 +626,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
             if (!nx || w >= A.nw) continue;   // (wave-uniform)
             const int jj = w * 64 + lane;
             const uint8_t k8 = jj < n ? kstp(k)[jj] : 0;
-            const uint64_t m = __ballot((k8 & 64) && ((k8 & 32) || (int)(k8 & 31) <= Bk));
+            const uint64_t m = __ballot((k8 & kPbCand) && ((k8 & kPbDone) || (int)(k8 & kPbKM) <= Bk));
             if (lane == 0) A.Smat[((size_t)(s + 1) * C + gc) * A.nw + w] = m;
         }
 #pragma unroll
@@ -602,13 +647,26 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 pof[k] = 0;   // (same thread: read before)
             }
         }
-        if (t >= 64 && t < 64 + PP * 32) ((int32_t*)(lds + K::O_HIST))[t - 64] = 0;
+        if (t >= 64 && t < 64 + PP * 64) ((int32_t*)(lds + K::O_HIST))[t - 64] = 0;
         if (t == 200) misc[2] = 0;
+        PB_PROF(10);
 #pragma unroll
         for (int k = 0; k < PP; k++) {
-            if constexpr (kMerged) rb_store(rawn[k], winp(k), np1[k], bpar(s));
-            else if (np1[k] > 0) rebase(winp(k), offs[k], kstar[k], np1[k], bpar(s));
+            if constexpr (kMerged) {
+                rb_store(rawn[k], winp(k), np1[k], bpar(s));
+            } else if constexpr (kPipe) {
+                if (kPipeBufs == 2) {
+                    if (k + 1 < PP) rb_load(rawn[(k + 1) % kPipeBufs], offs[k + 1], kstar[k + 1], np1[k + 1]);
+                    rb_store(rawn[k % kPipeBufs], winp(k), np1[k], bpar(s));
+                } else {
+                    if (k > 0) rb_load(rawn[0], offs[k], kstar[k], np1[k]);
+                    rb_store(rawn[0], winp(k), np1[k], bpar(s));
+                }
+            } else if (np1[k] > 0) {
+                rebase(winp(k), offs[k], kstar[k], np1[k], bpar(s));
+            }
             bs[k] = kstar[k];
+            PB_PROF(11 + k);
         }
         if (pfx == 0xFFFFFFFFu) misc[7] = 1;   // (the prefetch's use: never true, keeps the loads)
         pb_lds_barrier();
@@ -686,10 +744,10 @@ __global__ void k_round_pb_silent(RoundArgs A, int r_lo, int r_hi) {
 }
 
 namespace {
-template <typename CT, int HD>
+template <typename CT, int HD, int NP>
 hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus, bool init) {
-    typedef PbCfg<HD> K;
-    const void* f = (const void*)k_round_pb<CT, HD>;
+    typedef PbCfg<HD, NP> K;
+    const void* f = (const void*)k_round_pb<CT, HD, NP>;
     int per_cu = 0;
     hipError_t e = ensure_lds_limit(f, K::LDS);
     if (e == hipSuccess) e = blocks_per_cu(f, K::T, K::LDS, &per_cu);
@@ -702,7 +760,7 @@ hipError_t pb_launch(hipStream_t st, const RoundPbArgs& P, int num_cus, bool ini
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_round_pb<CT, HD>), dim3(nblk), dim3(K::T), K::LDS, st, P);
+    hipLaunchKernelGGL((k_round_pb<CT, HD, NP>), dim3(nblk), dim3(K::T), K::LDS, st, P);
     return hipGetLastError();
 }
 }  // namespace
@@ -726,11 +784,17 @@ hipError_t launch_round_pb(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, u
     // row dwords per lane by the chains with events (coordinate slots = 32 HD)
     if (na > 1024) return hipErrorInvalidValue;
     const int hd = na <= 512 ? 16 : na <= 768 ? 24 : 32;
+    // (63-probe windows where three fit the LDS with compact coordinates)
+#ifdef HGX_PB_NP31
     if (A.compact)
-        return hd == 16 ? pb_launch<uint16_t, 16>(st, P, num_cus, init)
-                        : hd == 24 ? pb_launch<uint16_t, 24>(st, P, num_cus, init) : pb_launch<uint16_t, 32>(st, P, num_cus, init);
-    return hd == 16 ? pb_launch<int32_t, 16>(st, P, num_cus, init)
-                    : hd == 24 ? pb_launch<int32_t, 24>(st, P, num_cus, init) : pb_launch<int32_t, 32>(st, P, num_cus, init);
+        return hd == 16 ? pb_launch<uint16_t, 16, 31>(st, P, num_cus, init)
+                        : hd == 24 ? pb_launch<uint16_t, 24, 31>(st, P, num_cus, init) : pb_launch<uint16_t, 32, 31>(st, P, num_cus, init);
+#endif
+    if (A.compact)
+        return hd == 16 ? pb_launch<uint16_t, 16, 63>(st, P, num_cus, init)
+                        : hd == 24 ? pb_launch<uint16_t, 24, 63>(st, P, num_cus, init) : pb_launch<uint16_t, 32, 31>(st, P, num_cus, init);
+    return hd == 16 ? pb_launch<int32_t, 16, 31>(st, P, num_cus, init)
+                    : hd == 24 ? pb_launch<int32_t, 24, 31>(st, P, num_cus, init) : pb_launch<int32_t, 32, 31>(st, P, num_cus, init);
 }
 
 void launch_round_pb_silent(hipStream_t st, const RoundArgs& A, int r_lo, int r_hi) {

@@ -38,6 +38,28 @@ def test_pb_matches_oracle(n, E, seed, silent, stale):
     _compare(h, hgref.oracle_run(t))
 
 
+@pytest.mark.parametrize("n,E,seed,spread", [(600, 12000, 151, "random"), (520, 12000, 152, "every7"),
+                                              (1024, 9000, 153, "every3")])
+def test_pb_silent_chains_between_active_ones(n, E, seed, spread):
+    """Silent peers spread over the chain order instead of a tail: the coordinate slots (the chains with
+    events) are then not one run of consecutive chains, so a window row's 16-byte slot groups fall back
+    to one gather per slot (every group for a random order, some groups for a regular spread). The
+    trace's creators are relabelled; the hashgraph is the same up to that relabelling."""
+    silent = n // 4 if spread == "random" else (n + 6) // 7 if spread == "every7" else (n + 2) // 3
+    t = gtrace.gossip(n, E, seed, n_silent=silent, stale_prob=0.2, stale_depth=3)
+    if spread == "random":
+        perm = np.random.default_rng(seed).permutation(n)
+    else:
+        step = 7 if spread == "every7" else 3
+        sil = [c for c in range(n) if c % step == 0][:silent]
+        act = [c for c in range(n) if c not in set(sil)]
+        perm = np.array(act + sil)   # active creator a -> chain act[a], silent ones -> every step-th chain
+    t.creator = perm[t.creator].astype(np.int32)
+    h = _run(t, mode="auto")
+    _check_pb(h)
+    _compare(h, hgref.oracle_run(t))
+
+
 @pytest.mark.parametrize("n,E,seed,silent", [(300, 60000, 111, 0), (600, 100000, 112, 0), (1024, 200000, 113, 341)])
 def test_pb_equals_per_launch_steps(n, E, seed, silent):
     """Round, witness and the strongly-see rows feeding fame: identical to the k_round_k steps."""

@@ -1,0 +1,18 @@
+# k_round_pb 63-probe windows (A/B: exp1 one row set, exp2 31-probe windows): probe, c5 lines, phases, tests
+set -o pipefail
+mkdir -p gpurun_out/r05
+O=gpurun_out/r05
+export TMPDIR=/tmp
+line() {
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels_per_pass']; p=d['config']['phase_ms_last_step']; print(sys.argv[2], 'ms/step %.2f' % d['ms_per_step'], 'rounds %.2f order %.2f coords %.2f' % (p['rounds_ms'], p['order_ms'], p['coords_ms']), 'rp', p['round_p_runs'], p['round_p_fallbacks'], {x: round(k[x]['ms'],3) for x in ('layout','order_sort','round_search')})" $1 $2
+}
+PYTHONPATH=. timeout -k 10 400 python -u tools/probe/pb_diff.py > $O/b8_diff.log 2>&1 || { tail -30 $O/b8_diff.log; exit 1; }
+grep -c "mismatch=0" $O/b8_diff.log
+for v in libhgx.so libhgx_exp1.so libhgx_exp2.so libhgx.so; do
+  HGX_LIB=$v timeout -k 10 300 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked > $O/b8_c5_$v.json 2> $O/b8_c5_$v.log || exit $?
+  line $O/b8_c5_$v.json c5_$v
+done
+HGX_LIB=libhgx_prof.so timeout -k 10 300 python -u tools/phase_timing.py c5 2 > $O/b8_ph_c5.log 2>&1 || { tail -20 $O/b8_ph_c5.log; exit 1; }
+grep -E "k_round_pb clk" $O/b8_ph_c5.log | tail -1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_round_pb.py -x -q --timeout 200 --timeout-method thread > $O/b8_tests.log 2>&1 || { tail -40 $O/b8_tests.log; exit 1; }
+tail -1 $O/b8_tests.log
