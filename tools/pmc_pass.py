@@ -19,9 +19,9 @@ from collections import defaultdict
 
 ROLES = {
     "layout": r"k_layout|k_ck_pack",
-    "la_sweep": r"k_la_sweep|k_la_wave|k_la_small",
+    "la_sweep": r"k_la_sweep|k_la_wave|k_la_small|k_la_seg",
     "fd_build": r"k_fd_build",
-    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin|k_round_p_post|k_round_p_tail|k_round_p_init|k_round_pb_silent",
+    "round_gather": r"k_round_gather|k_round_k_gather|k_wcoin|k_round_p_post|k_round_p_tail|k_round_p_init|k_round_pb_init|k_round_pb_silent",
     "round_search": r"k_round_k<|k_round_step|k_round_p<|k_round_pb<|k_round_g<",
     "fame": r"k_fame",
     "threshold": r"k_threshold|k_wla_transpose",
