@@ -293,14 +293,24 @@ DevArrays Engine::arrays() {
 // ---- per-kernel timing (only when time_kernels) ---------------------------------
 // count = launches the window covers (a hipGraph replay of round steps); sample = false
 // counts them without timing (a per-launch average from the timed sample: KernelStat.timed)
+// HGX_HOST_TIME_KERNELS=1 (diagnostic): every timed window also drained and timed by the host clock,
+// one stderr line per window (a cross-check of the HIP-event and profiler kernel times)
+static const bool g_host_time = getenv("HGX_HOST_TIME_KERNELS") != nullptr;
+static std::chrono::steady_clock::time_point g_host_t0;
+
 void Engine::kbeg(int k, bool sample, int64_t count) {
     kstat[k].launches += count;
     if (!((time_mask >> k) & 1u) || !sample) return;
+    if (g_host_time) {
+        (void)hipStreamSynchronize(stream);
+        g_host_t0 = std::chrono::steady_clock::now();
+    }
     while (kev.size() < kev_used + 2) {
         hipEvent_t e;
         // timing only (nothing on the host waits on them): no system-scope fences, so that the
         // events bracketing every round-step replay cost the timed region as little as possible
-        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return;
+        static const bool sysfence = getenv("HGX_EVENT_SYSFENCE") != nullptr;   // (A/B of the event flavour)
+        if (hipEventCreateWithFlags(&e, sysfence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess) return;
         kev.push_back(e);
     }
     (void)hipEventRecord(kev[kev_used], stream);
@@ -314,6 +324,13 @@ void Engine::kend(int k, double bytes) {
     Open& o = kopen.back();
     o.bytes = bytes;
     (void)hipEventRecord(kev[o.e0 + 1], stream);
+    if (g_host_time) {
+        (void)hipStreamSynchronize(stream);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_host_t0).count();
+        float ev = 0.f;
+        (void)hipEventElapsedTime(&ev, kev[o.e0], kev[o.e0 + 1]);
+        fprintf(stderr, "[hgx host-timed] kernel %d host %.4f ms events %.4f ms\n", k, ms, (double)ev);
+    }
 }
 
 // bytes known only after the launch completed (attributed to the last open launch of k)

@@ -13,7 +13,8 @@ for c in ${CFGS:-c3 c1 c2 c4 c5}; do
     cp gpurun_out/pmc_write_counters.csv gpurun_out/r05f/${c}_pmc_write_counters.csv
     cp gpurun_out/pmc_valu_counters_$c.csv gpurun_out/pmc_valu_stats_$c.csv gpurun_out/r05f/
     rm -rf /tmp/prof_c
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked > gpurun_out/r05f/${c}_prof.log 2>&1 || exit 1
+    # (no warm-up context: its calls would enter the per-kernel averages, 7 timed passes + 1 tiny call)
+    HGX_NO_WARMUP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-ingest --no-check --no-chunked > gpurun_out/r05f/${c}_prof.log 2>&1 || exit 1
     python3 tools/rocpd_export.py stats /tmp/prof_c/run_results.db gpurun_out/r05f/${c}_kernel_stats.csv || exit 1
     if [ "$c" = "c3" ]; then
         timeout -k 10 600 python3 -u bench.py > gpurun_out/r05f/c3_bench.json 2> gpurun_out/r05f/c3_bench.err || exit 1
