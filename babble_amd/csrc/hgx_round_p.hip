@@ -175,34 +175,47 @@ __device__ __forceinline__ uint32_t rp_ld_abort(const int32_t* p) {
 __device__ __forceinline__ void rp_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void rp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// A candidate's granule and this lane's HD dwords of its row, sc1 loads (every load of handed-off
-// bytes), issued AND waited for in ONE asm statement: an asm load's destination registers are
-// written when the data returns, so a load left in flight across compiler-visible code lets the
-// register allocator copy (or reuse) them before the data lands.
+// The rows' layout in a buffer, chunk-major: part q of candidate gc (HD dwords, what lane q of the
+// candidate compares) in chunks of CS = min(4, HD) dwords, chunk k of (gc, q) at ((k C + gc) Q + q) CS.
+// A poll instruction's 64 lanes (64 / Q candidates, chunk k of every part) then read one contiguous
+// 1 KB instead of 16-byte pieces of 16 rows (the request rate of the polls, k_round_pb's lesson);
+// HD <= 4 is plain row-major.
+__host__ __device__ constexpr int rp_q_of(int ndw) { return ndw == 2 || ndw == 8 ? 2 : 4; }
+__host__ __device__ constexpr size_t rp_chunk_off(int k, int gc, int q, int C, int Q, int CS) {
+    return (((size_t)k * C + gc) * Q + q) * CS;
+}
+
+// A candidate's granule and this lane's HD dwords of its row (chunk k at p + k cst dwords), sc1 loads
+// (every load of handed-off bytes), issued AND waited for in ONE asm statement: an asm load's
+// destination registers are written when the data returns, so a load left in flight across
+// compiler-visible code lets the register allocator copy (or reuse) them before the data lands.
 template <int HD>
-__device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p, uint64_t& gv, uint32_t (&v)[HD]) {
+__device__ __forceinline__ void rp_ld_cand(const uint64_t* gp, const uint32_t* p, size_t cst, uint64_t& gv,
+                                           uint32_t (&v)[HD]) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     if constexpr (HD == 16) {
         u32x4 a, b, c, d;
+        const uint32_t *p1 = p + cst, *p2 = p + 2 * cst, *p3 = p + 3 * cst;
         asm volatile(
             "global_load_dwordx2 %0, %5, off sc1\n\t"
             "global_load_dwordx4 %1, %6, off sc1\n\t"
-            "global_load_dwordx4 %2, %6, off offset:16 sc1\n\t"
-            "global_load_dwordx4 %3, %6, off offset:32 sc1\n\t"
-            "global_load_dwordx4 %4, %6, off offset:48 sc1\n\t"
+            "global_load_dwordx4 %2, %7, off sc1\n\t"
+            "global_load_dwordx4 %3, %8, off sc1\n\t"
+            "global_load_dwordx4 %4, %9, off sc1\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(p) : "memory");
+            : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(p), "v"(p1), "v"(p2), "v"(p3) : "memory");
         const u32x4 q4[4] = {a, b, c, d};
 #pragma unroll
         for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
     } else if constexpr (HD == 8) {
         u32x4 a, b;
+        const uint32_t* p1 = p + cst;
         asm volatile(
             "global_load_dwordx2 %0, %3, off sc1\n\t"
             "global_load_dwordx4 %1, %4, off sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:16 sc1\n\t"
+            "global_load_dwordx4 %2, %5, off sc1\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(gv), "=&v"(a), "=&v"(b) : "v"(gp), "v"(p) : "memory");
+            : "=&v"(gv), "=&v"(a), "=&v"(b) : "v"(gp), "v"(p), "v"(p1) : "memory");
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
     } else if constexpr (HD == 4) {
         u32x4 a;
@@ -320,7 +333,7 @@ struct RpCfg {
 
 struct RoundPArgs {
     RoundArgs A;
-    uint32_t* FD8p;     // [4][C][ndw] rebased candidate rows, row-major (round s: buffer s % 4, bit 7 of
+    uint32_t* FD8p;     // [4][C ndw] rebased candidate rows, chunk-major (rp_chunk_off; round s: buffer s % 4, bit 7 of
                         // every byte = v(s) = (s >> 2) & 1)
     uint64_t* gran;     // [kRpSlots][C]
     int32_t* st;        // [0] abort, [1] max over graphs of the round each stopped at, [2] graphs that
@@ -492,7 +505,14 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     rp_lds_barrier();   // the first window is rebased (every later round: the barrier ending (e))
     // the first poll's loads (each round issues the next round's)
     auto gran_at = [&](int r) { return P.gran + (size_t)(r % kRpSlots) * C + g0 + (jv ? j : 0); };
-    auto row_at = [&](int r) { return P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD; };
+    constexpr int CS = HD < 4 ? HD : 4;   // chunk dwords (rp_chunk_off)
+    static_assert(rp_q_of(NDW) == Q, "k_round_p: Q as rp_q_of");
+    const size_t cst = (size_t)C * Q * CS;   // chunk stride (dwords)
+    auto row_at = [&](int r) {
+        if constexpr (HD <= 4)   // (one chunk per part: the row-major address, as computed before the layout)
+            return P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD;
+        return P.FD8p + (size_t)(r & (kRoundPBufs - 1)) * C * NDW + rp_chunk_off(0, g0 + (jv ? j : 0), q, C, Q, CS);
+    };
     int s = P.r0;
     bool failed = false;
     int s_r = -1, s_k = 0;   // the round whose Bm / S row is still to be written (by wave 0, after the next barrier)
@@ -518,7 +538,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             // the youngest waves (last in the age order) would otherwise issue their loads last
             __builtin_amdgcn_s_setprio(3);
             for (int spins = 0;; spins++) {
-                if (!ok) rp_ld_cand<HD>(gp, rowp, gv, fd);   // (a lane whose candidate is complete keeps it)
+                if (!ok) rp_ld_cand<HD>(gp, rowp, cst, gv, fd);   // (a lane whose candidate is complete keeps it)
                 uint32_t bad = 0;
 #pragma unroll
                 for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
@@ -679,7 +699,11 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             bool of = false;
             if (nx) {
                 const uint32_t vb1 = (((s + 1) >> kRoundPShift) & 1) ? 0x80808080u : 0u;
-                const size_t roff = ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;
+                const size_t roff = ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW;   // (row-major: HD < 4)
+                // lane l's 16 bytes (dwords 4l .. 4l + 3): chunk (4l % HD) / 4 of part 4l / HD
+                const size_t boff = (size_t)((s + 1) & (kRoundPBufs - 1)) * C * NDW;
+                const size_t coff = HD > 4 ? boff + rp_chunk_off((4 * lane % HD) / 4, gc, 4 * lane / HD, C, Q, 4)
+                                           : roff + 4 * lane;   // (HD <= 4: row-major)
                 static_assert(NDW <= 64, "k_round_p: one row dword per lane of wave 0");
                 const int d = lane;
                 uint32_t w = 0;
@@ -706,12 +730,12 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     const uint4 w4 = rp_gather4(w);
                     if (lane < NDW / 4) {
                         if (!SH) {
-                            rp_st4_sc1(P.FD8p + roff + 4 * lane, w4);
+                            rp_st4_sc1(P.FD8p + coff, w4);
                         } else {
                             const RoundPWindows* __restrict__ Wd = P.Wd;
                             for (int wi = 0; wi < P.nwin; wi++) {
-                                if ((Wd->remote >> wi) & 1u) rp_st4_sys(Wd->FD8p[wi] + roff + 4 * lane, w4);
-                                else rp_st4_sc1(Wd->FD8p[wi] + roff + 4 * lane, w4);
+                                if ((Wd->remote >> wi) & 1u) rp_st4_sys(Wd->FD8p[wi] + coff, w4);
+                                else rp_st4_sc1(Wd->FD8p[wi] + coff, w4);
                             }
                         }
                     }
@@ -833,15 +857,17 @@ __global__ void __launch_bounds__(64) k_round_p_init(RoundPArgs P, int ndw) {
             w |= v << (8 * u);
         }
         // into every shard's window (write-through; the launches that read them start after this
-        // kernel has completed on every shard)
+        // kernel has completed on every shard), dword d at its place in the chunk-major layout
+        const int Q = rp_q_of(ndw), HD = ndw / Q, CS = HD < 4 ? HD : 4;
+        const size_t dof = rp_chunk_off((d % HD) / CS, gc, d / HD, C, Q, CS) + (d % HD) % CS;
         for (int wi = 0; wi < P.nwin; wi++) {
             const bool rem = P.nwin > 1 && ((P.Wd->remote >> wi) & 1u);
             uint32_t* fw = P.nwin > 1 ? P.Wd->FD8p[wi] : P.FD8p;
             const uint32_t v0 = w | ((((r >> kRoundPShift) & 1) ? 0x80808080u : 0u));
-            uint32_t* p0 = fw + ((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d;
+            uint32_t* p0 = fw + (size_t)(r & (kRoundPBufs - 1)) * C * ndw + dof;
             if (rem) rp_st_sys(p0, v0); else rp_st_sc1(p0, v0);
             for (int k = 1; k < kRoundPBufs; k++) {
-                uint32_t* pk = fw + ((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d;
+                uint32_t* pk = fw + (size_t)((r + k) & (kRoundPBufs - 1)) * C * ndw + dof;
                 const uint32_t vk = (((r + k) >> kRoundPShift) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu;   // bit 7 = !v(r + k)
                 if (rem) rp_st_sys(pk, vk); else rp_st_sc1(pk, vk);
             }
