@@ -1809,11 +1809,8 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
         const int s0 = st[i];
         const bool member = s0 != i || (i + 1 < len && st[i + 1] == i);
         if (member) {
-            const uint8_t* sp = g_S + (size_t)p_gid[sv[i]] * 32;
-            uint64_t v = 0;
-#pragma unroll
-            for (int b = 0; b < 8; b++) v = (v << 8) | sp[b];
-            sk[i] = v;
+            // (S rows are 32-byte aligned: the big-endian prefix is one 8-byte load, byte-swapped)
+            sk[i] = __builtin_bswap64(*(const uint64_t*)(g_S + (size_t)p_gid[sv[i]] * 32));
         }
     }
     sync();
@@ -1881,11 +1878,7 @@ __global__ void k_tie_prefix(int32_t m, const uint32_t* __restrict__ vals, const
     const uint64_t k = keys[i];
     const bool tie = (i > 0 && keys[i - 1] == k) || (i + 1 < m && keys[i + 1] == k);
     if (!tie) return;
-    const uint8_t* sp = g_S + (size_t)p_gid[vals[i]] * 32;
-    uint64_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 8; b++) v = (v << 8) | sp[b];
-    pre[i] = v;
+    pre[i] = __builtin_bswap64(*(const uint64_t*)(g_S + (size_t)p_gid[vals[i]] * 32));   // (big-endian prefix)
 }
 
 __global__ void k_tiefix_rank(int32_t m, const uint32_t* __restrict__ vals, uint32_t* __restrict__ out,
