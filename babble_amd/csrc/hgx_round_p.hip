@@ -102,9 +102,10 @@ void round_p_prof_dump() {
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(hgx_rp_prof), sizeof(h)) != hipSuccess) return;
     const double r = h[15] ? (double)h[15] : 1.0;
     fprintf(stderr, "[hgx] k_round_p clk per block-round (thread 0): poll %.0f bases+flags %.0f S row %.0f staging issue %.0f "
-            "search-levels %.0f drain+barrier %.0f scan %.0f publish..poll-issue %.0f | block-rounds %llu, synchronous "
-            "stagings %llu, later windows %llu\n",
-            h[1] / r, h[6] / r, h[7] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[5] / r, h[15], h[10], h[11]);
+            "search-levels %.0f drain+barrier %.0f scan %.0f publish %.0f slice %.0f end barrier %.0f | block-rounds %llu, "
+            "synchronous stagings %llu, later windows %llu\n",
+            h[1] / r, h[6] / r, h[7] / r, h[2] / r, h[13] / r, h[3] / r, h[4] / r, h[8] / r, h[9] / r, h[5] / r, h[15], h[10],
+            h[11]);
     unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(hgx_rp_prof), z, sizeof(z));
     if (const char* path = getenv("HGX_RP_TRACE_FILE")) {
@@ -767,6 +768,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             }
             if (of && lane == 0) atomicAdd(&P.st[3], 1);   // rows counted exactly (instrumentation)
         }
+        RP_PROF(8);
         if (NW == 1) {
             if (nx) rebase(kstar, np1, bs1, t, T);
         } else if (wave > 0) {
@@ -787,6 +789,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             s_k = kstar;
         }
         b = kstar;
+        RP_PROF(9);
         // the next window's rebase, the S-row slices and the publish are complete before any wave
         // polls: each wave then searches as soon as its own candidates arrived (no barrier between
         // the poll and the search; the histogram barrier joins the waves)

@@ -53,43 +53,61 @@ __device__ __forceinline__ uint32_t pb_ld_abort(const int32_t* p) {
 __device__ __forceinline__ void pb_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void pb_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// a candidate's granule and this lane's HD dwords of its row (sc1 loads, issued and waited for in one
-// asm statement: see rp_ld_cand, hgx_round_p.hip)
+// Candidate rows CHUNK-MAJOR (as k_round_p's rp_chunk_off): part q (HD dwords, lane q of the candidate)
+// of chain gc in 16-byte chunks, chunk k at ((k C + gc) Q + q) x 16 bytes of the round's buffer, so a poll
+// instruction's 64 lanes (8 candidates x 8 parts, chunk k of each) read one contiguous KB.
+__host__ __device__ constexpr size_t pb_chunk_off(int k, int gc, int q, int C) { return (((size_t)k * C + gc) * 8 + q) * 4; }
+
+// a wave-uniform pointer held in SGPRs (the base of a chunk's loads)
+__device__ __forceinline__ const uint32_t* pb_uniform(const uint32_t* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return (const uint32_t*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+}
+
+// a candidate's granule and this lane's HD dwords of its row: chunk k at sb + k cst (SGPR base, uniform)
+// + vo bytes (this lane's (gc, q) offset), sc1 loads issued and waited for in one asm statement (see
+// rp_ld_cand, hgx_round_p.hip)
 template <int HD>
-__device__ __forceinline__ void pb_ld_cand(const uint64_t* gp, const uint32_t* p, uint64_t& gv, uint32_t (&v)[HD]) {
+__device__ __forceinline__ void pb_ld_cand(const uint64_t* gp, const uint32_t* sb, size_t cst, uint32_t vo, uint64_t& gv,
+                                           uint32_t (&v)[HD]) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     static_assert(HD == 16 || HD == 24 || HD == 32, "pb_ld_cand: HD in {16, 24, 32}");
+    const uint32_t *s0 = pb_uniform(sb), *s1 = pb_uniform(sb + cst), *s2 = pb_uniform(sb + 2 * cst), *s3 = pb_uniform(sb + 3 * cst);
     u32x4 a, b, c, d;
     asm volatile(
         "global_load_dwordx2 %0, %5, off sc1\n\t"
-        "global_load_dwordx4 %1, %6, off sc1\n\t"
-        "global_load_dwordx4 %2, %6, off offset:16 sc1\n\t"
-        "global_load_dwordx4 %3, %6, off offset:32 sc1\n\t"
-        "global_load_dwordx4 %4, %6, off offset:48 sc1\n\t"
+        "global_load_dwordx4 %1, %6, %7 sc1\n\t"
+        "global_load_dwordx4 %2, %6, %8 sc1\n\t"
+        "global_load_dwordx4 %3, %6, %9 sc1\n\t"
+        "global_load_dwordx4 %4, %6, %10 sc1\n\t"
         "s_waitcnt vmcnt(0)"
-        : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(p) : "memory");
+        : "=&v"(gv), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(gp), "v"(vo), "s"(s0), "s"(s1), "s"(s2), "s"(s3) : "memory");
     const u32x4 q4[4] = {a, b, c, d};
 #pragma unroll
     for (int k = 0; k < 4; k++) { v[4 * k] = q4[k].x; v[4 * k + 1] = q4[k].y; v[4 * k + 2] = q4[k].z; v[4 * k + 3] = q4[k].w; }
     if constexpr (HD == 32) {
+        const uint32_t *s4 = pb_uniform(sb + 4 * cst), *s5 = pb_uniform(sb + 5 * cst), *s6 = pb_uniform(sb + 6 * cst),
+                       *s7 = pb_uniform(sb + 7 * cst);
         u32x4 e, f, g, h;
         asm volatile(
-            "global_load_dwordx4 %0, %4, off offset:64 sc1\n\t"
-            "global_load_dwordx4 %1, %4, off offset:80 sc1\n\t"
-            "global_load_dwordx4 %2, %4, off offset:96 sc1\n\t"
-            "global_load_dwordx4 %3, %4, off offset:112 sc1\n\t"
+            "global_load_dwordx4 %0, %4, %5 sc1\n\t"
+            "global_load_dwordx4 %1, %4, %6 sc1\n\t"
+            "global_load_dwordx4 %2, %4, %7 sc1\n\t"
+            "global_load_dwordx4 %3, %4, %8 sc1\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(e), "=&v"(f), "=&v"(g), "=&v"(h) : "v"(p) : "memory");
+            : "=&v"(e), "=&v"(f), "=&v"(g), "=&v"(h) : "v"(vo), "s"(s4), "s"(s5), "s"(s6), "s"(s7) : "memory");
         const u32x4 r4[4] = {e, f, g, h};
 #pragma unroll
         for (int k = 0; k < 4; k++) { v[16 + 4 * k] = r4[k].x; v[17 + 4 * k] = r4[k].y; v[18 + 4 * k] = r4[k].z; v[19 + 4 * k] = r4[k].w; }
     } else if constexpr (HD == 24) {
+        const uint32_t *s4 = pb_uniform(sb + 4 * cst), *s5 = pb_uniform(sb + 5 * cst);
         u32x4 e, f;
         asm volatile(
-            "global_load_dwordx4 %0, %2, off offset:64 sc1\n\t"
-            "global_load_dwordx4 %1, %2, off offset:80 sc1\n\t"
+            "global_load_dwordx4 %0, %2, %3 sc1\n\t"
+            "global_load_dwordx4 %1, %2, %4 sc1\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(e), "=&v"(f) : "v"(p) : "memory");
+            : "=&v"(e), "=&v"(f) : "v"(vo), "s"(s4), "s"(s5) : "memory");
         const u32x4 r4[2] = {e, f};
 #pragma unroll
         for (int k = 0; k < 2; k++) { v[16 + 4 * k] = r4[k].x; v[17 + 4 * k] = r4[k].y; v[18 + 4 * k] = r4[k].z; v[19 + 4 * k] = r4[k].w; }
@@ -392,11 +410,13 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 uint64_t gv = 0;
                 uint32_t fd[HD];
                 const uint64_t* gp = P.gran + (size_t)(s % kPbSlots) * C + (live ? j : 0);
-                const uint32_t* rowp = P.FD8p + ((size_t)(s & (kRoundPBufs - 1)) * C + (live ? j : 0)) * NDW + q * HD;
+                // (chunk-major: the buffer's base in SGPRs, this lane's (chain, part) offset in bytes)
+                const uint32_t* rsb = P.FD8p + (size_t)(s & (kRoundPBufs - 1)) * C * NDW;
+                const uint32_t rvo = (uint32_t)(pb_chunk_off(0, live ? j : 0, q, C) * 4);
                 // (a wave of this workgroup gave up: no further waits)
                 bool wfail = wfail_w || *(volatile int32_t*)&misc[3] != 0;
                 if (!wfail && __any(live)) {
-                    pb_ld_cand<HD>(gp, rowp, gv, fd);
+                    pb_ld_cand<HD>(gp, rsb, (size_t)C * 8 * 4, rvo, gv, fd);
                     uint32_t bad = 0;
 #pragma unroll
                     for (int d = 0; d < HD; d++) bad |= (fd[d] ^ vbit) & 0x80808080u;
@@ -599,7 +619,8 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
                 const uint4 w4 = make_uint4((uint32_t)__shfl((int)wv, src), (uint32_t)__shfl((int)wv, src + 1),
                                             (uint32_t)__shfl((int)wv, src + 2), (uint32_t)__shfl((int)wv, src + 3));
                 if (lane < 16)
-                    pb_st4_sc1(P.FD8p + ((size_t)((s + 1) & (kRoundPBufs - 1)) * C + gc) * NDW + (d - lane) + 4 * lane, w4);
+                    pb_st4_sc1(P.FD8p + (size_t)((s + 1) & (kRoundPBufs - 1)) * C * NDW +
+                                   pb_chunk_off(((d - lane + 4 * lane) % HD) / 4, gc, (d - lane + 4 * lane) / HD, C), w4);
                 if (of) pof[kk] = 1;
             }
             PB_PROF(8);
@@ -724,10 +745,13 @@ __global__ void __launch_bounds__(64) k_round_pb_init(RoundPbArgs P, int ndw) {
             }
             w |= v << (8 * u);
         }
-        pb_st_sc1(P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + gc) * ndw + d,
+        // (chunk-major, pb_chunk_off: dword d is dword (d % HD) % 4 of chunk (d % HD) / 4 of part d / HD)
+        const int hd = ndw / 8;
+        const size_t dof = pb_chunk_off((d % hd) / 4, gc, d / hd, C) + (d % hd) % 4;
+        pb_st_sc1(P.FD8p + (size_t)(r & (kRoundPBufs - 1)) * C * ndw + dof,
                   w | (((r >> kRoundPShift) & 1) ? 0x80808080u : 0u));
         for (int k = 1; k < kRoundPBufs; k++)
-            pb_st_sc1(P.FD8p + ((size_t)((r + k) & (kRoundPBufs - 1)) * C + gc) * ndw + d,
+            pb_st_sc1(P.FD8p + (size_t)((r + k) & (kRoundPBufs - 1)) * C * ndw + dof,
                       (((r + k) >> kRoundPShift) & 1) ? 0x7F7F7F7Fu : 0xFFFFFFFFu);   // bit 7 = !v(r + k)
     }
     of = __any(of);
