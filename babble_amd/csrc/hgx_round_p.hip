@@ -77,10 +77,13 @@ __device__ uint32_t hgx_rp_trace2[64 * 256 * 16 * 2];
             _p[0] = _tr0; _p[1] = _tr1; _p[2] = _tr2; _p[3] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
         }                                                                                        \
     } while (0)
+#ifndef HGX_PROF_T
+#define HGX_PROF_T 0   // the profiled thread (64: wave 1, a rebasing wave)
+#endif
 #define RP_PROF_BEGIN() long long _pt = clock64(); unsigned long long _pa[16] = {}
 #define RP_PROF(i)                                                \
     do {                                                          \
-        if (threadIdx.x == 0) {                                   \
+        if (threadIdx.x == HGX_PROF_T) {                          \
             const long long _t = clock64();                       \
             _pa[i] += (unsigned long long)(_t - _pt);             \
             _pt = _t;                                             \
@@ -89,11 +92,11 @@ __device__ uint32_t hgx_rp_trace2[64 * 256 * 16 * 2];
     } while (0)
 #define RP_PROF_COUNT(i)                                          \
     do {                                                          \
-        if (threadIdx.x == 0) _pa[i] += 1;                        \
+        if (threadIdx.x == HGX_PROF_T) _pa[i] += 1;               \
     } while (0)
 #define RP_PROF_END()                                                              \
     do {                                                                           \
-        if (threadIdx.x == 0)                                                      \
+        if (threadIdx.x == HGX_PROF_T)                                             \
             for (int _i = 0; _i < 16; _i++)                                        \
                 if (_pa[_i]) atomicAdd(&hgx_rp_prof[_i], _pa[_i]);                 \
     } while (0)
