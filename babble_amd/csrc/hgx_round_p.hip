@@ -487,17 +487,23 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     // round r's S row from the waves' slices (LDS buffer r & 1) and its Bm, by wave 0 after the
     // barrier that follows them
     constexpr int CPW = 64 / Q;   // candidates per wave
+    // (the output columns' addresses once, outside the loop: the kernel-argument reloads they took
+    // inside it sat on wave 0's path between its poll and its search)
+    int32_t* const bm_col = A.Bm + gc;
+    const int nw_s = A.nw;
+    uint64_t* const sm_row = A.Smat + (size_t)gc * nw_s;
+    const size_t sm_stride = (size_t)C * nw_s;
     auto s_row = [&](int r, int kst) {
-        if (lane == 0) A.Bm[(size_t)(r + 1) * C + gc] = kst;
+        if (lane == 0) bm_col[(size_t)(r + 1) * C] = kst;
         if (kst >= len) return;   // no new candidate: no S row
         const uint64_t* sl = (const uint64_t*)(lds + K::O_SL) + (r & 1) * NW;
         constexpr int WPW = 64 / CPW;   // waves per 64-bit word
-        if (lane < A.nw) {
+        if (lane < nw_s) {
             uint64_t w = 0;
 #pragma unroll
             for (int k = 0; k < WPW; k++)
                 if (lane * WPW + k < NW) w |= sl[lane * WPW + k] << (k * CPW);
-            A.Smat[((size_t)(r + 1) * C + gc) * A.nw + lane] = w;
+            sm_row[(size_t)(r + 1) * sm_stride + lane] = w;
         }
     };
     RP_PROF_BEGIN();
