@@ -514,15 +514,17 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
     if (b < len) rebase(b, min(kRpP, len - b), bases(P.r0 - 1), t, T);
     rp_lds_barrier();   // the first window is rebased (every later round: the barrier ending (e))
     // the first poll's loads (each round issues the next round's)
-    auto gran_at = [&](int r) { return P.gran + (size_t)(r % kRpSlots) * C + g0 + (jv ? j : 0); };
+    // (this lane's poll addresses and the publish's bases once, outside the loop: see bm_col)
     constexpr int CS = HD < 4 ? HD : 4;   // chunk dwords (rp_chunk_off)
     static_assert(rp_q_of(NDW) == Q, "k_round_p: Q as rp_q_of");
     const size_t cst = (size_t)C * Q * CS;   // chunk stride (dwords)
-    auto row_at = [&](int r) {
-        if constexpr (HD <= 4)   // (one chunk per part: the row-major address, as computed before the layout)
-            return P.FD8p + ((size_t)(r & (kRoundPBufs - 1)) * C + g0 + (jv ? j : 0)) * NDW + q * HD;
-        return P.FD8p + (size_t)(r & (kRoundPBufs - 1)) * C * NDW + rp_chunk_off(0, g0 + (jv ? j : 0), q, C, Q, CS);
-    };
+    const uint64_t* const gran_lane = P.gran + g0 + (jv ? j : 0);
+    const uint32_t* const row_lane =
+        P.FD8p + (HD <= 4 ? (size_t)(g0 + (jv ? j : 0)) * NDW + q * HD : rp_chunk_off(0, g0 + (jv ? j : 0), q, C, Q, CS));
+    uint32_t* const fd8_out = P.FD8p;
+    uint64_t* const gran_out = P.gran + gc;
+    auto gran_at = [&](int r) { return gran_lane + (size_t)(r % kRpSlots) * C; };
+    auto row_at = [&](int r) { return row_lane + (size_t)(r & (kRoundPBufs - 1)) * C * NDW; };
     int s = P.r0;
     bool failed = false;
     int s_r = -1, s_k = 0;   // the round whose Bm / S row is still to be written (by wave 0, after the next barrier)
@@ -740,7 +742,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     const uint4 w4 = rp_gather4(w);
                     if (lane < NDW / 4) {
                         if (!SH) {
-                            rp_st4_sc1(P.FD8p + coff, w4);
+                            rp_st4_sc1(fd8_out + coff, w4);
                         } else {
                             const RoundPWindows* __restrict__ Wd = P.Wd;
                             for (int wi = 0; wi < P.nwin; wi++) {
@@ -751,7 +753,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                     }
                 } else if (d < NDW) {
                     if (!SH) {
-                        rp_st_sc1(P.FD8p + roff + d, w);
+                        rp_st_sc1(fd8_out + roff + d, w);
                     } else {
                         const RoundPWindows* __restrict__ Wd = P.Wd;
                         for (int wi = 0; wi < P.nwin; wi++) {
@@ -766,7 +768,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 const uint64_t gw = ((uint64_t)(uint32_t)(s + 2) << 32) | (uint32_t)kstar | (nx ? kRpEx : 0u) | (of ? kRpOv : 0u);
                 const size_t go = (size_t)((s + 1) % kRpSlots) * C + gc;
                 if (!SH) {
-                    rp_st_gran(P.gran + go, gw);
+                    rp_st_gran(gran_out + (go - gc), gw);
                 } else {
                     const RoundPWindows* __restrict__ Wd = P.Wd;
                     for (int wi = 0; wi < P.nwin; wi++) {
