@@ -548,7 +548,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             bool ok = false;
             // the poll at the top priority: the waves whose candidates arrived search meanwhile, and
             // the youngest waves (last in the age order) would otherwise issue their loads last
+#ifndef HGX_RP_NOPOLLPRIO
             __builtin_amdgcn_s_setprio(3);
+#endif
             for (int spins = 0;; spins++) {
                 if (!ok) rp_ld_cand<HD>(gp, rowp, cst, gv, fd);   // (a lane whose candidate is complete keeps it)
                 uint32_t bad = 0;
@@ -613,7 +615,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         // histogram barrier: the younger half searches at a higher priority (c3 rounds 22.9 ->
         // 21.2 ms; graded priorities by age measured the same, priority kept through the publish
         // and the poll 7x slower)
+#ifndef HGX_RP_NOPRIO
         if (NW >= 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(2);
+#endif
         for (;;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
@@ -649,7 +653,9 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 }
             }
             const int Kw = lo;
+#ifndef HGX_RP_NOPRIO
             if (NW >= 8) __builtin_amdgcn_s_setprio(0);
+#endif
             RP_PROF(13);
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
             // (d) the histogram is complete (and the staging issued in round s - 1 has landed: the
