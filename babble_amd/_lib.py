@@ -40,6 +40,13 @@ class hgx_events32(C.Structure):
                 ("creator", "index", "self_parent", "other_parent", "timestamp_ns", "coin", "sig_s", "ntx")]
 
 
+class hgx_events_packed(C.Structure):
+    _fields_ = [(nm, C.c_void_p) for nm in ("creator", "index", "self_parent_back", "other_parent_back")] + \
+               [("n_exc", C.c_int64)] + \
+               [(nm, C.c_void_p) for nm in ("exc_pos", "exc_self_parent", "exc_other_parent", "timestamp_ns", "coin",
+                                            "sig_s", "ntx")]
+
+
 class hgx_wire_events(C.Structure):
     _fields_ = [(nm, C.c_void_p) for nm in
                 ("creator_id", "index", "self_parent_index", "other_parent_creator", "other_parent_index",
@@ -106,6 +113,10 @@ def lib():
     _sig(L, "hgx_insert_and_run", i32, [p, C.POINTER(hgx_events), i64, C.POINTER(C.c_int64), E])
     for nm in ("hgx_insert_events32", "hgx_insert_and_run32"):
         _sig(L, nm, i32, [p, C.POINTER(hgx_events32), i64, C.POINTER(C.c_int64), E])
+    for nm in ("hgx_insert_events_packed", "hgx_insert_and_run_packed"):
+        _sig(L, nm, i32, [p, C.POINTER(hgx_events_packed), i64, C.POINTER(C.c_int64), E])
+    _sig(L, "hgx_pack_events32", i32, [C.POINTER(hgx_events32), i64, i64, p, p, p, p, p, p, i64,
+                                       C.POINTER(C.c_int64), E])
     _sig(L, "hgx_set_participant_keys", i32, [p, p, E])
     for nm in ("hgx_insert_events_verified", "hgx_insert_events_verified_device"):
         _sig(L, nm, i32, [p, C.POINTER(hgx_events), p, p, i64, C.POINTER(C.c_int64), E])

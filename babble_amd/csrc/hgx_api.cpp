@@ -594,6 +594,49 @@ int32_t hgx_insert_events32(hgx_ctx* c, const hgx_events32* ev, int64_t count, i
     return insert_events32_one(c, ev, count, n_inserted, err);
 }
 
+// the rest of a compact-payload insert_and_run once the structure is committed and the payload copy
+// started (hgx_insert_and_run32 / _packed): DivideRounds beside the copy, then DecideFame, FindOrder
+static int32_t run_after_split32(hgx_ctx* c, int64_t E0, hgx::InsertOut& out, int64_t* n_inserted, hgx_error* err,
+                                 const char* who) {
+    hipError_t e;
+    // S lands last (FindOrder's sort waits for it); on every way out the caller's S buffer has been
+    // read completely
+    struct WaitS {
+        hgx::Engine& eng;
+        ~WaitS() { (void)eng.payload_wait_S(); }
+    } wait_s{c->eng};
+    hgx::InsertOut head = out;
+    head.graph_loaded.assign(c->g_loaded.begin(), c->g_loaded.end());
+    hgx_error ins_err{};
+    const int32_t ins_rc = finish_insert(c, head, n_inserted, &ins_err);
+    int32_t rc = ins_rc ? ins_rc : hgx_divide_rounds(c, err);
+    const bool laid_out = ins_rc == 0 && rc == 0;
+    std::vector<uint64_t> loaded;
+    e = c->eng.payload_end(E0, out.accepted, laid_out, c->rh.r_lo, loaded);
+    if (e != hipSuccess) return dev_err(err, e, who);
+    for (int g = 0; g < c->G; g++) {
+        const int64_t l = (int64_t)loaded[g];
+        c->gs[g].pending_loaded += l - c->g_loaded[g];
+        c->g_loaded[g] = l;
+    }
+    c->mirror_ok = false;
+    if (ins_rc) {
+        if (err) *err = ins_err;
+        return ins_rc;
+    }
+    if (rc) return rc;
+    rc = hgx_decide_fame(c, err);
+    if (rc) return rc;
+    rc = hgx_find_order(c, err);
+    if (rc) return rc;
+    // the S copy's outcome is reported here (FindOrder waits for it only when it sorts; a skipped
+    // FindOrder would leave a failed copy unnoticed and g_S stale for a later tie-break); the
+    // guard's wait stays for the early ways out
+    e = c->eng.payload_wait_S();
+    if (e != hipSuccess) return dev_err(err, e, who);
+    return ok(err);
+}
+
 // hgx_insert_and_run with the compact columns: the structure columns (16 bytes per event) are
 // validated and committed first, the payload (45 bytes) copied beside DivideRounds
 int32_t hgx_insert_and_run32(hgx_ctx* c, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err) {
@@ -614,41 +657,127 @@ int32_t hgx_insert_and_run32(hgx_ctx* c, const hgx_events32* ev, int64_t count, 
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
     e = c->eng.payload_begin32(ev->timestamp_ns, ev->coin, ev->sig_s, ev->ntx, out.accepted);
     if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
-    // S lands last (FindOrder's sort waits for it); on every way out the caller's S buffer has been
-    // read completely
-    struct WaitS {
-        hgx::Engine& eng;
-        ~WaitS() { (void)eng.payload_wait_S(); }
-    } wait_s{c->eng};
-    hgx::InsertOut head = out;
-    head.graph_loaded.assign(c->g_loaded.begin(), c->g_loaded.end());
-    hgx_error ins_err{};
-    const int32_t ins_rc = finish_insert(c, head, n_inserted, &ins_err);
-    int32_t rc = ins_rc ? ins_rc : hgx_divide_rounds(c, err);
-    const bool laid_out = ins_rc == 0 && rc == 0;
-    std::vector<uint64_t> loaded;
-    e = c->eng.payload_end(E0, out.accepted, laid_out, c->rh.r_lo, loaded);
-    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
-    for (int g = 0; g < c->G; g++) {
-        const int64_t l = (int64_t)loaded[g];
-        c->gs[g].pending_loaded += l - c->g_loaded[g];
-        c->g_loaded[g] = l;
+    return run_after_split32(c, E0, out, n_inserted, err, "hgx_insert_and_run32");
+}
+
+// ---- hgx_events_packed (include/hgx.h): 10-byte structure columns, decoded on the device ----
+static bool bad_packed(const hgx_events_packed* ev, int64_t count) {
+    if (!ev || count < 0) return true;
+    if (count == 0) return false;
+    if (!ev->creator || !ev->index || !ev->self_parent_back || !ev->other_parent_back || !ev->timestamp_ns ||
+        !ev->coin || !ev->sig_s || !ev->ntx || ev->n_exc < 0 || ev->n_exc > count)
+        return true;
+    if (ev->n_exc == 0) return false;
+    if (!ev->exc_pos || !ev->exc_self_parent || !ev->exc_other_parent) return true;
+    // the device scatters the exceptions unchecked: positions in the batch and distinct
+    std::vector<int64_t> p(ev->exc_pos, ev->exc_pos + ev->n_exc);
+    std::sort(p.begin(), p.end());
+    return p.front() < 0 || p.back() >= count || std::adjacent_find(p.begin(), p.end()) != p.end();
+}
+
+static hgx::Engine::Packed packed_of(const hgx_events_packed* ev) {
+    return hgx::Engine::Packed{ev->creator, ev->index, ev->self_parent_back, ev->other_parent_back,
+                               ev->n_exc, ev->exc_pos, ev->exc_self_parent, ev->exc_other_parent};
+}
+
+static int32_t insert_events_packed_one(hgx_ctx* c, const hgx_events_packed* ev, int64_t count, int64_t* n_inserted,
+                                        hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (c->rooted) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events_packed: a reset context checks Root.Others by event id: use hgx_insert_events");
+        return HGX_ERR_INVALID;
     }
-    c->mirror_ok = false;
-    if (ins_rc) {
-        if (err) *err = ins_err;
-        return ins_rc;
+    DeviceGuard dg(c);
+    hgx::InsertIn in{};
+    if (count > 0) {
+        hipError_t e = c->eng.stage_packed(packed_of(ev), count, in, ev->timestamp_ns, ev->coin, ev->sig_s, ev->ntx);
+        if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events_packed");
     }
-    if (rc) return rc;
-    rc = hgx_decide_fame(c, err);
-    if (rc) return rc;
-    rc = hgx_find_order(c, err);
-    if (rc) return rc;
-    // the S copy's outcome is reported here (FindOrder waits for it only when it sorts; a skipped
-    // FindOrder would leave a failed copy unnoticed and g_S stale for a later tie-break); the
-    // guard's wait stays for the early ways out
-    e = c->eng.payload_wait_S();
-    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run32");
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert(in, count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_events_packed");
+    return finish_insert(c, out, n_inserted, err);
+}
+
+int32_t hgx_insert_events_packed(hgx_ctx* c, const hgx_events_packed* ev, int64_t count, int64_t* n_inserted,
+                                 hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || bad_packed(ev, count)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_events_packed: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (c->grp)
+        return on_shards(c, err, [&](hgx_ctx* x, hgx_error* e) {
+            return insert_events_packed_one(x, ev, count, x == c ? n_inserted : nullptr, e);
+        });
+    return insert_events_packed_one(c, ev, count, n_inserted, err);
+}
+
+// hgx_insert_and_run32 with the packed structure columns: 10 bytes per event staged, decoded and
+// validated before DivideRounds, the payload (45 bytes) copied beside it as in hgx_insert_and_run32
+int32_t hgx_insert_and_run_packed(hgx_ctx* c, const hgx_events_packed* ev, int64_t count, int64_t* n_inserted,
+                                  hgx_error* err) {
+    if (n_inserted) *n_inserted = 0;
+    if (!c || bad_packed(ev, count)) {
+        set_err(err, HGX_ERR_INVALID, "hgx_insert_and_run_packed: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    if (count < 65536 || c->rooted || c->shard_world > 1) {
+        int32_t rc = hgx_insert_events_packed(c, ev, count, n_inserted, err);
+        if (rc) return rc;
+        return hgx_run_consensus(c, err);
+    }
+    DeviceGuard dg(c);
+    const int64_t E0 = c->eng.E;
+    hgx::InsertOut out;
+    hipError_t e = c->eng.insert_split_begin_packed(packed_of(ev), count, out);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run_packed");
+    e = c->eng.payload_begin32(ev->timestamp_ns, ev->coin, ev->sig_s, ev->ntx, out.accepted);
+    if (e != hipSuccess) return dev_err(err, e, "hgx_insert_and_run_packed");
+    return run_after_split32(c, E0, out, n_inserted, err, "hgx_insert_and_run_packed");
+}
+
+int32_t hgx_pack_events32(const hgx_events32* ev, int64_t count, int64_t base, uint16_t* creator16, uint16_t* sp_back,
+                          uint16_t* op_back, int64_t* exc_pos, int32_t* exc_sp, int32_t* exc_op, int64_t exc_cap,
+                          int64_t* n_exc, hgx_error* err) {
+    if (n_exc) *n_exc = 0;
+    if (bad_events32(ev, count) || base < 0 || exc_cap < 0 || !n_exc ||
+        (count > 0 && (!creator16 || !sp_back || !op_back)) || (exc_cap > 0 && (!exc_pos || !exc_sp || !exc_op))) {
+        set_err(err, HGX_ERR_INVALID, "hgx_pack_events32: bad arguments");
+        return HGX_ERR_INVALID;
+    }
+    // a parent's distance back from gid g, or the escape (a parent the form cannot hold: later than
+    // g, more than 65 534 back, or a negative value other than "")
+    auto back = [](int64_t p, int64_t g) -> uint32_t {
+        if (p == -1) return 0;
+        return p >= 0 && p < g && g - p < HGX_PARENT_ESCAPE ? (uint32_t)(g - p) : (uint32_t)HGX_PARENT_ESCAPE;
+    };
+    int64_t x = 0;
+    for (int64_t k = 0; k < count; k++) {
+        const int32_t cr = ev->creator[k];
+        if (cr < 0 || cr > 0xFFFF) {
+            set_err(err, HGX_ERR_INVALID, "hgx_pack_events32: creator outside 0..65535");
+            return HGX_ERR_INVALID;
+        }
+        const int64_t g = base + k;
+        const uint32_t s = back(ev->self_parent[k], g), o = back(ev->other_parent[k], g);
+        creator16[k] = (uint16_t)cr;
+        sp_back[k] = (uint16_t)s;
+        op_back[k] = (uint16_t)o;
+        if (s == HGX_PARENT_ESCAPE || o == HGX_PARENT_ESCAPE) {
+            if (x < exc_cap) {
+                exc_pos[x] = k;
+                exc_sp[x] = ev->self_parent[k];
+                exc_op[x] = ev->other_parent[k];
+            }
+            x++;
+        }
+    }
+    *n_exc = x;
+    if (x > exc_cap) {
+        set_err(err, HGX_ERR_INVALID, "hgx_pack_events32: exception list full");
+        return HGX_ERR_INVALID;
+    }
     return ok(err);
 }
 

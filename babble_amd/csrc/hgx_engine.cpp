@@ -627,6 +627,44 @@ hipError_t Engine::insert_split_begin32(const int32_t* creator, const int32_t* i
     return insert_impl(in, count, out, nullptr, kCommitStructure);
 }
 
+hipError_t Engine::stage_packed(const Packed& pk, int64_t count, InsertIn& in, const int64_t* ts, const uint8_t* coin,
+                                const uint8_t* S, const int32_t* ntx) {
+    const size_t c = (size_t)count, x = (size_t)pk.n_exc;
+    in = InsertIn{};
+    HGX_TRY(stage_col(st_c16, pk.creator, c, 1, stream));
+    HGX_TRY(stage_col(st_index32, pk.index, c, 1, stream));
+    HGX_TRY(stage_col(st_spb, pk.spb, c, 1, stream));
+    HGX_TRY(stage_col(st_opb, pk.opb, c, 1, stream));
+    if (st_creator.n < c) HGX_TRY(st_creator.alloc(c));
+    if (st_sp32.n < c) HGX_TRY(st_sp32.alloc(c));
+    if (st_op32.n < c) HGX_TRY(st_op32.alloc(c));
+    if (x) {
+        HGX_TRY(stage_col(st_exc_pos, pk.exc_pos, x, 1, stream));
+        HGX_TRY(stage_col(st_exc_sp, pk.exc_sp, x, 1, stream));
+        HGX_TRY(stage_col(st_exc_op, pk.exc_op, x, 1, stream));
+    }
+    launch_unpack_packed(stream, count, E, st_c16.p, st_spb.p, st_opb.p, pk.n_exc, st_exc_pos.p, st_exc_sp.p,
+                         st_exc_op.p, st_creator.p, st_sp32.p, st_op32.p);
+    HGX_TRY(hipGetLastError());
+    in.creator = st_creator.p; in.index32 = st_index32.p; in.sp32 = st_sp32.p; in.op32 = st_op32.p;
+    if (ts) {
+        HGX_TRY(stage_col(st_ts, ts, c, 1, stream));
+        HGX_TRY(stage_col(st_coin, coin, c, 1, stream));
+        HGX_TRY(stage_col(st_S, S, c, 32, stream));
+        HGX_TRY(stage_col(st_ntx, ntx, c, 1, stream));
+        in.ts = st_ts.p; in.coin = st_coin.p; in.S = st_S.p; in.ntx = st_ntx.p;
+        if (count > 0) ids_known = false;
+    }
+    return hipSuccess;
+}
+
+hipError_t Engine::insert_split_begin_packed(const Packed& pk, int64_t count, InsertOut& out) {
+    InsertIn in;
+    HGX_TRY(stage_packed(pk, count, in));   // (no payload yet)
+    split32 = true;
+    return insert_impl(in, count, out, nullptr, kCommitStructure);
+}
+
 hipError_t Engine::payload_begin32(const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx,
                                    int64_t m_ok) {
     if (!stream2) {

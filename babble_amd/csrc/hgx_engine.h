@@ -161,6 +161,22 @@ class Engine {
     hipError_t insert_split_begin32(const int32_t* creator, const int32_t* index, const int32_t* sp, const int32_t* op,
                                     int64_t count, InsertOut& out);
     hipError_t payload_begin32(const int64_t* ts, const uint8_t* coin, const uint8_t* S, const int32_t* ntx, int64_t m_ok);
+    // hgx_events_packed's structure columns (10 bytes per event) copied to HBM and decoded into
+    // the hgx_events32 staging columns (launch_unpack_packed); exceptions already checked
+    struct Packed {
+        const uint16_t* creator;
+        const int32_t* index;
+        const uint16_t* spb;
+        const uint16_t* opb;
+        int64_t n_exc;
+        const int64_t* exc_pos;
+        const int32_t* exc_sp;
+        const int32_t* exc_op;
+    };
+    // (with the payload columns when ts is not null: hgx_insert_events_packed)
+    hipError_t stage_packed(const Packed& pk, int64_t count, InsertIn& in, const int64_t* ts = nullptr,
+                            const uint8_t* coin = nullptr, const uint8_t* S = nullptr, const int32_t* ntx = nullptr);
+    hipError_t insert_split_begin_packed(const Packed& pk, int64_t count, InsertOut& out);
     // forget every event (a fresh NewHashgraph); allocations are kept
     hipError_t clear();
     // per-event columns (gid order) for the host-side getters
@@ -318,6 +334,9 @@ class Engine {
     DBuf<int64_t> st_index, st_sp, st_op, st_ts;
     DBuf<uint8_t> st_hash, st_S, st_dig, st_r;
     DBuf<int32_t> st_index32, st_sp32, st_op32;   // hgx_events32 columns
+    DBuf<uint16_t> st_c16, st_spb, st_opb;        // hgx_events_packed columns
+    DBuf<int64_t> st_exc_pos;
+    DBuf<int32_t> st_exc_sp, st_exc_op;
     DBuf<uint8_t> st_coin;
     // batches of at most kPackEvents from host memory: the columns packed in one pinned buffer,
     // one H2D copy into st_pack

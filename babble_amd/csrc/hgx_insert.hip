@@ -331,4 +331,58 @@ void launch_insert_unclaim(hipStream_t s, int64_t m, const unsigned long long* f
         hipLaunchKernelGGL(k_insert_unclaim, dim3(nblocks(m)), dim3(256), 0, s, m, fail, fail_sig, E0, cap, C, in, st);
 }
 
+// hgx_events_packed's structure columns decoded into the hgx_events32 form (include/hgx.h): a parent
+// d back from the event's gid E0 + k, 0 = "", kEscape = its exception entry (k_unpack_exc, launched
+// after this on the same stream; without one it reads as HGX_UNKNOWN_PARENT). Two events per thread:
+// 4-byte loads of the u16 columns, 8-byte stores.
+constexpr int kEscape = 0xFFFF;
+constexpr int kUnknownParent = -2;
+
+__device__ __forceinline__ int32_t unpack_parent(uint32_t d, int64_t gid) {
+    return d == 0 ? -1 : d == (uint32_t)kEscape ? kUnknownParent : (int32_t)(gid - (int64_t)d);
+}
+
+__global__ void __launch_bounds__(256) k_unpack_packed(int64_t m, int64_t E0, const uint16_t* __restrict__ c16,
+                                                       const uint16_t* __restrict__ spb,
+                                                       const uint16_t* __restrict__ opb, int32_t* __restrict__ cr,
+                                                       int32_t* __restrict__ sp, int32_t* __restrict__ op) {
+    const int64_t pairs = (m + 1) / 2;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < pairs; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = 2 * t;
+        if (k + 1 < m) {   // (the staging buffers are 256-byte aligned: k even keeps both loads aligned)
+            const uint32_t c = *(const uint32_t*)(c16 + k), s = *(const uint32_t*)(spb + k),
+                           o = *(const uint32_t*)(opb + k);
+            const int64_t g = E0 + k;
+            *(int2*)(cr + k) = make_int2((int)(c & 0xFFFF), (int)(c >> 16));
+            *(int2*)(sp + k) = make_int2(unpack_parent(s & 0xFFFF, g), unpack_parent(s >> 16, g + 1));
+            *(int2*)(op + k) = make_int2(unpack_parent(o & 0xFFFF, g), unpack_parent(o >> 16, g + 1));
+        } else {
+            cr[k] = c16[k];
+            sp[k] = unpack_parent(spb[k], E0 + k);
+            op[k] = unpack_parent(opb[k], E0 + k);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_unpack_exc(int64_t n_exc, const int64_t* __restrict__ pos,
+                                                    const int32_t* __restrict__ esp, const int32_t* __restrict__ eop,
+                                                    int32_t* __restrict__ sp, int32_t* __restrict__ op) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_exc) {   // (positions checked on the host: in the batch and distinct)
+        sp[pos[j]] = esp[j];
+        op[pos[j]] = eop[j];
+    }
+}
+
+void launch_unpack_packed(hipStream_t s, int64_t m, int64_t E0, const uint16_t* c16, const uint16_t* spb,
+                          const uint16_t* opb, int64_t n_exc, const int64_t* exc_pos, const int32_t* exc_sp,
+                          const int32_t* exc_op, int32_t* cr, int32_t* sp, int32_t* op) {
+    if (m <= 0) return;
+    const int64_t pairs = (m + 1) / 2;
+    const unsigned grid = nblocks(pairs) < 8192u ? nblocks(pairs) : 8192u;
+    hipLaunchKernelGGL(k_unpack_packed, dim3(grid), dim3(256), 0, s, m, E0, c16, spb, opb, cr, sp, op);
+    if (n_exc > 0)
+        hipLaunchKernelGGL(k_unpack_exc, dim3(nblocks(n_exc)), dim3(256), 0, s, n_exc, exc_pos, exc_sp, exc_op, sp, op);
+}
+
 }  // namespace hgx

@@ -330,5 +330,9 @@ bool launch_insert_fused(hipStream_t s, int64_t m, const unsigned long long* fai
 // verify results vout[k] (1 valid, 0 invalid, 2 key not a point) -> *fail = min (k << 8 | code)
 void launch_insert_sig_first(hipStream_t s, int64_t m, int C, const int32_t* creator, const uint8_t* vout,
                              unsigned long long* fail);
+// hgx_events_packed -> the hgx_events32 creator / parent columns (cr, sp, op: m entries each)
+void launch_unpack_packed(hipStream_t s, int64_t m, int64_t E0, const uint16_t* c16, const uint16_t* spb,
+                          const uint16_t* opb, int64_t n_exc, const int64_t* exc_pos, const int32_t* exc_sp,
+                          const int32_t* exc_op, int32_t* cr, int32_t* sp, int32_t* op);
 
 }  // namespace hgx

@@ -34,6 +34,39 @@ def compact_columns(t) -> dict:
                 s=np.ascontiguousarray(t.s, np.uint8), ntx=ntx)
 
 
+def pack_columns(cols: dict, base: int) -> dict:
+    """hgx_events_packed columns (include/hgx.h) of compact_columns() whose first event gets gid
+    `base` (hgx_num_events of the context it goes into): creator as u16, each parent as its
+    distance back (0 = "", 0xFFFF = the exception list), built by libhgx's hgx_pack_events32. The
+    payload columns are shared with `cols`."""
+    L = _lib.lib()
+    m = len(cols["creator"])
+    _, ev = _events32_of(cols, 0, m)
+    out = dict(creator16=np.empty(m, np.uint16), sp_back=np.empty(m, np.uint16), op_back=np.empty(m, np.uint16))
+    cap = max(16, m // 64)
+    while True:
+        x = dict(exc_pos=np.empty(cap, np.int64), exc_sp=np.empty(cap, np.int32), exc_op=np.empty(cap, np.int32))
+        n_exc = C.c_int64(0)
+        err = hgx_error()
+        rc = L.hgx_pack_events32(C.byref(ev), m, base, ptr(out["creator16"]), ptr(out["sp_back"]),
+                                 ptr(out["op_back"]), ptr(x["exc_pos"]), ptr(x["exc_sp"]), ptr(x["exc_op"]), cap,
+                                 C.byref(n_exc), C.byref(err))
+        if rc == 0:
+            break
+        if n_exc.value <= cap:
+            _lib.check(rc, err)
+        cap = n_exc.value
+    k = n_exc.value
+    out.update({nm: np.ascontiguousarray(v[:k]) for nm, v in x.items()})
+    out.update(index=cols["index"], ts=cols["ts"], coin=cols["coin"], s=cols["s"], ntx=cols["ntx"])
+    return out
+
+
+def _events32_of(cols: dict, lo: int, hi: int):
+    a = {k: v[lo:hi] for k, v in cols.items()}
+    return a, _lib.hgx_events32(*[ptr(a[k]) for k in ("creator", "index", "sp", "op", "ts", "coin", "s", "ntx")])
+
+
 class Hashgraph:
     """One context = NewHashgraph(participants, NewInmemStore(participants, cap)) (hashgraph.go:39-66).
 
@@ -200,8 +233,7 @@ class Hashgraph:
         return n_ins.value
 
     def _events32(self, cols: dict, lo: int, hi: int):
-        a = {k: v[lo:hi] for k, v in cols.items()}
-        return a, _lib.hgx_events32(*[ptr(a[k]) for k in ("creator", "index", "sp", "op", "ts", "coin", "s", "ntx")])
+        return _events32_of(cols, lo, hi)
 
     def insert_events32(self, cols: dict, lo: int = 0, hi: Optional[int] = None) -> int:
         """InsertEvent from the compact columns of compact_columns() (hgx_insert_events32)."""
@@ -232,6 +264,34 @@ class Hashgraph:
         if cb_err is not None:
             raise cb_err
         return n_ins.value
+
+    def _packed_call(self, fn, pk: dict) -> int:
+        m = len(pk["creator16"])
+        ev = _lib.hgx_events_packed(ptr(pk["creator16"]), ptr(pk["index"]), ptr(pk["sp_back"]), ptr(pk["op_back"]),
+                                    len(pk["exc_pos"]), ptr(pk["exc_pos"]), ptr(pk["exc_sp"]), ptr(pk["exc_op"]),
+                                    ptr(pk["ts"]), ptr(pk["coin"]), ptr(pk["s"]), ptr(pk["ntx"]))
+        err = hgx_error()
+        n_ins = C.c_int64(0)
+        self._cb_error = None
+        rc = fn(self.ctx, C.byref(ev), m, C.byref(n_ins), C.byref(err))
+        if rc:
+            e = HgxError(int(err.code or rc), err.msg.decode(errors="replace"))
+            e.inserted = n_ins.value
+            raise e
+        cb_err, self._cb_error = getattr(self, "_cb_error", None), None
+        if cb_err is not None:
+            raise cb_err
+        return n_ins.value
+
+    def insert_events_packed(self, pk: dict) -> int:
+        """InsertEvent from pack_columns() output (hgx_insert_events_packed); its base must be
+        num_events() now."""
+        return self._packed_call(self.L.hgx_insert_events_packed, pk)
+
+    def insert_and_run_packed(self, pk: dict) -> int:
+        """insert_and_run from pack_columns() output (hgx_insert_and_run_packed: 10-byte structure
+        columns + the 45-byte compact payload)."""
+        return self._packed_call(self.L.hgx_insert_and_run_packed, pk)
 
     def InsertEvent(self, creator: int, index: int, self_parent: int, other_parent: int, timestamp_ns: int,
                     hash32: bytes, s32: bytes, transactions: Optional[Sequence[bytes]]):

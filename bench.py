@@ -595,8 +595,10 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the full-size property checks")
     ap.add_argument("--no-chunked", action="store_true", help="skip the SyncLimit-chunked schedule leg")
     ap.add_argument("--sync-limit", type=int, default=1000)
-    ap.add_argument("--wide", action="store_true", help="hand the events over as hgx_events (108 B/event) "
-                                                        "instead of hgx_events32 (61 B/event)")
+    ap.add_argument("--columns", default="packed", choices=["packed", "compact", "wide"],
+                    help="how the caller hands the events over: hgx_events_packed (10 B structure + 45 B payload "
+                         "per event, the default), hgx_events32 (61 B) or hgx_events (108 B)")
+    ap.add_argument("--wide", action="store_true", help="= --columns wide")
     ap.add_argument("--sharded", action="store_true",
                     help="C3's single-graph mode in one process: the round recurrence chain-sharded over --gpus devices "
                          "(shards share a device when there are fewer; strong scaling) instead of replicas")
@@ -626,8 +628,10 @@ def main():
             raise SystemExit("--sharded-ranks needs torch.distributed.run with >= 2 ranks")
         return run_sharded_ranks(args, red, world, rank, local_rank)
 
-    from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns
+    from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns, pack_columns
     n, E, G, *_ = CONFIGS[args.config]
+    if args.wide:
+        args.columns = "wide"
     t0 = time.time()
     tr, G = make_trace(args.config, rank)
     log(f"[rank {rank}] trace {tr.E} events generated in {time.time() - t0:.1f}s")
@@ -637,16 +641,23 @@ def main():
         h.set_round_kernel(args.round_kernel)
     if args.round_shards > 1:   # the one-GPU rehearsal of a chain-sharded recurrence
         h.set_round_shards(args.round_shards)
-    # the columns as the caller hands them over, built before the clock: hgx_events32 (int32 Index
-    # and parents, the coin byte, ntx -1 = nil; 61 B per event) unless --wide (hgx_events, 108 B)
-    cols = None if args.wide else compact_columns(tr)
+    # the columns as the caller hands them over, built before the clock: hgx_events_packed (u16
+    # creator, int32 Index, u16 parent distances + exceptions; the 45-byte compact payload), or
+    # hgx_events32 (int32 Index and parents, the coin byte, ntx -1 = nil; 61 B per event), or
+    # hgx_events (108 B)
+    cols = None if args.columns == "wide" else compact_columns(tr)
+    pk = pack_columns(cols, 0) if args.columns == "packed" else None
+    if pk is not None:
+        log(f"[rank {rank}] packed columns: {len(pk['exc_pos'])} exceptions")
 
     def step():
         """from the first event append (the trace in host RAM, as the caller holds
         it: the H2D copy of every event column is inside the step) to the order in host memory.
         One hgx_insert_and_run = hgx_insert_events + DivideRounds + DecideFame + FindOrder."""
         h.clear()
-        if cols is None:
+        if pk is not None:
+            h.insert_and_run_packed(pk)
+        elif cols is None:
             h.insert_and_run(tr)
         else:
             h.insert_and_run32(cols)
@@ -772,12 +783,17 @@ def main():
             "config": {"workload": CONFIGS[args.config][6], "config": args.config, "peers": n,
                        "events_per_gpu": int(tr.E), "graphs_per_gpu": G,
                        "ordered_events_per_step_per_gpu": int(m_pass),
-                       "step": ("clear + hgx_insert_and_run" + ("" if args.wide else "32") +
+                       "step": ("clear + hgx_insert_and_run" +
+                                {"wide": "", "compact": "32", "packed": "_packed"}[args.columns] +
                                 ": InsertEvent (H2D of the event columns + device validation) + DivideRounds + "
                                 "DecideFame + FindOrder, the payload columns' H2D beside DivideRounds; order in "
                                 "host memory"),
-                       "host_columns": "hgx_events (108 B/event)" if args.wide else
-                                       "hgx_events32 (int32 Index/parents, coin byte, ntx -1 = nil: 61 B/event)",
+                       "host_columns": {
+                           "wide": "hgx_events (108 B/event)",
+                           "compact": "hgx_events32 (int32 Index/parents, coin byte, ntx -1 = nil: 61 B/event)",
+                           "packed": "hgx_events_packed (u16 creator, int32 Index, u16 parent distances: 10 B "
+                                     "structure + 45 B payload per event; %d exceptions)" % (
+                                         len(pk["exc_pos"]) if pk is not None else 0)}[args.columns],
                        "parallelism": f"replicas x{world} (seed-sharded)" +
                                       (f"; recurrence rehearsed in {args.round_shards} chain blocks on one GPU"
                                        if args.round_shards > 1 else ""),

@@ -137,6 +137,41 @@ typedef struct {
 int32_t hgx_insert_events32(hgx_ctx* ctx, const hgx_events32* ev, int64_t count, int64_t* n_inserted, hgx_error* err);
 int32_t hgx_insert_and_run32(hgx_ctx* ctx, const hgx_events32* ev, int64_t count, int64_t* n_inserted,
                              hgx_error* err);
+/* The same batch with its structure columns in 10 instead of 16 bytes per event (what
+ * validation and DivideRounds wait for; the payload columns are those of hgx_events32). Event k
+ * of the batch gets gid base + k, base = hgx_num_events(ctx) at the call. A parent is stored as
+ * its distance back from that gid: 0 = "" (-1), 1..65534 = gid base + k - d, HGX_PARENT_ESCAPE =
+ * the event's entry in the exception list (exc_pos: batch positions, distinct, any order;
+ * exc_self_parent / exc_other_parent: both parents as hgx_events32 holds them, HGX_UNKNOWN_PARENT
+ * included). An escaped parent without an entry reads as HGX_UNKNOWN_PARENT. The columns are
+ * decoded on the device into the hgx_events32 form, so results, errors and counters are those of
+ * hgx_insert_events32 / hgx_insert_and_run32 on the decoded batch. hgx_pack_events32 builds them. */
+#define HGX_PARENT_ESCAPE 0xFFFF
+typedef struct {
+    const uint16_t* creator;            /* participant id (global id in a batched ctx), < 65536 */
+    const int32_t* index;               /* Body.Index */
+    const uint16_t* self_parent_back;   /* distance back, 0 = "", HGX_PARENT_ESCAPE */
+    const uint16_t* other_parent_back;
+    int64_t n_exc;                      /* exception list (host memory) */
+    const int64_t* exc_pos;
+    const int32_t* exc_self_parent;
+    const int32_t* exc_other_parent;
+    const int64_t* timestamp_ns;        /* the payload columns, as in hgx_events32 */
+    const uint8_t* coin;
+    const uint8_t* sig_s;
+    const int32_t* ntx;
+} hgx_events_packed;
+int32_t hgx_insert_events_packed(hgx_ctx* ctx, const hgx_events_packed* ev, int64_t count, int64_t* n_inserted,
+                                 hgx_error* err);
+int32_t hgx_insert_and_run_packed(hgx_ctx* ctx, const hgx_events_packed* ev, int64_t count, int64_t* n_inserted,
+                                  hgx_error* err);
+/* Host helper (no device): the packed structure columns of an hgx_events32 batch whose first
+ * event will get gid `base`. Writes creator16 / sp_back / op_back (count each) and up to exc_cap
+ * exceptions; *n_exc = the number needed (HGX_ERR_INVALID "exception list full" if > exc_cap,
+ * HGX_ERR_INVALID "creator outside 0..65535" for a creator the form cannot hold). */
+int32_t hgx_pack_events32(const hgx_events32* ev, int64_t count, int64_t base, uint16_t* creator16, uint16_t* sp_back,
+                          uint16_t* op_back, int64_t* exc_pos, int32_t* exc_self_parent, int32_t* exc_other_parent,
+                          int64_t exc_cap, int64_t* n_exc, hgx_error* err);
 /* The same with every hgx_events column a DEVICE pointer on the context's device (events
  * decoded / hashed on the GPU, or a trace resident in HBM). hash and sig_s must be
  * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */

@@ -180,3 +180,104 @@ def test_compact_refused_after_reset():
     with pytest.raises(HgxError) as ei:
         a.insert_events32(compact_columns(t))
     assert "use hgx_insert_events" in ei.value.msg
+
+
+# ---- the packed structure columns (hgx_events_packed: 10 bytes per event, decoded on the device) ----
+
+def _far_parents(cols, every=997, back=70000):
+    """Valid other-parents more than 65 534 events back (CheckOtherParent only asks that the parent
+    is known): the packed form carries them in its exception list."""
+    op = cols["op"].copy()
+    cr = cols["creator"]
+    for k in range(back + 1, len(op), every):
+        j = k - back
+        while cr[j] == cr[k]:
+            j -= 1
+        op[k] = j
+    return {**cols, "op": op}
+
+
+@pytest.mark.parametrize("n,E,seed", [(16, 70000, 21), (64, 160000, 22), (256, 200000, 23)])
+def test_packed_equal_compact(n, E, seed):
+    from babble_amd.hashgraph import compact_columns, pack_columns
+    cols = compact_columns(_with_nil(gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3)))
+    if E > 70001:
+        cols = _far_parents(cols)
+    pk = pack_columns(cols, 0)
+    assert (E <= 70001) or len(pk["exc_pos"]) > 0
+    a = _hg(n, E)
+    assert a.insert_and_run_packed(pk) == E
+    b = _hg(n, E)
+    assert b.insert_and_run32(cols) == E
+    _same(a, b)
+    if n <= 16:
+        t = gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3)
+        compare(a, hgref.oracle_run(_with_nil(t)), _with_nil(t), hashes=False)
+
+
+def test_packed_small_batches_and_batched_graphs():
+    """Sync-sized batches (hgx_insert_events_packed, base = the context's event count) and a
+    batched context equal the compact columns' path."""
+    from babble_amd.hashgraph import compact_columns, pack_columns
+    n, E, chunk = 32, 30000, 1000
+    cols = compact_columns(_with_nil(gtrace.gossip(n, E, 24, stale_prob=0.2, stale_depth=3), every=5))
+    a, b = _hg(n, E), _hg(n, E)
+    for lo in range(0, E, chunk):
+        hi = min(E, lo + chunk)
+        sub = {k: v[lo:hi] for k, v in cols.items()}
+        assert a.insert_events_packed(pack_columns(sub, a.num_events())) == hi - lo
+        a.RunConsensus()
+        assert b.insert_events32(cols, lo, hi) == hi - lo
+        b.RunConsensus()
+    _same(a, b)
+    G, E1 = 8, 12000
+    t = gtrace.concat_graphs([gtrace.gossip(16, E1, 80 + g, stale_prob=0.1, stale_depth=2) for g in range(G)])
+    cols = compact_columns(t)
+    a, b = _hg(16, t.E, graphs=G), _hg(16, t.E, graphs=G)
+    assert a.insert_and_run_packed(pack_columns(cols, 0)) == t.E
+    b.insert_and_run32(cols)
+    _same(a, b, graphs=G)
+
+
+@pytest.mark.parametrize("kind", ["other_parent", "passed_index", "self_parent", "escape_without_entry"])
+def test_packed_insert_error(kind):
+    """The errors of the decoded batch are those of hgx_insert_and_run32 on the same batch."""
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns, pack_columns
+    n, E, k0 = 32, 100000, 81234
+    cols = compact_columns(gtrace.gossip(n, E, 25))
+    if kind == "other_parent":
+        cols["op"][k0] = -2
+    elif kind == "passed_index":
+        cols["index"][k0] -= 1
+    elif kind == "self_parent":
+        cols["sp"][k0] = cols["sp"][k0] - 1 if cols["sp"][k0] > 0 else 0
+    pk = pack_columns(cols, 0)
+    if kind == "escape_without_entry":   # reads as HGX_UNKNOWN_PARENT
+        pk["op_back"] = pk["op_back"].copy()
+        pk["op_back"][k0] = 0xFFFF
+        cols["op"][k0] = -2
+    a = _hg(n, E)
+    with pytest.raises(HgxError) as ei:
+        a.insert_and_run_packed(pk)
+    assert ei.value.inserted == k0 and a.num_events() == k0
+    b = _hg(n, E)
+    with pytest.raises(HgxError) as ec:
+        b.insert_and_run32(cols)
+    assert ei.value.msg == ec.value.msg and ei.value.code == ec.value.code and ec.value.inserted == k0
+
+
+def test_packed_bad_exception_list():
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns, pack_columns
+    cols = compact_columns(gtrace.gossip(8, 2000, 26))
+    pk = pack_columns(cols, 0)
+    a = _hg(8, 4000)
+    for pos in ([5, 5], [2000], [-1]):
+        bad = {**pk, "exc_pos": np.asarray(pos, np.int64), "exc_sp": np.full(len(pos), -1, np.int32),
+               "exc_op": np.full(len(pos), -1, np.int32)}
+        with pytest.raises(HgxError) as ei:
+            a.insert_events_packed(bad)
+        assert "bad arguments" in ei.value.msg
+    assert a.num_events() == 0
+    assert a.insert_events_packed(pk) == 2000
