@@ -36,7 +36,9 @@
 extern "C" {
 #endif
 
-#define HGX_ABI_VERSION 4   /* 4: hgx_create_sharded (chain-sharded recurrence over devices);
+#define HGX_ABI_VERSION 5   /* 5: hgx_events_packed (hgx_insert_events_packed, hgx_insert_and_run_packed,
+                                 hgx_pack_events32);
+                              4: hgx_create_sharded (chain-sharded recurrence over devices);
                               3: HGX_ROOT_OTHER needs its key registered (hgx_set_root_others) */
 
 /* Error codes. 1..5 mirror common.StoreErrType + 1 (common/errors.go:7-13). */
