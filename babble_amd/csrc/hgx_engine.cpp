@@ -467,30 +467,37 @@ static hipError_t stage_col(DBuf<T>& b, const T* src, size_t count, size_t per, 
     return hipMemcpyAsync(b.p, src, count * per * sizeof(T), hipMemcpyHostToDevice, s);
 }
 
+// a sync-sized batch (at most kPackEvents): the k host columns packed into pinned memory and sent as
+// one copy into st_pack (k pageable copies cost a staged, blocking transfer each); off[i] = column i's
+// byte offset in st_pack
+hipError_t Engine::stage_pinned(int k, const void* const* src, const size_t* bytes, size_t* off) {
+    size_t total = 0;
+    for (int i = 0; i < k; i++) {
+        off[i] = total;
+        total += (bytes[i] + 255) & ~(size_t)255;
+    }
+    if (st_pack.n < total) HGX_TRY(st_pack.alloc(std::max(total, (size_t)2 * st_pack.n)));
+    if (h_pack_cap < total) {   // (every insert synchronized before returning: the buffer is free)
+        if (h_pack) (void)hipHostFree(h_pack);
+        h_pack = nullptr;
+        h_pack_cap = 0;
+        HGX_TRY(hipHostMalloc((void**)&h_pack, std::max(total, (size_t)2 * st_pack.n), hipHostMallocDefault));
+        h_pack_cap = std::max(total, (size_t)2 * st_pack.n);
+    }
+    for (int i = 0; i < k; i++)
+        if (bytes[i]) std::memcpy(h_pack + off[i], src[i], bytes[i]);
+    return hipMemcpyAsync(st_pack.p, h_pack, total, hipMemcpyHostToDevice, stream);
+}
+
 hipError_t Engine::stage_host(const int32_t* creator, const int64_t* index, const int64_t* sp, const int64_t* op,
                               const int64_t* ts, const uint8_t* hash, const uint8_t* S, const int32_t* ntx,
                               const int32_t* nil, int64_t count, InsertIn& in) {
     const size_t c = (size_t)count;
     if (count <= kPackEvents) {
-        // a sync-sized batch: the nine columns packed into pinned memory and sent as one copy
-        // (nine pageable copies cost a staged, blocking transfer each)
         const void* src[9] = {creator, index, sp, op, ts, hash, S, ntx, nil};
         const size_t bytes[9] = {4 * c, 8 * c, 8 * c, 8 * c, 8 * c, 32 * c, 32 * c, 4 * c, 4 * c};
-        size_t off[9], total = 0;
-        for (int i = 0; i < 9; i++) {
-            off[i] = total;
-            total += (bytes[i] + 255) & ~(size_t)255;
-        }
-        if (st_pack.n < total) HGX_TRY(st_pack.alloc(std::max(total, (size_t)2 * st_pack.n)));
-        if (h_pack_cap < total) {   // (every insert synchronized before returning: the buffer is free)
-            if (h_pack) (void)hipHostFree(h_pack);
-            h_pack = nullptr;
-            h_pack_cap = 0;
-            HGX_TRY(hipHostMalloc((void**)&h_pack, std::max(total, (size_t)2 * st_pack.n), hipHostMallocDefault));
-            h_pack_cap = std::max(total, (size_t)2 * st_pack.n);
-        }
-        for (int i = 0; i < 9; i++) std::memcpy(h_pack + off[i], src[i], bytes[i]);
-        HGX_TRY(hipMemcpyAsync(st_pack.p, h_pack, total, hipMemcpyHostToDevice, stream));
+        size_t off[9];
+        HGX_TRY(stage_pinned(9, src, bytes, off));
         uint8_t* d = st_pack.p;
         in.creator = (const int32_t*)(d + off[0]); in.index = (const int64_t*)(d + off[1]);
         in.sp = (const int64_t*)(d + off[2]); in.op = (const int64_t*)(d + off[3]); in.ts = (const int64_t*)(d + off[4]);
@@ -519,21 +526,8 @@ hipError_t Engine::stage_host32(const int32_t* creator, const int32_t* index, co
     if (count <= kPackEvents) {   // one pinned packed copy (as stage_host)
         const void* src[8] = {creator, index, sp, op, ts, coin, S, ntx};
         const size_t bytes[8] = {4 * c, 4 * c, 4 * c, 4 * c, 8 * c, c, 32 * c, 4 * c};
-        size_t off[8], total = 0;
-        for (int i = 0; i < 8; i++) {
-            off[i] = total;
-            total += (bytes[i] + 255) & ~(size_t)255;
-        }
-        if (st_pack.n < total) HGX_TRY(st_pack.alloc(std::max(total, (size_t)2 * st_pack.n)));
-        if (h_pack_cap < total) {
-            if (h_pack) (void)hipHostFree(h_pack);
-            h_pack = nullptr;
-            h_pack_cap = 0;
-            HGX_TRY(hipHostMalloc((void**)&h_pack, std::max(total, (size_t)2 * st_pack.n), hipHostMallocDefault));
-            h_pack_cap = std::max(total, (size_t)2 * st_pack.n);
-        }
-        for (int i = 0; i < 8; i++) std::memcpy(h_pack + off[i], src[i], bytes[i]);
-        HGX_TRY(hipMemcpyAsync(st_pack.p, h_pack, total, hipMemcpyHostToDevice, stream));
+        size_t off[8];
+        HGX_TRY(stage_pinned(8, src, bytes, off));
         uint8_t* d = st_pack.p;
         in.creator = (const int32_t*)(d + off[0]); in.index32 = (const int32_t*)(d + off[1]);
         in.sp32 = (const int32_t*)(d + off[2]); in.op32 = (const int32_t*)(d + off[3]);
@@ -631,13 +625,30 @@ hipError_t Engine::stage_packed(const Packed& pk, int64_t count, InsertIn& in, c
                                 const uint8_t* S, const int32_t* ntx) {
     const size_t c = (size_t)count, x = (size_t)pk.n_exc;
     in = InsertIn{};
+    if (st_creator.n < c) HGX_TRY(st_creator.alloc(c));
+    if (st_sp32.n < c) HGX_TRY(st_sp32.alloc(c));
+    if (st_op32.n < c) HGX_TRY(st_op32.alloc(c));
+    if (ts && count <= kPackEvents) {   // a sync-sized batch: one pinned packed copy (as stage_host32)
+        const void* src[11] = {pk.creator, pk.index, pk.spb, pk.opb, ts, coin, S, ntx, pk.exc_pos, pk.exc_sp, pk.exc_op};
+        const size_t bytes[11] = {2 * c, 4 * c, 2 * c, 2 * c, 8 * c, c, 32 * c, 4 * c, 8 * x, 4 * x, 4 * x};
+        size_t off[11];
+        HGX_TRY(stage_pinned(11, src, bytes, off));
+        uint8_t* d = st_pack.p;
+        launch_unpack_packed(stream, count, E, (const uint16_t*)(d + off[0]), (const uint16_t*)(d + off[2]),
+                             (const uint16_t*)(d + off[3]), pk.n_exc, (const int64_t*)(d + off[8]),
+                             (const int32_t*)(d + off[9]), (const int32_t*)(d + off[10]), st_creator.p, st_sp32.p,
+                             st_op32.p);
+        HGX_TRY(hipGetLastError());
+        in.creator = st_creator.p; in.index32 = (const int32_t*)(d + off[1]); in.sp32 = st_sp32.p;
+        in.op32 = st_op32.p; in.ts = (const int64_t*)(d + off[4]); in.coin = d + off[5]; in.S = d + off[6];
+        in.ntx = (const int32_t*)(d + off[7]);
+        if (count > 0) ids_known = false;
+        return hipSuccess;
+    }
     HGX_TRY(stage_col(st_c16, pk.creator, c, 1, stream));
     HGX_TRY(stage_col(st_index32, pk.index, c, 1, stream));
     HGX_TRY(stage_col(st_spb, pk.spb, c, 1, stream));
     HGX_TRY(stage_col(st_opb, pk.opb, c, 1, stream));
-    if (st_creator.n < c) HGX_TRY(st_creator.alloc(c));
-    if (st_sp32.n < c) HGX_TRY(st_sp32.alloc(c));
-    if (st_op32.n < c) HGX_TRY(st_op32.alloc(c));
     if (x) {
         HGX_TRY(stage_col(st_exc_pos, pk.exc_pos, x, 1, stream));
         HGX_TRY(stage_col(st_exc_sp, pk.exc_sp, x, 1, stream));

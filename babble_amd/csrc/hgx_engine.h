@@ -341,6 +341,7 @@ class Engine {
     // batches of at most kPackEvents from host memory: the columns packed in one pinned buffer,
     // one H2D copy into st_pack
     static constexpr int64_t kPackEvents = 65536;
+    hipError_t stage_pinned(int k, const void* const* src, const size_t* bytes, size_t* off);
     DBuf<uint8_t> st_pack;
     uint8_t* h_pack = nullptr;
     size_t h_pack_cap = 0;

@@ -344,9 +344,12 @@ def chunked_leg(h, tr, sync_limit, check):
     (cmd/babble/main.go:83-85) and Core.RunConsensus follows every sync (node/core.go:190-303);
     the incremental DivideRounds/FindOrder work on the new events only. Wall clock over the
     whole trace; every sync's events come from host memory, as Core hands them over."""
+    import gc
     h.clear()
     h.set_kernel_timing(False)
     calls, worst = 0, 0.0
+    gc.collect()
+    gc.disable()   # (a collector pause of this process is not the library's latency: one measured 14.7 ms call)
     t0 = time.perf_counter()
     for lo in range(0, tr.E, sync_limit):
         c0 = time.perf_counter()
@@ -355,6 +358,7 @@ def chunked_leg(h, tr, sync_limit, check):
         worst = max(worst, time.perf_counter() - c0)
         calls += 1
     el = time.perf_counter() - t0
+    gc.enable()
     ordered = int(h.L.hgx_consensus_events_count(h.ctx, 0))
     res = {"sync_limit": sync_limit, "calls": calls, "events": int(tr.E), "ordered": ordered,
            "value": ordered / el, "unit": "consensus-ordered events/s", "inserted_events_per_s": tr.E / el,
