@@ -1116,8 +1116,17 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
     // a rebuild of one large graph runs the wavefront on time segments in parallel (their
     // rows are lower bounds), then a verify sweep and the dirty sweeps complete them
     la_wave_segs = 1;
-    if (la_wave_used && rebuild && G == 1 && En >= (int64_t)kLaSegMinRows * C)
-        la_wave_segs = la_segs_override > 0 ? la_segs_override : la_wave_segments(n, compact, num_cus, kLaMaxSegs);
+    if (la_wave_used && rebuild && G == 1 && En >= (int64_t)kLaSegMinRows * C) {
+        // as many segments as the CUs hold, of at least 2 x kLaHeadRows rows per chain: c2 (64 chains
+        // of 16 384 rows, 4 column blocks) took 2.04 ms at 16 segments, 0.69 at 128, and at 192 its
+        // exactness check failed (the verify sweep ran); c3 keeps its LDS-bound 16 (profiles/r05/b28_*, b29_*)
+#ifdef HGX_LA_SEG_FILL
+        const int cap = (int)std::max<int64_t>(kLaMaxSegs, En / C / (2 * kLaHeadRows));
+#else
+        const int cap = kLaMaxSegs;
+#endif
+        la_wave_segs = la_segs_override > 0 ? la_segs_override : la_wave_segments(n, compact, num_cus, cap);
+    }
     if (rebuild) {   // (the wavefront writes every row it builds before anything reads it)
         if (!la_wave_used) HGX_TRY(hipMemsetAsync(LA.p, compact ? 0x00 : 0xFF, (size_t)h_off[C] * n * csz, stream));
     } else {
