@@ -1120,9 +1120,9 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // as many segments as the CUs hold, of at least 2 x kLaHeadRows rows per chain: c2 (64 chains
         // of 16 384 rows, 4 column blocks) took 2.04 ms at 16 segments, 0.69 at 128, and at 192 its
         // exactness check failed (the verify sweep ran); c3 keeps its LDS-bound 16 (profiles/r05/b28_*, b29_*)
-#ifdef HGX_LA_SEG_FILL
+#ifndef HGX_LA_SEG_CAP16
         const int cap = (int)std::max<int64_t>(kLaMaxSegs, En / C / (2 * kLaHeadRows));
-#else
+#else   // (the round-4 cap, for A/B)
         const int cap = kLaMaxSegs;
 #endif
         la_wave_segs = la_segs_override > 0 ? la_segs_override : la_wave_segments(n, compact, num_cus, cap);
