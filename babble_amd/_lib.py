@@ -178,6 +178,8 @@ def lib():
     _sig(L, "hgx_set_round_kernel", i32, [p, i32])
     _sig(L, "hgx_set_sort_kernel", i32, [p, i32])
     _sig(L, "hgx_set_round_shards", i32, [p, i32])
+    _sig(L, "hgx_set_shard_remote", i32, [p, i32])
+    _sig(L, "hgx_exchange_floor_bench", i32, [i32, i32, i32, i32, C.POINTER(C.c_double)])
     _sig(L, "hgx_set_cts_kernel", i32, [p, i32])
     _sig(L, "hgx_set_root_others", i32, [p, p, i64, p])
     _sig(L, "hgx_set_la_kernel", i32, [p, i32])

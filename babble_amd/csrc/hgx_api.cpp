@@ -2480,8 +2480,10 @@ static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error
             drop_group(c);
             return err ? err->code : HGX_ERR_DEVICE;
         }
-        // the shard 0 settings (hgx_set_*) so far
+        // the shard 0 settings (hgx_set_*) so far: every Engine field an hgx_set_* call writes
+        // through each_shard
         q->eng.force_coord32 = c->eng.force_coord32;
+        q->eng.la_verify_always = c->eng.la_verify_always;
         q->eng.time_mask = c->eng.time_mask;
         q->eng.fame_tally = c->eng.fame_tally;
         q->eng.la_kernel = c->eng.la_kernel;
@@ -2507,6 +2509,12 @@ static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error
         sh[k]->eng.shard_hi = g->c_split[k + 1];
     }
     return ok(err);
+}
+
+int32_t hgx_set_shard_remote(hgx_ctx* c, int32_t on) {
+    if (!c || !c->grp || on < 0 || on > 1) return HGX_ERR_INVALID;
+    c->grp->force_remote = on != 0;
+    return HGX_OK;
 }
 
 int32_t hgx_set_round_shards(hgx_ctx* c, int32_t shards) {

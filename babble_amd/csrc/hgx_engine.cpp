@@ -1120,11 +1120,8 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
         // as many segments as the CUs hold, of at least 2 x kLaHeadRows rows per chain: c2 (64 chains
         // of 16 384 rows, 4 column blocks) took 2.04 ms at 16 segments, 0.69 at 128, and at 192 its
         // exactness check failed (the verify sweep ran); c3 keeps its LDS-bound 16 (profiles/r05/b28_*, b29_*)
-#ifndef HGX_LA_SEG_CAP16
+        // (the round-4 cap of kLaMaxSegs alone: c2 2.04 ms)
         const int cap = (int)std::max<int64_t>(kLaMaxSegs, En / C / (2 * kLaHeadRows));
-#else   // (the round-4 cap, for A/B)
-        const int cap = kLaMaxSegs;
-#endif
         la_wave_segs = la_segs_override > 0 ? la_segs_override : la_wave_segments(n, compact, num_cus, cap);
     }
     if (rebuild) {   // (the wavefront writes every row it builds before anything reads it)
@@ -1365,7 +1362,7 @@ hipError_t Engine::divide_rounds(int64_t En, const std::vector<int32_t>& chain_l
                 win.gran[k] = q->rp_gran.p;
                 win.st[k] = q->rp_st.p;
                 win.FDT[k] = q->FDT.p;
-                if (grp->dev[k] != dev) win.remote |= 1u << k;
+                if (grp->dev[k] != dev || (grp->force_remote && k != shard)) win.remote |= 1u << k;
             }
             if (rp_win.n < sizeof(RoundPWindows)) HGX_TRY(rp_win.alloc(sizeof(RoundPWindows)));
             HGX_TRY(hipMemcpyAsync(rp_win.p, &win, sizeof(RoundPWindows), hipMemcpyHostToDevice, stream));
@@ -1838,11 +1835,17 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         const int seg_bits = bitlen((uint64_t)G * (uint64_t)R - 1);
         uint64_t* keys = nullptr;
         kbeg(K_SORT);
-        if (seg_try && cts_bits + seg_bits <= 64 && mm[2] >= 1 && mm[2] <= (unsigned long long)seg_sort_cap()) {
-            launch_sort_seg(stream, a, m, cmin, cts_bits, R, n, nseg, seg_off.p, seg_cur.p, (int)mm[2], &vals, &keys);
+        // (a refused LDS limit for the 1 024-thread bucket sort is reported before anything is
+        // launched, and the radix passes run instead)
+        const bool seg = seg_try && cts_bits + seg_bits <= 64 && mm[2] >= 1 &&
+                         mm[2] <= (unsigned long long)seg_sort_cap() &&
+                         launch_sort_seg(stream, a, m, cmin, cts_bits, R, n, nseg, seg_off.p, seg_cur.p, (int)mm[2],
+                                         &vals, &keys) == hipSuccess;
+        if (seg) {
             sort_seg_runs++;
             kend(K_SORT, (double)m * 24.0 * 2);   // (bucket scatter + in-LDS sort: two passes' bytes)
         } else {
+            (void)hipGetLastError();
             launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
             kend(K_SORT, (double)m * 24.0 *
                              (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8

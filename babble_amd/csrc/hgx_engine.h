@@ -107,6 +107,9 @@ struct ShardGroup {
     int32_t c_split[kMaxShards + 1] = {};
     Engine* eng[kMaxShards] = {};
     int32_t st[kMaxShards][4] = {};   // every shard's status words after its last persistent launch
+    // hgx_set_shard_remote (test switch): every other shard's window is written as if it were on
+    // another device (system-scope stores), so one GPU runs the instructions an 8-GPU node runs
+    bool force_remote = false;
     bool wait();                      // false: a shard failed (or 120 s passed): leave with an error
     void fail();
     void rearm();                     // before a group call (no thread inside the group)

@@ -338,8 +338,12 @@ void launch_insert_unclaim(hipStream_t s, int64_t m, const unsigned long long* f
 constexpr int kEscape = 0xFFFF;
 constexpr int kUnknownParent = -2;
 
+// A distance that reaches back before gid 0 names no event: HGX_UNKNOWN_PARENT, as an unknown id
+// would be (a malformed batch must not decode to gid -1, the empty parent).
 __device__ __forceinline__ int32_t unpack_parent(uint32_t d, int64_t gid) {
-    return d == 0 ? -1 : d == (uint32_t)kEscape ? kUnknownParent : (int32_t)(gid - (int64_t)d);
+    return d == 0 ? -1
+         : (d == (uint32_t)kEscape || (int64_t)d > gid) ? kUnknownParent
+         : (int32_t)(gid - (int64_t)d);
 }
 
 __global__ void __launch_bounds__(256) k_unpack_packed(int64_t m, int64_t E0, const uint16_t* __restrict__ c16,

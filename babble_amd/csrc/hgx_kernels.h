@@ -237,6 +237,9 @@ struct RoundPWindows {
 // block with its nwin = W windows (win_dev: a RoundPWindows in device memory; the W shards' launches
 // run concurrently, on W devices or W streams of one); init 2 = the initial rows and granules only
 // (of the launch's chains, into every window)
+// the recurrence's exchange floor (k_xchg_floor, hgx_round_p.hip): C resident workgroups publish and poll
+// one n-coordinate row each per round, `rounds` rounds; rows [4][C n/4] u32, gran [4][C], st[0] = give-up
+hipError_t launch_xchg_floor(hipStream_t s, int C, int n, int rounds, uint32_t* rows, uint64_t* gran, int32_t* st);
 hipError_t launch_round_p(hipStream_t s, const RoundArgs& A, uint32_t* FD8p, uint64_t* gran, int32_t* status,
                           int32_t* fin, int r0, int r_end, int init, int num_cus, int c_lo = 0, int c_hi = -1,
                           const RoundPWindows* win_dev = nullptr, int nwin = 1);
@@ -297,7 +300,7 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
 int seg_sort_cap();
 void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n, int nseg, uint32_t* segc,
                       unsigned long long* max_out);
-void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
+hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
                      uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys);
 // m <= 4096: one block sorts (graph, rr, cts, S) (no cts range needed)
 bool sort_small_ok(int32_t m);

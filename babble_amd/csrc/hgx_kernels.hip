@@ -2540,16 +2540,21 @@ void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n
                        max_out);
 }
 
-void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
-                     uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys) {
+hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
+                           int nseg, uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals,
+                           uint64_t** final_keys) {
     uint64_t* kb = a.key_b;
     uint32_t *va = a.val_a, *vb = a.val_b;
+    int cap = 2;
+    while (cap < max_seg) cap <<= 1;
+    if (cap > 512) {   // (before anything is launched: the caller takes the radix passes on a refusal)
+        const hipError_t e = ensure_lds_limit((const void*)k_seg_sort<1024, 1024>, (size_t)cap * 16);
+        if (e != hipSuccess) return e;
+    }
     scan_u32(s, a, segoff, nseg);   // bucket counts -> bucket starts
     (void)hipMemsetAsync(segcur, 0, (size_t)nseg * 4, s);
     hipLaunchKernelGGL(k_seg_keys_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain,
                        a.p_rr, cmin, cts_bits, R, n, segoff, segcur, kb, vb);
-    int cap = 2;
-    while (cap < max_seg) cap <<= 1;
     // (the runs of equal keys are ordered by S inside k_seg_sort: the final values land in va)
     if (cap <= 512) {   // a wave per bucket, four per workgroup
         const size_t lds = (size_t)4 * cap * 16;
@@ -2557,12 +2562,12 @@ void launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin,
                            a.p_gid, a.g_S, va, cap);
     } else {
         const size_t lds = (size_t)cap * 16;
-        (void)ensure_lds_limit((const void*)k_seg_sort<1024, 1024>, lds);
         hipLaunchKernelGGL((k_seg_sort<1024, 1024>), dim3(nseg), dim3(1024), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
                            a.g_S, va, cap);
     }
     *final_vals = va;
     *final_keys = kb;
+    return hipGetLastError();
 }
 
 void launch_root_floor(hipStream_t s, const DevArrays& a, const int32_t* root_round, int32_t* gfl, int32_t* gB,

@@ -30,6 +30,7 @@
 // is counted with exact int32 compares (k_round_k flags the whole round instead).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +38,7 @@
 #include <vector>
 
 #include "hgx_device.h"
+#include "hgx.h"
 #include "hgx_kernels.h"
 
 namespace hgx {
@@ -548,9 +550,8 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
             bool ok = false;
             // the poll at the top priority: the waves whose candidates arrived search meanwhile, and
             // the youngest waves (last in the age order) would otherwise issue their loads last
-#ifndef HGX_RP_NOPOLLPRIO
+            // (without it: c3 round_search 15.80 -> 16.41-16.49 ms)
             __builtin_amdgcn_s_setprio(3);
-#endif
             for (int spins = 0;; spins++) {
                 if (!ok) rp_ld_cand<HD>(gp, rowp, cst, gv, fd);   // (a lane whose candidate is complete keeps it)
                 uint32_t bad = 0;
@@ -615,9 +616,8 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
         // histogram barrier: the younger half searches at a higher priority (c3 rounds 22.9 ->
         // 21.2 ms; graded priorities by age measured the same, priority kept through the publish
         // and the poll 7x slower)
-#ifndef HGX_RP_NOPRIO
+        // (without it: c3 round_search 15.80 -> 16.64-16.74 ms)
         if (NW >= 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(2);
-#endif
         for (;;) {
             int lo = 0, hi = kRpP;
             if (wave_cand) {
@@ -653,9 +653,7 @@ __global__ void __launch_bounds__((4 * NDW * Q < 64) ? 64 : 4 * NDW * Q) k_round
                 }
             }
             const int Kw = lo;
-#ifndef HGX_RP_NOPRIO
             if (NW >= 8) __builtin_amdgcn_s_setprio(0);
-#endif
             RP_PROF(13);
             if (cand && q == 0 && !done && Kw < np) atomicAdd(&hist[Kw], 1);
             // (d) the histogram is complete (and the staging issued in round s - 1 has landed: the
@@ -1024,4 +1022,126 @@ hipError_t launch_round_p(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, ui
                      : rp_launch_t<int32_t, false>(st, P, num_cus, c_hi - c_lo);
 }
 
+// ---- the recurrence's exchange floor (bench.py roofline.latency) --------------------------------
+// k_round_p with the search taken out: C resident workgroups (one per CU, the recurrence's LDS carve)
+// and per round s every workgroup publishes an NDW-dword row (16-byte write-through stores, chunk-major,
+// every dword = s + 1) and an 8-byte granule {s + 1}, then every lane polls its candidate's granule and
+// row part (Q lanes per candidate, HD = NDW / Q dwords each, sc1 loads issued and waited for together,
+// rp_ld_cand) until all of them carry s + 1, then one workgroup barrier. Rows in 4 buffers by s % 4, as
+// the recurrence's. The time per round is the all-to-all hand-off a round of the recurrence cannot go
+// below (C = 2: one 1-to-1 hand-off each way). Every wait is bounded (st[0] = 1: gave up).
+template <int NDW, int Q>
+__global__ void __launch_bounds__(4 * NDW * Q) k_xchg_floor(int C, int rounds, uint32_t* __restrict__ rows,
+                                                            uint64_t* __restrict__ gran, int32_t* __restrict__ st,
+                                                            long long tmo) {
+    constexpr int HD = NDW / Q, CS = HD < 4 ? HD : 4;
+    const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int j = t / Q, q = t % Q;
+    const size_t buf = (size_t)C * NDW, cst = (size_t)C * Q * CS;
+    bool failed = false;
+    for (int s = 0; s < rounds && !failed; s++) {
+        const uint32_t tag = (uint32_t)(s + 1);
+        uint32_t* rb = rows + (size_t)(s & 3) * buf;
+        uint64_t* gb = gran + (size_t)(s & 3) * C;
+        if (wave == 0) {   // publish: lane l < NDW / 4 writes 16 bytes, (q, k) = its part and chunk
+            if (lane < NDW / 4) {
+                const int pq = lane / (HD / CS > 0 ? HD / CS : 1), pk = lane % (HD / CS > 0 ? HD / CS : 1);
+                rp_st4_sc1(rb + rp_chunk_off(pk, c, pq, C, Q, CS), make_uint4(tag, tag, tag, tag));
+            }
+            if (lane == 0) rp_st_gran(gb + c, (uint64_t)tag << 32);
+        }
+        if (j < C) {
+            const long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                uint64_t gv;
+                uint32_t v[HD];
+                rp_ld_cand<HD>(gb + j, rb + rp_chunk_off(0, j, q, C, Q, CS), cst, gv, v);
+                bool ok = (uint32_t)(gv >> 32) == tag;
+#pragma unroll
+                for (int d = 0; d < HD; d++) ok = ok && v[d] == tag;
+                if (ok) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > tmo || rp_ld_abort(st) != 0) {
+                    failed = true;
+                    break;
+                }
+            }
+        }
+        if (failed) __hip_atomic_store((gu32*)st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        failed = rp_ld_abort(st) != 0;
+    }
+}
+
+template <int NDW, int Q>
+static hipError_t xchg_launch(hipStream_t s, int C, int rounds, uint32_t* rows, uint64_t* gran, int32_t* st) {
+    const void* f = (const void*)k_xchg_floor<NDW, Q>;
+    const size_t lds = 84 * 1024;   // one workgroup per CU, as k_round_p
+    const hipError_t e = ensure_lds_limit(f, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_xchg_floor<NDW, Q>), dim3(C), dim3(4 * NDW * Q), lds, s, C, rounds, rows, gran, st,
+                       (long long)2000000);
+    return hipGetLastError();
+}
+
+hipError_t launch_xchg_floor(hipStream_t s, int C, int n, int rounds, uint32_t* rows, uint64_t* gran, int32_t* st) {
+    switch (round_k_ndw(n)) {   // the geometry k_round_p takes at this n
+        case 16: return xchg_launch<16, 4>(s, C, rounds, rows, gran, st);
+        case 32: return xchg_launch<32, 4>(s, C, rounds, rows, gran, st);
+        case 64: return xchg_launch<64, 4>(s, C, rounds, rows, gran, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace hgx
+
+// Measurement entry for bench.py (roofline.latency): the exchange floor of a recurrence round with
+// `chains` workgroups of k_round_p's geometry at n coordinates (16 < n <= 256), one warm-up launch, then
+// one timed launch of `rounds` rounds (HIP events on the launch stream). HGX_ERR_DEVICE when a
+// workgroup gave up waiting (not all resident) or on any HIP error.
+extern "C" int32_t hgx_exchange_floor_bench(int32_t device, int32_t chains, int32_t n, int32_t rounds,
+                                            double* us_per_round) {
+    if (chains < 2 || chains > 1024 || n <= 16 || n > 256 || rounds < 1 || !us_per_round) return HGX_ERR_INVALID;
+    int prev = 0, cus = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) return HGX_ERR_DEVICE;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || chains > cus) {
+        (void)hipSetDevice(prev);
+        return HGX_ERR_INVALID;   // one resident workgroup per CU
+    }
+    const int ndw = hgx::round_k_ndw(n);
+    uint32_t* rows = nullptr;
+    uint64_t* gran = nullptr;
+    int32_t* st = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int32_t h_st = 0;
+    float ms = 0.f;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMalloc((void**)&rows, (size_t)4 * chains * ndw * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&gran, (size_t)4 * chains * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&st, 16);
+    for (int it = 0; it < 2 && e == hipSuccess; it++) {   // (a warm-up launch, then the timed one)
+        e = hipMemsetAsync(rows, 0, (size_t)4 * chains * ndw * 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(gran, 0, (size_t)4 * chains * 8, s);
+        if (e == hipSuccess) e = hipMemsetAsync(st, 0, 16, s);
+        if (e == hipSuccess && it) e = hipEventRecord(e0, s);
+        if (e == hipSuccess) e = hgx::launch_xchg_floor(s, chains, n, it ? rounds : std::min(rounds, 64), rows, gran, st);
+        if (e == hipSuccess && it) e = hipEventRecord(e1, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&h_st, st, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess && h_st != 0) e = hipErrorLaunchTimeOut;
+    }
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (rows) (void)hipFree(rows);
+    if (gran) (void)hipFree(gran);
+    if (st) (void)hipFree(st);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return HGX_ERR_DEVICE;
+    *us_per_round = (double)ms * 1e3 / rounds;
+    return HGX_OK;
+}

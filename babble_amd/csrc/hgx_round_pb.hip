@@ -575,11 +575,7 @@ __global__ void __launch_bounds__(1024) k_round_pb(RoundPbArgs P) {
         // (63-probe windows: prober 0's rows now, the others' after the barrier, one row set in registers)
         constexpr bool kMerged = sizeof(CT) == 2 && kPbP == 31;
         constexpr bool kPipe = sizeof(CT) == 2 && kPbP == 63;
-#ifdef HGX_PB_PIPE2
-        constexpr int kPipeBufs = 2;   // (experiment: the next prober's rows in flight during a rebase)
-#else
-        constexpr int kPipeBufs = 1;   // (two row sets spilled and measured no faster)
-#endif
+        constexpr int kPipeBufs = 1;   // (two row sets in flight spilled and measured no faster)
         RawRows rawn[kMerged ? PP : kPipe ? kPipeBufs : 1];
         int np1[PP];
         {
@@ -809,11 +805,7 @@ hipError_t launch_round_pb(hipStream_t st, const RoundArgs& A, uint32_t* FD8p, u
     if (na > 1024) return hipErrorInvalidValue;
     const int hd = na <= 512 ? 16 : na <= 768 ? 24 : 32;
     // (63-probe windows where three fit the LDS with compact coordinates)
-#ifdef HGX_PB_NP31
-    if (A.compact)
-        return hd == 16 ? pb_launch<uint16_t, 16, 31>(st, P, num_cus, init)
-                        : hd == 24 ? pb_launch<uint16_t, 24, 31>(st, P, num_cus, init) : pb_launch<uint16_t, 32, 31>(st, P, num_cus, init);
-#endif
+    // (31-probe windows at every width: c5 6.0 -> 8.1 ms)
     if (A.compact)
         return hd == 16 ? pb_launch<uint16_t, 16, 63>(st, P, num_cus, init)
                         : hd == 24 ? pb_launch<uint16_t, 24, 63>(st, P, num_cus, init) : pb_launch<uint16_t, 32, 31>(st, P, num_cus, init);

@@ -699,6 +699,12 @@ class Hashgraph:
             raise ValueError(f"invalid shard count {shards} (an empty context, 1..8 shards, "
                              f"GPU_MAX_HW_QUEUES >= shards + 2 for shards sharing a device)")
 
+    def set_shard_remote(self, on: bool = True):
+        """Test switch (hgx_set_shard_remote): the shards' window stores take the cross-device
+        (system-scope) path even where the shards share a device."""
+        if self.L.hgx_set_shard_remote(self.ctx, 1 if on else 0) != 0:
+            raise ValueError("hgx_set_shard_remote: not a chain-sharded context")
+
     def set_cts_kernel(self, mode):
         """FindOrder consensus timestamps: "auto" = "tile" (default: one tile of 8 positions per
         block) or "pipe" (resident blocks with several tiles' loads in flight, hgx_cts.hip)."""

@@ -23,7 +23,13 @@ by (round received, consensus timestamp, S), rounds monotone along every chain, 
 consistent). A failed check exits non-zero without a result line.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c2|c4|c5]
-  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N; without a launcher,
+  --gpus N > 1 starts that launcher itself as a child process before any GPU call and exits with
+  its status, so the line always carries N ranks' work)
+
+At N > 1 the line also carries `sharded`: C3's single-graph mode (one graph whose round recurrence is
+chain-sharded over all N devices, hgx_create_sharded) timed by rank 0 in a child process
+after every rank has released its GPU memory (the other ranks wait on the host).
 """
 from __future__ import annotations
 
@@ -255,10 +261,14 @@ class Reducer:
     the same code testable on CPU (tests/test_dist.py)."""
 
     def __init__(self, world, local_rank=0, backend="nccl"):
-        self.world, self.dist, self.device = world, None, "cpu"
+        self.world, self.dist, self.device, self.cpu_group = world, None, "cpu", None
         if world > 1:
+            import datetime
             import torch
             import torch.distributed as dist
+            if backend == "auto":   # RCCL when every rank has a GPU of its own, else gloo (ranks share one)
+                backend = "nccl" if torch.cuda.device_count() >= world else "gloo"
+            self.backend = backend
             if backend == "nccl":
                 torch.cuda.set_device(local_rank)
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -266,6 +276,13 @@ class Reducer:
             elif not dist.is_initialized():
                 dist.init_process_group(backend)
             self.dist = dist
+            # host-side waits (the sharded leg: no collective kernel may sit on a GPU it uses)
+            self.cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=3600)) \
+                if backend != "gloo" else None
+
+    def cpu_barrier(self):
+        if self.dist is not None:
+            self.dist.barrier(group=self.cpu_group)
 
     def barrier(self):
         if self.dist is not None:
@@ -488,6 +505,39 @@ def device_of(local_rank):
     return local_rank % nd if nd > 0 else local_rank
 
 
+def exchange_floor(dev, chains, n, rounds):
+    """roofline.latency's measured floor (hgx_exchange_floor_bench): per round of the persistent
+    recurrence, every chain's workgroup publishes its n-byte candidate row + granule and polls every
+    other chain's -- k_round_p's all-to-all hand-off with the search taken out; chains = 2 is one
+    1-to-1 hand-off each way. Returns (us per round at `chains`, us per 1-to-1 round) or None."""
+    import ctypes as C
+    from babble_amd import _lib
+    L = _lib.lib()
+    out = []
+    for c in (chains, 2):
+        us = C.c_double(0.0)
+        if L.hgx_exchange_floor_bench(int(dev), int(c), int(n), int(max(1, rounds)), C.byref(us)) != 0:
+            return None
+        out.append(us.value)
+    return out
+
+
+def latency_roofline(dev, n, chains, rounds, ms_per_pass):
+    """The recurrence is a latency chain (neither HBM nor VALU bound): its floor is rounds x the
+    exchange of one round. frac = floor / the kernel's measured time per pass."""
+    if not (16 < n <= 256) or chains < 2 or rounds < 1 or ms_per_pass <= 0:
+        return None
+    fl = exchange_floor(dev, chains, n, min(rounds, 4096))
+    if fl is None:
+        return {"error": "hgx_exchange_floor_bench failed"}
+    floor_ms = rounds * fl[0] * 1e-3
+    return {"rounds": int(rounds), "exchange_us_per_round": fl[0], "handoff_1to1_us_per_round": fl[1],
+            "floor_ms": floor_ms, "frac": floor_ms / ms_per_pass, "us_per_round_measured": ms_per_pass * 1e3 / rounds,
+            "note": f"floor = rounds x the measured all-to-all exchange of one round ({chains} resident workgroups "
+                    f"publishing an {n}-byte row + granule write-through and polling all the others', no search; "
+                    "hgx_exchange_floor_bench, this run, same GPU); frac = floor / the kernel's ms per pass"}
+
+
 def run_sharded(args):
     """C3's north-star single-graph mode (BASELINE configs[2]): ONE graph whose round recurrence is
     chain-sharded over `--gpus` devices in one process (hgx_create_sharded): shard k
@@ -495,17 +545,22 @@ def run_sharded(args):
     candidate rows and granules written into every shard's window over the peer mapping) and their
     consensus timestamps; inserts, lastAncestors, fame, round received and the sort are replicated.
     With fewer devices than shards, shards share a device (the same code: its windows are then local).
+    The columns are handed over as the headline's (hgx_events32, host RAM at the start of each step).
     Strong scaling: value = the graph's ordered events per step / the step's wall time."""
     from babble_amd import trace
     from babble_amd.hashgraph import Hashgraph, compact_columns
     import torch
     n, E, G, silent, stale, depth, desc = CONFIGS[args.config]
-    if G != 1:
-        raise SystemExit("--sharded: one graph per run (c1, c2, c3, c5)")
+    if G != 1 or n > 256:
+        raise SystemExit("--sharded: one graph of at most 256 peers per run (c1, c2, c3)")
     ndev = max(1, torch.cuda.device_count())
     devs = [k % ndev for k in range(args.gpus)]
+    if args.remote_windows and len(set(devs)) == len(devs):
+        args.remote_windows = False   # (every window is remote already)
     tr = trace.gossip(n, E, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
     h = Hashgraph(n, capacity=tr.E, shard_devices=devs)
+    if args.remote_windows:
+        h.set_shard_remote(True)
     cols = compact_columns(tr)
 
     def step():
@@ -513,10 +568,17 @@ def run_sharded(args):
         h.insert_and_run32(cols)
         return int(h.L.hgx_consensus_events_count(h.ctx, 0))
 
+    h.set_kernel_timing(False)
     for w in range(max(1, args.warmup)):
         tw = time.time()
         ordered = step()
         log(f"[sharded x{len(devs)}] warmup {w}: {ordered} ordered in {time.time() - tw:.2f}s  {h.phase_times()}")
+    # shard 0's kernels on one untimed pass (HIP events on its stream)
+    h.set_kernel_timing(True)
+    h.reset_stats()
+    step()
+    ks_w = h.kernel_stats()
+    h.set_kernel_timing(False)
     t0 = time.perf_counter()
     ordered = 0
     for _ in range(args.steps):
@@ -528,19 +590,77 @@ def run_sharded(args):
     checks = {"full_size": "skipped"}
     if not args.no_check:
         checks["full_size"] = full_size_checks(h, tr, 1)
-    print(json.dumps({
+    rounds = int(h.LastRound()) + 1
+    rs = ks_w.get("round_search", {"ms": 0.0, "launches": 0})
+    line = {
         "metric": "consensus-ordered events/sec at N=256 peers (1 GPU and 8-GPU batched sims)",
         "value": ordered * args.steps / t_el, "unit": "consensus-ordered events/s", "n_gpus": len(set(devs)),
         "shards": len(devs), "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_el * 1e3 / args.steps,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic (seeded random-gossip trace), in host RAM at the start of every step",
         "config": {"workload": desc, "config": args.config, "peers": n, "events": int(tr.E),
-                   "shard_devices": devs,
+                   "shard_devices": devs, "windows": "remote (system-scope stores, test switch)" if args.remote_windows
+                   else ("peer-mapped across devices" if len(set(devs)) > 1 else "local (shards share the device)"),
+                   "host_columns": "hgx_events32 (61 B/event)",
                    "parallelism": f"one graph, round recurrence chain-sharded x{len(devs)} over devices {devs} "
                                   f"(firstDescendants, recurrence workgroups and consensus timestamps per chain "
                                   f"block; the rest replicated), one process",
                    "phase_ms_last_step": {k: round(float(v), 3) for k, v in ph.items()}},
-        "checks": checks}), flush=True)
+        "rounds": rounds,
+        "kernels_shard0_ms": {k: round(v["ms"], 4) for k, v in ks_w.items()},
+        "checks": checks}
+    if rs["ms"] > 0:
+        b = kernel_bytes("round_search", n, tr.E, 0, ph["compact"])
+        ach = b / (rs["ms"] * 1e-3) / 1e9
+        line["roofline"] = {"kernel": "round_search", "bound": BOUND["round_search"], "achieved": ach,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                            "ms_per_pass": rs["ms"], "algorithmic_bytes_per_pass": b,
+                            "note": "shard 0's k_round_p launch (its chain block; every shard's launch spans the "
+                                    "whole recurrence, the rounds are shared)"}
+    if not args.no_cpu_baseline:
+        sample = min(E, SAMPLE.get(n, 20000))
+        ts = trace.gossip(n, sample, 1, n_silent=silent, stale_prob=stale, stale_depth=depth)
+        line["cpu_baseline"], _ = cpu_baseline(ts, n, desc)
+    print(json.dumps(line), flush=True)
+
+
+def sharded_leg(args, world):
+    """rank 0 of an N-rank run: C3's single-graph mode over all N devices, in a child process
+    (bench.py --sharded --gpus N) so that a failure there cannot take the replica line with it.
+    Returns the child's line, or an error record."""
+    import subprocess
+    n, E, G, *_ = CONFIGS[args.config]
+    if G != 1 or n > 256 or world > n:
+        return {"skipped": f"{args.config}: the chain-sharded mode takes one graph of at most 256 peers and at "
+                           f"most one shard per chain"}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+                        "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE")}
+    try:
+        import torch
+        ndev = max(1, torch.cuda.device_count())
+    except Exception:
+        ndev = 1
+    per_dev = -(-world // ndev)
+    if per_dev > 1:   # shards sharing a device need a hardware queue each (hgx_create_sharded)
+        env["GPU_MAX_HW_QUEUES"] = str(max(int(env.get("GPU_MAX_HW_QUEUES", "4")), per_dev + 4))
+    cmd = [sys.executable, os.path.abspath(__file__), "--sharded", "--gpus", str(world), "--config", args.config,
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline"]
+    if args.no_check:
+        cmd.append("--no-check")
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        return {"error": "the sharded leg did not finish within 900 s"}
+    sys.stderr.write(r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit status {r.returncode}", "stderr_tail": r.stderr[-1500:]}
+    d = json.loads(lines[-1])
+    d["leg_seconds"] = round(time.time() - t0, 1)
+    return d
 
 
 def run_sharded_ranks(args, red, world, rank, local_rank):
@@ -588,6 +708,21 @@ def run_sharded_ranks(args, red, world, rank, local_rank):
               flush=True)
 
 
+def self_launch(args) -> int:
+    """`--gpus N` (N > 1) without torch.distributed.run: run it as a child process -- one rank per GPU,
+    127.0.0.1 rendezvous, this script with the same arguments -- and return its exit status. Nothing in
+    this process has initialised a GPU at this point."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[launch] --gpus {args.gpus} without a launcher: {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -599,16 +734,23 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the full-size property checks")
     ap.add_argument("--no-chunked", action="store_true", help="skip the SyncLimit-chunked schedule leg")
     ap.add_argument("--sync-limit", type=int, default=1000)
-    ap.add_argument("--columns", default="packed", choices=["packed", "compact", "wide"],
-                    help="how the caller hands the events over: hgx_events_packed (10 B structure + 45 B payload "
-                         "per event, the default), hgx_events32 (61 B) or hgx_events (108 B)")
+    ap.add_argument("--columns", default="compact", choices=["packed", "compact", "wide"],
+                    help="how the caller hands the events over: hgx_events32 (61 B per event, the default: what a "
+                         "caller fills from its events), hgx_events_packed (10 B structure + 45 B payload, built from "
+                         "hgx_events32 by a host pass the `packed_columns` leg times) or hgx_events (108 B)")
     ap.add_argument("--wide", action="store_true", help="= --columns wide")
     ap.add_argument("--sharded", action="store_true",
                     help="C3's single-graph mode in one process: the round recurrence chain-sharded over --gpus devices "
                          "(shards share a device when there are fewer; strong scaling) instead of replicas")
     ap.add_argument("--sharded-ranks", action="store_true",
                     help="C3's mode over torch.distributed ranks: consensus timestamps per creator block, all-gathered")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="rank reductions: auto = RCCL when every rank has its own GPU, else gloo")
+    ap.add_argument("--remote-windows", action="store_true",
+                    help="--sharded: the shards' window stores take the cross-device path even on a shared device")
+    ap.add_argument("--no-sharded-leg", action="store_true", help="N > 1: skip the single-graph sharded leg")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="ranks meet, reduce and report only (no GPU work): the self-launch's CPU test")
     ap.add_argument("--round-kernel", default="auto",
                     help="DivideRounds' round kernel (Hashgraph.set_round_kernel; measurement A/B, e.g. auto-steps)")
     ap.add_argument("--round-shards", type=int, default=1,
@@ -619,6 +761,7 @@ def main():
         # other): set before the HIP runtime starts
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(args.gpus, args.round_shards) + 4))
 
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -626,7 +769,22 @@ def main():
         if world > 1:
             raise SystemExit("--sharded runs one process over --gpus devices (not under torch.distributed.run)")
         return run_sharded(args)
+    if not launched and args.gpus > 1:
+        # no launcher: start one (a child process; nothing here has touched a GPU) and take its status
+        return self_launch(args)
+    if launched and world > 1 and args.gpus not in (1, world):
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
     red = Reducer(world, local_rank, backend=args.backend)
+    if args.launch_check:
+        red.barrier()
+        ranks = int(red.sum(1.0))
+        t_max = red.max(float(rank))
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_reporting": ranks, "max_rank": t_max,
+                              "backend": getattr(red, "backend", None)}), flush=True)
+        if red.dist is not None:
+            red.dist.destroy_process_group()
+        return 0
     if args.sharded_ranks:
         if world < 2:
             raise SystemExit("--sharded-ranks needs torch.distributed.run with >= 2 ranks")
@@ -720,6 +878,29 @@ def main():
         tc = time.time()
         checks["full_size"] = full_size_checks(h, tr, G)
         log(f"[rank {rank}] full-size checks passed in {time.time() - tc:.1f}s")
+    rounds_pass = int(h.LastRound()) + 1 if G == 1 else None
+
+    # side leg: the packed columns (hgx_events_packed) built from the headline's columns by
+    # the host pass a caller holding hgx_events32 would run (hgx_pack_events32), timed inside the step
+    packed = None
+    if cols is not None and args.columns == "compact":
+        h.clear()
+        h.insert_and_run_packed(pack_columns(cols, 0))
+        t_pack, tq0 = 0.0, time.perf_counter()
+        for _ in range(args.steps):
+            tq = time.perf_counter()
+            pk2 = pack_columns(cols, 0)
+            t_pack += time.perf_counter() - tq
+            h.clear()
+            h.insert_and_run_packed(pk2)
+        t_all = (time.perf_counter() - tq0) / args.steps
+        t_pack /= args.steps
+        m1 = total // max(1, args.steps)
+        packed = {"value_incl_pack": m1 / t_all, "ms_per_step_incl_pack": t_all * 1e3, "pack_ms": t_pack * 1e3,
+                  "value_excl_pack": m1 / (t_all - t_pack), "ms_per_step_excl_pack": (t_all - t_pack) * 1e3,
+                  "exceptions": int(len(pk2["exc_pos"])), "unit": "consensus-ordered events/s",
+                  "note": "hgx_insert_and_run_packed (10 B structure + 45 B payload per event cross PCIe) after "
+                          "hgx_pack_events32 on the host (one thread) inside the step; not the headline"}
 
     result = None
     if rank == 0:
@@ -814,12 +995,18 @@ def main():
                                  "rate from SQ_INSTS_VALU (profiles/valu_<cfg>.json)"},
             "kernels_per_pass": per_pass,
             "sort_radix_passes": sort_passes,
+            "packed_columns": packed,
             "hbm_resident": {"value": total // max(1, args.steps) / t_hbm, "unit": "consensus-ordered events/s",
                              "ms_per_step": t_hbm * 1e3,
                              "note": "the same step with the event columns already in HBM (hgx_insert_events_device, "
                                      "no H2D inside the step); not the headline"},
             "checks": checks,
         }
+        if dom == "round_search" and rounds_pass and phases.get("round_p_runs", 0) > 0:
+            try:
+                result["roofline"]["latency"] = latency_roofline(dev, n, n, rounds_pass, dom_ms)
+            except Exception as e:  # reported, never fatal
+                result["roofline"]["latency"] = {"error": str(e)}
         if not args.no_ingest:
             try:
                 result["ingest_sha256"] = ingest_leg(int(tr.E), args.steps, args.warmup, dev)
@@ -856,10 +1043,29 @@ def main():
             result["cpu_baseline"] = base
             checks["prefix_parity"] = prefix_parity(ts, o, dev)
             log(f"[rank {rank}] prefix parity ({sample} events) bit-exact")
+    if world > 1 and not args.no_sharded_leg:
+        # C3's single-graph mode over all N devices: every rank releases its GPU memory first, and the
+        # other ranks wait on the host (no collective kernel may occupy a GPU the leg's persistent
+        # recurrence needs whole)
+        h.close()
+        dtr.close()
+        try:
+            import torch
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        except Exception:
+            pass
+        red.cpu_barrier()
+        if rank == 0:
+            tsl = time.time()
+            result["sharded"] = sharded_leg(args, world)
+            log(f"[rank 0] sharded leg in {time.time() - tsl:.1f}s")
+        red.cpu_barrier()
+    if rank == 0:
         print(json.dumps(result), flush=True)
     if red.dist is not None:
         red.dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

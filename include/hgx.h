@@ -437,6 +437,13 @@ int32_t hgx_sha256_bench(int32_t device, int64_t count, int32_t min_len, int32_t
                          int32_t warmup, int32_t iters, double* ms_per_launch, int64_t* total_bytes,
                          int64_t* n_blocks, int64_t n_sample, uint8_t* sample32);
 
+/* Measurement (bench.py roofline.latency): the exchange floor of one round of the persistent
+ * recurrence -- `chains` resident workgroups of k_round_p's geometry at n coordinates (16 < n <= 256,
+ * chains <= the device's CUs) that per round only publish their n-byte candidate row and granule
+ * (write-through) and poll every other one's (sc1), no search. *us_per_round from HIP events over one
+ * launch of `rounds` rounds after a warm-up launch; chains = 2 is one 1-to-1 hand-off each way. */
+int32_t hgx_exchange_floor_bench(int32_t device, int32_t chains, int32_t n, int32_t rounds, double* us_per_round);
+
 /* ---- ingest front end: batched ECDSA P-256 verify ------ */
 /* Event.Verify (hashgraph/event.go:142-152) for a whole sync batch: crypto.ToECDSAPub of
  * Body.Creator (crypto/utils.go:22-28) and crypto.Verify (crypto/utils.go:41-43) = Go's
@@ -513,6 +520,11 @@ int32_t hgx_set_sort_kernel(hgx_ctx* ctx, int32_t mode);
  * context), on an empty context only (before the first insert). W shards on one device need
  * GPU_MAX_HW_QUEUES >= W + 2 (HGX_ERR_INVALID otherwise). Same results. */
 int32_t hgx_set_round_shards(hgx_ctx* ctx, int32_t shards);
+/* Test switch of a chain-sharded context (hgx_create_sharded / hgx_set_round_shards): on = 1 writes
+ * every other shard's window as a window on another device (system-scope write-through stores, the
+ * peer path), also where the shards share a device, so a one-GPU box runs the instructions the
+ * shards of an 8-GPU node run. HGX_ERR_INVALID on a context without shards. Same results. */
+int32_t hgx_set_shard_remote(hgx_ctx* ctx, int32_t on);
 /* FindOrder consensus timestamps: 0 = default = 1: one tile of 8 positions per block (k_cts_small /
  * k_cts_tile, hgx_kernels.hip); 2 = resident blocks with three tiles' loads in flight behind the
  * selects of a fourth (hgx_cts.hip) where it applies (32 < n <= 512, at most 4096 chains),

@@ -64,6 +64,10 @@ static void hm_grow(hmap* m) {
     for (int64_t i = 0; i < o.cap; i++) if (o.k[i] != -1) hm_put(m, o.k[i], o.v[i]);
     hm_free(&o);
 }
+static void hm_clear(hmap* m) {
+    for (int64_t i = 0; i < m->cap; i++) m->k[i] = -1;
+    m->n = 0;
+}
 static void hm_put(hmap* m, int64_t key, uint8_t val) {
     if (2 * (m->n + 1) > m->cap) hm_grow(m);
     uint64_t i = mix64((uint64_t)key) & (uint64_t)(m->cap - 1);
@@ -221,11 +225,18 @@ static int strongly_see_raw(const hgo* h, int64_t x, int64_t y) { /* :179-198 */
     for (int i = 0; i < h->n; i++) if (lx[i] >= fy[i]) c++;
     return c >= h->sm;
 }
+/* The memo is a bounded cache like the reference's stronglySeeCache (an LRU of cacheSize entries,
+ * hashgraph.go:170-177): StronglySee is a pure function of the DAG, so dropping entries changes no
+ * result. Bounded at 2^25 entries (~600 MB) so a 10 M-event trace fits the build container. */
+#ifndef HGO_SS_MEMO_MAX
+#define HGO_SS_MEMO_MAX ((int64_t)1 << 25)
+#endif
 int hgo_strongly_see(hgo* h, int64_t x, int64_t y) {    /* :170-177 (memoised) */
     uint8_t v;
     int64_t key = pair_key(x + 2, y + 2);
     if (hm_get(&h->ss_memo, key, &v)) return v;
     int s = strongly_see_raw(h, x, y);
+    if (h->ss_memo.n >= HGO_SS_MEMO_MAX) hm_clear(&h->ss_memo);
     hm_put(&h->ss_memo, key, (uint8_t)s);
     return s;
 }
@@ -591,6 +602,11 @@ int hgo_decide_fame(hgo* h, char* err, int errlen) {
                 }
             }
         }
+        /* votes[y][x] is only ever read for the x it was written for (:671-716), and every x of
+         * round i is done here: Go's one map per call, restated per round so that a call over
+         * thousands of rounds holds one round's votes (same results) */
+        hm_free(&votes);
+        hm_init(&votes, 1 << 10);
         if (witnesses_decided(h, i)) {
             decided_pos[pos] = 1;
             if (!h->has_lcr || i > h->lcr) {            /* setLastConsensusRound (:743-750) */

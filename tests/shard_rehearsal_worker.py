@@ -1,7 +1,9 @@
 """Child process of test_gpu_sharded.py: the chain-sharded recurrence rehearsal with W shard streams,
 run where GPU_MAX_HW_QUEUES >= W + 2 was set before the HIP runtime started (each shard's launch
 needs a hardware queue of its own: its workgroups wait for the other shards' granules). Prints
-"OK <rounds_ms>" when the run is bit-exact with the single persistent launch and the oracle."""
+"OK <rounds_ms>" when the run is bit-exact with the single persistent launch and the oracle.
+argv: n E seed shards [remote [chunk]]: remote = 1 writes the other shards' windows through the
+cross-device path (hgx_set_shard_remote); chunk = events per RunConsensus call (0 = one call)."""
 import sys
 
 import numpy as np
@@ -11,6 +13,8 @@ from babble_amd import trace as gtrace
 from babble_amd.hashgraph import Hashgraph
 
 n, E, seed, shards = (int(a) for a in sys.argv[1:5])
+remote = len(sys.argv) > 5 and sys.argv[5] == "1"
+chunk = int(sys.argv[6]) if len(sys.argv) > 6 and int(sys.argv[6]) > 0 else E
 t = gtrace.gossip(n, E, seed, stale_prob=0.1, stale_depth=3)
 
 
@@ -19,8 +23,11 @@ def run(w):
     h.set_round_shards(w)
     if w == 1:
         h.set_round_kernel("persistent")
-    h.insert_trace(t)
-    h.RunConsensus()
+    elif remote:
+        h.set_shard_remote(True)
+    for lo in range(0, E, chunk):
+        h.insert_trace(t, lo, min(E, lo + chunk))
+        h.RunConsensus()
     return h
 
 
@@ -31,7 +38,7 @@ a, b = hs.results(), h1.results()
 for k in ("round", "witness", "famous", "rr", "cts"):
     assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 assert list(a["order"]) == list(b["order"])
-o = hgref.oracle_run(t).results()
+o = (hgref.oracle_run(t, chunk) if chunk < E else hgref.oracle_run(t)).results()
 for k in ("round", "rr", "cts"):
     assert np.array_equal(np.asarray(a[k]), np.asarray(o[k])), k
 assert list(a["order"]) == list(o["order"])

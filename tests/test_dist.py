@@ -53,3 +53,26 @@ def test_reducer_single_rank_is_identity():
     red = bench.Reducer(1)
     red.barrier()
     assert red.max(3.5) == 3.5 and red.sum(7.0) == 7.0
+
+
+def test_bench_self_launch_without_launcher():
+    """`bench.py --gpus 2` with no torch.distributed.run around it starts the launcher itself (a child
+    process) instead of printing a one-GPU line: both ranks meet and reduce over gloo (no GPU here)."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]   # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_reporting"] == 2 and d["max_rank"] == 1.0 and d["backend"] == "gloo"
+
+
+def test_bench_refuses_mismatched_launcher():
+    """Under a launcher, --gpus must equal the ranks it started (never a line whose n_gpus disagrees)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--launch-check"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode != 0 and "launcher started 2 ranks" in r.stderr

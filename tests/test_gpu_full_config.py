@@ -1,8 +1,9 @@
 """Bit-exact parity at the bench's own full workloads (BASELINE.json configs c2 and c4): the same
 seeded traces bench.py times (bench.make_trace), handed over as it hands them (the packed host
 columns, hgx_insert_and_run_packed), against the C oracle (oracle/, hashgraph.go's loops) on every
-event -- not only the 100 k-event prefix the bench line checks. c3 (10 M events at 256 peers) and c5
-stay covered by prefixes and order properties: the single-threaded oracle would need ~20 min."""
+event -- not only the 100 k-event prefix the bench line checks, block hashes included. c3 (10 M events
+at 256 peers) and c5 are pinned in full by the oracle's digests (test_gpu_full_digests.py): the
+single-threaded oracle needs ~25 / ~40 min for them."""
 import os
 import sys
 
@@ -27,7 +28,7 @@ def test_c2_full_workload_bit_exact():
     assert G == 1 and t.E == 1 << 20
     h = Hashgraph(64, capacity=t.E)
     assert h.insert_and_run_packed(pack_columns(compact_columns(t), 0)) == t.E
-    compare(h, hgref.oracle_run(t), t, hashes=False)
+    compare(h, hgref.oracle_run(t), t, hashes=True)
 
 
 def test_c4_full_workload_bit_exact():

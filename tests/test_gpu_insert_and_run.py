@@ -281,3 +281,26 @@ def test_packed_bad_exception_list():
         assert "bad arguments" in ei.value.msg
     assert a.num_events() == 0
     assert a.insert_events_packed(pk) == 2000
+
+
+@pytest.mark.parametrize("back", ["gid_plus_1", "far_before_0"])
+def test_packed_distance_before_the_first_event(back):
+    """A parent distance that reaches before gid 0 names no event: the decoded parent is
+    HGX_UNKNOWN_PARENT (CheckOtherParent / CheckSelfParent fail, hashgraph.go:404-445), never gid -1
+    (the empty parent) -- ADVICE r05. Same error and accepted prefix as the compact columns with -2."""
+    from babble_amd._lib import HgxError
+    from babble_amd.hashgraph import compact_columns, pack_columns
+    n, E, k0 = 16, 3000, 700
+    cols = compact_columns(gtrace.gossip(n, E, 27))
+    pk = pack_columns(cols, 0)
+    pk["op_back"] = pk["op_back"].copy()
+    pk["op_back"][k0] = k0 + 1 if back == "gid_plus_1" else 0xFFFE
+    cols["op"][k0] = -2
+    a = _hg(n, E)
+    with pytest.raises(HgxError) as ei:
+        a.insert_and_run_packed(pk)
+    b = _hg(n, E)
+    with pytest.raises(HgxError) as ec:
+        b.insert_and_run32(cols)
+    assert ei.value.inserted == k0 == ec.value.inserted and a.num_events() == k0
+    assert ei.value.msg == ec.value.msg and ei.value.code == ec.value.code

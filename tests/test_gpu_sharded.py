@@ -157,14 +157,39 @@ def test_chain_sharded_recurrence_rehearsal(n, E, seed, shards, chunk):
     assert list(a["order"]) == list(o["order"])
 
 
+def _rehearse(n, E, seed, shards, remote=0, chunk=0):
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(shards + 4), PYTHONPATH=os.pathsep.join([HERE, os.path.dirname(HERE)]))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "shard_rehearsal_worker.py"), str(n), str(E), str(seed),
+                        str(shards), str(remote), str(chunk)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), (r.stdout[-2000:], r.stderr[-3000:])
+
+
 @pytest.mark.parametrize("n,E,seed,shards", [(64, 16000, 82, 4), (256, 30000, 84, 4), (256, 30000, 86, 8)])
 def test_chain_sharded_recurrence_rehearsal_more_streams(n, E, seed, shards):
     """W = 4, 8 shard streams: a child process with GPU_MAX_HW_QUEUES = W + 4 (one hardware queue
     per shard, so the shards' workgroups are resident together)."""
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(shards + 4), PYTHONPATH=os.pathsep.join([HERE, os.path.dirname(HERE)]))
-    r = subprocess.run([sys.executable, os.path.join(HERE, "shard_rehearsal_worker.py"), str(n), str(E), str(seed),
-                        str(shards)], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and r.stdout.startswith("OK"), (r.stdout[-2000:], r.stderr[-3000:])
+    _rehearse(n, E, seed, shards)
+
+
+@pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 87, 3, 0), (64, 16000, 88, 5, 4000),
+                                                   (256, 30000, 89, 7, 0), (100, 20000, 90, 6, 5000)])
+def test_chain_sharded_uneven_chain_blocks(n, E, seed, shards, chunk):
+    """Shard chain blocks of unequal size (W does not divide the chains: C k / W rounds down), one-shot
+    and chunked: every split-dependent piece -- the firstDescendants target range, the recurrence's
+    workgroups, the timestamp tiles of a block and the exchange offsets -- must agree on the split."""
+    _rehearse(n, E, seed, shards, 0, chunk)
+
+
+@pytest.mark.parametrize("n,E,seed,shards,chunk", [(64, 16000, 82, 2, 0), (64, 16000, 82, 4, 0),
+                                                   (256, 30000, 86, 8, 0), (256, 24000, 85, 4, 6000),
+                                                   (100, 20000, 90, 3, 5000)])
+def test_chain_sharded_cross_device_instructions(n, E, seed, shards, chunk):
+    """hgx_set_shard_remote: every other shard's window is written through the cross-device path
+    (system-scope sc0 sc1 stores of the candidate rows and granules, as into a peer-mapped window on
+    another GPU; the round rows and timestamps always go through the device-to-device copies), so the
+    one-GPU box executes the instructions an 8-GPU node's shards execute: bit-exact with one context
+    and the oracle, no fallback."""
+    _rehearse(n, E, seed, shards, 1, chunk)
 
 
 @pytest.mark.parametrize("n,E,seed,chunk", [(64, 12000, 91, None), (256, 24000, 93, 4000)])
