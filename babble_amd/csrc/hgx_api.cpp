@@ -1856,6 +1856,14 @@ int32_t hgx_find_order(hgx_ctx* c, hgx_error* err) {
 
 // ---- row-sharded graph --------------------------------------------------
 static void shard_range(const hgx_ctx* c, int32_t rank, int* lo, int* hi) {
+    // (a chain-sharded group's shards use the group's split: every split-dependent piece -- the
+    // firstDescendants target range, the recurrence's workgroups, the timestamp tiles and this
+    // exchange -- must agree on it)
+    if (c->eng.grp && c->eng.grp->W == c->shard_world) {
+        *lo = c->eng.grp->c_split[rank];
+        *hi = c->eng.grp->c_split[rank + 1];
+        return;
+    }
     *lo = (int)((int64_t)c->C * rank / c->shard_world);
     *hi = (int)((int64_t)c->C * (rank + 1) / c->shard_world);
 }
@@ -2413,6 +2421,17 @@ int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     return HGX_OK;
 }
 
+// The first chain of shard k of W: C k / W, rounded down to a multiple of 8 where every shard still gets
+// a non-empty block (C >= 8 W). Each shard launches one workgroup per chain of its block; the hardware
+// deals a launch's workgroups to the 8 XCDs in turn from wherever its dispatcher stands, so W launches
+// sharing a device stay within each XCD's 32 CUs only if every launch puts the same number on each XCD
+// (a multiple of 8 workgroups): C = 256, W = 6 or 7 with blocks of 42-43 / 36-37 chains could not be
+// resident at once (every workgroup waited, gave up and fell back; tools/gpurun/r06_diag_w7.sh).
+static int32_t shard_split(int32_t C, int32_t W, int32_t k) {
+    const int64_t even = (int64_t)C * k / W;
+    return (int32_t)(C >= 8 * W ? even / 8 * 8 : even);
+}
+
 // W shards of one graph: shard 0 is `c` (on devs[0] == its device), shard k a new
 // context on devs[k]; every shard holds the whole DAG, shard k owns chains [C k / W, C (k + 1) / W)
 static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error* err) {
@@ -2470,7 +2489,7 @@ static int32_t setup_group(hgx_ctx* c, int32_t W, const int32_t* devs, hgx_error
     g->W = W;
     for (int k = 0; k < W; k++) {
         g->dev[k] = devs[k];
-        g->c_split[k] = (int32_t)((int64_t)c->C * k / W);
+        g->c_split[k] = shard_split(c->C, W, k);
     }
     g->c_split[W] = c->C;
     c->grp = g;

@@ -17,10 +17,15 @@ template <int HD>
 __device__ __forceinline__ uint32_t swar_ge_count(const uint32_t (&v)[HD], const uint32_t (&nf)[HD]) {
     uint32_t c = 0;
     if constexpr (HD % 2 == 0) {
+        // one chain of v_bcnt_u32_b32 with its accumulate operand (the empty asm keeps the compiler from
+        // re-associating the sum into bcnt(x, 0) + v_add3 trees: 2.5 instead of 3 VALU per dword)
 #pragma unroll
         for (int i = 0; i < HD / 2; i++) {
             const uint64_t s = ((((uint64_t)v[2 * i + 1]) << 32) | v[2 * i]) + ((((uint64_t)nf[2 * i + 1]) << 32) | nf[2 * i]);
-            c += __builtin_popcount((uint32_t)s & 0x80808080u) + __builtin_popcount((uint32_t)(s >> 32) & 0x80808080u);
+            c = __builtin_popcount((uint32_t)s & 0x80808080u) + c;
+            asm volatile("" : "+v"(c));
+            c = __builtin_popcount((uint32_t)(s >> 32) & 0x80808080u) + c;
+            asm volatile("" : "+v"(c));
         }
     } else {
 #pragma unroll

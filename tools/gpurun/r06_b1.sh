@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/r06
 O=gpurun_out/r06
 timeout -k 10 1000 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_bench_dist.py tests/test_gpu_insert_and_run.py \
-  tests/test_gpu_full_config.py tests/test_gpu_sort_seg.py -x -v --timeout 300 --timeout-method thread > $O/b1_tests.log 2>&1 \
+  tests/test_gpu_full_config.py tests/test_gpu_full_digests.py tests/test_gpu_sort_seg.py -x -v --timeout 300 --timeout-method thread > $O/b1_tests.log 2>&1 \
   || { tail -60 $O/b1_tests.log; exit 1; }
 tail -1 $O/b1_tests.log
 timeout -k 10 300 python -u bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-ingest --no-chunked \
