@@ -2421,15 +2421,9 @@ int32_t hgx_set_round_kernel(hgx_ctx* c, int32_t mode) {
     return HGX_OK;
 }
 
-// The first chain of shard k of W: C k / W, rounded down to a multiple of 8 where every shard still gets
-// a non-empty block (C >= 8 W). Each shard launches one workgroup per chain of its block; the hardware
-// deals a launch's workgroups to the 8 XCDs in turn from wherever its dispatcher stands, so W launches
-// sharing a device stay within each XCD's 32 CUs only if every launch puts the same number on each XCD
-// (a multiple of 8 workgroups): C = 256, W = 6 or 7 with blocks of 42-43 / 36-37 chains could not be
-// resident at once (every workgroup waited, gave up and fell back; tools/gpurun/r06_diag_w7.sh).
+// The first chain of shard k of W: C k / W (every split-dependent piece reads c_split or shard_range)
 static int32_t shard_split(int32_t C, int32_t W, int32_t k) {
-    const int64_t even = (int64_t)C * k / W;
-    return (int32_t)(C >= 8 * W ? even / 8 * 8 : even);
+    return (int32_t)((int64_t)C * k / W);
 }
 
 // W shards of one graph: shard 0 is `c` (on devs[0] == its device), shard k a new
