@@ -365,21 +365,30 @@ def chunked_leg(h, tr, sync_limit, check):
     h.clear()
     h.set_kernel_timing(False)
     calls, worst = 0, 0.0
+    per_call = []
     gc.collect()
     gc.disable()   # (a collector pause of this process is not the library's latency: one measured 14.7 ms call)
     t0 = time.perf_counter()
     for lo in range(0, tr.E, sync_limit):
         c0 = time.perf_counter()
         h.insert_trace(tr, lo, min(tr.E, lo + sync_limit))
+        c1 = time.perf_counter()
         h.RunConsensus()
-        worst = max(worst, time.perf_counter() - c0)
+        c2 = time.perf_counter()
+        per_call.append((c2 - c0, c1 - c0))
+        worst = max(worst, c2 - c0)
         calls += 1
     el = time.perf_counter() - t0
     gc.enable()
+    # the five slowest calls: (call index, ms, of which insert ms) -- where the outliers sit in the run
+    top = sorted(range(calls), key=lambda i: -per_call[i][0])[:5]
+    worst_calls = [[i, round(per_call[i][0] * 1e3, 3), round(per_call[i][1] * 1e3, 3)] for i in top]
     ordered = int(h.L.hgx_consensus_events_count(h.ctx, 0))
     res = {"sync_limit": sync_limit, "calls": calls, "events": int(tr.E), "ordered": ordered,
            "value": ordered / el, "unit": "consensus-ordered events/s", "inserted_events_per_s": tr.E / el,
            "ms_per_call": el * 1e3 / calls, "worst_call_ms": worst * 1e3, "seconds": el,
+           "worst_calls": worst_calls,
+           "p99_call_ms": sorted(x[0] for x in per_call)[int(0.99 * (calls - 1))] * 1e3,
            "note": "RunConsensus after every SyncLimit inserted events; same trace as the headline"}
     if check:
         res["full_size_checks"] = full_size_checks(h, tr, 1)["result"]
