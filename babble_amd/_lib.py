@@ -117,6 +117,8 @@ def lib():
         _sig(L, nm, i32, [p, C.POINTER(hgx_events_packed), i64, C.POINTER(C.c_int64), E])
     _sig(L, "hgx_pack_events32", i32, [C.POINTER(hgx_events32), i64, i64, p, p, p, p, p, p, i64,
                                        C.POINTER(C.c_int64), E])
+    _sig(L, "hgx_host_alloc", p, [i64])
+    _sig(L, "hgx_host_free", None, [p])
     _sig(L, "hgx_set_participant_keys", i32, [p, p, E])
     for nm in ("hgx_insert_events_verified", "hgx_insert_events_verified_device"):
         _sig(L, nm, i32, [p, C.POINTER(hgx_events), p, p, i64, C.POINTER(C.c_int64), E])

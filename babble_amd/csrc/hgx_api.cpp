@@ -781,6 +781,19 @@ int32_t hgx_pack_events32(const hgx_events32* ev, int64_t count, int64_t base, u
     return ok(err);
 }
 
+// page-locked, portable (any device's context may copy from it), not mapped: the column copies are
+// plain DMA transfers from it
+void* hgx_host_alloc(int64_t bytes) {
+    if (bytes <= 0) return nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, (size_t)bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
+
+void hgx_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int32_t hgx_set_participant_keys(hgx_ctx* c, const uint8_t* keys65, hgx_error* err) {
     if (!c || !keys65) {
         set_err(err, HGX_ERR_INVALID, "hgx_set_participant_keys: bad arguments");

@@ -34,6 +34,43 @@ def compact_columns(t) -> dict:
                 s=np.ascontiguousarray(t.s, np.uint8), ntx=ntx)
 
 
+class HostBuffer:
+    """One page-locked host allocation (hgx_host_alloc), freed with the object. `.array` is a numpy
+    view over it; the caller keeps the HostBuffer alive while the view is in use."""
+
+    def __init__(self, shape, dtype):
+        dt = np.dtype(dtype)
+        nbytes = max(1, int(np.prod(shape)) * dt.itemsize)
+        self._L = _lib.lib()
+        self.p = self._L.hgx_host_alloc(nbytes)
+        if not self.p:
+            raise MemoryError(f"hgx_host_alloc({nbytes}) failed")
+        raw = (C.c_uint8 * nbytes).from_address(self.p)
+        self.array = np.frombuffer(raw, dtype=np.uint8)[:int(np.prod(shape)) * dt.itemsize].view(dt).reshape(shape)
+
+    def __del__(self):
+        p, self.p = getattr(self, "p", None), None
+        if p:
+            self.array = None
+            self._L.hgx_host_free(p)
+
+
+def pinned_columns(cols: dict) -> dict:
+    """The same columns copied into page-locked host memory (hgx_host_alloc), as a caller that keeps
+    its sync buffers there hands them over. The returned dict holds the buffers under "_buffers"."""
+    out, bufs = {}, []
+    for k, v in cols.items():
+        if isinstance(v, np.ndarray):
+            b = HostBuffer(v.shape, v.dtype)
+            b.array[...] = v
+            bufs.append(b)
+            out[k] = b.array
+        else:
+            out[k] = v
+    out["_buffers"] = bufs
+    return out
+
+
 def pack_columns(cols: dict, base: int) -> dict:
     """hgx_events_packed columns (include/hgx.h) of compact_columns() whose first event gets gid
     `base` (hgx_num_events of the context it goes into): creator as u16, each parent as its

@@ -748,6 +748,9 @@ def main():
                          "caller fills from its events), hgx_events_packed (10 B structure + 45 B payload, built from "
                          "hgx_events32 by a host pass the `packed_columns` leg times) or hgx_events (108 B)")
     ap.add_argument("--wide", action="store_true", help="= --columns wide")
+    ap.add_argument("--host-memory", default="pageable", choices=["pageable", "pinned"],
+                    help="where the caller keeps the host columns: ordinary (pageable) memory, or page-locked "
+                         "buffers from hgx_host_alloc (Core's sync buffers allocated once through the C ABI)")
     ap.add_argument("--sharded", action="store_true",
                     help="C3's single-graph mode in one process: the round recurrence chain-sharded over --gpus devices "
                          "(shards share a device when there are fewer; strong scaling) instead of replicas")
@@ -762,6 +765,8 @@ def main():
                     help="ranks meet, reduce and report only (no GPU work): the self-launch's CPU test")
     ap.add_argument("--round-kernel", default="auto",
                     help="DivideRounds' round kernel (Hashgraph.set_round_kernel; measurement A/B, e.g. auto-steps)")
+    ap.add_argument("--fame-tally", default="popc", choices=["popc", "vote", "mfma"],
+                    help="DecideFame's vote tally (Hashgraph.set_fame_tally; measurement A/B)")
     ap.add_argument("--round-shards", type=int, default=1,
                     help="the chain-sharded recurrence with W shards on this rank's GPU (measurement)")
     args = ap.parse_args()
@@ -799,7 +804,7 @@ def main():
             raise SystemExit("--sharded-ranks needs torch.distributed.run with >= 2 ranks")
         return run_sharded_ranks(args, red, world, rank, local_rank)
 
-    from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns, pack_columns
+    from babble_amd.hashgraph import DeviceTrace, Hashgraph, compact_columns, pack_columns, pinned_columns
     n, E, G, *_ = CONFIGS[args.config]
     if args.wide:
         args.columns = "wide"
@@ -810,6 +815,8 @@ def main():
     h = Hashgraph(n, capacity=tr.E, device=dev, n_graphs=G)
     if args.round_kernel != "auto":
         h.set_round_kernel(args.round_kernel)
+    if args.fame_tally != "popc":
+        h.set_fame_tally(args.fame_tally)
     if args.round_shards > 1:   # the one-GPU rehearsal of a chain-sharded recurrence
         h.set_round_shards(args.round_shards)
     # the columns as the caller hands them over, built before the clock: hgx_events_packed (u16
@@ -817,6 +824,8 @@ def main():
     # hgx_events32 (int32 Index and parents, the coin byte, ntx -1 = nil; 61 B per event), or
     # hgx_events (108 B)
     cols = None if args.columns == "wide" else compact_columns(tr)
+    if cols is not None and args.host_memory == "pinned":
+        cols = pinned_columns(cols)
     pk = pack_columns(cols, 0) if args.columns == "packed" else None
     if pk is not None:
         log(f"[rank {rank}] packed columns: {len(pk['exc_pos'])} exceptions")
@@ -988,6 +997,7 @@ def main():
                            "packed": "hgx_events_packed (u16 creator, int32 Index, u16 parent distances: 10 B "
                                      "structure + 45 B payload per event; %d exceptions)" % (
                                          len(pk["exc_pos"]) if pk is not None else 0)}[args.columns],
+                       "host_memory": args.host_memory if cols is not None else "pageable",
                        "parallelism": f"replicas x{world} (seed-sharded)" +
                                       (f"; recurrence rehearsed in {args.round_shards} chain blocks on one GPU"
                                        if args.round_shards > 1 else ""),

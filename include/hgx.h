@@ -174,6 +174,13 @@ int32_t hgx_insert_and_run_packed(hgx_ctx* ctx, const hgx_events_packed* ev, int
 int32_t hgx_pack_events32(const hgx_events32* ev, int64_t count, int64_t base, uint16_t* creator16, uint16_t* sp_back,
                           uint16_t* op_back, int64_t* exc_pos, int32_t* exc_self_parent, int32_t* exc_other_parent,
                           int64_t exc_cap, int64_t* n_exc, hgx_error* err);
+/* Page-locked host memory for the caller's event columns (Core's sync buffers, allocated once and
+ * reused: C memory, so cgo may hand Go slices over it with unsafe.Slice). Every insert call accepts
+ * pageable memory as well; from page-locked memory the column copies are DMA transfers at the host
+ * link's rate instead of staged copies. NULL on failure or bytes <= 0; hgx_host_free(NULL) is a no-op.
+ * Usable with a context on any device. */
+void* hgx_host_alloc(int64_t bytes);
+void hgx_host_free(void* p);
 /* The same with every hgx_events column a DEVICE pointer on the context's device (events
  * decoded / hashed on the GPU, or a trace resident in HBM). hash and sig_s must be
  * 16-byte aligned. Synchronous: the columns may be reused when the call returns. */

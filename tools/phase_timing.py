@@ -16,6 +16,8 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 n, E, G, *_ = bench.CONFIGS[cfg]
 tr, G = bench.make_trace(cfg, 0)
 h = Hashgraph(n, capacity=tr.E, device=0, n_graphs=G)
+if os.environ.get("HGX_FAME_TALLY"):   # (A/B of DecideFame's tally: popc, vote, mfma)
+    h.set_fame_tally(os.environ["HGX_FAME_TALLY"])
 h.insert_trace(tr)
 for rep in range(reps):
     t = {}
