@@ -2047,11 +2047,15 @@ __global__ void k_root_bound(const int32_t* __restrict__ c_off, const int32_t* _
 // order of a small received set (m <= kSortSmallMax, the incremental schedule's usual
 // case) by ranks: an event's place is the number of events before it in (graph, rr, cts, S)
 // order (consensus_sorter.go:36-51), S compared from HBM only when the first 8 bytes tie.
-// A (256 events) x (256 events) tile per workgroup, the column tile's keys broadcast from
-// LDS, partial counts added to rank[]; then one scatter. 16 x 16 workgroups at m = 4096
-// instead of one workgroup's 78 bitonic stages (LDS-bandwidth bound, 145 us per call).
+// A (256 events) x (64 events) tile per workgroup, the column tile's keys broadcast from LDS,
+// partial counts added to rank[]; then one scatter. One workgroup's 78 bitonic stages were
+// LDS-bandwidth bound (145 us per call); 256 x 256 tiles with a branchy compare loop took 46 us at
+// m ~ 3 500 (the chunked schedule's FindOrder at c3: 196 workgroups, under one wave per SIMD, each
+// thread 256 dependent LDS round trips). 64-key tiles put ~12 waves on every CU and the compare is
+// branch-free (the full-S tie path only on 24 equal key bytes).
 constexpr int kSortSmallMax = 4096;
 constexpr int kRankTile = 256;
+constexpr int kRankJT = 64;
 
 struct SortKey {
     uint64_t hi, lo, s8;   // (graph << 32 | rr), cts with the sign flipped, S's first 8 bytes
@@ -2076,11 +2080,11 @@ __global__ void __launch_bounds__(256) k_sort_rank(int32_t m, const int32_t* __r
                                                     const int32_t* __restrict__ p_rr, const int32_t* __restrict__ p_gid,
                                                     const uint8_t* __restrict__ g_S, int n,
                                                     uint32_t* __restrict__ rank) {
-    __shared__ uint64_t jhi[kRankTile], jlo[kRankTile], js8[kRankTile];
-    __shared__ int32_t jp[kRankTile];
+    __shared__ uint64_t jhi[kRankJT], jlo[kRankJT], js8[kRankJT];
+    __shared__ int32_t jp[kRankJT];
     const int i = blockIdx.x * kRankTile + threadIdx.x;
-    const int j0 = blockIdx.y * kRankTile;
-    const int jn = min(kRankTile, m - j0);
+    const int j0 = blockIdx.y * kRankJT;
+    const int jn = min(kRankJT, m - j0);
     if ((int)threadIdx.x < jn) {
         const SortKey k = sort_key(list[j0 + threadIdx.x], p_cts, p_chain, p_rr, p_gid, g_S, n);
         jhi[threadIdx.x] = k.hi;
@@ -2088,22 +2092,30 @@ __global__ void __launch_bounds__(256) k_sort_rank(int32_t m, const int32_t* __r
         js8[threadIdx.x] = k.s8;
         jp[threadIdx.x] = k.p;
     }
+    const bool ok = i < m;
+    SortKey me{};
+    if (ok) me = sort_key(list[i], p_cts, p_chain, p_rr, p_gid, g_S, n);
     __syncthreads();
-    if (i >= m) return;
-    const SortKey me = sort_key(list[i], p_cts, p_chain, p_rr, p_gid, g_S, n);
+    if (!ok) return;
     uint32_t cnt = 0;
-    for (int jj = 0; jj < jn; jj++) {
-        const uint64_t h = jhi[jj], l = jlo[jj], q = js8[jj];
-        bool before;
-        if (h != me.hi) before = h < me.hi;
-        else if (l != me.lo) before = l < me.lo;
-        else if (q != me.s8) before = q < me.s8;
-        else if (j0 + jj == i) before = false;   // itself (without this, every diagonal step reads S from HBM)
-        else {   // 8 equal bytes of S: the whole S, then the list order
-            const int c = cmp_s(g_S + (size_t)p_gid[jp[jj]] * 32, g_S + (size_t)p_gid[me.p] * 32);
-            before = c < 0 || (c == 0 && j0 + jj < i);
+    bool tie = false;   // some key of the tile equals this one in all 24 compared bytes (not itself)
+#pragma unroll 8
+    for (int jj = 0; jj < kRankJT; jj++) {
+        if (jj < jn) {
+            const uint64_t h = jhi[jj], l = jlo[jj], q = js8[jj];
+            const bool eh = h == me.hi, el = l == me.lo;
+            const bool before = h < me.hi || (eh && (l < me.lo || (el && q < me.s8)));
+            cnt += before ? 1u : 0u;
+            tie |= eh && el && q == me.s8 && j0 + jj != i;
         }
-        cnt += before ? 1u : 0u;
+    }
+    if (tie) {   // 8 equal bytes of S: the whole S, then the list order
+        const uint8_t* si = g_S + (size_t)p_gid[me.p] * 32;
+        for (int jj = 0; jj < jn; jj++) {
+            if (jhi[jj] != me.hi || jlo[jj] != me.lo || js8[jj] != me.s8 || j0 + jj == i) continue;
+            const int c = cmp_s(g_S + (size_t)p_gid[jp[jj]] * 32, si);
+            cnt += (c < 0 || (c == 0 && j0 + jj < i)) ? 1u : 0u;
+        }
     }
     if (cnt) atomicAdd(&rank[i], cnt);
 }
@@ -2609,8 +2621,8 @@ bool sort_small_ok(int32_t m) { return m <= kSortSmallMax; }
 
 void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals) {
     // (rank[] = val_b[0, m) zeroed by the caller)
-    const unsigned t = (unsigned)((m + kRankTile - 1) / kRankTile);
-    hipLaunchKernelGGL(k_sort_rank, dim3(t, t), dim3(kRankTile), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr,
+    const unsigned t = (unsigned)((m + kRankTile - 1) / kRankTile), tj = (unsigned)((m + kRankJT - 1) / kRankJT);
+    hipLaunchKernelGGL(k_sort_rank, dim3(t, tj), dim3(kRankTile), 0, s, m, a.recv_list, a.p_cts, a.p_chain, a.p_rr,
                        a.p_gid, a.g_S, n, a.val_b);
     hipLaunchKernelGGL(k_sort_place, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.val_b, a.val_a);
     *final_vals = a.val_a;

@@ -773,7 +773,8 @@ def main():
     if args.sharded or args.round_shards > 1:
         # shards that share a device need a hardware queue each (their launches wait for each
         # other): set before the HIP runtime starts
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(args.gpus, args.round_shards) + 4))
+        need = max(args.gpus, args.round_shards) + 4
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), need))
 
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
