@@ -309,8 +309,7 @@ void Engine::kbeg(int k, bool sample, int64_t count) {
         hipEvent_t e;
         // timing only (nothing on the host waits on them): no system-scope fences, so that the
         // events bracketing every round-step replay cost the timed region as little as possible
-        static const bool sysfence = getenv("HGX_EVENT_SYSFENCE") != nullptr;   // (A/B of the event flavour)
-        if (hipEventCreateWithFlags(&e, sysfence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess) return;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return;
         kev.push_back(e);
     }
     (void)hipEventRecord(kev[kev_used], stream);

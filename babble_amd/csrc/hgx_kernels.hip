@@ -97,94 +97,6 @@ __global__ void __launch_bounds__(256) k_layout_direct(int64_t E0, int64_t E, co
                p_ts, p_rr, p_cts, C, n, seg);
 }
 
-__global__ void __launch_bounds__(256) k_layout(int64_t E0, int64_t E, const int32_t* __restrict__ g_creator,
-                                                const int32_t* __restrict__ g_index, const int64_t* __restrict__ g_ck,
-                                                const int32_t* __restrict__ g_op,
-                                                const int64_t* __restrict__ g_ts, const int32_t* __restrict__ g_rr,
-                                                const int64_t* __restrict__ g_cts, const int32_t* __restrict__ c_off,
-                                                const int32_t* __restrict__ c_base, int32_t* __restrict__ g_pos,
-                                                int32_t* __restrict__ p_gid, int32_t* __restrict__ p_chain,
-                                                int32_t* __restrict__ p_op, int32_t* __restrict__ p_opu,
-                                                int32_t* __restrict__ p_opk, int64_t* __restrict__ p_ts,
-                                                int32_t* __restrict__ p_rr, int64_t* __restrict__ p_cts, int C, int n,
-                                                int seg) {
-    __shared__ int32_t s_cnt[kLayoutH], s_min[kLayoutH];
-    __shared__ int32_t s_slot[kLayoutB];   // slot -> gid offset in the block
-    __shared__ int32_t s_lo, s_hi;
-    // XCD-grouped block order: blocks b, b + 8, b + 16, ... run on one XCD (the dispatcher's b % 8
-    // placement, for speed only), so each XCD takes one contiguous eighth of the gids in order and
-    // the op parents its blocks look up (mostly recent events) sit in its own L2
-    const int nbk = (int)gridDim.x, q8 = nbk / 8, r8 = nbk % 8, x8 = (int)blockIdx.x % 8;
-    const int lb = x8 * q8 + min(x8, r8) + (int)blockIdx.x / 8;   // XCD x8's j-th block (a bijection)
-    const int64_t g0 = E0 + (int64_t)lb * kLayoutB;
-    const int nb = (int)min<int64_t>(kLayoutB, E - g0);
-    if (threadIdx.x == 0) { s_lo = 0x7FFFFFFF; s_hi = -1; }
-    for (int h = threadIdx.x; h < kLayoutH; h += 256) { s_cnt[h] = 0; s_min[h] = 0x7FFFFFFF; }
-    __syncthreads();
-    int lo = 0x7FFFFFFF, hi = -1;
-    for (int t = threadIdx.x; t < nb; t += 256) {
-        const int c = g_creator[g0 + t];
-        lo = min(lo, c);
-        hi = max(hi, c);
-    }
-    for (int o = 32; o >= 1; o >>= 1) { lo = min(lo, __shfl_xor(lo, o)); hi = max(hi, __shfl_xor(hi, o)); }
-    if ((threadIdx.x & 63) == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
-    __syncthreads();
-    const int clo = s_lo;
-    if (s_hi - clo >= kLayoutH) {   // block-uniform: too many chains to group, direct scatter
-        for (int t = threadIdx.x; t < nb; t += 256) {
-            const int64_t gid = g0 + t;
-            const int c = g_creator[gid];
-            const int p = c_off[c] + g_index[gid] - c_base[c];
-            g_pos[gid] = p;
-            layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op,
-                       p_opu, p_opk, p_ts, p_rr, p_cts, C, n, seg);
-        }
-        return;
-    }
-    // per chain: events in the block and their smallest index
-    for (int t = threadIdx.x; t < nb; t += 256) {
-        const int64_t gid = g0 + t;
-        const int h = g_creator[gid] - clo;
-        atomicAdd(&s_cnt[h], 1);
-        atomicMin(&s_min[h], g_index[gid]);
-    }
-    __syncthreads();
-    // exclusive scan of the counts (one wave)
-    if (threadIdx.x < 64) {
-        constexpr int PER = kLayoutH / 64;
-        int v[PER], sum = 0;
-#pragma unroll
-        for (int k = 0; k < PER; k++) { v[k] = s_cnt[threadIdx.x * PER + k]; sum += v[k]; }
-        int incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if ((int)threadIdx.x >= o) incl += y;
-        }
-        int run = incl - sum;
-#pragma unroll
-        for (int k = 0; k < PER; k++) { s_cnt[threadIdx.x * PER + k] = run; run += v[k]; }
-    }
-    __syncthreads();
-    // slot of an event = run start of its chain + (index - smallest index of the chain in the block)
-    for (int t = threadIdx.x; t < nb; t += 256) {
-        const int64_t gid = g0 + t;
-        const int c = g_creator[gid];
-        const int h = c - clo;
-        const int idx = g_index[gid];
-        s_slot[s_cnt[h] + idx - s_min[h]] = t;
-        g_pos[gid] = c_off[c] + idx - c_base[c];
-    }
-    __syncthreads();
-    // consecutive slots = consecutive positions within a chain's run
-    for (int sl = threadIdx.x; sl < nb; sl += 256) {
-        const int64_t gid = g0 + s_slot[sl];
-        const int c = g_creator[gid];
-        const int p = c_off[c] + g_index[gid] - c_base[c];
-        layout_one(gid, p, g_creator, g_ck, g_op, g_ts, g_rr, g_cts, c_off, c_base, p_gid, p_chain, p_op, p_opu,
-                   p_opk, p_ts, p_rr, p_cts, C, n, seg);
-    }
-}
 
 // Round 5: the same grouping, with every input column read in gid order (coalesced) and written out in
 // slot order (coalesced) through an LDS stage: the slot-order pass of k_layout read six columns scattered
@@ -2254,8 +2166,6 @@ void launch_copy_many(hipStream_t s, const CopyRange* r, int count) {
 }
 
 void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int C, int n, int seg) {
-    // (HGX_LAYOUT_ROUND4=1 in the environment: the round-4 k_layout, for A/B measurements)
-    static const bool layout_staged = getenv("HGX_LAYOUT_ROUND4") == nullptr;
     if (E <= E0) return;
     hipLaunchKernelGGL(k_ck_pack, dim3(nblk(E - E0, 256)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.c_base,
                        a.g_ck);
@@ -2265,14 +2175,9 @@ void launch_layout(hipStream_t s, int64_t E0, int64_t E, const DevArrays& a, int
                            a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
         return;
     }
-    if (layout_staged)
-        hipLaunchKernelGGL(k_layout_staged, dim3(nblk(E - E0, kLayoutB2)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index,
-                           a.g_ck, a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
-                           a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
-    else
-        hipLaunchKernelGGL(k_layout, dim3(nblk(E - E0, kLayoutB)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index, a.g_ck,
-                           a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op, a.p_opu,
-                           a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
+    hipLaunchKernelGGL(k_layout_staged, dim3(nblk(E - E0, kLayoutB2)), dim3(256), 0, s, E0, E, a.g_creator, a.g_index,
+                       a.g_ck, a.g_op, a.g_ts, a.g_rr, a.g_cts, a.c_off, a.c_base, a.g_pos, a.p_gid, a.p_chain, a.p_op,
+                       a.p_opu, a.p_opk, a.p_ts, a.p_rr, a.p_cts, C, n, seg);
 }
 
 void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int seg, int first, int32_t* chg,
