@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define HGX_ABI_VERSION 5   /* 5: hgx_events_packed (hgx_insert_events_packed, hgx_insert_and_run_packed,
+#define HGX_ABI_VERSION 6   /* 6: hgx_host_alloc / hgx_host_free (page-locked caller buffers);
+                              5: hgx_events_packed (hgx_insert_events_packed, hgx_insert_and_run_packed,
                                  hgx_pack_events32);
                               4: hgx_create_sharded (chain-sharded recurrence over devices);
                               3: HGX_ROOT_OTHER needs its key registered (hgx_set_root_others) */

@@ -29,7 +29,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().hgx_abi_version() == 5
+    assert _lib.lib().hgx_abi_version() == 6
 
 
 def test_create_fails_loudly_without_gpu():
