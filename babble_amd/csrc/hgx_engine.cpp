@@ -1818,8 +1818,14 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         const bool seg_try = sort_seg_enabled && nseg64 >= 1 && nseg64 <= (int64_t)1 << 24;
         const int nseg = (int)nseg64;
         if (seg_try) {   // (the bucket counts with the timestamp range, one pass)
-            if (seg_off.n < (size_t)nseg + 1) HGX_TRY(seg_off.alloc((size_t)nseg + 1));
-            if (seg_cur.n < (size_t)nseg + 1) HGX_TRY(seg_cur.alloc((size_t)nseg + 1));
+            // sized for the round tables' capacity (then doubled): an exact-size reallocation whenever R
+            // had grown since the last bucket sort was a hipFree + hipMalloc inside a chunked-schedule
+            // FindOrder (1-2 ms calls)
+            if (seg_off.n < (size_t)nseg + 1) {
+                const size_t cap = std::max({(size_t)nseg + 1, (size_t)G * std::max(r_cap, 1) + 1, 2 * seg_off.n});
+                HGX_TRY(seg_off.alloc(cap));
+                HGX_TRY(seg_cur.alloc(cap));
+            }
             HGX_TRY(hipMemsetAsync(seg_off.p, 0, (size_t)nseg * 4, stream));
             launch_seg_count(stream, a, m, R, n, nseg, seg_off.p, (unsigned long long*)minmax.p + 2);
         } else {
