@@ -434,13 +434,17 @@ __device__ __forceinline__ uint32_t wave_incl_max_u(uint32_t x) {
 
 // ---------------------------------------------------------------------------------
 // firstDescendants: FD[(d,j)][c] = min{k : LA[(c,k)][d] >= j}, written
-// column-major FDT[c][pos(d,j)]. Block = (chain c, tile of FT rows). Each (d, j, c)
-// is written exactly once; j beyond the chain's last LA value gets MaxInt32.
+// column-major FDT[c][pos(d,j)]. Block = (chain c, tile of FT rows, block of DB target chains).
+// Each (d, j, c) is written exactly once; j beyond the chain's last LA value gets MaxInt32.
+// The tile holds only the block's DB target columns of its rows, so the rows per tile need not
+// shrink as n grows (round 6: n = 1 024 held all 1 024 columns of 16-row tiles, each (tile,
+// target) pair's fixed cost spread over 16 rows; now 64 rows x 256 targets per block).
 template <typename CT>
 __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int n, int nwd,
-                           int FT, int64_t P, const int32_t* __restrict__ c_old, int d_lo, int d_hi) {
+                           int FT, int64_t P, const int32_t* __restrict__ c_old, int d_lo, int d_hi, int DB, int zs) {
     typedef Coord<CT> K;
+    constexpr int CPW = (int)(4 / sizeof(CT));   // coordinates per LA word
     extern __shared__ __attribute__((aligned(16))) int32_t sm[];
     const int c = blockIdx.x;
     const int len = c_len[c];
@@ -459,52 +463,59 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
         if ((int)blockIdx.y >= ntiles) return;
         k0 = (int)blockIdx.y * FT;
     }
+    // this block's target chains [db0, db1): column block blockIdx.z / zs; the zs blocks of a column
+    // block split its targets (a resumed call with a few new rows per chain)
+    const int zb = (int)blockIdx.z, cb = zs == 1 ? zb : zb / zs, sub = zb - cb * zs;
+    const int db0 = d_lo + cb * DB, db1 = min(d_hi, db0 + DB);
+    if (db0 >= db1) return;
+    const int wb0 = db0 / CPW, wdw = (db1 + CPW - 1) / CPW - wb0;   // LA words of a tile row
+    const int tb = wb0 * CPW;                                      // first coordinate the tile holds
     const int k1 = min(len, k0 + FT), rows = k1 - k0;
     const int off = c_off[c], base_c = c_base[c];
     const int g = c / n, cl = c % n;
-    // per target chain d of this graph, then the (FT+1)-row tile (row 0 = row k0-1),
-    // rows padded to ldw words against bank conflicts of the per-d searches
+    // per target chain d of the block (index d - db0), then the (FT+1)-row tile (row 0 = row
+    // k0-1), rows padded to ldw words against bank conflicts of the per-d searches
     int32_t* m_len = sm;
-    int32_t* m_base = m_len + n;
-    int32_t* m_off = m_base + n;
-    uint32_t* tw = (uint32_t*)(m_off + n);
-    const int ldw = nwd + 1;
-    const int ld = ldw * (int)(4 / sizeof(CT));   // in coordinates
+    int32_t* m_base = m_len + DB;
+    int32_t* m_off = m_base + DB;
+    uint32_t* tw = (uint32_t*)(m_off + DB);
+    const int ldw = wdw + 1;
+    const int ld = ldw * CPW;   // in coordinates
     const CT* __restrict__ tile = (const CT*)tw;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        m_len[i] = c_len[g * n + i];
-        m_base[i] = c_base[g * n + i];
-        m_off[i] = c_off[g * n + i];
+    for (int i = threadIdx.x; i < db1 - db0; i += blockDim.x) {
+        m_len[i] = c_len[g * n + db0 + i];
+        m_base[i] = c_base[g * n + db0 + i];
+        m_off[i] = c_off[g * n + db0 + i];
     }
-    {   // rows k0-1 .. k1-1 are contiguous in LA
+    {   // words [wb0, wb0 + wdw) of rows k0-1 .. k1-1
         const int r0 = (k0 > 0) ? 0 : 1;   // tile row 0 is unused when k0 == 0
-        const uint32_t* __restrict__ src = LA + (size_t)(off + k0 - 1) * nwd;
-        if (nwd >= 32) {
+        const uint32_t* __restrict__ src = LA + (size_t)(off + k0 - 1) * nwd + wb0;
+        if (wdw >= 32) {
             // straight into LDS (global_load_lds): one wave instruction = <= 64 words of one row
             typedef __attribute__((address_space(3))) void* lds_ptr_t;
             const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-            const int per_row = (nwd + 63) >> 6;
+            const int per_row = (wdw + 63) >> 6;
             for (int q = wave + r0 * per_row; q < (rows + 1) * per_row; q += nwaves) {
                 const int rr = q / per_row, cc = (q % per_row) << 6;
-                if (cc + lane < nwd)
+                if (cc + lane < wdw)
                     __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)rr * nwd + cc + lane),
                                                      (lds_ptr_t)(tw + rr * ldw + cc), 4, 0, 0);
             }
             __builtin_amdgcn_s_waitcnt(0);
         } else {
-            const int nel = (rows + 1 - r0) * nwd;
+            const int nel = (rows + 1 - r0) * wdw;
             const uint32_t* __restrict__ s0 = src + (size_t)r0 * nwd;
             for (int t0 = threadIdx.x; t0 < nel; t0 += 4 * blockDim.x) {
                 uint32_t v[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int tt = t0 + u * blockDim.x;
-                    v[u] = (tt < nel) ? s0[tt] : 0u;
+                    v[u] = (tt < nel) ? s0[(size_t)(tt / wdw) * nwd + tt % wdw] : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int tt = t0 + u * blockDim.x;
-                    if (tt < nel) tw[(tt / nwd + r0) * ldw + (tt % nwd)] = v[u];
+                    if (tt < nel) tw[(tt / wdw + r0) * ldw + (tt % wdw)] = v[u];
                 }
             }
         }
@@ -526,25 +537,22 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     // read while the current one is written: no dependent LDS round trip per chain.
     int32_t* slot = (int32_t*)(tw + (FT + 1) * ldw) + 64 * wave;
     const int ownv = base_c + k0;
-    // gridDim.z > 1 (a resumed call: a few new rows per chain): the target chains are split over
-    // z blocks, so a block's serial per-target loop is z times shorter
-    const int S = __builtin_amdgcn_readfirstlane(nwaves * (int)gridDim.z);   // target stride
-    // the events' chains d in [d_lo, d_hi) (all of them but in the sharded rehearsal)
-    for (int d0 = __builtin_amdgcn_readfirstlane(d_lo + wave + nwaves * (int)blockIdx.z); d0 < d_hi; d0 += S * 64) {
+    const int S = __builtin_amdgcn_readfirstlane(nwaves * zs);   // target stride
+    for (int d0 = __builtin_amdgcn_readfirstlane(db0 + wave + nwaves * sub); d0 < db1; d0 += S * 64) {
         const int dq = d0 + S * lane;
         int q_len = 0, q_base = 0, q_off = 0, q_lo = 0, q_hv = 0;
-        if (dq < d_hi) {
-            q_len = m_len[dq];
-            q_base = m_base[dq];
-            q_off = m_off[dq];
-            q_lo = (k0 > 0) ? K::la(tile[dq]) : q_base - 1;
-            if (rows > 0) q_hv = K::la(tile[rows * ld + dq]);
+        if (dq < db1) {
+            q_len = m_len[dq - db0];
+            q_base = m_base[dq - db0];
+            q_off = m_off[dq - db0];
+            q_lo = (k0 > 0) ? K::la(tile[dq - tb]) : q_base - 1;
+            if (rows > 0) q_hv = K::la(tile[rows * ld + dq - tb]);
         }
-        const int nq = __builtin_amdgcn_readfirstlane(min(64, (d_hi - d0 + S - 1) / S));
-        int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0]) : 0;
+        const int nq = __builtin_amdgcn_readfirstlane(min(64, (db1 - d0 + S - 1) / S));
+        int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0 - tb]) : 0;
         for (int q = 0; q < nq; q++) {
             const int vraw = vnext;
-            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + S * (q + 1)]);
+            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + S * (q + 1) - tb]);
             const int len_d = __builtin_amdgcn_readlane(q_len, q);
             if (len_d == 0) continue;
             const int base_d = __builtin_amdgcn_readlane(q_base, q);
@@ -2207,33 +2215,39 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 }
 
 int fd_tile_rows(int n, int compact) {
-    // <= 64 rows (one per lane), ~33 KB of LDS per block: 4 blocks (32 waves) per CU
-    // (measured at c3: 16 rows 17.2 ms, 32 rows 10.0, 64 rows 6.8; 128 rows in 64-row
-    // chunks 8.9 and 256 rows 14.9 -- fewer resident blocks. The kernel is bound by the
-    // per-(tile, target chain) latency chain, not by bytes.)
-    int ft = (compact ? 16384 : 8192) / n;
-    if (ft > 64) ft = 64;
-    if (ft < 4) ft = 4;
-    return ft;
+    // 64 rows (one per lane) of at most kFdCols target columns (~38 KB of LDS per block: 4 blocks,
+    // 32 waves per CU). Measured at c3 (all 256 columns): 16 rows 17.2 ms, 32 rows 10.0, 64 rows 6.8;
+    // 128 rows in 64-row chunks 8.9 and 256 rows 14.9 -- fewer resident blocks. The kernel is bound by
+    // the per-(tile, target chain) latency chain, not by bytes. Round 6: the rows no longer shrink
+    // with n (n = 1 024 had 16-row tiles of every column); the targets are split into column blocks.
+    (void)n;
+    (void)compact;
+    return 64;
 }
+
+int fd_cols(int compact) { return compact ? 256 : 128; }   // target columns per block (512 bytes a row)
 
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
                      int max_new, int d_lo, int d_hi) {
     if (d_hi < 0) d_hi = n;
+    if (d_hi <= d_lo) return;
     const int ft = fd_tile_rows(n, a.compact);
     // incremental (c_old): tiles from each chain's first new row; max_new = the most new rows of a chain
     const int tiles = c_old ? max(1, (max_new + ft - 1) / ft) : max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
-    // + 8 waves x 64 owner slots
-    const size_t lds = ((size_t)(ft + 1) * (nwd + 1) + 3 * (size_t)n + 8 * 64) * sizeof(int32_t);
-    // a resumed call with a few new rows per chain: target chains split over up to 8 blocks
-    const int z = (c_old && max_new <= ft) ? max(1, min(8, n / 64)) : 1;
+    const int DB = std::min(fd_cols(a.compact), d_hi - d_lo);
+    const int ncb = (d_hi - d_lo + DB - 1) / DB;
+    const int wdw = DB / (a.compact ? 2 : 1) + 1;   // words of a tile row, the worst alignment
+    // tile + per-target scalars + 8 waves x 64 owner slots
+    const size_t lds = ((size_t)(ft + 1) * (wdw + 1) + 3 * (size_t)DB + 8 * 64) * sizeof(int32_t);
+    // a resumed call with a few new rows per chain: a column block's targets split over up to 8 blocks
+    const int zs = (c_old && max_new <= ft) ? max(1, min(8, DB / 64)) : 1;
     if (a.compact)
-        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi);
+        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles, ncb * zs), dim3(512), lds, s, (const uint32_t*)a.LA,
+                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi, DB, zs);
     else
-        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles, z), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi);
+        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles, ncb * zs), dim3(512), lds, s, (const uint32_t*)a.LA,
+                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi, DB, zs);
 }
 
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
