@@ -439,7 +439,7 @@ __device__ __forceinline__ uint32_t wave_incl_max_u(uint32_t x) {
 // The tile holds only the block's DB target columns of its rows, so the rows per tile need not
 // shrink as n grows (round 6: n = 1 024 held all 1 024 columns of 16-row tiles, each (tile,
 // target) pair's fixed cost spread over 16 rows; now 64 rows x 256 targets per block).
-template <typename CT>
+template <typename CT, int RPL>
 __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT, const int32_t* __restrict__ c_off,
                            const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base, int n, int nwd,
                            int FT, int64_t P, const int32_t* __restrict__ c_old, int d_lo, int d_hi, int DB, int zs) {
@@ -549,10 +549,20 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
             if (rows > 0) q_hv = K::la(tile[rows * ld + dq - tb]);
         }
         const int nq = __builtin_amdgcn_readfirstlane(min(64, (db1 - d0 + S - 1) / S));
-        int vnext = (lane < rows) ? K::la(tile[(lane + 1) * ld + d0 - tb]) : 0;
+        // this lane's RPL consecutive tile rows r = RPL lane + u (tile row r + 1: row 0 is k0 - 1)
+        int vnext[RPL];
+#pragma unroll
+        for (int u = 0; u < RPL; u++)
+            vnext[u] = (RPL * lane + u < rows) ? K::la(tile[(RPL * lane + u + 1) * ld + d0 - tb]) : 0;
         for (int q = 0; q < nq; q++) {
-            const int vraw = vnext;
-            if (q + 1 < nq && lane < rows) vnext = K::la(tile[(lane + 1) * ld + d0 + S * (q + 1) - tb]);
+            int vraw[RPL];
+#pragma unroll
+            for (int u = 0; u < RPL; u++) vraw[u] = vnext[u];
+            if (q + 1 < nq) {
+#pragma unroll
+                for (int u = 0; u < RPL; u++)
+                    if (RPL * lane + u < rows) vnext[u] = K::la(tile[(RPL * lane + u + 1) * ld + d0 + S * (q + 1) - tb]);
+            }
             const int len_d = __builtin_amdgcn_readlane(q_len, q);
             if (len_d == 0) continue;
             const int base_d = __builtin_amdgcn_readlane(q_base, q);
@@ -563,19 +573,28 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
             const int hi_val = (rows > 0) ? __builtin_amdgcn_readlane(q_hv, q) : lo;
             const int hi = last ? vmax : min(hi_val, vmax);
             CT* __restrict__ out = FDT + (size_t)cl * P + off_d - base_d;
-            const int v = (lane < rows) ? min(max(vraw, lo), vmax) : hi_val;
-            // first position of this lane's range = previous lane's v + 1 (lane 0: lo + 1)
-            const int start = __builtin_amdgcn_update_dpp(lo, v, 0x138, 0xf, 0xf, false) + 1;   // wave_shr:1
-            const bool own = lane < rows && v >= start;
+            int v[RPL], start[RPL];
+            bool own[RPL];
+#pragma unroll
+            for (int u = 0; u < RPL; u++) v[u] = (RPL * lane + u < rows) ? min(max(vraw[u], lo), vmax) : hi_val;
+            // first position of each row's range = the previous row's v + 1 (row 0: lo + 1); the previous
+            // row of a lane's first row is the last row of the lane before
+            start[0] = __builtin_amdgcn_update_dpp(lo, v[RPL - 1], 0x138, 0xf, 0xf, false) + 1;   // wave_shr:1
+#pragma unroll
+            for (int u = 1; u < RPL; u++) start[u] = v[u - 1] + 1;
+#pragma unroll
+            for (int u = 0; u < RPL; u++) own[u] = RPL * lane + u < rows && v[u] >= start[u];
             const int vlast = max(lo, min(hi_val, vmax));   // end of the tile's last range
             // slots hold owner + 1 (0 = no range starts here)
             uint32_t carry = 0;
             for (int j0 = lo + 1; j0 <= hi; j0 += 64) {   // scalar loop
                 slot[lane] = 0;
                 wave_lds_fence();
-                if (own && (unsigned)(start - j0) < 64u) slot[start - j0] = lane + 1;
-                // past the last row (last tile only): none = MaxInt32, sentinel owner 64
-                if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 65;
+#pragma unroll
+                for (int u = 0; u < RPL; u++)
+                    if (own[u] && (unsigned)(start[u] - j0) < 64u) slot[start[u] - j0] = RPL * lane + u + 1;
+                // past the last row (last tile only): none = MaxInt32, sentinel owner FT
+                if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 64 * RPL + 1;
                 wave_lds_fence();
                 const uint32_t o1 = max(wave_incl_max_u((uint32_t)slot[lane]), carry);
                 carry = (uint32_t)__builtin_amdgcn_readlane((int)o1, 63);
@@ -2215,17 +2234,17 @@ void launch_la_sweep(hipStream_t s, const DevArrays& a, int C, int n, int max_le
 }
 
 int fd_tile_rows(int n, int compact) {
-    // 64 rows (one per lane) of at most kFdCols target columns (~38 KB of LDS per block: 4 blocks,
-    // 32 waves per CU). Measured at c3 (all 256 columns): 16 rows 17.2 ms, 32 rows 10.0, 64 rows 6.8;
-    // 128 rows in 64-row chunks 8.9 and 256 rows 14.9 -- fewer resident blocks. The kernel is bound by
-    // the per-(tile, target chain) latency chain, not by bytes. Round 6: the rows no longer shrink
-    // with n (n = 1 024 had 16-row tiles of every column); the targets are split into column blocks.
-    (void)n;
+    // one 64-row tile per block up to round 5 (measured at c3, all 256 columns in LDS: 16 rows 17.2 ms,
+    // 32 rows 10.0, 64 rows 6.8; 128 rows as two 64-row chunks 8.9, 256 rows 14.9 -- fewer resident
+    // blocks). Round 6: the tile holds fd_cols target columns (~38 KB of LDS at any n, 4 blocks per CU)
+    // and each lane owns 2 consecutive tile rows (4 at n <= 32), so a (tile, target) pair's fixed cost
+    // -- the scalars, the first chunk -- is spread over 128 (256) rows: k_fd_build at c3 5.2 -> 4.35 ms,
+    // c5 2.05 -> 1.75, c4 0.68 -> 0.42 -> 0.33 ms
     (void)compact;
-    return 64;
+    return n <= 32 ? 256 : 128;
 }
 
-int fd_cols(int compact) { return compact ? 256 : 128; }   // target columns per block (512 bytes a row)
+int fd_cols(int compact, int ft) { return (compact ? 256 : 128) * 64 / ft; }   // target columns per block
 
 void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_len, int64_t P, const int32_t* c_old,
                      int max_new, int d_lo, int d_hi) {
@@ -2235,19 +2254,27 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     // incremental (c_old): tiles from each chain's first new row; max_new = the most new rows of a chain
     const int tiles = c_old ? max(1, (max_new + ft - 1) / ft) : max(1, (max_len + ft - 1) / ft);
     const int nwd = a.compact ? n / 2 : n;
-    const int DB = std::min(fd_cols(a.compact), d_hi - d_lo);
+    const int DB = std::min(fd_cols(a.compact, ft), d_hi - d_lo);
     const int ncb = (d_hi - d_lo + DB - 1) / DB;
     const int wdw = DB / (a.compact ? 2 : 1) + 1;   // words of a tile row, the worst alignment
     // tile + per-target scalars + 8 waves x 64 owner slots
     const size_t lds = ((size_t)(ft + 1) * (wdw + 1) + 3 * (size_t)DB + 8 * 64) * sizeof(int32_t);
     // a resumed call with a few new rows per chain: a column block's targets split over up to 8 blocks
     const int zs = (c_old && max_new <= ft) ? max(1, min(8, DB / 64)) : 1;
-    if (a.compact)
-        hipLaunchKernelGGL(k_fd_build<uint16_t>, dim3(C, tiles, ncb * zs), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (uint16_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi, DB, zs);
-    else
-        hipLaunchKernelGGL(k_fd_build<int32_t>, dim3(C, tiles, ncb * zs), dim3(512), lds, s, (const uint32_t*)a.LA,
-                           (int32_t*)a.FDT, a.c_off, a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi, DB, zs);
+    const dim3 grid(C, tiles, ncb * zs);
+#define FD_LAUNCH(CT_, RPL_)                                                                                    \
+    hipLaunchKernelGGL((k_fd_build<CT_, RPL_>), grid, dim3(512), lds, s, (const uint32_t*)a.LA, (CT_*)a.FDT, a.c_off, \
+                       a.c_len, a.c_base, n, nwd, ft, P, c_old, d_lo, d_hi, DB, zs)
+    if (a.compact) {
+        if (ft == 256) FD_LAUNCH(uint16_t, 4);
+        else if (ft == 128) FD_LAUNCH(uint16_t, 2);
+        else FD_LAUNCH(uint16_t, 1);
+    } else {
+        if (ft == 256) FD_LAUNCH(int32_t, 4);
+        else if (ft == 128) FD_LAUNCH(int32_t, 2);
+        else FD_LAUNCH(int32_t, 1);
+    }
+#undef FD_LAUNCH
 }
 
 void launch_round_gather(hipStream_t s, const DevArrays& a, int r, int C, int n, int64_t P) {
