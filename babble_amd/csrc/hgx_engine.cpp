@@ -1805,6 +1805,19 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         launch_fill_many(stream, fr, small ? 5 : 4);
         HGX_TRY(hipGetLastError());
     }
+    // a large order (a full pass: 40 MB at c3) is written straight into the pinned host arena
+    // (coalesced writes over the host link while the kernel runs) instead of a D2H copy after it --
+    // by the bucket sort itself, which finishes every bucket it places (k_seg_sort, SortFinish: its
+    // host-link writes overlap the other buckets' sorting), or by k_finish_order after the other
+    // sorts; a small one comes back with the block tables in the copy launch
+    bool direct = false, finished = false;
+    if (order_dst && (size_t)m * 4 > kCopyKernelMax) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, order_dst, 0) == hipSuccess && d) {
+            a.order_gid = (int32_t*)d;
+            direct = true;
+        }
+    }
     if (small) {
         kbeg(K_SORT);
         launch_sort_small(stream, a, m, n, &vals);
@@ -1848,6 +1861,7 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
                                          &vals, &keys) == hipSuccess;
         if (seg) {
             sort_seg_runs++;
+            finished = true;
             kend(K_SORT, (double)m * 24.0 * 2);   // (bucket scatter + in-LDS sort: two passes' bytes)
         } else {
             (void)hipGetLastError();
@@ -1857,18 +1871,7 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
                                                         : (cts_bits + 7) / 8 + (seg_bits + 7) / 8));
         }
     }
-    // a large order (a full pass: 40 MB at c3) is written by k_finish_order straight into the
-    // pinned host arena (coalesced writes over the host link while the kernel runs) instead of a
-    // D2H copy after it; a small one comes back with the block tables in the copy launch
-    bool direct = false;
-    if (order_dst && (size_t)m * 4 > kCopyKernelMax) {
-        void* d = nullptr;
-        if (hipHostGetDevicePointer(&d, order_dst, 0) == hipSuccess && d) {
-            a.order_gid = (int32_t*)d;
-            direct = true;
-        }
-    }
-    launch_finish_order(stream, a, m, vals, R, n);
+    if (!finished) launch_finish_order(stream, a, m, vals, R, n);
     launch_fu_advance(stream, a, C);
     for (int c = 0; c < C; c++) h_fu[c] += fo_cnt[c];
     stage_out.clear();

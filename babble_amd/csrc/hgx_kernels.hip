@@ -1665,6 +1665,26 @@ __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
     return 0;
 }
 
+// What k_finish_order does for an element of the order, done by the sort that places it (the bucket
+// sort's buckets are the blocks: bucket = graph * R + rr): the order's gid (written straight into the
+// pinned host arena when order_gid points there, so the host-link writes overlap the other buckets'
+// sorting), rr and the timestamp back in gid order, and the block's count, transactions, loaded events
+// and nil-ness (its first event's) written by the bucket's own group, no atomics.
+struct SortFinish {
+    const int32_t* p_rr;
+    const int64_t* p_cts;
+    const int32_t* g_ntx;
+    const uint8_t* g_loaded;
+    const uint8_t* g_txnil;
+    int32_t* order_gid;
+    int32_t* g_rr;
+    int64_t* g_cts;
+    int32_t* blk_cnt;
+    int64_t* blk_ntx;
+    int32_t* blk_loaded;
+    uint8_t* blk_nil;
+};
+
 // One bucket per group of GS threads (a workgroup of 1 024 threads, or a wave, GS = 64, four buckets
 // per workgroup when every bucket holds <= 512 events: 256 threads per bucket at c3 left the LDS latency
 // of the compare-exchange stages exposed, 1.14 ms per pass): bitonic sort of its (key, value) pairs in LDS
@@ -1672,13 +1692,15 @@ __device__ __forceinline__ int cmp_s(const uint8_t* a, const uint8_t* b) {
 // rr and timestamp) ordered by S in the same kernel: a run's members get the first 8 bytes of their S
 // (big-endian) in place of the key they share, and each member's place in its run is its rank by
 // (S prefix, full S on equal prefixes, index) -- the radix path's k_tie_prefix / k_tiefix_rank, with
-// the run in LDS (consensus_sorter.go:36-51). Writes the final values.
+// the run in LDS (consensus_sorter.go:36-51). Writes the final values and finishes them (SortFinish).
 template <int GS, int TB>
 __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
                                                   const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                   const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S,
-                                                  uint32_t* __restrict__ vout, int cap) {
+                                                  uint32_t* __restrict__ vout, int cap, SortFinish F) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    __shared__ int64_t red_ntx[TB / 64];
+    __shared__ int32_t red_ld[TB / 64];
     constexpr int NG = TB / GS;   // groups (buckets) per workgroup
     const int grp = (int)threadIdx.x / GS, t = (int)threadIdx.x % GS;
     uint64_t* sk = smem + (size_t)grp * cap;                               // [cap] keys, then S prefixes
@@ -1693,8 +1715,40 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
         o = (int)segoff[sgi];
         len = (sgi + 1 < nseg ? (int)segoff[sgi + 1] : m) - o;
     }
+    // element o + i of the order is position p
+    int64_t ntx = 0;
+    int ld = 0;
+    auto emit = [&](int i, uint32_t p) {
+        vout[o + i] = p;
+        const int gid = p_gid[p];
+        F.order_gid[o + i] = gid;
+        F.g_rr[gid] = F.p_rr[p];
+        F.g_cts[gid] = F.p_cts[p];
+        ntx += F.g_ntx[gid];
+        ld += F.g_loaded[gid] ? 1 : 0;
+        if (i == 0) F.blk_nil[sgi] = F.g_txnil[gid];   // NewBlock(rr, first.Transactions()), hashgraph.go:838-845
+    };
+    // the block's totals (group-uniform: every way out of the kernel goes through here)
+    auto block_totals = [&]() {
+        for (int w = 32; w >= 1; w >>= 1) {
+            ntx += __shfl_xor(ntx, w);
+            ld += __shfl_xor(ld, w);
+        }
+        if constexpr (GS > 64) {
+            if (lane_id() == 0) { red_ntx[threadIdx.x >> 6] = ntx; red_ld[threadIdx.x >> 6] = ld; }
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (int w = 1; w < TB / 64; w++) { ntx += red_ntx[w]; ld += red_ld[w]; }
+        }
+        if (t == 0 && len > 0) {
+            F.blk_cnt[sgi] = len;
+            F.blk_ntx[sgi] = ntx;
+            F.blk_loaded[sgi] = ld;
+        }
+    };
     if (len <= 1) {   // (group-uniform)
-        if (len == 1 && t == 0) vout[o] = vin[o];
+        if (len == 1 && t == 0) emit(0, vin[o]);
+        block_totals();
         return;
     }
     int P = 2;
@@ -1730,7 +1784,8 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
     }
     if constexpr (GS == 64) tie_any = __any(tie_any); else tie_any = __syncthreads_or(tie_any);
     if (!tie_any) {   // (group-uniform) every key distinct: the values are final
-        for (int i = t; i < len; i += GS) vout[o + i] = sv[i];
+        for (int i = t; i < len; i += GS) emit(i, sv[i]);
+        block_totals();
         return;
     }
     sync();
@@ -1757,7 +1812,7 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
         const int s0 = st[i];
         const bool member = s0 != i || (i + 1 < len && st[i + 1] == i);
         if (!member) {
-            vout[o + i] = sv[i];
+            emit(i, sv[i]);
             continue;
         }
         const uint64_t my = sk[i];
@@ -1769,8 +1824,9 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
             const int c = pj != my ? (pj < my ? -1 : 1) : (jx == i ? 0 : cmp_s(g_S + (size_t)p_gid[sv[jx]] * 32, si));
             rank += c < 0 || (c == 0 && jx < i);   // equal S (never in a valid trace): stable
         }
-        vout[o + s0 + rank] = vi;
+        emit(s0 + rank, vi);
     }
+    block_totals();
 }
 
 // grid-stride min/max of the received events' timestamps (biased to unsigned order);
@@ -2514,14 +2570,16 @@ hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t
     hipLaunchKernelGGL(k_seg_keys_scatter, dim3(nblk(m, 256)), dim3(256), 0, s, m, a.recv_list, a.p_cts, a.p_chain,
                        a.p_rr, cmin, cts_bits, R, n, segoff, segcur, kb, vb);
     // (the runs of equal keys are ordered by S inside k_seg_sort: the final values land in va)
+    const SortFinish F{a.p_rr, a.p_cts, a.g_ntx, a.g_loaded, a.g_txnil, a.order_gid, a.g_rr, a.g_cts,
+                       a.blk_cnt, a.blk_ntx, a.blk_loaded, a.blk_nil};
     if (cap <= 512) {   // a wave per bucket, four per workgroup
         const size_t lds = (size_t)4 * cap * 16;
         hipLaunchKernelGGL((k_seg_sort<64, 256>), dim3((nseg + 3) / 4), dim3(256), lds, s, nseg, m, segoff, kb, vb,
-                           a.p_gid, a.g_S, va, cap);
+                           a.p_gid, a.g_S, va, cap, F);
     } else {
         const size_t lds = (size_t)cap * 16;
         hipLaunchKernelGGL((k_seg_sort<1024, 1024>), dim3(nseg), dim3(1024), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
-                           a.g_S, va, cap);
+                           a.g_S, va, cap, F);
     }
     *final_vals = va;
     *final_keys = kb;
