@@ -535,7 +535,7 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
     // Per-d values are wave-uniform (SGPRs, and so is the chunk loop). The per-d scalars of up to 64 of the wave's chains are read in one LDS batch (lane q
     // holds chain d0 + nwaves*q) and taken with readlane, and the next chain's tile column is
     // read while the current one is written: no dependent LDS round trip per chain.
-    int32_t* slot = (int32_t*)(tw + (FT + 1) * ldw) + 64 * wave;
+    int32_t* slot = sm + ((3 * DB + (FT + 1) * ldw + 1) & ~1) + 128 * wave;   // 128 positions per chunk, 8-byte aligned
     const int ownv = base_c + k0;
     const int S = __builtin_amdgcn_readfirstlane(nwaves * zs);   // target stride
     for (int d0 = __builtin_amdgcn_readfirstlane(db0 + wave + nwaves * sub); d0 < db1; d0 += S * 64) {
@@ -585,21 +585,27 @@ __global__ void k_fd_build(const uint32_t* __restrict__ LA, CT* __restrict__ FDT
 #pragma unroll
             for (int u = 0; u < RPL; u++) own[u] = RPL * lane + u < rows && v[u] >= start[u];
             const int vlast = max(lo, min(hi_val, vmax));   // end of the tile's last range
-            // slots hold owner + 1 (0 = no range starts here)
+            // slots hold owner + 1 (0 = no range starts here); a chunk is 128 positions, two per lane
+            // (positions j0 + 2 lane and j0 + 2 lane + 1): half the chunk iterations of one per lane
             uint32_t carry = 0;
-            for (int j0 = lo + 1; j0 <= hi; j0 += 64) {   // scalar loop
-                slot[lane] = 0;
+            for (int j0 = lo + 1; j0 <= hi; j0 += 128) {   // scalar loop
+                *(uint2*)(slot + 2 * lane) = make_uint2(0u, 0u);
                 wave_lds_fence();
 #pragma unroll
                 for (int u = 0; u < RPL; u++)
-                    if (own[u] && (unsigned)(start[u] - j0) < 64u) slot[start[u] - j0] = RPL * lane + u + 1;
+                    if (own[u] && (unsigned)(start[u] - j0) < 128u) slot[start[u] - j0] = RPL * lane + u + 1;
                 // past the last row (last tile only): none = MaxInt32, sentinel owner FT
-                if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 64u) slot[vlast + 1 - j0] = 64 * RPL + 1;
+                if (last && lane == 0 && (unsigned)(vlast + 1 - j0) < 128u) slot[vlast + 1 - j0] = 64 * RPL + 1;
                 wave_lds_fence();
-                const uint32_t o1 = max(wave_incl_max_u((uint32_t)slot[lane]), carry);
-                carry = (uint32_t)__builtin_amdgcn_readlane((int)o1, 63);
-                const int o = (int)o1 - 1;
-                if (j0 + lane <= hi) out[j0 + lane] = K::enc_fd(o < rows ? ownv + o : kMaxI32);
+                const uint2 ab = *(const uint2*)(slot + 2 * lane);
+                const uint32_t inc = wave_incl_max_u(max(ab.x, ab.y));
+                // the owners before this lane's pair: the inclusive scan one lane back (lane 0: the carry)
+                const uint32_t before = max((uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, false), carry);
+                const uint32_t oa = max(before, ab.x), ob = max(oa, ab.y);
+                carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)inc, 63));
+                const int ja = j0 + 2 * lane;
+                if (ja <= hi) out[ja] = K::enc_fd((int)oa - 1 < rows ? ownv + (int)oa - 1 : kMaxI32);
+                if (ja + 1 <= hi) out[ja + 1] = K::enc_fd((int)ob - 1 < rows ? ownv + (int)ob - 1 : kMaxI32);
             }
         }
     }
@@ -2314,7 +2320,7 @@ void launch_fd_build(hipStream_t s, const DevArrays& a, int C, int n, int max_le
     const int ncb = (d_hi - d_lo + DB - 1) / DB;
     const int wdw = DB / (a.compact ? 2 : 1) + 1;   // words of a tile row, the worst alignment
     // tile + per-target scalars + 8 waves x 64 owner slots
-    const size_t lds = ((size_t)(ft + 1) * (wdw + 1) + 3 * (size_t)DB + 8 * 64) * sizeof(int32_t);
+    const size_t lds = ((size_t)(ft + 1) * (wdw + 1) + 1 + 3 * (size_t)DB + 8 * 128) * sizeof(int32_t);
     // a resumed call with a few new rows per chain: a column block's targets split over up to 8 blocks
     const int zs = (c_old && max_new <= ft) ? max(1, min(8, DB / 64)) : 1;
     const dim3 grid(C, tiles, ncb * zs);
