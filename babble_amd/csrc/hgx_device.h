@@ -243,4 +243,32 @@ __device__ uint32_t wave_select_kth32(const uint32_t (&v)[CPL], const bool (&ok)
     return lo + prefix;
 }
 
+// The same k-th smallest by bisection on the value: each step counts the valid values <= mid with
+// CPL compares whose ballots are popcounted in SGPRs (no LDS, no atomics). For rows whose values
+// crowd into a few buckets (the witnesses' lastAncestors of one chain in k_threshold span a few
+// dozen indices), the radix select's LDS atomics hit the same bins from most lanes and serialise;
+// here a step costs CPL VALU compares and a handful of scalar ops, log2(range) steps.
+template <int CPL>
+__device__ uint32_t wave_select_kth32_bisect(const uint32_t (&v)[CPL], const bool (&ok)[CPL], int K) {
+    uint32_t lo = 0xffffffffu, hi = 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++)
+        if (ok[q]) { lo = min(lo, v[q]); hi = max(hi, v[q]); }
+    lo = wave_reduce_min_u32(lo);
+    hi = wave_reduce_max_u32(hi);
+    uint32_t a = 0, b = hi - lo;   // answer in [a, b]: the smallest t with #(v - lo <= t) > K
+    uint32_t d[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; q++) d[q] = ok[q] ? v[q] - lo : 0xffffffffu;   // (invalid: above every t < 2^32 - 1)
+    while (a < b) {
+        const uint32_t mid = a + ((b - a) >> 1);
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) cnt += __popcll(__ballot(d[q] <= mid));
+        if (cnt > K) b = mid;
+        else a = mid + 1;
+    }
+    return lo + a;
+}
+
 }  // namespace hgx

@@ -1032,6 +1032,28 @@ __global__ void __launch_bounds__(256) k_wla_transpose(int R, int r0, int G, int
     if (!elig[(size_t)g * R + i]) return;
     const int nt = (n + 63) / 64, tc = blockIdx.x % nt, td = blockIdx.x / nt;
     const size_t base = ((size_t)i * C + (size_t)g * n) * n;
+    if ((n & 63) == 0) {   // whole 64 x 64 tiles: 16-byte loads and stores (thread = 4 coordinates x 4 rows)
+        const uint8_t* __restrict__ fwr = fw + (size_t)i * C + (size_t)g * n + tc * 64;
+        const int c4 = (threadIdx.x & 15) * 4, r4 = threadIdx.x >> 4;   // 16 threads per 256-byte row
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int r = r4 + 16 * h;   // candidate tc * 64 + r, coordinates td * 64 + c4 ..
+            const int4 v = *(const int4*)(WLA + base + (size_t)(tc * 64 + r) * n + td * 64 + c4);
+            const bool f = fwr[r] != 0;
+            t[r][c4] = f ? v.x : kWlatNotFamous;
+            t[r][c4 + 1] = f ? v.y : kWlatNotFamous;
+            t[r][c4 + 2] = f ? v.z : kWlatNotFamous;
+            t[r][c4 + 3] = f ? v.w : kWlatNotFamous;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int d = r4 + 16 * h;   // coordinate td * 64 + d, candidates tc * 64 + c4 ..
+            *(int4*)(WLAT + base + (size_t)(td * 64 + d) * n + tc * 64 + c4) =
+                make_int4(t[c4][d], t[c4 + 1][d], t[c4 + 2][d], t[c4 + 3][d]);
+        }
+        return;
+    }
     for (int k = threadIdx.x; k < 64 * 64; k += 256) {
         const int r = k >> 6, col = k & 63, c = tc * 64 + r, d = td * 64 + col;
         t[r][col] = (c < n && d < n) ? (fw[(size_t)i * C + (size_t)g * n + c] ? WLA[base + (size_t)c * n + d]
@@ -1056,7 +1078,6 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
     const int i = r0 + (int)(item / C), gd = (int)(item % C);
     const int g = gd / n;
     if (!elig[(size_t)g * R + i]) return;
-    __shared__ __attribute__((aligned(16))) uint32_t whist[4][256];
     const int lane = lane_id();
     const size_t row = ((size_t)i * C + gd) * n;
     uint32_t v[CPL];   // int32 order as u32: sign bit flipped
@@ -1072,7 +1093,7 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
     }
     int32_t res = -1;
     if (m > 0) {   // (m/2)-th largest = (m-1-m/2)-th smallest
-        const uint32_t u = wave_select_kth32<CPL>(v, ok, m - 1 - m / 2, whist[(threadIdx.x >> 6) & 3]);
+        const uint32_t u = wave_select_kth32_bisect<CPL>(v, ok, m - 1 - m / 2);
         res = (int32_t)(u ^ 0x80000000u);
     }
     if (lane == 0) T[(size_t)i * C + gd] = res;
@@ -1084,6 +1105,11 @@ __global__ void __launch_bounds__(256) k_threshold(int R, int r0, const uint8_t*
 // of a chain are always a prefix of it: a famous witness that sees x sees x's self-parent,
 // so rr(self-parent) <= rr(x) under the same eligible rounds (hashgraph.go:753-799). So the
 // newly received events of chain c are [fu[c], fu[c] + rcnt[c]).
+// A block takes kRrPer x 256 consecutive positions of one chain (thread t: t, t + 256, ...); the received
+// lanes of each batch get their slots from the waves' ballots (no LDS atomics), and the block appends
+// once to the global list (one global atomic per kRrPer x 256 events: at c3 39 k blocks with one
+// returning atomic each on the same word were the kernel's tail).
+constexpr int kRrPer = 4;
 __global__ void __launch_bounds__(256) k_round_received(int R, const int32_t* __restrict__ c_off,
                                  const int32_t* __restrict__ c_len, const int32_t* __restrict__ c_base,
                                  const int32_t* __restrict__ fu, const int32_t* __restrict__ p_round,
@@ -1091,37 +1117,53 @@ __global__ void __launch_bounds__(256) k_round_received(int R, const int32_t* __
                                  const uint8_t* __restrict__ ur_empty, const int32_t* __restrict__ T,
                                  int32_t* __restrict__ p_rr, int32_t* __restrict__ rcnt, int32_t* __restrict__ recv_list,
                                  int32_t* __restrict__ counters, int C, int n) {
-    __shared__ int32_t s_cnt, s_base;
+    __shared__ int32_t s_wcnt[kRrPer][4], s_base;
     const int gc = blockIdx.y;
-    const int k = fu[gc] + blockIdx.x * 256 + threadIdx.x;
+    const int f = fu[gc];
     const int len = c_len[gc];
-    if (fu[gc] + (int)blockIdx.x * 256 >= len) return;   // block-uniform
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    int slot = -1;
-    const int64_t p = (int64_t)c_off[gc] + k;
-    if (k < len) {
-        const int g = gc / n;
-        const int j = c_base[gc] + k;
-        const int r = p_round[p];
-        const int LR = lr[g];
-        if (r + 1 <= LR && ur_empty[g]) atomicOr(&counters[1], 1);   // Go panics on UndecidedRounds[0]
-        int rr = -1;
-        for (int i = r + 1; i <= LR; i++) {
-            if (elig[(size_t)g * R + i] && j <= T[(size_t)i * C + gc]) { rr = i; break; }
+    const int k0 = f + blockIdx.x * (256 * kRrPer);
+    if (k0 >= len) return;   // block-uniform
+    const int g = gc / n;
+    const int LR = lr[g];
+    const int64_t co = c_off[gc];
+    const int jb = c_base[gc];
+    const int w = threadIdx.x >> 6;
+    const uint8_t* el = elig + (size_t)g * R;
+    bool got[kRrPer];
+    uint32_t below[kRrPer];   // received lanes of this wave below this lane, per batch
+#pragma unroll
+    for (int q = 0; q < kRrPer; q++) {
+        const int k = k0 + q * 256 + (int)threadIdx.x;
+        got[q] = false;
+        if (k < len) {
+            const int64_t p = co + k;
+            const int j = jb + k;
+            const int r = p_round[p];
+            if (r + 1 <= LR && ur_empty[g]) atomicOr(&counters[1], 1);   // Go panics on UndecidedRounds[0]
+            for (int i = r + 1; i <= LR; i++) {
+                if (el[i] && j <= T[(size_t)i * C + gc]) {
+                    p_rr[p] = i;
+                    got[q] = true;
+                    break;
+                }
+            }
         }
-        if (rr >= 0) {
-            p_rr[p] = rr;
-            slot = atomicAdd(&s_cnt, 1);
-        }
+        const uint64_t b = __ballot(got[q]);
+        below[q] = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (lane_id() == 0) s_wcnt[q][w] = __popcll(b);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && s_cnt) {
-        s_base = atomicAdd(&counters[0], s_cnt);
-        atomicAdd(&rcnt[gc], s_cnt);
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int q = 0; q < kRrPer; q++)
+            for (int v = 0; v < 4; v++) { const int c = s_wcnt[q][v]; s_wcnt[q][v] = tot; tot += c; }   // exclusive
+        s_base = tot ? atomicAdd(&counters[0], tot) : 0;
+        if (tot) atomicAdd(&rcnt[gc], tot);
     }
     __syncthreads();
-    if (slot >= 0) recv_list[s_base + slot] = (int32_t)p;
+#pragma unroll
+    for (int q = 0; q < kRrPer; q++)
+        if (got[q]) recv_list[s_base + s_wcnt[q][w] + (int)below[q]] = (int32_t)(co + k0 + q * 256 + (int)threadIdx.x);
 }
 
 // fu[c] += rcnt[c] after the order of a FindOrder is written
@@ -2405,7 +2447,7 @@ void launch_threshold(hipStream_t s, const DevArrays& a, int r0, int R, int C, i
 
 void launch_round_received(hipStream_t s, const DevArrays& a, int R, int C, int n, int max_unrecv) {
     if (max_unrecv <= 0) return;
-    hipLaunchKernelGGL(k_round_received, dim3(nblk(max_unrecv, 256), C), dim3(256), 0, s, R, a.c_off, a.c_len,
+    hipLaunchKernelGGL(k_round_received, dim3(nblk(max_unrecv, 256 * kRrPer), C), dim3(256), 0, s, R, a.c_off, a.c_len,
                        a.c_base, a.fu, a.p_round, a.lr, a.elig, a.ur_empty, a.T, a.p_rr, a.rcnt, a.recv_list,
                        a.counters, C, n);
 }

@@ -974,7 +974,15 @@ __global__ void __launch_bounds__(256) k_round_p_post(RoundArgs A, int r_lo, int
             if (kq >= len) continue;   // (wave-uniform)
             const CT* row = LA + (size_t)(off + kq) * n;
             int32_t* dst = A.WLA + ((size_t)(r0 + q + 1) * C + gc) * n;
-            for (int i = lane; i < n; i += 64) dst[i] = Coord<CT>::la(row[i]);
+            if (sizeof(CT) == 2 && (n & 1) == 0) {   // compact: two coordinates per lane (4-byte loads, 8-byte stores)
+                const uint32_t* row2 = (const uint32_t*)row;
+                for (int i = lane; i < n / 2; i += 64) {
+                    const uint32_t v = row2[i];
+                    *(int2*)(dst + 2 * i) = make_int2(Coord<CT>::la(v & 0xFFFFu), Coord<CT>::la(v >> 16));
+                }
+            } else {
+                for (int i = lane; i < n; i += 64) dst[i] = Coord<CT>::la(row[i]);
+            }
         }
     }
 }

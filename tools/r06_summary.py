@@ -19,6 +19,9 @@ if d.get("packed_columns"):
     out["packed"] = {k: round(pc[k], 3) for k in ("ms_per_step_incl_pack", "pack_ms", "ms_per_step_excl_pack")}
 k = d.get("kernels_per_pass") or {}
 out["kernels"] = {x: v["ms"] for x, v in sorted(k.items(), key=lambda kv: -kv[1]["ms"])[:8]}
+for x in ("round_received", "threshold", "order_sort"):
+    if x in k:
+        out[x] = k[x]["ms"]
 if d.get("sharded"):
     s = d["sharded"]
     out["sharded"] = s if "error" in s or "skipped" in s else {
