@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 
 namespace hgx {
 
@@ -134,6 +135,11 @@ Engine::~Engine() {
     if (h_ins) (void)hipHostFree(h_ins);
     if (h_cpar) (void)hipHostFree(h_cpar);
     if (h_flag) (void)hipHostFree(h_flag);
+    if (h_segc) (void)hipHostFree(h_segc);
+    if (stream_o) (void)hipStreamSynchronize(stream_o);
+    for (auto e : ev_o)
+        if (e) (void)hipEventDestroy(e);
+    if (stream_o) (void)hipStreamDestroy(stream_o);
     for (auto e : flag_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : la_ev)
@@ -1810,15 +1816,23 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
     // by the bucket sort itself, which finishes every bucket it places (k_seg_sort, SortFinish: its
     // host-link writes overlap the other buckets' sorting), or by k_finish_order after the other
     // sorts; a small one comes back with the block tables in the copy launch
-    bool direct = false, finished = false;
-    if (order_dst && (size_t)m * 4 > kCopyKernelMax) {
-        void* d = nullptr;
-        if (hipHostGetDevicePointer(&d, order_dst, 0) == hipSuccess && d) {
-            a.order_gid = (int32_t*)d;
+    // A large order into a pinned order_dst: the bucket sort runs in kOrderParts parts of about equal
+    // event counts, each part's order copied to the host (DMA on stream_o) while the next part sorts
+    // (round 6: the sort writing the gids over the host link itself took as long as sorting and copying
+    // one after the other, c3 1.0 + 0.85 ms); the other sorts write the order straight into the arena.
+    void* dst_dev = nullptr;
+    const bool big_dst = order_dst && (size_t)m * 4 > kCopyKernelMax &&
+                         hipHostGetDevicePointer(&dst_dev, order_dst, 0) == hipSuccess && dst_dev;
+    if (order_dst && !big_dst) (void)hipGetLastError();   // (a pageable order_dst: the query's error is not sticky)
+    bool direct = false, finished = false, piped = false;
+    auto go_direct = [&]() {
+        if (big_dst) {
+            a.order_gid = (int32_t*)dst_dev;
             direct = true;
         }
-    }
+    };
     if (small) {
+        go_direct();
         kbeg(K_SORT);
         launch_sort_small(stream, a, m, n, &vals);
         kend(K_SORT, (double)m * 24.0);
@@ -1844,6 +1858,19 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         } else {
             launch_minmax(stream, a, m);
         }
+        // (the bucket counts come back in the same round trip; below kOrderPipeMin the parts' launch tails
+        // cost more than the copy they hide -- c2, 4 MB: order sort 0.23 -> 0.43 ms -- and the sort writes
+        // the order straight into the arena)
+        const bool want_cuts = seg_try && big_dst && (size_t)m * 4 >= kOrderPipeMin;
+        if (want_cuts && h_segc_n < (size_t)nseg) {
+            if (h_segc) HGX_TRY(hipHostFree(h_segc));
+            h_segc = nullptr;
+            h_segc_n = 0;
+            const size_t cap = std::max((size_t)nseg, (size_t)G * std::max(r_cap, 1));
+            HGX_TRY(hipHostMalloc((void**)&h_segc, cap * 4, hipHostMallocDefault));
+            h_segc_n = cap;
+        }
+        if (want_cuts) HGX_TRY(hipMemcpyAsync(h_segc, seg_off.p, (size_t)nseg * 4, hipMemcpyDeviceToHost, stream));
         unsigned long long mm[3];
         HGX_TRY(hipMemcpyAsync(mm, minmax.p, 24, hipMemcpyDeviceToHost, stream));
         HGX_TRY(hipStreamSynchronize(stream));
@@ -1855,16 +1882,61 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
         kbeg(K_SORT);
         // (a refused LDS limit for the 1 024-thread bucket sort is reported before anything is
         // launched, and the radix passes run instead)
-        const bool seg = seg_try && cts_bits + seg_bits <= 64 && mm[2] >= 1 &&
-                         mm[2] <= (unsigned long long)seg_sort_cap() &&
-                         launch_sort_seg(stream, a, m, cmin, cts_bits, R, n, nseg, seg_off.p, seg_cur.p, (int)mm[2],
-                                         &vals, &keys) == hipSuccess;
+        const bool seg_ok = seg_try && cts_bits + seg_bits <= 64 && mm[2] >= 1 &&
+                            mm[2] <= (unsigned long long)seg_sort_cap();
+        // parts: cuts[k] = the first bucket of part k, off[k] = its first element of the order
+        std::vector<int> cuts;
+        std::vector<int64_t> off;
+        if (seg_ok && want_cuts) {
+            cuts.push_back(0);
+            off.push_back(0);
+            int64_t cum = 0;
+            for (int sg = 0; sg < nseg && (int)cuts.size() < kOrderParts; sg++) {
+                cum += h_segc[sg];
+                if (cum * kOrderParts >= (int64_t)m * (int64_t)cuts.size() && sg + 1 < nseg) {
+                    cuts.push_back(sg + 1);
+                    off.push_back(cum);
+                }
+            }
+            cuts.push_back(nseg);
+            off.push_back(m);
+            piped = cuts.size() > 2;
+            if (piped && !stream_o) {
+                HGX_TRY(hipStreamCreateWithFlags(&stream_o, hipStreamNonBlocking));
+                for (auto& e : ev_o) HGX_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            }
+        }
+        // (a failure here is fatal, not a fallback to the radix passes: earlier parts' copies are queued)
+        hipError_t part_err = hipSuccess;
+        const std::function<hipError_t(int)> copy_part = [&](int k) -> hipError_t {
+            const int64_t o0 = off[k], cnt = off[k + 1] - off[k];
+            if (cnt <= 0) return hipSuccess;
+            part_err = hipEventRecord(ev_o[k], stream);
+            if (part_err == hipSuccess) part_err = hipStreamWaitEvent(stream_o, ev_o[k], 0);
+            if (part_err == hipSuccess)
+                part_err = hipMemcpyAsync(order_dst + o0, order_gid.p + o0, (size_t)cnt * 4, hipMemcpyDeviceToHost,
+                                          stream_o);
+            return part_err;
+        };
+        if (seg_ok && !piped) go_direct();
+        const bool seg = seg_ok && launch_sort_seg(stream, a, m, cmin, cts_bits, R, n, nseg, seg_off.p, seg_cur.p,
+                                                   (int)mm[2], &vals, &keys, piped ? &cuts : nullptr,
+                                                   piped ? copy_part : nullptr) == hipSuccess;
+        HGX_TRY(part_err);
         if (seg) {
             sort_seg_runs++;
             finished = true;
+            if (piped) {   // the stream waits for the last part's copy
+                HGX_TRY(hipEventRecord(ev_o[kOrderParts], stream_o));
+                HGX_TRY(hipStreamWaitEvent(stream, ev_o[kOrderParts], 0));
+            }
             kend(K_SORT, (double)m * 24.0 * 2);   // (bucket scatter + in-LDS sort: two passes' bytes)
         } else {
             (void)hipGetLastError();
+            piped = false;
+            direct = false;
+            a.order_gid = order_gid.p;
+            go_direct();
             launch_sort(stream, a, m, cmin, cts_bits, R, n, seg_bits, &vals, &keys);
             kend(K_SORT, (double)m * 24.0 *
                              (cts_bits + seg_bits <= 64 ? (cts_bits + seg_bits + 7) / 8
@@ -1881,7 +1953,7 @@ hipError_t Engine::find_order_end(OrderHost& out, int32_t* order_dst) {
     HGX_TRY(stage_d2h(out.blk_ntx.data(), blk_ntx.p, (size_t)G * R * 8));
     HGX_TRY(stage_d2h(out.blk_loaded.data(), blk_loaded.p, (size_t)G * R * 4));
     HGX_TRY(stage_d2h(out.blk_nil.data(), blk_nil.p, (size_t)G * R));
-    if (order_dst && !direct) HGX_TRY(copy_to_pinned(order_dst, order_gid.p, (size_t)m * 4));
+    if (order_dst && !direct && !piped) HGX_TRY(copy_to_pinned(order_dst, order_gid.p, (size_t)m * 4));
     HGX_TRY(stage_issue());
     HGX_TRY(hipEventRecord(ph1, stream));
     HGX_TRY(hipEventSynchronize(ph1));

@@ -425,6 +425,14 @@ class Engine {
     hipError_t copy_from_pinned(void* dev, const void* pinned_src, size_t bytes);
     hipError_t stage_issue();
     void stage_flush();   // after the stream synchronized: copy the D2H tables out, reset the cursor
+    // the bucket sort's parts (find_order_end): bucket counts read back with the timestamp range, the
+    // order's D2H copies on their own stream behind each part
+    static constexpr int kOrderParts = 4;
+    static constexpr size_t kOrderPipeMin = 16u << 20;   // order bytes from which the parts pay
+    uint32_t* h_segc = nullptr;
+    size_t h_segc_n = 0;
+    hipStream_t stream_o = nullptr;
+    hipEvent_t ev_o[kOrderParts + 1] = {};
     int32_t* h_flag = nullptr;    // host-mapped, coherent: the round-step batches' "candidates left" flags
     int32_t* d_flag = nullptr;    // its device address
     // timing

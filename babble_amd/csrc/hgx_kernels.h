@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <vector>
 
 namespace hgx {
 
@@ -300,8 +302,12 @@ void launch_sort(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int
 int seg_sort_cap();
 void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n, int nseg, uint32_t* segc,
                       unsigned long long* max_out);
+// (cuts: optional bucket boundaries 0 = c_0 < ... < c_K = nseg; the parts are launched in order and
+// after_part(k) runs on the host behind part k's launch)
 hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n, int nseg,
-                     uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys);
+                     uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals, uint64_t** final_keys,
+                     const std::vector<int>* cuts = nullptr,
+                     const std::function<hipError_t(int)>& after_part = nullptr);
 // m <= 4096: one block sorts (graph, rr, cts, S) (no cts range needed)
 bool sort_small_ok(int32_t m);
 void launch_sort_small(hipStream_t s, const DevArrays& a, int32_t m, int n, uint32_t** final_vals);

@@ -1742,7 +1742,7 @@ struct SortFinish {
 // (S prefix, full S on equal prefixes, index) -- the radix path's k_tie_prefix / k_tiefix_rank, with
 // the run in LDS (consensus_sorter.go:36-51). Writes the final values and finishes them (SortFinish).
 template <int GS, int TB>
-__global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint32_t* __restrict__ segoff,
+__global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int seg0, int seg1, int32_t m, const uint32_t* __restrict__ segoff,
                                                   const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                   const int32_t* __restrict__ p_gid, const uint8_t* __restrict__ g_S,
                                                   uint32_t* __restrict__ vout, int cap, SortFinish F) {
@@ -1757,9 +1757,9 @@ __global__ void __launch_bounds__(TB) k_seg_sort(int nseg, int32_t m, const uint
     auto sync = [&]() {
         if constexpr (GS == 64) wave_lds_fence(); else __syncthreads();
     };
-    const int sgi = (int)blockIdx.x * NG + grp;
+    const int sgi = seg0 + (int)blockIdx.x * NG + grp;   // buckets [seg0, seg1) of nseg
     int o = 0, len = 0;
-    if (sgi < nseg) {
+    if (sgi < seg1) {
         o = (int)segoff[sgi];
         len = (sgi + 1 < nseg ? (int)segoff[sgi + 1] : m) - o;
     }
@@ -2604,7 +2604,8 @@ void launch_seg_count(hipStream_t s, const DevArrays& a, int32_t m, int R, int n
 
 hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t cmin, int cts_bits, int R, int n,
                            int nseg, uint32_t* segoff, uint32_t* segcur, int max_seg, uint32_t** final_vals,
-                           uint64_t** final_keys) {
+                           uint64_t** final_keys, const std::vector<int>* cuts,
+                           const std::function<hipError_t(int)>& after_part) {
     uint64_t* kb = a.key_b;
     uint32_t *va = a.val_a, *vb = a.val_b;
     int cap = 2;
@@ -2620,14 +2621,26 @@ hipError_t launch_sort_seg(hipStream_t s, const DevArrays& a, int32_t m, int64_t
     // (the runs of equal keys are ordered by S inside k_seg_sort: the final values land in va)
     const SortFinish F{a.p_rr, a.p_cts, a.g_ntx, a.g_loaded, a.g_txnil, a.order_gid, a.g_rr, a.g_cts,
                        a.blk_cnt, a.blk_ntx, a.blk_loaded, a.blk_nil};
-    if (cap <= 512) {   // a wave per bucket, four per workgroup
-        const size_t lds = (size_t)4 * cap * 16;
-        hipLaunchKernelGGL((k_seg_sort<64, 256>), dim3((nseg + 3) / 4), dim3(256), lds, s, nseg, m, segoff, kb, vb,
-                           a.p_gid, a.g_S, va, cap, F);
-    } else {
-        const size_t lds = (size_t)cap * 16;
-        hipLaunchKernelGGL((k_seg_sort<1024, 1024>), dim3(nseg), dim3(1024), lds, s, nseg, m, segoff, kb, vb, a.p_gid,
-                           a.g_S, va, cap, F);
+    // the buckets in parts [cuts[k], cuts[k + 1]) (one part without cuts), after_part(k) behind each part's
+    // launch (the caller's D2H of that part's order, overlapping the next part's sort)
+    const int np = cuts ? (int)cuts->size() - 1 : 1;
+    for (int k = 0; k < np; k++) {
+        const int s0 = cuts ? (*cuts)[k] : 0, s1 = cuts ? (*cuts)[k + 1] : nseg;
+        if (s1 > s0) {
+            if (cap <= 512) {   // a wave per bucket, four per workgroup
+                const size_t lds = (size_t)4 * cap * 16;
+                hipLaunchKernelGGL((k_seg_sort<64, 256>), dim3((s1 - s0 + 3) / 4), dim3(256), lds, s, nseg, s0, s1, m,
+                                   segoff, kb, vb, a.p_gid, a.g_S, va, cap, F);
+            } else {
+                const size_t lds = (size_t)cap * 16;
+                hipLaunchKernelGGL((k_seg_sort<1024, 1024>), dim3(s1 - s0), dim3(1024), lds, s, nseg, s0, s1, m, segoff,
+                                   kb, vb, a.p_gid, a.g_S, va, cap, F);
+            }
+        }
+        if (after_part) {
+            const hipError_t e = after_part(k);
+            if (e != hipSuccess) return e;
+        }
     }
     *final_vals = va;
     *final_keys = kb;
