@@ -93,10 +93,12 @@ __device__ __forceinline__ void settle(uint32_t (&v)[DW]) {
 template <int DW>
 __device__ __forceinline__ void ring_load(const uint32_t* p, uint32_t (&v)[DW]) {
     HGX_CB();
-    if constexpr (DW == 8) {
-        const uint4 x = *(const uint4*)p, y = *(const uint4*)(p + 4);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    if constexpr (DW % 8 == 0) {   // 8 or 16 words: 16-byte accesses
+#pragma unroll
+        for (int k = 0; k < DW / 4; k++) {
+            const uint4 x = ((const uint4*)p)[k];
+            v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
+        }
     } else if constexpr (DW == 4) {
         const uint4 x = *(const uint4*)p;
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
@@ -111,9 +113,9 @@ __device__ __forceinline__ void ring_load(const uint32_t* p, uint32_t (&v)[DW]) 
 template <int DW>
 __device__ __forceinline__ void ring_store(uint32_t* p, const uint32_t (&v)[DW]) {
     HGX_CB();
-    if constexpr (DW == 8) {
-        *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
-        *(uint4*)(p + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+    if constexpr (DW % 8 == 0) {
+#pragma unroll
+        for (int k = 0; k < DW / 4; k++) ((uint4*)p)[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     } else if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
     else if constexpr (DW == 2) *(uint2*)p = make_uint2(v[0], v[1]);
     else *p = v[0];
@@ -121,9 +123,9 @@ __device__ __forceinline__ void ring_store(uint32_t* p, const uint32_t (&v)[DW])
 }
 template <int DW>
 __device__ __forceinline__ void row_store(uint32_t* p, const uint32_t (&v)[DW]) {
-    if constexpr (DW == 8) {
-        *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
-        *(uint4*)(p + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+    if constexpr (DW % 8 == 0) {
+#pragma unroll
+        for (int k = 0; k < DW / 4; k++) ((uint4*)p)[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     } else if constexpr (DW == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
     else if constexpr (DW == 2) *(uint2*)p = make_uint2(v[0], v[1]);
     else *p = v[0];
@@ -334,7 +336,9 @@ __global__ void __launch_bounds__(1024) k_la_wave(uint32_t* __restrict__ LA, con
         }
         // the store of row k - R (this slot's previous row) must be complete before the
         // slot is reused: at least R - 1 later stores of this lane were issued since
-        if constexpr (R >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        // (64-byte blocks: four stores per row, so 23 outstanding = at most rows k - 1 .. k - 6)
+        if constexpr (DW == 16 && R == 8) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+        else if constexpr (R >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
         const int ws = (((unsigned)k % R) << lgnp) + i;
         lds_st(&ring_t[ws], kTagBusy);
@@ -383,6 +387,10 @@ struct SegCfg {
     int dw, r, q;
 };
 inline SegCfg seg_cfg(int n, int nwd) {
+    // n in (128, 256]: 64-byte blocks (half the column blocks, so twice the time segments fill the CUs: a
+    // segment's pass walks half the DAG depth), the descriptor queue at 16 to keep one workgroup's LDS
+    // under 160 KB
+    if (n > 128 && n <= 256 && nwd % 16 == 0) return {16, 8, 16};
     if (n <= 256) return {nwd % 8 == 0 ? 8 : (nwd % 4 == 0 ? 4 : 1), 8, 32};
     if (n <= 512) return {nwd % 4 == 0 ? 4 : 1, 8, 16};
     return {nwd % 2 == 0 ? 2 : 1, 8, 8};
@@ -399,6 +407,7 @@ hipError_t la_wave_dispatch(hipStream_t s, const DevArrays& a, int G, int n, con
                                                                           na)                                          \
                     : la_wave_launch1<CT, DW_, R_, Q_, NLW_, J_, CH_, 2>(s, a, G, n, nullptr, E, nts, 0, err, lmap, na)
         if (n <= 256) {
+            if (g.dw == 16) SEG(16, 8, 16, 1, 4, 8);
             if (g.dw == 8) SEG(8, 8, 32, 1, 4, 8);
             if (g.dw == 4) SEG(4, 8, 32, 1, 4, 8);
             SEG(1, 8, 32, 1, 4, 8);
